@@ -1,0 +1,293 @@
+"""ctypes wrapper over oracle/liboracle.so -- the CPU restatement of the reference path.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker.  The product package never imports this module.
+Each function names the reference code it restates (see hrf_oracle.c for the full
+citations).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    src = os.path.join(_HERE, "hrf_oracle.c")
+    if not os.path.exists(_LIB) or os.path.getmtime(src) > os.path.getmtime(_LIB):
+        subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+    return _LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        _lib = ctypes.CDLL(_LIB)
+        _lib.oracle_segcos.restype = ctypes.c_double
+        _lib.oracle_label.restype = ctypes.c_int32
+        _lib.oracle_relabel_sequential.restype = ctypes.c_int32
+        _lib.oracle_kmeans_1d.restype = ctypes.c_int
+        _lib.oracle_kmeans_scale.restype = ctypes.c_int
+        _lib.oracle_kmeans_scale.argtypes = [ctypes.c_double, ctypes.c_int64]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+I64 = ctypes.c_int64
+
+
+# ---- a5/a7 ---------------------------------------------------------------------------
+def lp_table_2d(patch=11, nphi=9):
+    """neighbor2d.pyx:32-55 -> int32 [nphi, patch, 2]"""
+    out = np.zeros((nphi, patch, 2), np.int32)
+    lib().oracle_lp_table_2d(patch, nphi, _p(out))
+    return out
+
+
+def lp_table_3d(patch=11, ntheta=9, nphi=9):
+    """neighbor.pyx:209-243 -> int32 [(ntheta-1)*nphi, patch, 3]"""
+    out = np.zeros(((ntheta - 1) * nphi, patch, 3), np.int32)
+    lib().oracle_lp_table_3d(patch, ntheta, nphi, _p(out))
+    return out
+
+
+def line_profile_2d(pad, patch=11, nphi=9):
+    """neighbor2d.line_profile_2d_v2 (neighbor2d.pyx:8-64)"""
+    pad = _c(pad, np.float64)
+    hp, wp = pad.shape
+    out = np.zeros((hp - patch + 1, wp - patch + 1, nphi, patch), np.float64)
+    lib().oracle_line_profile_2d(_p(pad), I64(hp), I64(wp), patch, nphi, _p(out))
+    return out
+
+
+def enhance_2d(pad, patch=11, nphi=9):
+    """multispecies_spectral_image_measurement.py:110-124 -> final (H, W) f64"""
+    pad = _c(pad, np.float64)
+    hp, wp = pad.shape
+    out = np.zeros((hp - patch + 1, wp - patch + 1), np.float64)
+    lib().oracle_enhance_2d(_p(pad), I64(hp), I64(wp), patch, nphi, _p(out))
+    return out
+
+
+def line_profile_3d(pad, patch=11, ntheta=9, nphi=9):
+    """neighbor.line_profile_v2 (neighbor.pyx:115-181)"""
+    pad = _c(pad, np.float64)
+    xp, yp, zp = pad.shape
+    nd = (ntheta - 1) * nphi
+    out = np.zeros((xp - patch + 1, yp - patch + 1, zp - patch + 1, nd, patch), np.float64)
+    lib().oracle_line_profile_3d(_p(pad), I64(xp), I64(yp), I64(zp), patch, ntheta, nphi, _p(out))
+    return out
+
+
+def line_profile_3d_norm(pad, patch=11, ntheta=9, nphi=9):
+    """neighbor.line_profile_memory_efficient_v2 (neighbor.pyx:186-263)"""
+    pad = _c(pad, np.float64)
+    xp, yp, zp = pad.shape
+    nd = (ntheta - 1) * nphi
+    out = np.zeros((xp - patch + 1, yp - patch + 1, zp - patch + 1, nd), np.float64)
+    lib().oracle_line_profile_3d_norm(_p(pad), I64(xp), I64(yp), I64(zp), patch, ntheta, nphi, _p(out))
+    return out
+
+
+def enhance_3d(pad, patch=11, ntheta=9, nphi=9):
+    """biofilm_analysis.py:811-817 -> final (X, Y, Z) f64"""
+    pad = _c(pad, np.float64)
+    xp, yp, zp = pad.shape
+    out = np.zeros((xp - patch + 1, yp - patch + 1, zp - patch + 1), np.float64)
+    lib().oracle_enhance_3d(_p(pad), I64(xp), I64(yp), I64(zp), patch, ntheta, nphi, _p(out))
+    return out
+
+
+# ---- a9/a10/a12/a13 ------------------------------------------------------------------
+def label(img, conn=2):
+    """skimage.measure.label(img, connectivity=conn) (background 0, equal-value components)"""
+    img = _c(img, np.int32)
+    out = np.zeros(img.shape, np.int32)
+    n = lib().oracle_label(_p(img), I64(img.shape[0]), I64(img.shape[1]), conn, _p(out))
+    return out, int(n)
+
+
+def erode(mask, border=1):
+    m = _c(mask, np.uint8)
+    out = np.zeros(m.shape, np.uint8)
+    lib().oracle_erode(_p(m), I64(m.shape[0]), I64(m.shape[1]), border, _p(out))
+    return out.astype(bool)
+
+
+def dilate(mask):
+    m = _c(mask, np.uint8)
+    out = np.zeros(m.shape, np.uint8)
+    lib().oracle_dilate(_p(m), I64(m.shape[0]), I64(m.shape[1]), _p(out))
+    return out.astype(bool)
+
+
+def opening(mask):
+    return dilate(erode(mask))
+
+
+def remove_small_objects_mask(mask, min_size, conn=1):
+    m = _c(mask, np.uint8)
+    out = np.zeros(m.shape, np.uint8)
+    lib().oracle_rso_mask(_p(m), I64(m.shape[0]), I64(m.shape[1]), I64(min_size), conn, _p(out))
+    return out.astype(bool)
+
+
+def remove_small_objects_labels(lab, min_size):
+    l = _c(lab, np.int32)
+    out = np.zeros(l.shape, np.int32)
+    lib().oracle_rso_labels(_p(l), I64(l.shape[0]), I64(l.shape[1]), I64(min_size), _p(out))
+    return out
+
+
+def remove_small_holes(mask, thr=64, conn=1):
+    m = _c(mask, np.uint8)
+    out = np.zeros(m.shape, np.uint8)
+    lib().oracle_remove_small_holes(_p(m), I64(m.shape[0]), I64(m.shape[1]), I64(thr), conn, _p(out))
+    return out.astype(bool)
+
+
+def fill_holes(mask):
+    m = _c(mask, np.uint8)
+    out = np.zeros(m.shape, np.uint8)
+    lib().oracle_fill_holes(_p(m), I64(m.shape[0]), I64(m.shape[1]), _p(out))
+    return out.astype(bool)
+
+
+def clear_border(lab):
+    l = _c(lab, np.int32)
+    out = np.zeros(l.shape, np.int32)
+    lib().oracle_clear_border(_p(l), I64(l.shape[0]), I64(l.shape[1]), _p(out))
+    return out
+
+
+def relabel_sequential(lab):
+    l = _c(lab, np.int32)
+    out = np.zeros(l.shape, np.int32)
+    n = lib().oracle_relabel_sequential(_p(l), I64(l.size), _p(out))
+    return out, int(n)
+
+
+def watershed(img, markers, mask=None):
+    im = _c(img, np.float64)
+    mk = _c(markers, np.int32)
+    out = np.zeros(mk.shape, np.int32)
+    mp = None
+    if mask is not None:
+        m = _c(mask, np.uint8)
+        mp = _p(m)
+    lib().oracle_watershed(_p(im), _p(mk), mp, I64(im.shape[0]), I64(im.shape[1]), _p(out))
+    return out
+
+
+# ---- a14/a15/a20 ---------------------------------------------------------------------
+def region_stats(lab, nlab=None):
+    """-> [(nlab+1), 8]: area, cen_r, cen_c, major, minor, ecc, orient, present"""
+    l = _c(lab, np.int32)
+    if nlab is None:
+        nlab = int(l.max()) if l.size else 0
+    out = np.zeros((nlab + 1, 8), np.float64)
+    lib().oracle_region_stats(_p(l), I64(l.shape[0]), I64(l.shape[1]), ctypes.c_int32(nlab), _p(out))
+    return out
+
+
+def label_sums(stack, lab, nlab=None):
+    s = _c(stack, np.float32)
+    l = _c(lab, np.int32)
+    C = s.shape[-1]
+    if nlab is None:
+        nlab = int(l.max()) if l.size else 0
+    sums = np.zeros((nlab + 1, C), np.float64)
+    counts = np.zeros(nlab + 1, np.int64)
+    lib().oracle_label_sums(_p(s), _p(l), I64(l.size), C, ctypes.c_int32(nlab), _p(sums), _p(counts))
+    return sums, counts
+
+
+# ---- a19 -----------------------------------------------------------------------------
+def segcos(x, y, bounds, variant=0, fx=None, fy=None):
+    x = _c(x, np.float64)
+    y = _c(y, np.float64)
+    b = _c(bounds, np.int32)
+    nseg = len(b) - 1
+    fxp = fyp = None
+    if fx is not None:
+        fxa = _c(fx, np.float64)
+        fya = _c(fy, np.float64)
+        fxp, fyp = _p(fxa), _p(fya)
+    return lib().oracle_segcos(_p(x), _p(y), _p(b), nseg, variant, fxp, fyp)
+
+
+def classify(x, ref, bounds, variant=0, fx=None, fr=None):
+    x = _c(x, np.float64)
+    ref = _c(ref, np.float64)
+    b = _c(bounds, np.int32)
+    n, C = x.shape
+    R = ref.shape[0]
+    arg = np.zeros(n, np.int32)
+    dmin = np.zeros(n, np.float64)
+    fxa = _c(fx, np.float64) if fx is not None else None
+    fra = _c(fr, np.float64) if fr is not None else None
+    lib().oracle_classify(_p(x), I64(n), _p(ref), R, C, _p(b), len(b) - 1, variant,
+                          _p(fxa) if fxa is not None else None, _p(fra) if fra is not None else None,
+                          _p(arg), _p(dmin))
+    return arg, dmin
+
+
+# ---- a8 ------------------------------------------------------------------------------
+def kmeans_1d(x, k, valid=None):
+    xv = _c(x, np.float64).ravel()
+    lab = np.zeros(xv.size, np.int32)
+    cen = np.zeros(k, np.float64)
+    vp = None
+    if valid is not None:
+        va = _c(valid, np.uint8).ravel()
+        vp = _p(va)
+    it = lib().oracle_kmeans_1d(_p(xv), vp, I64(xv.size), k, _p(lab), _p(cen))
+    return lab.reshape(np.shape(x)), cen, int(it)
+
+
+# ---- a21/a22/a23 ---------------------------------------------------------------------
+def rag_edges(lab, nlab=None):
+    l = _c(lab, np.int32)
+    if nlab is None:
+        nlab = int(l.max())
+    e = np.zeros((nlab + 1, nlab + 1), np.uint8)
+    lib().oracle_rag_edges(_p(l), I64(l.shape[0]), I64(l.shape[1]), ctypes.c_int32(nlab), _p(e))
+    return e
+
+
+def barcode_adjacency(edge, bc_of_label, R):
+    e = _c(edge, np.uint8)
+    nlab = e.shape[0] - 1
+    bc = _c(bc_of_label, np.int32)
+    adj = np.zeros((R, R), np.int64)
+    lib().oracle_barcode_adjacency(_p(e), ctypes.c_int32(nlab), _p(bc), R, _p(adj))
+    return adj
+
+
+def barcode_counts(bc, R):
+    b = _c(bc, np.int32)
+    out = np.zeros(R, np.int64)
+    lib().oracle_barcode_counts(_p(b), I64(b.size), R, _p(out))
+    return out
+
+
+def paint_ids(lab, code):
+    l = _c(lab, np.int32)
+    c = _c(code, np.int32)
+    out = np.zeros(l.shape, np.int32)
+    lib().oracle_paint_ids(_p(l), I64(l.size), _p(c), ctypes.c_int32(c.size), _p(out))
+    return out

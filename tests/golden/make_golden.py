@@ -1,0 +1,167 @@
+"""Generate the committed golden fixtures in tests/golden/*.npz from the REFERENCE itself.
+
+Runs only in the build container (needs /root/reference).  Nothing here ships to the GPU
+box except the .npz data it writes.  Reference code is executed, never copied:
+
+* neighbor2d.line_profile_2d_v2 / neighbor.line_profile_v2 / line_profile_memory_efficient_v2
+  -- the reference's own Cython, compiled from /root/reference by oracle/build_ref.sh.
+* the 2-D enhancement post-chain -- lines 111-124 of
+  hiprfish-image-analysis-synthetic-community/hiprfish_imaging_multispecies_spectral_image_measurement.py
+  read from the reference file at run time and exec'd on the Cython output.
+* the 3-D post-chain -- lines 812-817 of hiprfish-image-analysis-biofilm/hiprfish_imaging_biofilm_analysis.py.
+* the segmented-cosine metrics -- the functions channel_cosine_intensity,
+  channel_cosine_intensity_7b_v2 and channel_cosine_intensity_violet_derivative_v2 AST-extracted
+  from hiprfish-image-analysis-reference-training/hiprfish_imaging_train_reference.py with the
+  @numba.njit decorator dropped (numba is absent), run as plain Python.
+* CC labelling against scipy.ndimage.label (raster-first numbering, the semantics skimage.label
+  shares), and the partition sklearn 1.7.2 KMeans(random_state=0, n_init=10) finds on 1-D data.
+
+Usage: python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+"""
+import ast
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+MULTI = REF + "/hiprfish-image-analysis-synthetic-community/hiprfish_imaging_multispecies_spectral_image_measurement.py"
+BIOF = REF + "/hiprfish-image-analysis-biofilm/hiprfish_imaging_biofilm_analysis.py"
+TRAIN = REF + "/hiprfish-image-analysis-reference-training/hiprfish_imaging_train_reference.py"
+
+
+def ref_lines(path, lo, hi):
+    with open(path) as f:
+        lines = f.readlines()
+    return "".join(l.lstrip() for l in lines[lo - 1:hi])
+
+
+def ref_functions(path, names):
+    src = open(path).read()
+    tree = ast.parse(src)
+    ns = {"np": np}
+    for node in tree.body:
+        if isinstance(node, ast.FunctionDef) and node.name in names:
+            node.decorator_list = []
+            mod = ast.Module(body=[node], type_ignores=[])
+            exec(compile(mod, path, "exec"), ns)
+    return {n: ns[n] for n in names}
+
+
+def edge_pad(img, w=5):
+    return np.pad(img, w, mode="edge")
+
+
+def main():
+    subprocess.check_call([os.path.join(REPO, "oracle", "build_ref.sh")])
+    sys.path.insert(0, os.path.join(REPO, "oracle", "_ref"))
+    import neighbor2d  # reference Cython
+    import neighbor
+
+    rng = np.random.default_rng(20190101)
+
+    # ---- offset tables (decoded from index images) ---------------------------------
+    H = W = 25
+    idx = np.arange(H * W, dtype=np.float64).reshape(H, W)
+    v = neighbor2d.line_profile_2d_v2(idx, 11, 9)[0, 0].astype(np.int64)
+    table2d = np.stack([v // W, v % W], -1).astype(np.int32)
+    X = Y = Z = 13
+    idx3 = np.arange(X * Y * Z, dtype=np.float64).reshape(X, Y, Z)
+    v = neighbor.line_profile_v2(idx3, 11, 9, 9)[0, 0, 0].astype(np.int64)
+    table3d = np.stack([v // (Y * Z), (v // Z) % Y, v % Z], -1).astype(np.int32)
+
+    # ---- 2-D line profiles + enhancement chain --------------------------------------
+    chain2d = ref_lines(MULTI, 111, 124)
+    cases = {}
+    img_a = rng.random((18, 23))                       # ragged, generic
+    img_b = rng.random((12, 12)) ** 3                  # skewed intensities
+    img_c = np.full((14, 16), 0.25)                    # flat -> NaN path
+    img_c[4:9, 6:11] = rng.random((5, 5))
+    img_d = rng.random((1, 7))                         # single row
+    for name, img in [("a", img_a), ("b", img_b), ("c", img_c), ("d", img_d)]:
+        pad = edge_pad(img)
+        lp = neighbor2d.line_profile_2d_v2(pad.astype(np.float64), 11, 9)
+        ns = {"np": np, "image_lp": lp.copy()}
+        with np.errstate(all="ignore"):
+            exec(chain2d, ns)
+        cases["pad_" + name] = pad
+        cases["final_" + name] = ns["image_final"]
+        if name in ("a", "d"):
+            cases["lp_" + name] = lp
+    np.savez_compressed(os.path.join(HERE, "neighbor2d.npz"), table=table2d, **cases)
+
+    # ---- 3-D -----------------------------------------------------------------------
+    chain3d = ref_lines(BIOF, 812, 817)
+    vol = rng.random((8, 7, 5))
+    pad3 = edge_pad(vol)
+    lp3n = neighbor.line_profile_memory_efficient_v2(pad3, 11, 9, 9)
+    ns = {"np": np, "image_lp": lp3n.copy()}
+    with np.errstate(all="ignore"):
+        exec(chain3d, ns)
+    vol_s = rng.random((4, 3, 3))
+    pad3s = edge_pad(vol_s)
+    lp3 = neighbor.line_profile_v2(pad3s, 11, 9, 9)
+    np.savez_compressed(os.path.join(HERE, "neighbor3d.npz"), table=table3d, pad=pad3, lp_norm=lp3n,
+                        final=ns["image_final"], pad_small=pad3s, lp_small=lp3)
+
+    # ---- segmented cosine metrics ---------------------------------------------------
+    fns = ref_functions(TRAIN, ["channel_cosine_intensity", "channel_cosine_intensity_7b_v2",
+                                "channel_cosine_intensity_violet_derivative_v2"])
+    n = 160
+    # 95-ch + 5 flags (channel_cosine_intensity), flags agree on half of the pairs
+    x95 = rng.random((n, 100))
+    y95 = rng.random((n, 100))
+    fl = (rng.random((n, 5)) > 0.3).astype(np.float64)
+    x95[:, 95:100] = fl
+    y95[:, 95:100] = np.where(rng.random((n, 1)) < 0.5, fl, (rng.random((n, 5)) > 0.3).astype(np.float64))
+    x95[:20, 32:55] = 0.0                 # zero-norm segments
+    y95[10:30, 32:55] = 0.0
+    d95 = np.array([fns["channel_cosine_intensity"](x95[i], y95[i]) for i in range(n)])
+    x67 = rng.random((n, 67))
+    y67 = rng.random((n, 67))
+    fl = (rng.random((n, 4)) > 0.3).astype(np.float64)
+    x67[:, 63:67] = fl
+    y67[:, 63:67] = np.where(rng.random((n, 1)) < 0.5, fl, (rng.random((n, 4)) > 0.3).astype(np.float64))
+    x67[:15, 57:63] = 0.0
+    y67[5:25, 57:63] = 0.0
+    d7b = np.array([float(fns["channel_cosine_intensity_7b_v2"](x67[i], y67[i])) for i in range(n)])
+    x132 = rng.random((n, 132))
+    y132 = rng.random((n, 132))
+    fl = (rng.random((n, 6)) > 0.3).astype(np.float64)
+    x132[:, 126:132] = fl
+    y132[:, 126:132] = np.where(rng.random((n, 1)) < 0.5, fl, (rng.random((n, 6)) > 0.3).astype(np.float64))
+    dvd = np.array([fns["channel_cosine_intensity_violet_derivative_v2"](x132[i], y132[i]) for i in range(n)])
+    np.savez_compressed(os.path.join(HERE, "metrics.npz"), x95=x95, y95=y95, d95=d95, x67=x67, y67=y67,
+                        d7b=d7b, x132=x132, y132=y132, dvd=dvd)
+
+    # ---- connected components (scipy raster numbering) ------------------------------
+    from scipy import ndimage as ndi
+    m = rng.random((64, 80)) > 0.55
+    l8, n8 = ndi.label(m, structure=np.ones((3, 3), int))
+    l4, n4 = ndi.label(m)
+    np.savez_compressed(os.path.join(HERE, "label.npz"), mask=m, l8=l8.astype(np.int32), l4=l4.astype(np.int32))
+
+    # ---- 1-D KMeans partitions (sklearn, 2019 defaults forced) ----------------------
+    from sklearn.cluster import KMeans
+    km = {}
+    for k, (name, x) in enumerate([
+        ("bimodal", np.concatenate([rng.normal(0.1, 0.03, 3000), rng.normal(0.7, 0.1, 2000)])),
+        ("logsum", np.log(np.concatenate([rng.gamma(2.0, 0.01, 4000), rng.gamma(9.0, 0.5, 1500)]) + 1e-2)),
+        ("trimodal", np.concatenate([rng.normal(0, 0.1, 2000), rng.normal(2, 0.2, 1500), rng.normal(5, 0.3, 800)])),
+    ]):
+        kk = 3 if name == "trimodal" else 2
+        lab = KMeans(n_clusters=kk, random_state=0, n_init=10).fit_predict(x.reshape(-1, 1))
+        km["x_" + name] = x
+        km["lab_" + name] = lab.astype(np.int32)
+        km["k_" + name] = np.int32(kk)
+        lab3 = KMeans(n_clusters=3, random_state=0, n_init=10).fit_predict(x.reshape(-1, 1))
+        km["lab3_" + name] = lab3.astype(np.int32)
+    np.savez_compressed(os.path.join(HERE, "kmeans.npz"), **km)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

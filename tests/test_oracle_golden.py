@@ -1,0 +1,101 @@
+"""Pin the CPU restatement (oracle/) against fixtures generated from the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+
+def test_tables(orc, golden):
+    g2 = golden("neighbor2d")
+    assert np.array_equal(orc.lp_table_2d(11, 9), g2["table"])
+    g3 = golden("neighbor3d")
+    assert np.array_equal(orc.lp_table_3d(11, 9, 9), g3["table"])
+    # the centre tap is always the pixel itself
+    assert (g2["table"][:, 5] == 5).all() and (g3["table"][:, 5] == 5).all()
+
+
+@pytest.mark.parametrize("case", ["a", "d"])
+def test_line_profile_2d(orc, golden, case):
+    g = golden("neighbor2d")
+    assert np.array_equal(orc.line_profile_2d(g["pad_" + case]), g["lp_" + case])
+
+
+@pytest.mark.parametrize("case", ["a", "b", "c", "d"])
+def test_enhance_2d_bitexact(orc, golden, case):
+    g = golden("neighbor2d")
+    got = orc.enhance_2d(g["pad_" + case])
+    ref = g["final_" + case]
+    assert got.shape == ref.shape
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(got[~np.isnan(ref)], ref[~np.isnan(ref)])
+    if case == "c":
+        assert np.isnan(ref).any()  # the flat-window NaN path is exercised
+
+
+def test_line_profile_3d(orc, golden):
+    g = golden("neighbor3d")
+    assert np.array_equal(orc.line_profile_3d(g["pad_small"]), g["lp_small"])
+    assert np.array_equal(orc.line_profile_3d_norm(g["pad"]), g["lp_norm"])
+
+
+def test_enhance_3d_bitexact(orc, golden):
+    g = golden("neighbor3d")
+    assert np.array_equal(orc.enhance_3d(g["pad"]), g["final"])
+
+
+def test_metric_channel_cosine_intensity(orc, golden):
+    g = golden("metrics")
+    b = [0, 32, 55, 75, 89, 95]
+    for i in range(len(g["d95"])):
+        x, y = g["x95"][i], g["y95"][i]
+        d = orc.segcos(x[:95], y[:95], b, 1, x[95:100], y[95:100])
+        assert d == pytest.approx(g["d95"][i], rel=1e-12, abs=1e-12)
+
+
+def test_metric_7b_v2(orc, golden):
+    g = golden("metrics")
+    b = [0, 23, 43, 57, 63]
+    for i in range(len(g["d7b"])):
+        x, y = g["x67"][i], g["y67"][i]
+        d = orc.segcos(x[:63], y[:63], b, 2, x[63:67], y[63:67])
+        assert d == pytest.approx(g["d7b"][i], rel=1e-12, abs=1e-12)
+
+
+def test_metric_violet_derivative_segments(orc, golden):
+    """_violet_derivative_v2 returns a 6-tuple (train_reference.py:731); its 5 spectral
+    segment distances equal the gated per-segment distances of the 95-channel metric."""
+    g = golden("metrics")
+    b = [0, 32, 55, 75, 89, 95]
+    for i in range(len(g["dvd"])):
+        x, y = g["x132"][i], g["y132"][i]
+        tup = g["dvd"][i]
+        gate = np.sum(np.abs(x[126:132] - y[126:132])) < 0.01
+        for s in range(5):
+            single = [b[s], b[s + 1]]
+            d = orc.segcos(x[:95], y[:95], single, 0)
+            if gate and x[126 + s] == 0:
+                d = 0.0
+            assert d == pytest.approx(tup[1 + s], rel=1e-12, abs=1e-12)
+        assert tup[0] == (0.0 if gate else 1.0)
+
+
+def test_label_raster_numbering(orc, golden):
+    g = golden("label")
+    l8, _ = orc.label(g["mask"].astype(np.int32), conn=2)
+    l4, _ = orc.label(g["mask"].astype(np.int32), conn=1)
+    assert np.array_equal(l8, g["l8"])
+    assert np.array_equal(l4, g["l4"])
+
+
+def _same_partition(a, b):
+    pairs = set(zip(a.tolist(), b.tolist()))
+    return len(pairs) == len(set(a.tolist())) == len(set(b.tolist()))
+
+
+@pytest.mark.parametrize("name", ["bimodal", "logsum", "trimodal"])
+def test_kmeans_partition_matches_sklearn(orc, golden, name):
+    g = golden("kmeans")
+    x = g["x_" + name]
+    k = int(g["k_" + name])
+    lab, cen, it = orc.kmeans_1d(x, k)
+    assert it < 300
+    assert _same_partition(lab, g["lab_" + name])
