@@ -1,0 +1,66 @@
+// common.hpp -- shared plumbing for libhrf.so (MI355X / gfx950 only).
+//
+// Every C-ABI entry point returns an hrf_status (0 = OK) and records a thread-local
+// message retrievable with hrf_last_error().  All device work is stream-ordered on the
+// caller's hipStream_t; nothing here synchronises unless an entry point says so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/hrf.h"
+
+namespace hrf {
+
+void set_error(const char *fmt, ...);
+
+struct Err {
+  hrf_status code;
+};
+
+#define HRF_REQUIRE(cond, ...)                    \
+  do {                                            \
+    if (!(cond)) {                                \
+      ::hrf::set_error(__VA_ARGS__);              \
+      return HRF_EINVAL;                          \
+    }                                             \
+  } while (0)
+
+#define HRF_HIP(expr)                                                               \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      ::hrf::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),      \
+                       __FILE__, __LINE__);                                         \
+      return HRF_EHIP;                                                              \
+    }                                                                               \
+  } while (0)
+
+#define HRF_LAUNCHED()                                                              \
+  do {                                                                              \
+    hipError_t e_ = hipGetLastError();                                              \
+    if (e_ != hipSuccess) {                                                         \
+      ::hrf::set_error("kernel launch failed: %s (%s:%d)", hipGetErrorString(e_),  \
+                       __FILE__, __LINE__);                                         \
+      return HRF_EHIP;                                                              \
+    }                                                                               \
+  } while (0)
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid for a grid-stride elementwise kernel: enough blocks to fill 256 CUs x 8.
+inline unsigned stream_grid(int64_t n, int block = 256) {
+  int64_t g = cdiv(n, block);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// Line-profile sampling tables (neighbor2d.pyx:32-55, neighbor.pyx:209-243), computed on
+// the host and uploaded per call.  tables.cpp.
+int lp_table_2d(int patch, int nphi, int32_t *off /*[nphi][patch][2]*/);
+int lp_table_3d(int patch, int ntheta, int nphi, int32_t *off /*[ndir][patch][3]*/);
+
+}  // namespace hrf

@@ -1,0 +1,59 @@
+"""CPU checks of the C-ABI boundary: libhrf.so builds for gfx950, loads, and exports every
+entry point include/hrf.h declares; host-side helpers behave.  No device compute here."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from hiprfish_image_analysis_amd import _lib
+
+
+def test_library_exports_every_declared_symbol():
+    decl = _lib.declared_functions()
+    assert len(decl) >= 10
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in decl if not hasattr(L, n)]
+    assert not missing, missing
+    # and nm agrees (dynamic symbol table, default visibility)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    assert set(decl) <= exported
+
+
+def test_code_object_is_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", _lib.LIB_PATH],
+                         capture_output=True, text=True)
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_host_tables_match_reference(golden):
+    t = np.zeros((9, 11, 2), np.int32)
+    _lib.call("hrf_lp_table_2d", 11, 9, t.ctypes.data)
+    assert np.array_equal(t, golden("neighbor2d")["table"])
+    t3 = np.zeros((72, 11, 3), np.int32)
+    _lib.call("hrf_lp_table_3d", 11, 9, 9, t3.ctypes.data)
+    assert np.array_equal(t3, golden("neighbor3d")["table"])
+
+
+def test_compile_time_tables_match_runtime(orc):
+    import importlib.util
+    p = os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc", "gen_tables.py")
+    spec = importlib.util.spec_from_file_location("gen_tables", p)
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    assert np.array_equal(np.array(g.table_2d()), orc.lp_table_2d(11, 9))
+    assert np.array_equal(np.array(g.table_3d()), orc.lp_table_3d(11, 9, 9))
+    # other parameter sets the generic kernels use
+    for patch, nphi in [(7, 5), (11, 12), (15, 9)]:
+        t = np.zeros((nphi, patch, 2), np.int32)
+        _lib.call("hrf_lp_table_2d", patch, nphi, t.ctypes.data)
+        assert np.array_equal(t, orc.lp_table_2d(patch, nphi))
+
+
+def test_bad_arguments_raise_value_error():
+    t = np.zeros(4, np.int32)
+    with pytest.raises(ValueError):
+        _lib.call("hrf_lp_table_2d", 0, 9, t.ctypes.data)
