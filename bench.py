@@ -1,0 +1,174 @@
+"""bench.py -- HiPR-FISH segment+classify throughput on MI355X (BASELINE.json metric).
+
+A step = one pass of the hot path over one synthetic 2048x2048x95 tile per rank, inputs
+resident in HBM: E. coli measurement (log-sum -> KMeans -> morphology -> erosion seeds ->
+watershed -> cleanup -> shape filter -> per-cell mean spectra), per-cell segmented-cosine
+classification against the 1023-barcode library, per-pixel classification (fused f32-MFMA
+GEMM + argmax), per-barcode counts and the identification map.  With N ranks every rank
+processes its own tiles (weak scaling) and the per-barcode counts are all-reduced over RCCL
+each step -- the path's only exchange (collect_measurement_results.py:92-98 across FOVs).
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+(for N > 1 launch with torch.distributed.run, one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+H = W = 2048
+C = 95
+NBIT = 10
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak
+
+
+def _cpu_baseline(ref, bounds):
+    """Oracle restatement (oracle/pipeline.py, single-threaded C + numpy) on a bounded sample of
+    the same workload: segment+measure+per-cell classify of a 1024x1024x95 tile, and per-pixel
+    classification of 4096 pixels; scaled to Mpixel-spectra/s of the full step."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import pipeline as OP
+
+    from hiprfish_image_analysis_amd import synthetic as S
+    O.build()
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    hs = 1024
+    lay = S.cell_layout(hs, hs, S.default_ncells(hs, hs), ref.shape[0], seed=99)
+    truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
+    st = S.render_stack(truth, lay, ref, seed=99, device="cpu", profile=prof).numpy()
+    t0 = time.perf_counter()
+    OP.process_tile(st, ref, bounds)
+    t_seg = (time.perf_counter() - t0) / (hs * hs)
+    npx = 4096
+    x = st.reshape(-1, C)[:npx].astype(np.float64)
+    t0 = time.perf_counter()
+    O.classify(x, ref.astype(np.float64), bounds, 0)
+    t_pix = (time.perf_counter() - t0) / npx
+    return {"value": round(1e-6 / (t_seg + t_pix), 4), "unit": "Mpixel-spectra/s", "cores": 1, "kind": "port",
+            "sample": "oracle/pipeline.py process_tile on a 1024x1024x95 tile (%.1f s) + per-pixel classify of "
+                      "%d pixels vs 1023 refs (%.1f s), 1 thread; per-pixel costs summed" %
+                      (t_seg * hs * hs, npx, t_pix * npx)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--tiles", type=int, default=2, help="distinct resident tiles per rank")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-pixel", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    bounds = S.ECOLI_BOUNDS
+    ref = S.reference_library(NBIT, bounds)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), bounds, NBIT)
+    lib.refx()
+    tiles = []
+    for t in range(args.tiles):
+        seed = 20190101 + rank * 1000 + t
+        lay = S.cell_layout(H, W, S.default_ncells(H, W), lib.R, seed)
+        truth, prof = S.render_truth(H, W, lay, with_profile=True)
+        tiles.append(S.render_stack(truth, lay, ref, seed=seed, device=dev, profile=prof))
+    torch.cuda.synchronize()
+
+    per_pixel = not args.no_per_pixel
+    stream = torch.cuda.current_stream()
+    ev = []
+
+    def step(i, timed):
+        stack = tiles[i % len(tiles)]
+        res = P.process_tile(stack, lib, per_pixel=False)
+        if per_pixel:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            res.pixel_idx, res.pixel_dist = P.classify_pixels(stack, lib)
+            e1.record(stream)
+            if timed:
+                ev.append((e0, e1))
+        if world > 1:
+            dist.all_reduce(res.counts, op=dist.ReduceOp.SUM)
+        return res
+
+    for i in range(args.warmup):
+        step(i, False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ncells = 0
+    for i in range(args.steps):
+        res = step(i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ncells = int(res.cell_idx.numel())
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    pixels = H * W * args.steps * world
+    value = pixels / elapsed / 1e6
+    out = {
+        "metric": "Mpixel-spectra/s (segment+classify) on 2048²×95 vs 1023 refs; 1/2/4/8 GPU",
+        "value": round(value, 3), "unit": "Mpixel-spectra/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "cfg3: 2048x2048x95 synthetic stack per rank per step, 1023-barcode library; "
+                               "E. coli segmentation + per-cell spectra + per-cell and per-pixel segmented-cosine "
+                               "classification + barcode counts" + (" (RCCL all-reduce of counts)" if world > 1 else ""),
+                   "H": H, "W": W, "C": C, "R": lib.R, "per_pixel": per_pixel, "cells_last_tile": ncells,
+                   "parallelism": "tile-sharded x%d" % world},
+    }
+    if per_pixel and ev:
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
+        ach = flops / (ms * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "classify_pixels_pmc.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out["roofline"] = {"bound": "mfma", "kernel": "classify_pixels_kernel<50>", "achieved": round(ach, 2),
+                           "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                           "kernel_ms": round(ms, 4)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_baseline(ref, bounds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,7 @@ _CT = {
     "hrf_stream_t": ctypes.c_void_p, "size_t": ctypes.c_size_t,
     "int64_t": ctypes.c_int64, "int32_t": ctypes.c_int32, "double": ctypes.c_double,
     "float": ctypes.c_float, "uint32_t": ctypes.c_uint32, "int": ctypes.c_int,
+    "const float *const *": ctypes.c_void_p,
 }
 
 
@@ -34,7 +35,7 @@ def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"^HRF_API (hrf_status|int32_t|const char \*)\s*(hrf_\w+)\s*\(([^)]*)\)\s*;", src, re.M):
+    for m in re.finditer(r"^HRF_API (hrf_status|int32_t|int64_t|const char \*)\s*(hrf_\w+)\s*\(([^)]*)\)\s*;", src, re.M):
         ret, name, args = m.group(1), m.group(2), m.group(3)
         argtypes = []
         args = " ".join(args.split())
@@ -47,7 +48,8 @@ def declared_functions():
                 if typ not in _CT:
                     raise TypeError("unmapped C type %r in %s" % (typ, name))
                 argtypes.append(_CT[typ])
-        restype = ctypes.c_char_p if ret.startswith("const char") else ctypes.c_int32
+        restype = (ctypes.c_char_p if ret.startswith("const char") else
+                   ctypes.c_int64 if ret == "int64_t" else ctypes.c_int32)
         out[name] = (restype, argtypes)
     return out
 

@@ -1,0 +1,349 @@
+// classify.hip -- segmented-cosine barcode classification (a19).
+//
+// Metric (train_reference.py channel_cosine_intensity :223-386 / _7b_v2 :993-1072): per
+// excitation segment s, d_s = 1 - <x_s, y_s>/(|x_s||y_s|) (0 if both norms are 0, 1 if one
+// is); the spectral distance is the mean over segments (gated variants below).
+//
+// Per pixel (north_star mode, ungated): argmin_r d(x, ref_r) = argmax_r sum_s cos'_s where
+// cos'_s is the cosine of the segment-normalised vectors, plus 1 where both segments are
+// zero.  Appending the S zero-segment indicators to both operands makes that ONE dense
+// GEMM  score = Xext (P x K) . Refext^T (K x R),  K = C + S padded to KP:
+//   * v_mfma_f32_32x32x2_f32 (exact f32 fmaf chain, 157 TF/s dense): fp32 because the
+//     scores must match the f64 restatement to 1e-5;
+//   * each wave keeps its 64 pixels' normalised spectra resident in VGPRs (B operand,
+//     KP/2 registers per 32-pixel group) for the whole reference sweep; references stream
+//     through LDS in 128-row chunks (A operand, ds_read_b64, conflict-free stride KP+2);
+//   * MFMA k-slot h of step s holds channel h*KP/2 + s (a fixed permutation of the shared
+//     reduction index), so each lane's operands are contiguous;
+//   * the argmax over R is fused into the epilogue (each lane owns one pixel column and 16
+//     reference rows of every 32x32 tile), so the P x R score matrix never exists.
+// Per cell (reference semantics, gated by presence flags): f64, exact channel order of the
+// restatement, one workgroup per cell -- bit-identical to oracle_segcos.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int SMAX = 8;
+struct Bounds {
+  int32_t b[SMAX + 1];
+  int32_t nseg;
+};
+
+constexpr int RCH = 128;  // references per LDS chunk
+
+// refx[r][0..C) = ref / |ref_seg| (0 if the norm is 0), refx[r][C+s] = (norm_s == 0),
+// zero padding to KP columns and to Rpad rows.
+__global__ void ref_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
+                                int32_t Rpad, float *__restrict__ refx) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= Rpad) return;
+  float *o = refx + r * KP;
+  for (int k = 0; k < KP; ++k) o[k] = 0.0f;
+  if (r >= R) return;
+  const float *x = ref + r * C;
+  for (int s = 0; s < bd.nseg; ++s) {
+    double nn = 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) nn += (double)x[c] * (double)x[c];
+    const double inv = nn > 0 ? 1.0 / sqrt(nn) : 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) o[c] = (float)((double)x[c] * inv);
+    o[C + s] = nn > 0 ? 0.0f : 1.0f;
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__restrict__ stack, int64_t P, int32_t C,
+                                                                  Bounds bd, const float *__restrict__ refx,
+                                                                  int32_t R, int32_t Rpad,
+                                                                  int32_t *__restrict__ best_idx,
+                                                                  float *__restrict__ best_dist) {
+  constexpr int KP = 2 * KS;
+  constexpr int STRIDE = KP + 2;  // == 2 (mod 4): conflict-free ds_read_b64 over 32 rows
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * 256 + w * 64;
+
+  // ---- stage this wave's two 32-pixel groups, build the B operand in registers ----
+  float bx[2][KS];
+  float *stg = lds + w * (32 * C);
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int64_t p0 = pbase + g * 32;
+    const int64_t np = std::max<int64_t>(0, std::min<int64_t>(32, P - p0));
+    const int64_t nel = np * C;
+    const float *src = stack + p0 * C;
+    for (int64_t e = lane; e < 32 * C; e += 64) stg[e] = e < nel ? src[e] : 0.0f;
+    __syncthreads();
+    // segment norms of pixel j (f64 accumulation, as the restatement)
+    float inv[SMAX];
+    float zf[SMAX];
+#pragma unroll
+    for (int s = 0; s < SMAX; ++s) {
+      inv[s] = 0.0f;
+      zf[s] = 0.0f;
+      if (s < bd.nseg) {
+        double nn = 0.0;
+        for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) {
+          const double v = (double)stg[j * C + c];
+          nn += v * v;
+        }
+        inv[s] = nn > 0 ? (float)(1.0 / sqrt(nn)) : 0.0f;
+        zf[s] = nn > 0 ? 0.0f : 1.0f;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = h * KS + s;
+      float v = 0.0f;
+      if (k < C) {
+        float iv = inv[0];
+#pragma unroll
+        for (int q = 1; q < SMAX; ++q)
+          if (q < bd.nseg && k >= bd.b[q]) iv = inv[q];
+        v = (float)((double)stg[j * C + k] * (double)iv);
+      } else if (k < C + bd.nseg) {
+        float z = zf[0];
+#pragma unroll
+        for (int q = 1; q < SMAX; ++q)
+          if (q == k - C) z = zf[q];
+        v = z;
+      }
+      bx[g][s] = v;
+    }
+    __syncthreads();
+  }
+
+  float best[2] = {-__builtin_inff(), -__builtin_inff()};
+  int bidx[2] = {0, 0};
+
+  // ---- sweep the reference library in LDS chunks ----
+  for (int r0 = 0; r0 < Rpad; r0 += RCH) {
+    __syncthreads();
+    const float2 *gsrc = reinterpret_cast<const float2 *>(refx + (int64_t)r0 * KP);
+    for (int e = tid; e < RCH * (KP / 2); e += 256) {
+      const int rr = e / (KP / 2), cc = e - rr * (KP / 2);
+      reinterpret_cast<float2 *>(lds + rr * STRIDE)[cc] = gsrc[e];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int rb = 0; rb < RCH; rb += 32) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      const float *arow = lds + (rb + j) * STRIDE + h * KS;
+#pragma unroll
+      for (int s = 0; s < KS; s += 2) {
+        const float2 a = *reinterpret_cast<const float2 *>(arow + s);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bx[0][s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bx[1][s], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bx[0][s + 1], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bx[1][s + 1], acc1, 0, 0, 0);
+      }
+      // rows (references) of this lane: (reg&3) + 8*(reg>>2) + 4*h, increasing in reg
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int r = r0 + rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const bool ok = r < R;
+        if (ok && acc0[reg] > best[0]) {
+          best[0] = acc0[reg];
+          bidx[0] = r;
+        }
+        if (ok && acc1[reg] > best[1]) {
+          best[1] = acc1[reg];
+          bidx[1] = r;
+        }
+      }
+    }
+  }
+  // merge the two lane halves holding the same pixel column
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const float ob = __shfl_xor(best[g], 32, 64);
+    const int oi = __shfl_xor(bidx[g], 32, 64);
+    if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
+      best[g] = ob;
+      bidx[g] = oi;
+    }
+    const int64_t p = pbase + g * 32 + j;
+    if (h == 0 && p < P) {
+      best_idx[p] = bidx[g];
+      best_dist[p] = ((float)bd.nseg - best[g]) / (float)bd.nseg;
+    }
+  }
+}
+
+// ---- per cell, f64, gated variants; one workgroup per cell ----
+__device__ double seg_dist(const double *x, const double *y, int lo, int hi) {
+  double d = 0, nx = 0, ny = 0;
+  for (int i = lo; i < hi; ++i) {
+    d += x[i] * y[i];
+    nx += x[i] * x[i];
+    ny += y[i] * y[i];
+  }
+  if (nx == 0.0 && ny == 0.0) return 0.0;
+  if (nx == 0.0 || ny == 0.0) return 1.0;
+  return 1.0 - d / sqrt(nx * ny);
+}
+
+__global__ __launch_bounds__(256) void classify_cells_kernel(const double *__restrict__ X, int64_t N,
+                                                             const double *__restrict__ ref, int32_t R, int32_t C,
+                                                             Bounds bd, int32_t variant,
+                                                             const double *__restrict__ fx,
+                                                             const double *__restrict__ fr,
+                                                             int32_t *__restrict__ arg, double *__restrict__ dmin) {
+  extern __shared__ double xs[];
+  __shared__ double sbest[256];
+  __shared__ int sidx[256];
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int c = tid; c < C; c += 256) xs[c] = X[i * C + c];
+  __syncthreads();
+  const int S = bd.nseg;
+  double best = __builtin_inf();
+  int bi = 0x7fffffff;
+  for (int r = tid; r < R; r += 256) {
+    const double *y = ref + (int64_t)r * C;
+    double d;
+    if (variant == 0) {
+      double s = 0;
+      for (int k = 0; k < S; ++k) s += seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+      d = s / S;
+    } else {
+      double chk = 0;
+      for (int k = 0; k < S; ++k) chk += fabs(fx[i * S + k] - fr[(int64_t)r * S + k]);
+      if (chk < 0.01) {
+        double s = 0;
+        for (int k = 0; k < S; ++k) s += fx[i * S + k] == 0 ? 0.0 : seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+        d = variant == 1 ? s / S : 0.5 * s / S;
+      } else if (variant == 2) {
+        d = 1.0;
+      } else {
+        double s = 0;
+        for (int k = 0; k < S; ++k) s += seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+        d = s / S;
+      }
+    }
+    if (d < best) {
+      best = d;
+      bi = r;
+    }
+  }
+  sbest[tid] = best;
+  sidx[tid] = bi;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double b2 = sbest[tid + o];
+      const int i2 = sidx[tid + o];
+      if (b2 < sbest[tid] || (b2 == sbest[tid] && i2 < sidx[tid])) {
+        sbest[tid] = b2;
+        sidx[tid] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    arg[i] = sidx[0] == 0x7fffffff ? 0 : sidx[0];
+    dmin[i] = sbest[0];
+  }
+}
+
+int choose_ks(int K) {
+  static const int ks[] = {8, 16, 18, 24, 32, 34, 40, 50, 56, 64};
+  for (int v : ks)
+    if (2 * v >= K) return v;
+  return -1;
+}
+
+hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Bounds *bd) {
+  HRF_REQUIRE(nseg >= 1 && nseg <= SMAX && bounds_host, "classify: 1..8 segments required");
+  HRF_REQUIRE(bounds_host[0] == 0 && bounds_host[nseg] == C, "classify: segment bounds must span [0, C)");
+  for (int s = 0; s < nseg; ++s) HRF_REQUIRE(bounds_host[s] < bounds_host[s + 1], "classify: empty segment");
+  for (int s = 0; s <= SMAX; ++s) bd->b[s] = s <= nseg ? bounds_host[s] : C;
+  bd->nseg = nseg;
+  return HRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t *kp_host, int32_t *rpad_host) {
+  HRF_REQUIRE(C >= 1 && nseg >= 1 && nseg <= SMAX && R >= 1, "classify_geometry: bad arguments");
+  const int ks = choose_ks(C + nseg);
+  HRF_REQUIRE(ks > 0, "classify: C + nseg must be <= 128");
+  *kp_host = 2 * ks;
+  *rpad_host = (int32_t)(hrf::cdiv(R, RCH) * RCH);
+  return HRF_OK;
+}
+
+hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                                     float *refx, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, &kp, &rpad)) return s;
+  HRF_REQUIRE(ref && refx, "classify_prepare_refs: null buffer");
+  ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad, refx);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const float *refx, int32_t R,
+                               const int32_t *bounds_host, int32_t nseg, int32_t *best_idx, float *best_dist,
+                               hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, &kp, &rpad)) return s;
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(stack && refx && best_idx && best_dist, "classify_pixels: null buffer");
+  const int ks = kp / 2;
+  const size_t shm = sizeof(float) * std::max<size_t>((size_t)RCH * (kp + 2), (size_t)4 * 32 * C);
+  HRF_REQUIRE(shm <= 160 * 1024, "classify_pixels: C too large for LDS staging");
+  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
+  hipStream_t s = (hipStream_t)stream;
+#define HRF_CP(K)                                                                                          \
+  case K:                                                                                                  \
+    hipFuncSetAttribute((const void *)classify_pixels_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                        (int)shm);                                                                         \
+    classify_pixels_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, refx, R, rpad, best_idx, best_dist);   \
+    break;
+  switch (ks) {
+    HRF_CP(8)
+    HRF_CP(16)
+    HRF_CP(18)
+    HRF_CP(24)
+    HRF_CP(32)
+    HRF_CP(34)
+    HRF_CP(40)
+    HRF_CP(50)
+    HRF_CP(56)
+    HRF_CP(64)
+    default:
+      HRF_REQUIRE(false, "classify_pixels: unsupported K");
+  }
+#undef HRF_CP
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int32_t R, int32_t C,
+                              const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
+                              const double *fr, int32_t *arg, double *dmin, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  HRF_REQUIRE(variant >= 0 && variant <= 2, "classify_cells: variant must be 0, 1 or 2");
+  HRF_REQUIRE(variant == 0 || (fx && fr), "classify_cells: gated variants need presence flags");
+  HRF_REQUIRE(R >= 1 && C >= 1, "classify_cells: bad sizes");
+  if (N == 0) return HRF_OK;
+  HRF_REQUIRE(x && ref && arg && dmin, "classify_cells: null buffer");
+  classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, (hipStream_t)stream>>>(x, N, ref, R, C, bd, variant,
+                                                                                       fx, fr, arg, dmin);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,255 @@
+// kmeans.hip -- 1-D KMeans thresholding (a8).
+//
+// Reference: sklearn KMeans(n_clusters=k, random_state=0).fit_predict(x.reshape(-1,1))
+// (ecoli measurement.py:73,85; multispecies :125,141).  Restated (oracle/hrf_oracle.c
+// oracle_kmeans_1d) as Lloyd iterations from a deterministic init with EXACT centre updates:
+// each value is mapped to int64 fixed point q = rint(x * 2^s) once per pass and summed with
+// integer atomics, so the centres -- and therefore every label -- are independent of the
+// reduction order and identical to the CPU restatement bit for bit.
+//
+// Device-resident loop: accumulate (one streaming pass) -> update (1 thread) per iteration;
+// both early-exit once converged, so the host launches fixed batches and polls rarely.
+#include "common.hpp"
+#include "wave.hpp"
+
+namespace {
+
+constexpr int KMAX = 8;
+
+struct KmState {
+  double center[KMAX];
+  long long sum[KMAX];
+  unsigned long long cnt[KMAX];
+  unsigned long long lo_bits, hi_bits;  // order-preserving encodings of min / max
+  unsigned long long amax_bits;         // |x| max (non-negative doubles order as uint64)
+  unsigned long long nvalid;
+  int scale;
+  int converged;
+  int iters;
+  int k;
+};
+
+__device__ __forceinline__ unsigned long long ord_enc(double x) {
+  const unsigned long long b = __double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord_dec(unsigned long long e) {
+  const unsigned long long b = (e >> 63) ? (e & 0x7fffffffffffffffull) : ~e;
+  return __longlong_as_double((long long)b);
+}
+
+__global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
+                                 KmState *st) {
+  unsigned long long lo = ~0ull, hi = 0ull, am = 0ull, nv = 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    const double v = x[i];
+    const unsigned long long e = ord_enc(v);
+    lo = e < lo ? e : lo;
+    hi = e > hi ? e : hi;
+    const unsigned long long a = (unsigned long long)__double_as_longlong(fabs(v));
+    am = a > am ? a : am;
+    nv += 1;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64), a2 = __shfl_xor(am, o, 64);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+    am = a2 > am ? a2 : am;
+    nv += __shfl_xor(nv, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&st->lo_bits, lo);
+    atomicMax(&st->hi_bits, hi);
+    atomicMax(&st->amax_bits, am);
+    atomicAdd(&st->nvalid, nv);
+  }
+}
+
+__global__ void km_init_kernel(KmState *st, int k) {
+  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
+  const double amax = __longlong_as_double((long long)st->amax_bits);
+  int e = 0;
+  frexp(amax > 0 ? amax : 1.0, &e);
+  const unsigned long long nv = st->nvalid;
+  int ln = 0;
+  while ((1ull << ln) < (nv > 1 ? nv : 1ull)) ++ln;
+  st->scale = 61 - ln - e;
+  for (int j = 0; j < KMAX; ++j) {
+    st->center[j] = j < k ? mn + ((double)j + 0.5) * (mx - mn) / (double)k : 0.0;
+    st->sum[j] = 0;
+    st->cnt[j] = 0;
+  }
+  st->k = k;
+  st->converged = nv == 0;
+  st->iters = 0;
+}
+
+template <int K>
+__device__ __forceinline__ int km_assign(double v, const double *c) {
+  int bj = 0;
+  double bd = (v - c[0]) * (v - c[0]);
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    const double d = (v - c[j]) * (v - c[j]);
+    if (d < bd) {
+      bd = d;
+      bj = j;
+    }
+  }
+  return bj;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void km_accum_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid,
+                                                      int64_t n, KmState *st) {
+  if (st->converged) return;
+  double c[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) c[j] = st->center[j];
+  const int s = st->scale;
+  long long sum[K];
+  unsigned long long cnt[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    sum[j] = 0;
+    cnt[j] = 0;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !valid[i]) continue;
+    const double v = x[i];
+    const int bj = km_assign<K>(v, c);
+    const long long q = (long long)rint(ldexp(v, s));
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      sum[j] += bj == j ? q : 0;
+      cnt[j] += bj == j;
+    }
+  }
+  __shared__ long long ssum[4][K];
+  __shared__ unsigned long long scnt[4][K];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const long long a = hrf::wave_sum(sum[j]);
+    const unsigned long long b = hrf::wave_sum(cnt[j]);
+    if ((threadIdx.x & 63) == 0) {
+      ssum[w][j] = a;
+      scnt[w][j] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int j = threadIdx.x;
+    const long long a = ssum[0][j] + ssum[1][j] + ssum[2][j] + ssum[3][j];
+    const unsigned long long b = scnt[0][j] + scnt[1][j] + scnt[2][j] + scnt[3][j];
+    if (b) {
+      atomicAdd((unsigned long long *)&st->sum[j], (unsigned long long)a);
+      atomicAdd(&st->cnt[j], b);
+    }
+  }
+}
+
+__global__ void km_update_kernel(KmState *st, int max_iter) {
+  if (st->converged) return;
+  int changed = 0;
+  const int s = st->scale;
+  for (int j = 0; j < st->k; ++j) {
+    if (st->cnt[j]) {
+      const double c = ldexp((double)st->sum[j] / (double)st->cnt[j], -s);
+      if (c != st->center[j]) changed = 1;
+      st->center[j] = c;
+    }
+    st->sum[j] = 0;
+    st->cnt[j] = 0;
+  }
+  st->iters += 1;
+  if (!changed || st->iters >= max_iter) st->converged = 1;
+}
+
+template <int K>
+__global__ void km_label_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
+                                const KmState *st, int32_t *__restrict__ labels, uint8_t *__restrict__ top) {
+  double c[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) c[j] = st->center[j];
+  int jt = 0;
+#pragma unroll
+  for (int j = 1; j < K; ++j)
+    if (c[j] > c[jt]) jt = j;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool ok = !valid || valid[i];
+    const int bj = ok ? km_assign<K>(x[i], c) : -1;
+    if (labels) labels[i] = bj;
+    if (top) top[i] = (uint8_t)(bj == jt);
+  }
+}
+
+template <int K>
+hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels, uint8_t *top,
+                  double *centers_host, int32_t *iters_host, KmState *st, hipStream_t s) {
+  const unsigned g = hrf::stream_grid(n);
+  KmState init{};
+  for (int j = 0; j < KMAX; ++j) init.center[j] = 0;
+  init.lo_bits = ~0ull;
+  init.hi_bits = 0;
+  init.amax_bits = 0;
+  init.nvalid = 0;
+  HRF_HIP(hipMemcpyAsync(st, &init, sizeof(KmState), hipMemcpyHostToDevice, s));
+  if (n > 0) km_minmax_kernel<<<g, 256, 0, s>>>(x, valid, n, st);
+  km_init_kernel<<<1, 1, 0, s>>>(st, K);
+  HRF_LAUNCHED();
+  int done = 0;
+  int launched = 0;
+  int batch = 4;
+  int conv = 0;
+  while (!done) {
+    for (int b = 0; b < batch && launched < max_iter; ++b, ++launched) {
+      km_accum_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st);
+      km_update_kernel<<<1, 1, 0, s>>>(st, max_iter);
+    }
+    HRF_LAUNCHED();
+    HRF_HIP(hipMemcpyAsync(&conv, &st->converged, sizeof(int), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+    done = conv || launched >= max_iter;
+    batch = batch < 16 ? batch * 2 : 16;
+  }
+  if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
+  HRF_LAUNCHED();
+  KmState fin;
+  HRF_HIP(hipMemcpyAsync(&fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
+  HRF_HIP(hipStreamSynchronize(s));
+  if (centers_host)
+    for (int j = 0; j < K; ++j) centers_host[j] = fin.center[j];
+  if (iters_host) *iters_host = fin.iters;
+  return HRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrf_kmeans_state_bytes(void) { return (int64_t)sizeof(KmState); }
+
+hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
+                         int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host, void *state_ws,
+                         hrf_stream_t stream) {
+  HRF_REQUIRE(k >= 1 && k <= KMAX, "kmeans_1d: k must be 1..8");
+  HRF_REQUIRE(n >= 0 && max_iter >= 1 && state_ws, "kmeans_1d: bad arguments");
+  HRF_REQUIRE(n == 0 || x, "kmeans_1d: null input");
+  hipStream_t s = (hipStream_t)stream;
+  KmState *st = (KmState *)state_ws;
+  switch (k) {
+    case 1: return km_run<1>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 2: return km_run<2>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 3: return km_run<3>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 4: return km_run<4>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 5: return km_run<5>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 6: return km_run<6>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    case 7: return km_run<7>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+    default: return km_run<8>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
+  }
+}
+
+}  // extern "C"

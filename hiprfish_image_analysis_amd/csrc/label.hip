@@ -1,0 +1,608 @@
+// label.hip -- connected components and the binary-morphology / label-cleanup stages
+// (a9, a10, a13).
+//
+// Connected components (skimage.measure.label semantics: non-zero pixels connect when
+// EQUAL, 4- or 8-connectivity, raster-first numbering):
+//   1. cc_local   : 32x32 tile per workgroup, union-find in LDS with atomicMin linking
+//                   (larger root -> smaller root), so each local root is the tile-local
+//                   minimum index.
+//   2. cc_border  : the same union over tile-crossing neighbour pairs in global memory.
+//                   Reads may be stale; correctness comes from atomicMin's returned value
+//                   (retry on the true parent, indices strictly decrease).
+//   3. cc_compress: parent[p] = root = the component's minimum raster index.
+//   4. numbering  : roots ranked in raster order (wave ballots + block scan), which is
+//                   exactly "first appearance" numbering -- bit-identical to skimage/scipy.
+// Morphology kernels use the cross footprint of skimage's defaults.
+#include "common.hpp"
+#include "wave.hpp"
+
+namespace {
+
+constexpr int CC_T = 32;  // tile edge
+
+struct MaskV {
+  const uint8_t *p;
+  int inv;
+  __device__ __forceinline__ int32_t operator()(int64_t i) const { return (int32_t)((p[i] != 0) ^ inv); }
+};
+struct LabelV {
+  const int32_t *p;
+  __device__ __forceinline__ int32_t operator()(int64_t i) const { return p[i]; }
+};
+
+__device__ __forceinline__ int find_lds(volatile int32_t *lp, int x) {
+  int y = lp[x];
+  while (y != x) {
+    x = y;
+    y = lp[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ void union_lds(int32_t *lp, int a, int b) {
+  volatile int32_t *v = lp;
+  for (;;) {
+    a = find_lds(v, a);
+    b = find_lds(v, b);
+    if (a == b) return;
+    if (a < b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicMin(&lp[a], b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+__device__ __forceinline__ int32_t find_g(const int32_t *par, int32_t x) {
+  int32_t y = par[x];
+  while (y != x) {
+    x = y;
+    y = par[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ void union_g(int32_t *par, int32_t a, int32_t b) {
+  for (;;) {
+    a = find_g(par, a);
+    b = find_g(par, b);
+    if (a == b) return;
+    if (a < b) {
+      const int32_t t = a;
+      a = b;
+      b = t;
+    }
+    const int32_t old = atomicMin(&par[a], b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+template <class V, int CONN>
+__global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent) {
+  __shared__ int32_t lp[CC_T * CC_T];
+  __shared__ int32_t lv[CC_T * CC_T];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * CC_T, c0 = (int64_t)blockIdx.x * CC_T;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int li = tid + 256 * k, lr = li >> 5, lc = li & 31;
+    const int64_t gr = r0 + lr, gc = c0 + lc;
+    const int32_t v = (gr < H && gc < W) ? val(gr * W + gc) : 0;
+    lv[li] = v;
+    lp[li] = v ? li : -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int li = tid + 256 * k, lr = li >> 5, lc = li & 31;
+    const int32_t v = lv[li];
+    if (!v) continue;
+    if (lc > 0 && lv[li - 1] == v) union_lds(lp, li, li - 1);
+    if (lr > 0) {
+      if (lv[li - 32] == v) union_lds(lp, li, li - 32);
+      if (CONN == 2) {
+        if (lc > 0 && lv[li - 33] == v) union_lds(lp, li, li - 33);
+        if (lc < 31 && lv[li - 31] == v) union_lds(lp, li, li - 31);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int li = tid + 256 * k, lr = li >> 5, lc = li & 31;
+    const int64_t gr = r0 + lr, gc = c0 + lc;
+    if (gr >= H || gc >= W) continue;
+    int32_t g = -1;
+    if (lv[li]) {
+      const int rt = find_lds(lp, li);
+      g = (int32_t)((r0 + (rt >> 5)) * W + c0 + (rt & 31));
+    }
+    parent[gr * W + gc] = g;
+  }
+}
+
+template <class V, int CONN>
+__global__ void cc_border_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = blockIdx.y;
+  if (c >= W) return;
+  const int lr = (int)(r & 31), lc = (int)(c & 31);
+  if (lr != 0 && lc != 0 && lc != 31) return;
+  const int64_t p = r * W + c;
+  const int32_t v = val(p);
+  if (!v) return;
+  if (lc == 0 && c > 0 && val(p - 1) == v) union_g(parent, (int32_t)p, (int32_t)(p - 1));
+  if (r > 0) {
+    if (lr == 0 && val(p - W) == v) union_g(parent, (int32_t)p, (int32_t)(p - W));
+    if (CONN == 2) {
+      if ((lr == 0 || lc == 0) && c > 0 && val(p - W - 1) == v) union_g(parent, (int32_t)p, (int32_t)(p - W - 1));
+      if ((lr == 0 || lc == 31) && c + 1 < W && val(p - W + 1) == v) union_g(parent, (int32_t)p, (int32_t)(p - W + 1));
+    }
+  }
+}
+
+__global__ void cc_compress_kernel(int32_t *__restrict__ parent, int64_t n) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];
+    if (q >= 0 && q != p) parent[p] = find_g(parent, q);
+  }
+}
+
+// Numbering.  Block = 256 threads x 4 pixels = 1024 consecutive raster pixels.
+constexpr int NB = 1024;
+
+__global__ __launch_bounds__(256) void cc_count_roots_kernel(const int32_t *__restrict__ parent, int64_t n,
+                                                             int32_t *__restrict__ blk) {
+  __shared__ int32_t ws[4];
+  const int tid = threadIdx.x;
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t p = (int64_t)blockIdx.x * NB + k * 256 + tid;
+    cnt += (p < n && parent[p] == p);
+  }
+  cnt = hrf::wave_sum(cnt);
+  if ((tid & 63) == 0) ws[tid >> 6] = cnt;
+  __syncthreads();
+  if (tid == 0) blk[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Exclusive scan of nb block counts in one workgroup; total -> *total.
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(int32_t *__restrict__ blk, int64_t nb,
+                                                           int32_t *__restrict__ total) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  const int tid = threadIdx.x;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nb; base += 1024) {
+    const int64_t i = base + tid;
+    const int32_t v = i < nb ? blk[i] : 0;
+    const int32_t inc = hrf::wave_inclusive_scan(v);
+    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    if (tid < 64) {
+      const int32_t s = tid < 16 ? wsum[tid] : 0;
+      const int32_t si = hrf::wave_inclusive_scan(s);
+      if (tid < 16) wsum[tid] = si - s;
+    }
+    __syncthreads();
+    const int32_t excl = carry + wsum[tid >> 6] + inc - v;
+    if (i < nb) blk[i] = excl;
+    __syncthreads();
+    if (tid == 1023) carry = excl + v;
+    __syncthreads();
+  }
+  if (tid == 0) *total = carry;
+}
+
+// labels[root] = 1 + rank(root); background 0.  Non-roots filled by cc_fill_kernel.
+__global__ __launch_bounds__(256) void cc_rank_roots_kernel(const int32_t *__restrict__ parent, int64_t n,
+                                                            const int32_t *__restrict__ blk,
+                                                            int32_t *__restrict__ labels) {
+  __shared__ int32_t wc[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // pixel order inside the block: k*256 + tid; wave w covers [k*256 + 64w, +64)
+  int flags[4];
+  int pc[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t p = (int64_t)blockIdx.x * NB + k * 256 + tid;
+    flags[k] = (p < n && parent[p] == p);
+    const unsigned long long b = __ballot(flags[k]);
+    pc[k] = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wc[k * 4 + w] = __popcll(b);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t p = (int64_t)blockIdx.x * NB + k * 256 + tid;
+    if (p >= n) continue;
+    int before = 0;
+    for (int q = 0; q < k * 4 + w; ++q) before += wc[q];
+    if (flags[k]) labels[p] = blk[blockIdx.x] + before + pc[k] + 1;
+    else if (parent[p] < 0) labels[p] = 0;
+  }
+}
+
+__global__ void cc_fill_kernel(const int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ labels) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];
+    if (q >= 0 && q != p) labels[p] = labels[q];
+  }
+}
+
+// component sizes at the root index (size[] zeroed by the caller)
+__global__ void cc_sizes_kernel(const int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ size) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n_up = (n + 63) / 64 * 64;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_up; p += stride) {
+    const int32_t q = p < n ? parent[p] : -1;
+    hrf::agg_atomic_add<int32_t>(size, q < 0 ? 0 : q, 1, q >= 0);
+  }
+}
+
+// rso / remove_small_holes finish: out = (fg && size[root] >= thr) ^ inv
+__global__ void cc_keep_kernel(const int32_t *__restrict__ parent, const int32_t *__restrict__ size, int64_t n,
+                               int64_t thr, int inv, uint8_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];
+    const int keep = q >= 0 && (int64_t)size[q] >= thr;
+    out[p] = (uint8_t)(keep ^ inv);
+  }
+}
+
+// erosion-seed freeze step (ecoli measurement.py:102-106): components smaller than thr
+// join the seed mask, the others stay in play.
+__global__ void split_by_size_kernel(const int32_t *__restrict__ parent, const int32_t *__restrict__ size, int64_t n,
+                                     int64_t thr, uint8_t *__restrict__ small_or, uint8_t *__restrict__ large) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];
+    const bool fg = q >= 0;
+    const bool sm = fg && (int64_t)size[q] < thr;
+    if (sm) small_or[p] = 1;
+    large[p] = (uint8_t)(fg && !sm);
+  }
+}
+
+// flag[root] = 1 for components with a pixel on the 1-pixel frame
+__global__ void border_roots_kernel(const int32_t *__restrict__ parent, int64_t H, int64_t W,
+                                    int32_t *__restrict__ flag) {
+  const int64_t nb = 2 * W + 2 * H;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nb; e += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p;
+    if (e < W) p = e;
+    else if (e < 2 * W) p = (H - 1) * W + (e - W);
+    else if (e < 2 * W + H) p = (e - 2 * W) * W;
+    else p = (e - 2 * W - H) * W + (W - 1);
+    const int32_t q = parent[p];
+    if (q >= 0) flag[q] = 1;
+  }
+}
+
+__global__ void fill_holes_finish_kernel(const uint8_t *__restrict__ mask, const int32_t *__restrict__ parent,
+                                         const int32_t *__restrict__ flag, int64_t n, uint8_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];  // component of the background
+    out[p] = (uint8_t)(mask[p] != 0 || (q >= 0 && !flag[q]));
+  }
+}
+
+__global__ void clear_border_finish_kernel(const int32_t *__restrict__ lab, const int32_t *__restrict__ parent,
+                                           const int32_t *__restrict__ flag, int64_t n, int32_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t q = parent[p];
+    out[p] = (q >= 0 && flag[q]) ? 0 : lab[p];
+  }
+}
+
+// rso on an int label image: counts per label value
+__global__ void label_counts_kernel(const int32_t *__restrict__ lab, int64_t n, int32_t maxlab,
+                                    int32_t *__restrict__ cnt) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n_up = (n + 63) / 64 * 64;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_up; p += stride) {
+    const int32_t l = p < n ? lab[p] : 0;
+    const bool ok = l > 0 && l <= maxlab;
+    hrf::agg_atomic_add<int32_t>(cnt, ok ? l : 0, 1, ok);
+  }
+}
+
+__global__ void rso_labels_finish_kernel(const int32_t *__restrict__ lab, const int32_t *__restrict__ cnt,
+                                         int64_t n, int32_t maxlab, int64_t thr, int32_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = lab[p];
+    out[p] = (l > 0 && l <= maxlab && (int64_t)cnt[l] < thr) ? 0 : l;
+  }
+}
+
+// relabel_sequential: present flags -> exclusive scan -> map
+__global__ void present_kernel(const int32_t *__restrict__ lab, int64_t n, int32_t maxlab,
+                               int32_t *__restrict__ present) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = lab[p];
+    if (l > 0 && l <= maxlab) present[l] = 1;
+  }
+}
+
+__global__ __launch_bounds__(1024) void scan_present_kernel(int32_t *__restrict__ m, int64_t len,
+                                                            int32_t *__restrict__ total) {
+  // in-place inclusive scan of flags -> map[l] = rank (1-based) for present labels, 0 else
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  const int tid = threadIdx.x;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < len; base += 1024) {
+    const int64_t i = base + tid;
+    const int32_t v = i < len ? m[i] : 0;
+    const int32_t inc = hrf::wave_inclusive_scan(v);
+    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    if (tid < 64) {
+      const int32_t s = tid < 16 ? wsum[tid] : 0;
+      const int32_t si = hrf::wave_inclusive_scan(s);
+      if (tid < 16) wsum[tid] = si - s;
+    }
+    __syncthreads();
+    const int32_t incl = carry + wsum[tid >> 6] + inc;
+    if (i < len) m[i] = v ? incl : 0;
+    __syncthreads();
+    if (tid == 1023) carry = incl;
+    __syncthreads();
+  }
+  if (tid == 0) *total = carry;
+}
+
+__global__ void apply_map_kernel(const int32_t *__restrict__ lab, int64_t n, int32_t maxlab,
+                                 const int32_t *__restrict__ map, int32_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = lab[p];
+    out[p] = (l > 0 && l <= maxlab) ? map[l] : 0;
+  }
+}
+
+// ---- morphology (cross footprint) ------------------------------------------------------
+__global__ void erode_kernel(const uint8_t *__restrict__ m, int64_t H, int64_t W, int border,
+                             uint8_t *__restrict__ o) {
+  const int64_t n = H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / W, c = i - r * W;
+    int v = m[i] != 0;
+    v = v && (r > 0 ? m[i - W] != 0 : border);
+    v = v && (r + 1 < H ? m[i + W] != 0 : border);
+    v = v && (c > 0 ? m[i - 1] != 0 : border);
+    v = v && (c + 1 < W ? m[i + 1] != 0 : border);
+    o[i] = (uint8_t)v;
+  }
+}
+
+__global__ void dilate_kernel(const uint8_t *__restrict__ m, int64_t H, int64_t W, uint8_t *__restrict__ o) {
+  const int64_t n = H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / W, c = i - r * W;
+    const int v = m[i] || (r > 0 && m[i - W]) || (r + 1 < H && m[i + W]) || (c > 0 && m[i - 1]) ||
+                  (c + 1 < W && m[i + 1]);
+    o[i] = (uint8_t)v;
+  }
+}
+
+__global__ void count_u8_kernel(const uint8_t *__restrict__ m, int64_t n, unsigned long long *__restrict__ cnt) {
+  unsigned long long c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += m[i] != 0;
+  c = hrf::wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+__global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t *__restrict__ mx) {
+  int32_t m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = a[i] > m ? a[i] : m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int32_t u = __shfl_xor(m, o, 64);
+    m = u > m ? u : m;
+  }
+  if ((threadIdx.x & 63) == 0) atomicMax(mx, m);
+}
+
+template <class V>
+hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s) {
+  dim3 g((unsigned)hrf::cdiv(W, CC_T), (unsigned)hrf::cdiv(H, CC_T));
+  dim3 gb((unsigned)hrf::cdiv(W, 256), (unsigned)H);
+  if (conn == 2) {
+    cc_local_kernel<V, 2><<<g, 256, 0, s>>>(val, H, W, parent);
+    cc_border_kernel<V, 2><<<gb, 256, 0, s>>>(val, H, W, parent);
+  } else {
+    cc_local_kernel<V, 1><<<g, 256, 0, s>>>(val, H, W, parent);
+    cc_border_kernel<V, 1><<<gb, 256, 0, s>>>(val, H, W, parent);
+  }
+  cc_compress_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(parent, H * W);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status check_hw(int64_t H, int64_t W, const char *who) {
+  HRF_REQUIRE(H >= 0 && W >= 0 && H * W < (int64_t)INT32_MAX && H <= 65535, "%s: image too large (%lld x %lld)",
+              who, (long long)H, (long long)W);
+  return HRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+hrf_status hrf_cc_roots(const void *img, int32_t dtype, int64_t H, int64_t W, int32_t conn, int32_t *parent,
+                        hrf_stream_t stream) {
+  if (hrf_status s = check_hw(H, W, "cc_roots")) return s;
+  HRF_REQUIRE(conn == 1 || conn == 2, "cc_roots: connectivity must be 1 or 2");
+  HRF_REQUIRE(dtype == 0 || dtype == 1 || dtype == 2, "cc_roots: dtype must be 0 (u8), 1 (i32) or 2 (u8 inverted)");
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(img && parent, "cc_roots: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 1) return run_cc(LabelV{(const int32_t *)img}, H, W, conn, parent, s);
+  return run_cc(MaskV{(const uint8_t *)img, dtype == 2}, H, W, conn, parent, s);
+}
+
+hrf_status hrf_cc_number(const int32_t *parent, int64_t n, int32_t *labels, int32_t *blk_ws, int32_t *nlab_dev,
+                         hrf_stream_t stream) {
+  HRF_REQUIRE(n >= 0 && n < (int64_t)INT32_MAX, "cc_number: size out of range");
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    if (nlab_dev) HRF_HIP(hipMemsetAsync(nlab_dev, 0, sizeof(int32_t), s));
+    return HRF_OK;
+  }
+  HRF_REQUIRE(parent && labels && blk_ws && nlab_dev, "cc_number: null buffer");
+  const int64_t nb = hrf::cdiv(n, NB);
+  cc_count_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent, n, blk_ws);
+  scan_blocks_kernel<<<1, 1024, 0, s>>>(blk_ws, nb, nlab_dev);
+  cc_rank_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent, n, blk_ws, labels);
+  cc_fill_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent, n, labels);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_label(const void *img, int32_t dtype, int64_t H, int64_t W, int32_t conn, int32_t *labels,
+                     int32_t *parent_ws, int32_t *blk_ws, int32_t *nlab_dev, hrf_stream_t stream) {
+  if (hrf_status st = hrf_cc_roots(img, dtype, H, W, conn, parent_ws, stream)) return st;
+  return hrf_cc_number(parent_ws, H * W, labels, blk_ws, nlab_dev, stream);
+}
+
+hrf_status hrf_cc_sizes(const int32_t *parent, int64_t n, int32_t *size, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(parent && size, "cc_sizes: null buffer");
+  HRF_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * n, s));
+  cc_sizes_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent, n, size);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_remove_small_objects_mask(const uint8_t *mask, int64_t H, int64_t W, int64_t min_size, int32_t conn,
+                                         uint8_t *out, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
+  const int64_t n = H * W;
+  if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, stream)) return st;
+  if (n == 0) return HRF_OK;
+  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  cc_keep_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, min_size, 0, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_remove_small_holes(const uint8_t *mask, int64_t H, int64_t W, int64_t area_threshold, int32_t conn,
+                                  uint8_t *out, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
+  const int64_t n = H * W;
+  if (hrf_status st = hrf_cc_roots(mask, 2, H, W, conn, parent_ws, stream)) return st;
+  if (n == 0) return HRF_OK;
+  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  cc_keep_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, area_threshold, 1,
+                                                                        out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_split_by_size(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int64_t thr, uint8_t *small_or,
+                             uint8_t *large, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
+  const int64_t n = H * W;
+  if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, stream)) return st;
+  if (n == 0) return HRF_OK;
+  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  split_by_size_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, thr, small_or,
+                                                                              large);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_fill_holes(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, int32_t *parent_ws,
+                          int32_t *flag_ws, hrf_stream_t stream) {
+  const int64_t n = H * W;
+  hipStream_t s = (hipStream_t)stream;
+  if (hrf_status st = hrf_cc_roots(mask, 2, H, W, 1, parent_ws, stream)) return st;
+  if (n == 0) return HRF_OK;
+  HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * n, s));
+  border_roots_kernel<<<hrf::stream_grid(2 * (H + W)), 256, 0, s>>>(parent_ws, H, W, flag_ws);
+  fill_holes_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(mask, parent_ws, flag_ws, n, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_clear_border(const int32_t *labels, int64_t H, int64_t W, int32_t *out, int32_t *parent_ws,
+                            int32_t *flag_ws, hrf_stream_t stream) {
+  const int64_t n = H * W;
+  hipStream_t s = (hipStream_t)stream;
+  if (hrf_status st = hrf_cc_roots(labels, 1, H, W, 2, parent_ws, stream)) return st;
+  if (n == 0) return HRF_OK;
+  HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * n, s));
+  border_roots_kernel<<<hrf::stream_grid(2 * (H + W)), 256, 0, s>>>(parent_ws, H, W, flag_ws);
+  clear_border_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, parent_ws, flag_ws, n, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_remove_small_objects_labels(const int32_t *labels, int64_t n, int32_t maxlab, int64_t min_size,
+                                           int32_t *out, int32_t *cnt_ws, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(labels && out && cnt_ws && maxlab >= 0, "remove_small_objects_labels: bad arguments");
+  HRF_HIP(hipMemsetAsync(cnt_ws, 0, sizeof(int32_t) * ((size_t)maxlab + 1), s));
+  label_counts_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, n, maxlab, cnt_ws);
+  rso_labels_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, cnt_ws, n, maxlab, min_size, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_relabel_sequential(const int32_t *labels, int64_t n, int32_t maxlab, int32_t *out, int32_t *map_ws,
+                                  int32_t *nlab_dev, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(maxlab >= 0 && map_ws && nlab_dev, "relabel_sequential: bad arguments");
+  HRF_HIP(hipMemsetAsync(map_ws, 0, sizeof(int32_t) * ((size_t)maxlab + 1), s));
+  if (n > 0) present_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, n, maxlab, map_ws);
+  scan_present_kernel<<<1, 1024, 0, s>>>(map_ws, (int64_t)maxlab + 1, nlab_dev);
+  if (n > 0) apply_map_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, n, maxlab, map_ws, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_binary_erosion(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,
+                              hrf_stream_t stream) {
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(mask && out && mask != out, "binary_erosion: bad buffers (in-place not supported)");
+  erode_kernel<<<hrf::stream_grid(H * W), 256, 0, (hipStream_t)stream>>>(mask, H, W, border_value != 0, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_binary_dilation(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, hrf_stream_t stream) {
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(mask && out && mask != out, "binary_dilation: bad buffers (in-place not supported)");
+  dilate_kernel<<<hrf::stream_grid(H * W), 256, 0, (hipStream_t)stream>>>(mask, H, W, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_count_nonzero_u8(const uint8_t *mask, int64_t n, int64_t *count_dev, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(count_dev, "count_nonzero: null output");
+  HRF_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
+  if (n == 0) return HRF_OK;
+  count_u8_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(mask, n, (unsigned long long *)count_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(max_dev, "max_i32: null output");
+  HRF_HIP(hipMemsetAsync(max_dev, 0, sizeof(int32_t), s));
+  if (n == 0) return HRF_OK;
+  max_i32_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(a, n, max_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+}  // extern "C"

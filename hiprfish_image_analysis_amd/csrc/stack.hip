@@ -1,0 +1,216 @@
+// stack.hip -- spectral stack assembly and per-pixel channel reductions (a1-a3), plus the
+// small elementwise steps between pipeline stages.
+//
+// a1/a2 hrf_register_assemble: per-laser (H, W, C_l) stacks -> one (H, W, C) stack with each
+//   laser shifted by its integer registration vector and zero outside its coverage
+//   (ecoli measurement.py:51-70, multispecies :88-102), optionally multiplied by the
+//   intersection of all coverage masks (ecoli :69-70).  One pass, lanes along channels.
+// a3 hrf_channel_sum: per-pixel sum over C in numpy's pairwise order (8 accumulators,
+//   blocks of 128) so the f64 result equals np.sum(stack, axis=2) bit for bit, then
+//   log(s + 1e-2) (ecoli :72) / log10(s + 1) (biofilm :831) / identity, optionally negated
+//   (watershed input).
+#include "common.hpp"
+
+namespace {
+
+constexpr int LMAX = 8;
+struct Lasers {
+  const float *src[LMAX];
+  int32_t c0[LMAX + 1];  // channel offsets, c0[n] = C
+  int32_t dr[LMAX], dc[LMAX];
+  int32_t n;
+};
+
+__device__ __forceinline__ bool covered(int64_t r, int64_t c, int64_t H, int64_t W, int dr, int dc) {
+  // destination rows [max(0,dr), H + min(0,dr)), same for columns
+  return r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0) && c >= (dc > 0 ? dc : 0) && c < W + (dc < 0 ? dc : 0);
+}
+
+__global__ void assemble_kernel(Lasers L, int64_t H, int64_t W, int apply_mask, float *__restrict__ dst) {
+  const int C = L.c0[L.n];
+  const int64_t n = H * W * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = e / C;
+    const int ch = (int)(e - p * C);
+    const int64_t r = p / W, c = p - r * W;
+    int li = 0;
+#pragma unroll
+    for (int q = 1; q < LMAX; ++q)
+      if (q < L.n && ch >= L.c0[q]) li = q;
+    bool ok = true;
+    if (apply_mask) {
+#pragma unroll
+      for (int q = 0; q < LMAX; ++q)
+        if (q < L.n) ok = ok && covered(r, c, H, W, L.dr[q], L.dc[q]);
+    }
+    float v = 0.0f;
+    if (ok && covered(r, c, H, W, L.dr[li], L.dc[li])) {
+      const int cl = L.c0[li + 1] - L.c0[li];
+      v = L.src[li][((r - L.dr[li]) * W + (c - L.dc[li])) * cl + (ch - L.c0[li])];
+    }
+    dst[e] = v;
+  }
+}
+
+// numpy pairwise_sum over n f32 values (as f64), n <= 512
+__device__ double pw_block(const float *a, int n) {
+  if (n < 8) {
+    double res = 0.0;
+    for (int i = 0; i < n; ++i) res += (double)a[i];
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (double)a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += (double)a[i + j];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += (double)a[i];
+  return res;
+}
+__device__ double pw_l1(const float *a, int n) {
+  if (n <= 128) return pw_block(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_block(a, n2) + pw_block(a + n2, n - n2);
+}
+__device__ double pw_sum(const float *a, int n) {
+  if (n <= 256) return pw_l1(a, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_l1(a, n2) + pw_l1(a + n2, n - n2);
+}
+
+__global__ void channel_sum_kernel(const float *__restrict__ stack, int64_t npix, int C,
+                                   const uint8_t *__restrict__ mask, int mode, int negate, double *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    double s = (mask && !mask[p]) ? 0.0 : 0.0 + pw_sum(stack + p * C, C);
+    if (mode == 1) s = log(s + 1e-2);
+    else if (mode == 2) s = log10(s + 1.0);
+    out[p] = negate ? -s : s;
+  }
+}
+
+__global__ void max_f64_kernel(const double *__restrict__ a, int64_t n, unsigned long long *__restrict__ mx) {
+  // order-preserving encoding so atomicMax on uint64 is a max on doubles
+  unsigned long long m = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long b = __double_as_longlong(a[i]);
+    const unsigned long long e = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    m = e > m ? e : m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(m, o, 64);
+    m = u > m ? u : m;
+  }
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+
+__global__ void decode_max_kernel(unsigned long long *mx) {
+  const unsigned long long e = *mx;
+  const unsigned long long b = (e >> 63) ? (e & 0x7fffffffffffffffull) : ~e;
+  *reinterpret_cast<double *>(mx) = __longlong_as_double((long long)b);
+}
+
+__global__ void div_scalar_kernel(const double *__restrict__ a, int64_t n, const double *__restrict__ d,
+                                  double *__restrict__ o) {
+  const double v = *d;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = a[i] / v;
+}
+
+__global__ void pad_edge_kernel(const double *__restrict__ a, int64_t H, int64_t W, int w, double *__restrict__ o) {
+  const int64_t HP = H + 2 * w, WP = W + 2 * w;
+  const int64_t n = HP * WP;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / WP, c = i - r * WP;
+    int64_t rr = r - w, cc = c - w;
+    rr = rr < 0 ? 0 : (rr >= H ? H - 1 : rr);
+    cc = cc < 0 ? 0 : (cc >= W ? W - 1 : cc);
+    o[i] = a[rr * W + cc];
+  }
+}
+
+__global__ void mask_mul_kernel(const double *__restrict__ a, const uint8_t *__restrict__ m, int64_t n,
+                                double *__restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = a[i] * (double)(m[i] != 0);
+}
+
+}  // namespace
+
+extern "C" {
+
+hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *channels_host,
+                                 const int32_t *shifts_host, int32_t nlaser, int64_t H, int64_t W,
+                                 int32_t apply_mask, float *dst, hrf_stream_t stream) {
+  HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && shifts_host, "register_assemble: bad lasers");
+  Lasers L{};
+  L.n = nlaser;
+  L.c0[0] = 0;
+  for (int i = 0; i < nlaser; ++i) {
+    HRF_REQUIRE(channels_host[i] >= 1 && src_host[i], "register_assemble: laser %d empty", i);
+    L.src[i] = src_host[i];
+    L.c0[i + 1] = L.c0[i] + channels_host[i];
+    L.dr[i] = shifts_host[2 * i];
+    L.dc[i] = shifts_host[2 * i + 1];
+  }
+  for (int i = nlaser + 1; i <= LMAX; ++i) L.c0[i] = L.c0[nlaser];
+  const int64_t n = H * W * L.c0[nlaser];
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(dst, "register_assemble: null output");
+  assemble_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,
+                           int32_t negate, double *out, hrf_stream_t stream) {
+  HRF_REQUIRE(C >= 1 && C <= 512 && mode >= 0 && mode <= 2, "channel_sum: C must be 1..512, mode 0..2");
+  if (npix == 0) return HRF_OK;
+  HRF_REQUIRE(stack && out, "channel_sum: null buffer");
+  channel_sum_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+// *max_dev (an 8-byte device word) receives max(a) as a double
+hrf_status hrf_max_f64(const double *a, int64_t n, double *max_dev, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(max_dev && n >= 1 && a, "max_f64: bad arguments");
+  HRF_HIP(hipMemsetAsync(max_dev, 0, sizeof(double), s));
+  max_f64_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(a, n, (unsigned long long *)max_dev);
+  decode_max_kernel<<<1, 1, 0, s>>>((unsigned long long *)max_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_div_scalar_f64(const double *a, int64_t n, const double *divisor_dev, double *out,
+                              hrf_stream_t stream) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(a && divisor_dev && out, "div_scalar: null buffer");
+  div_scalar_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(a, n, divisor_dev, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32_t width, double *out, hrf_stream_t stream) {
+  HRF_REQUIRE(width >= 0 && H >= 1 && W >= 1 && a && out, "pad_edge: bad arguments");
+  pad_edge_kernel<<<hrf::stream_grid((H + 2 * width) * (W + 2 * width)), 256, 0, (hipStream_t)stream>>>(a, H, W, width,
+                                                                                                        out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out, hrf_stream_t stream) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(a && mask && out, "mask_mul: null buffer");
+  mask_mul_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(a, mask, n, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+}  // extern "C"

@@ -83,3 +83,394 @@ def enhance_3d(pad: torch.Tensor) -> torch.Tensor:
     out = torch.empty((xp - 10, yp - 10, zp - 10), dtype=torch.float64, device=pad.device)
     _lib.call("hrf_enhance_3d", _ptr(pad), xp, yp, zp, 11, 9, 9, _ptr(out), _stream())
     return out
+
+
+# ---- helpers --------------------------------------------------------------------------------
+def _u8(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError("%s must be a device tensor" % name)
+    if t.dtype == torch.bool:
+        t = t.contiguous().view(torch.uint8)
+    elif t.dtype != torch.uint8:
+        t = (t != 0).to(torch.uint8)
+    return t.contiguous()
+
+
+def _i32(t, name):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError("%s must be a device tensor" % name)
+    return t.contiguous() if t.dtype == torch.int32 else t.to(torch.int32).contiguous()
+
+
+def _scalar_i32(dev):
+    return int(dev.item())
+
+
+def _i32_host(seq):
+    import numpy as np
+    return np.ascontiguousarray(np.asarray(seq, dtype=np.int32))
+
+
+# ---- a1-a3 ----------------------------------------------------------------------------------
+def register_assemble(srcs, shifts, apply_mask=True):
+    """ecoli measurement.py:51-70: shift each (H,W,C_l) laser stack, concatenate on C."""
+    import ctypes
+    srcs = [_dev(s, torch.float32, "laser stack") for s in srcs]
+    H, W = srcs[0].shape[:2]
+    ch = _i32_host([s.shape[2] for s in srcs])
+    sh = _i32_host([v for d in shifts for v in (int(d[0]), int(d[1]))])
+    ptrs = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    out = torch.empty((H, W, int(ch.sum())), dtype=torch.float32, device=srcs[0].device)
+    _lib.call("hrf_register_assemble", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, sh.ctypes.data,
+              len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _stream())
+    return out
+
+
+def channel_sum(stack, mask=None, mode=0, negate=False):
+    """np.sum(stack, axis=2) (f64, numpy pairwise order); mode 1 -> log(s+1e-2), 2 -> log10(s+1)"""
+    stack = _dev(stack, torch.float32, "stack")
+    H, W, C = stack.shape
+    m = _u8(mask, "mask") if mask is not None else None
+    out = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    _lib.call("hrf_channel_sum", _ptr(stack), H * W, C, _ptr(m), mode, int(negate), _ptr(out), _stream())
+    return out
+
+
+def max_f64(a):
+    a = _dev(a, torch.float64, "a")
+    out = torch.empty(1, dtype=torch.float64, device=a.device)
+    _lib.call("hrf_max_f64", _ptr(a), a.numel(), _ptr(out), _stream())
+    return out
+
+
+def div_scalar(a, d):
+    a = _dev(a, torch.float64, "a")
+    out = torch.empty_like(a)
+    _lib.call("hrf_div_scalar_f64", _ptr(a), a.numel(), _ptr(_dev(d, torch.float64, "d")), _ptr(out), _stream())
+    return out
+
+
+def pad_edge(a, width=5):
+    a = _dev(a, torch.float64, "a")
+    H, W = a.shape
+    out = torch.empty((H + 2 * width, W + 2 * width), dtype=torch.float64, device=a.device)
+    _lib.call("hrf_pad_edge_f64", _ptr(a), H, W, width, _ptr(out), _stream())
+    return out
+
+
+def mask_mul(a, mask):
+    a = _dev(a, torch.float64, "a")
+    m = _u8(mask, "mask")
+    out = torch.empty_like(a)
+    _lib.call("hrf_mask_mul_f64", _ptr(a), _ptr(m), a.numel(), _ptr(out), _stream())
+    return out
+
+
+# ---- a8 -------------------------------------------------------------------------------------
+_KM_STATE = {}
+
+
+def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True):
+    """-> labels int32 (or None), top-cluster mask u8, centres (list), iterations"""
+    import ctypes
+    import numpy as np
+    x = _dev(x, torch.float64, "x")
+    n = x.numel()
+    dev = x.device
+    st = _KM_STATE.get(dev)
+    if st is None:
+        nb = _lib.lib().hrf_kmeans_state_bytes()
+        st = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
+        _KM_STATE[dev] = st
+    v = _u8(valid, "valid") if valid is not None else None
+    labels = torch.empty(x.shape, dtype=torch.int32, device=dev) if want_labels else None
+    top = torch.empty(x.shape, dtype=torch.uint8, device=dev)
+    cen = np.zeros(k, np.float64)
+    it = ctypes.c_int32(0)
+    _lib.call("hrf_kmeans_1d", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
+              ctypes.addressof(it), _ptr(st), _stream())
+    return labels, top, cen.tolist(), it.value
+
+
+# ---- a9/a10/a13 -----------------------------------------------------------------------------
+def _img(img):
+    if img.dtype == torch.int32:
+        return img.contiguous(), 1
+    return _u8(img, "img"), 0
+
+
+def cc_roots(img, conn=2):
+    t, dt = _img(img)
+    H, W = t.shape
+    parent = torch.empty((H, W), dtype=torch.int32, device=t.device)
+    _lib.call("hrf_cc_roots", _ptr(t), dt, H, W, conn, _ptr(parent), _stream())
+    return parent
+
+
+def label(img, conn=2, return_num=True):
+    """skimage.measure.label(img, connectivity=conn): raster-first numbering"""
+    t, dt = _img(img)
+    H, W = t.shape
+    dev = t.device
+    labels = torch.empty((H, W), dtype=torch.int32, device=dev)
+    parent = torch.empty((H, W), dtype=torch.int32, device=dev)
+    blk = torch.empty((H * W + 1023) // 1024 + 1, dtype=torch.int32, device=dev)
+    nlab = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("hrf_label", _ptr(t), dt, H, W, conn, _ptr(labels), _ptr(parent), _ptr(blk), _ptr(nlab), _stream())
+    if return_num:
+        return labels, _scalar_i32(nlab)
+    return labels, nlab
+
+
+def remove_small_objects(img, min_size=64, conn=1, maxlab=None):
+    """skimage.morphology.remove_small_objects: bool -> components, int32 -> label sizes"""
+    if img.dtype == torch.int32:
+        H, W = img.shape
+        if maxlab is None:
+            maxlab = max_i32(img)
+        cnt = torch.empty(maxlab + 1, dtype=torch.int32, device=img.device)
+        out = torch.empty_like(img)
+        _lib.call("hrf_remove_small_objects_labels", _ptr(img.contiguous()), H * W, maxlab, min_size, _ptr(out),
+                  _ptr(cnt), _stream())
+        return out
+    m = _u8(img, "mask")
+    H, W = m.shape
+    out = torch.empty_like(m)
+    parent = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    size = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    _lib.call("hrf_remove_small_objects_mask", _ptr(m), H, W, min_size, conn, _ptr(out), _ptr(parent), _ptr(size),
+              _stream())
+    return out
+
+
+def remove_small_holes(mask, area_threshold=64, conn=1):
+    m = _u8(mask, "mask")
+    H, W = m.shape
+    out = torch.empty_like(m)
+    parent = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    size = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    _lib.call("hrf_remove_small_holes", _ptr(m), H, W, area_threshold, conn, _ptr(out), _ptr(parent), _ptr(size),
+              _stream())
+    return out
+
+
+def fill_holes(mask):
+    m = _u8(mask, "mask")
+    H, W = m.shape
+    out = torch.empty_like(m)
+    parent = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    flag = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    _lib.call("hrf_fill_holes", _ptr(m), H, W, _ptr(out), _ptr(parent), _ptr(flag), _stream())
+    return out
+
+
+def clear_border(labels):
+    l = _i32(labels, "labels")
+    H, W = l.shape
+    out = torch.empty_like(l)
+    parent = torch.empty((H, W), dtype=torch.int32, device=l.device)
+    flag = torch.empty((H, W), dtype=torch.int32, device=l.device)
+    _lib.call("hrf_clear_border", _ptr(l), H, W, _ptr(out), _ptr(parent), _ptr(flag), _stream())
+    return out
+
+
+def relabel_sequential(labels, maxlab=None):
+    l = _i32(labels, "labels")
+    if maxlab is None:
+        maxlab = max_i32(l)
+    out = torch.empty_like(l)
+    m = torch.empty(maxlab + 1, dtype=torch.int32, device=l.device)
+    n = torch.zeros(1, dtype=torch.int32, device=l.device)
+    _lib.call("hrf_relabel_sequential", _ptr(l), l.numel(), maxlab, _ptr(out), _ptr(m), _ptr(n), _stream())
+    return out, _scalar_i32(n)
+
+
+def binary_erosion(mask, border_value=1):
+    m = _u8(mask, "mask")
+    H, W = m.shape
+    out = torch.empty_like(m)
+    _lib.call("hrf_binary_erosion", _ptr(m), H, W, int(border_value), _ptr(out), _stream())
+    return out
+
+
+def binary_dilation(mask):
+    m = _u8(mask, "mask")
+    H, W = m.shape
+    out = torch.empty_like(m)
+    _lib.call("hrf_binary_dilation", _ptr(m), H, W, _ptr(out), _stream())
+    return out
+
+
+def binary_opening(mask):
+    """skimage.morphology.binary_opening (cross): dilation(erosion(border=True))"""
+    return binary_dilation(binary_erosion(mask, 1))
+
+
+def count_nonzero(mask, sync=True):
+    m = _u8(mask, "mask")
+    c = torch.zeros(1, dtype=torch.int64, device=m.device)
+    _lib.call("hrf_count_nonzero_u8", _ptr(m), m.numel(), _ptr(c), _stream())
+    return int(c.item()) if sync else c
+
+
+def max_i32(a, sync=True):
+    a = _i32(a, "a")
+    m = torch.zeros(1, dtype=torch.int32, device=a.device)
+    _lib.call("hrf_max_i32", _ptr(a), a.numel(), _ptr(m), _stream())
+    return int(m.item()) if sync else m
+
+
+# ---- a12 ------------------------------------------------------------------------------------
+def watershed(image, markers, mask=None, negate=False, max_passes=100000):
+    """skimage.morphology.watershed(+/-image, markers, mask=mask), 4-connectivity"""
+    import ctypes
+    image = _dev(image, torch.float64, "image")
+    mk = _i32(markers, "markers")
+    H, W = image.shape
+    m = _u8(mask, "mask") if mask is not None else None
+    out = torch.empty((H, W), dtype=torch.int32, device=image.device)
+    ws = torch.empty(32 * H * W, dtype=torch.uint8, device=image.device)
+    fl = torch.empty(8, dtype=torch.int32, device=image.device)
+    passes = ctypes.c_int32(0)
+    _lib.call("hrf_watershed", _ptr(image), int(negate), _ptr(mk), _ptr(m), H, W, _ptr(out), _ptr(ws), _ptr(fl),
+              max_passes, ctypes.addressof(passes), _stream())
+    return out
+
+
+# ---- a14-a16, a20, a21, a23 -----------------------------------------------------------------
+def label_sums(stack, labels, maxlab, cal=None, cal_range=None):
+    stack = _dev(stack, torch.float32, "stack")
+    l = _i32(labels, "labels")
+    C = stack.shape[-1]
+    npix = l.numel()
+    sums = torch.empty((maxlab + 1, C), dtype=torch.float64, device=stack.device)
+    counts = torch.empty(maxlab + 1, dtype=torch.int64, device=stack.device)
+    c0, c1 = cal_range if cal_range is not None else (0, C)
+    calp = _ptr(_dev(cal, torch.float32, "cal")) if cal is not None else None
+    _lib.call("hrf_label_sums", _ptr(stack), _ptr(l), npix, C, maxlab, calp, c0, c1, _ptr(sums), _ptr(counts),
+              _stream())
+    return sums, counts
+
+
+def cell_table(sums, counts, maxlab, max_rows=None):
+    C = sums.shape[1]
+    dev = sums.device
+    if max_rows is None:
+        max_rows = maxlab
+    rol = torch.empty(maxlab + 1, dtype=torch.int32, device=dev)
+    lor = torch.empty(max(max_rows, 1), dtype=torch.int32, device=dev)
+    avg = torch.empty((max(max_rows, 1), C), dtype=torch.float64, device=dev)
+    avgn = torch.empty((max(max_rows, 1), C), dtype=torch.float64, device=dev)
+    nrows = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("hrf_cell_table", _ptr(sums), _ptr(counts), maxlab, C, max_rows, _ptr(rol), _ptr(lor), _ptr(avg),
+              _ptr(avgn), _ptr(nrows), _stream())
+    n = _scalar_i32(nrows)
+    return rol, lor[:n], avg[:n], avgn[:n]
+
+
+def region_props(labels, maxlab):
+    l = _i32(labels, "labels")
+    H, W = l.shape
+    mom = torch.empty((maxlab + 1, 6), dtype=torch.int64, device=l.device)
+    props = torch.empty((maxlab + 1, 8), dtype=torch.float64, device=l.device)
+    _lib.call("hrf_region_moments", _ptr(l), H, W, maxlab, _ptr(mom), _stream())
+    _lib.call("hrf_region_props", _ptr(mom), maxlab, _ptr(props), _stream())
+    return props
+
+
+def barcode_counts(bc, R):
+    b = _i32(bc, "bc")
+    out = torch.empty(R, dtype=torch.int64, device=b.device)
+    _lib.call("hrf_barcode_counts", _ptr(b), b.numel(), R, _ptr(out), _stream())
+    return out
+
+
+def paint_ids(labels, code):
+    l = _i32(labels, "labels")
+    c = _i32(code, "code")
+    out = torch.empty_like(l)
+    _lib.call("hrf_paint_ids", _ptr(l), l.numel(), _ptr(c), c.numel(), _ptr(out), _stream())
+    return out
+
+
+# ---- a19 ------------------------------------------------------------------------------------
+def classify_geometry(C, nseg, R):
+    import ctypes
+    kp, rp = ctypes.c_int32(0), ctypes.c_int32(0)
+    _lib.call("hrf_classify_geometry", C, nseg, R, ctypes.addressof(kp), ctypes.addressof(rp))
+    return kp.value, rp.value
+
+
+def classify_prepare(ref, bounds):
+    ref = _dev(ref, torch.float32, "ref")
+    R, C = ref.shape
+    b = _i32_host(bounds)
+    kp, rp = classify_geometry(C, len(b) - 1, R)
+    refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
+    _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, _ptr(refx), _stream())
+    return refx
+
+
+def classify_pixels(stack, refx, R, bounds):
+    stack = _dev(stack, torch.float32, "stack")
+    C = stack.shape[-1]
+    P = stack.numel() // C
+    b = _i32_host(bounds)
+    idx = torch.empty(stack.shape[:-1], dtype=torch.int32, device=stack.device)
+    dist = torch.empty(stack.shape[:-1], dtype=torch.float32, device=stack.device)
+    _lib.call("hrf_classify_pixels", _ptr(stack), P, C, _ptr(refx), R, b.ctypes.data, len(b) - 1, _ptr(idx),
+              _ptr(dist), _stream())
+    return idx, dist
+
+
+def classify_cells(x, ref, bounds, variant=0, fx=None, fr=None):
+    x = _dev(x, torch.float64, "x")
+    ref = _dev(ref, torch.float64, "ref")
+    N, C = x.shape
+    R = ref.shape[0]
+    b = _i32_host(bounds)
+    fxp = _ptr(_dev(fx, torch.float64, "fx")) if fx is not None else None
+    frp = _ptr(_dev(fr, torch.float64, "fr")) if fr is not None else None
+    arg = torch.empty(N, dtype=torch.int32, device=x.device)
+    dmin = torch.empty(N, dtype=torch.float64, device=x.device)
+    _lib.call("hrf_classify_cells", _ptr(x), N, _ptr(ref), R, C, b.ctypes.data, len(b) - 1, variant, fxp, frp,
+              _ptr(arg), _ptr(dmin), _stream())
+    return arg, dmin
+
+
+# ---- a22 ------------------------------------------------------------------------------------
+def rag_edges(labels, maxlab):
+    l = _i32(labels, "labels")
+    H, W = l.shape
+    e = torch.empty((maxlab + 1, maxlab + 1), dtype=torch.uint8, device=l.device)
+    _lib.call("hrf_rag_edges", _ptr(l), H, W, maxlab, _ptr(e), _stream())
+    return e
+
+
+def barcode_adjacency(edge, bc_of_label, R):
+    maxlab = edge.shape[0] - 1
+    bc = _i32(bc_of_label, "bc_of_label")
+    adj = torch.empty((R, R), dtype=torch.int64, device=edge.device)
+    _lib.call("hrf_barcode_adjacency", _ptr(edge.contiguous()), maxlab, _ptr(bc), R, _ptr(adj), _stream())
+    return adj
+
+
+def shape_filter(labels, props, maxlab, minor_lo=15.0, minor_hi=35.0):
+    l = _i32(labels, "labels")
+    H, W = l.shape
+    out = torch.empty_like(l)
+    _lib.call("hrf_shape_filter", _ptr(l), H, W, _ptr(props.contiguous()), maxlab, float(minor_lo), float(minor_hi),
+              _ptr(out), _stream())
+    return out
+
+
+def split_by_size(mask, thr, small_or, conn=2):
+    """freeze components smaller than thr into small_or (in place); returns the rest"""
+    m = _u8(mask, "mask")
+    H, W = m.shape
+    large = torch.empty_like(m)
+    parent = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    size = torch.empty((H, W), dtype=torch.int32, device=m.device)
+    _lib.call("hrf_split_by_size", _ptr(m), H, W, conn, thr, _ptr(small_or), _ptr(large), _ptr(parent), _ptr(size),
+              _stream())
+    return large

@@ -1,0 +1,152 @@
+"""Device pipelines: the reference's measurement and classification stages, every compute
+step a libhrf.so kernel (kernels.py).  Tensors stay resident in HBM from the (H, W, C) stack
+to the label map, per-cell spectra, barcode ids and counts.
+
+Each function cites the reference lines it stands in for.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import kernels as K
+
+ECOLI_BOUNDS = (0, 32, 55, 75, 89, 95)
+MULTI_BOUNDS = (0, 23, 43, 57, 63)
+
+
+# --------------------------------------------------------------------------------------------
+# E. coli / reference-library measurement (hiprfish_imaging_spectral_image_measurement.py)
+# --------------------------------------------------------------------------------------------
+def erosion_seeds(cell_sm: torch.Tensor, area_max: int = 600, min_obj: int = 10) -> torch.Tensor:
+    """ecoli measurement.py:97-110: freeze regions below `area_max` as seeds, erode the rest,
+    drop fragments < `min_obj` (4-connected), repeat until nothing is left.  -> seed mask u8"""
+    be = torch.zeros_like(K._u8(cell_sm, "cell_sm"))
+    m = K._u8(cell_sm, "cell_sm")
+    while K.count_nonzero(m) > 0:                      # markers = regionprops(dist_lab) non-empty
+        m = K.split_by_size(m, area_max, be, conn=2)   # :102-106 (dist_lab is 8-connected)
+        m = K.binary_erosion(m, 1)                     # :107
+        m = K.remove_small_objects(m, min_obj, conn=1)  # :108
+    return be
+
+
+def segment_ecoli(stack: torch.Tensor, keep: dict | None = None):
+    """ecoli measurement.py:44-127 on the registered stack.  -> (segmentation int32, max label)"""
+    image_cn = K.channel_sum(stack, mode=1)                              # :71-72 log(sum + 1e-2)
+    _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False)    # :73-84 brighter cluster
+    _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False)      # :85-94 brightest layer
+    opened = K.binary_opening(K.remove_small_holes(interior, 64, 1))      # :95
+    cell_sm = K.remove_small_objects(opened, 50, conn=1)                 # :96
+    be = erosion_seeds(cell_sm)                                          # :97-110
+    seeds_mask = K.remove_small_objects(be, 10, conn=2)                  # :111 rso(label(dist_be), 10)
+    seeds, nseeds = K.label(seeds_mask, conn=2)                          # :111-112
+    seg = K.watershed(image_cn, seeds, rough_mask, negate=True)          # :113 watershed(-image_cn)
+    seg = K.remove_small_objects(seg, 100, maxlab=nseeds)                # :114
+    seg = K.clear_border(seg)                                            # :115
+    props = K.region_props(seg, nseeds)                                  # :116 regionprops
+    final = K.shape_filter(seg, props, nseeds, 15.0, 35.0)               # :117-126
+    if keep is not None:
+        keep.update(image_cn=image_cn, rough_mask=rough_mask, interior=interior, cell_sm=cell_sm, seeds=seeds,
+                    watershed=seg)
+    return final, nseeds
+
+
+@dataclass
+class Measurement:
+    segmentation: torch.Tensor      # (H, W) int32 (labels not re-sequenced, as the reference)
+    maxlab: int
+    labels: torch.Tensor            # (N,) int32 label of each row (ascending, regionprops order)
+    avgint: torch.Tensor            # (N, C) f64 per-cell mean spectrum
+    avgint_norm: torch.Tensor       # (N, C) f64 max-normalised
+    extras: dict = field(default_factory=dict)
+
+
+def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, keep: dict | None = None):
+    """ecoli measurement.py:142-162: segment, flat-field channels 0..31 (load_calibration_images
+    :33-38 puts the calibration image on channels 0-31 and 1.0 elsewhere), per-cell means."""
+    seg, maxlab = segment_ecoli(stack, keep)
+    sums, counts = K.label_sums(stack, seg, maxlab, cal=calibration,
+                                cal_range=(0, 32) if calibration is not None else None)   # :147-155
+    _, lor, avgint, avgint_norm = K.cell_table(sums, counts, maxlab)                      # :151-157
+    return Measurement(seg, maxlab, lor, avgint, avgint_norm)
+
+
+# --------------------------------------------------------------------------------------------
+# Classification (segmented cosine against a reference library)
+# --------------------------------------------------------------------------------------------
+@dataclass
+class Library:
+    """Reference barcode library: row r is barcode r + 1 (mean spectrum of enc_{r+1},
+    train_reference.py:1397), max-normalised."""
+    spectra: torch.Tensor        # (R, C) f64
+    bounds: tuple
+    nbit: int
+    _refx: torch.Tensor | None = None
+
+    @property
+    def R(self):
+        return self.spectra.shape[0]
+
+    def refx(self):
+        if self._refx is None:
+            self._refx = K.classify_prepare(self.spectra.to(torch.float32), self.bounds)
+        return self._refx
+
+    def presence_flags(self, thr: float = 0.1) -> torch.Tensor:
+        """per-segment presence of the library rows (max over the segment > thr)"""
+        return segment_flags(self.spectra, self.bounds, thr)
+
+
+def segment_flags(x: torch.Tensor, bounds, thr: float = 0.1) -> torch.Tensor:
+    # tiny (N x nseg) host-side bookkeeping of the gated metric's inputs
+    cols = [x[:, bounds[k]:bounds[k + 1]].amax(dim=1) > thr for k in range(len(bounds) - 1)]
+    return torch.stack(cols, 1).to(torch.float64).contiguous()
+
+
+def classify_cells(avgint_norm: torch.Tensor, lib: Library, variant: int = 0, flag_thr: float = 0.1):
+    """image_classification.py:43-56 / classify_spectra.py:27-35 restated on the max-normalised
+    cell spectra (hrf_cell_table computes avgint / rowmax, :43): argmin of the segmented-cosine
+    distance over the library.  variant 0: ungated mean of segment distances; 1:
+    channel_cosine_intensity gating (train_reference.py:223-386); 2: _7b_v2 gating
+    (:993-1072).  -> (index, distance)"""
+    x = avgint_norm
+    fx = fr = None
+    if variant:
+        fx = segment_flags(x, lib.bounds, flag_thr)
+        fr = lib.presence_flags(flag_thr)
+    return K.classify_cells(x, lib.spectra, lib.bounds, variant, fx, fr)
+
+
+def classify_pixels(stack: torch.Tensor, lib: Library):
+    """north_star per-pixel mode: argmin over the library of the ungated segmented-cosine
+    distance for every pixel spectrum (one fused f32-MFMA GEMM + argmax)."""
+    return K.classify_pixels(stack, lib.refx(), lib.R, lib.bounds)
+
+
+def barcode_strings(idx, nbit: int):
+    """barcode number = library row + 1, written as the reference's binary code string"""
+    return [format(int(i) + 1, "0%db" % nbit) for i in idx]
+
+
+@dataclass
+class TileResult:
+    meas: Measurement
+    cell_idx: torch.Tensor
+    cell_dist: torch.Tensor
+    counts: torch.Tensor
+    identification: torch.Tensor
+    pixel_idx: torch.Tensor | None = None
+    pixel_dist: torch.Tensor | None = None
+
+
+def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0):
+    """One tile of the hot path: measure (segment + per-cell spectra) + classify + count."""
+    meas = measure_ecoli(stack, calibration)
+    idx, dist = classify_cells(meas.avgint_norm, lib, variant)
+    counts = K.barcode_counts(idx, lib.R)                       # collect_measurement_results.py:92-98
+    ident = K.paint_ids(meas.segmentation, idx + 1)             # image_classification.py:65-71
+    res = TileResult(meas, idx, dist, counts, ident)
+    if per_pixel:
+        res.pixel_idx, res.pixel_dist = classify_pixels(stack, lib)
+    return res

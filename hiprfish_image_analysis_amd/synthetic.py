@@ -1,0 +1,125 @@
+"""Synthetic HiPR-FISH tiles for tests and bench.py.
+
+The reference ships no images or classifier pickles, so every measurement uses synthetic
+(H, W, C) stacks of the shape the reference pipelines consume:
+
+* a barcode reference library: nbit fluorophores with Gaussian emission bands, each excited
+  by its own laser and weakly by the next one (the structure of the excitation matrix in
+  train_reference.py:1901-1904), summed over the barcode's set bits, max-normalised;
+* rod-shaped elliptical cells (minor axis 18-30 px, major 40-80 px), each carrying a random
+  barcode; pixel spectrum = a * dome * ref_r / mean(ref_r) * 0.3 + N(0, 0.02), a ~ U(0.5, 1),
+  clipped at 0 -- the cell's total brightness does not depend on how many bits its barcode
+  has, and the dome (1 at the centre, 0.6 at the rim) gives touching rods the intensity
+  valley the reference's watershed on -log(sum) separates them by;
+* background 0.01 + N(0, 0.005) so no line-profile window is flat.
+
+Geometry comes from numpy (seeded); the stack is rendered on the device with torch.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ECOLI_BOUNDS = (0, 32, 55, 75, 89, 95)        # 405/488/514/561/633 nm (train_reference.py:1401)
+MULTI_BOUNDS = (0, 23, 43, 57, 63)            # 488/514/561/633 nm (train_reference.py:1488)
+
+
+def reference_library(nbit: int = 10, bounds=ECOLI_BOUNDS, sigma: float = 0.12) -> np.ndarray:
+    """-> (2**nbit - 1, C) float32; row r is barcode r + 1 (binary code format(r+1, '0{nbit}b'))."""
+    bounds = list(bounds)
+    nl = len(bounds) - 1
+    C = bounds[-1]
+    # emission of fluorophore f in each channel, per laser segment
+    u = np.zeros(C)
+    seg = np.zeros(C, int)
+    for l in range(nl):
+        n = bounds[l + 1] - bounds[l]
+        u[bounds[l]:bounds[l + 1]] = (np.arange(n) + 0.5) / n
+        seg[bounds[l]:bounds[l + 1]] = l
+    peaks = (np.arange(nbit) + 0.5) / nbit
+    primary = (np.arange(nbit) * nl) // nbit
+    exc = np.zeros((nl, nbit))
+    exc[primary, np.arange(nbit)] = 1.0
+    nxt = np.minimum(primary + 1, nl - 1)
+    exc[nxt, np.arange(nbit)] = np.maximum(exc[nxt, np.arange(nbit)], 0.3)
+    emis = np.exp(-((u[None, :] - peaks[:, None]) ** 2) / (2 * sigma ** 2)) * exc.T[:, seg]
+    R = 2 ** nbit - 1
+    codes = ((np.arange(1, R + 1)[:, None] >> np.arange(nbit - 1, -1, -1)[None, :]) & 1).astype(np.float64)
+    spec = codes @ emis
+    spec /= spec.max(axis=1, keepdims=True)
+    return spec.astype(np.float32)
+
+
+def cell_layout(H: int, W: int, ncells: int, R: int, seed: int = 20190101):
+    """Random rod-shaped cells: arrays (cy, cx, a_major, b_minor, theta, barcode_index)."""
+    rng = np.random.default_rng(seed)
+    cy = rng.uniform(0, H, ncells)
+    cx = rng.uniform(0, W, ncells)
+    maj = rng.uniform(40, 80, ncells) / 2
+    mnr = rng.uniform(18, 30, ncells) / 2
+    th = rng.uniform(0, np.pi, ncells)
+    bc = rng.integers(0, R, ncells)
+    amp = rng.uniform(0.5, 1.0, ncells)
+    return cy, cx, maj, mnr, th, bc, amp
+
+
+def default_ncells(H: int, W: int) -> int:
+    return max(1, int(round(1500 * H * W / (2048 * 2048))))
+
+
+def render_truth(H: int, W: int, layout, with_profile: bool = False):
+    """Ground-truth cell index map (int32, 0 = background, i+1 = cell i; later cells on top),
+    optionally with the per-pixel dome intensity profile (float32)."""
+    cy, cx, maj, mnr, th, _, _ = layout
+    lab = np.zeros((H, W), np.int32)
+    prof = np.zeros((H, W), np.float32)
+    for i in range(len(cy)):
+        r = int(np.ceil(maj[i])) + 1
+        r0, r1 = max(0, int(cy[i]) - r), min(H, int(cy[i]) + r + 1)
+        c0, c1 = max(0, int(cx[i]) - r), min(W, int(cx[i]) + r + 1)
+        if r0 >= r1 or c0 >= c1:
+            continue
+        yy, xx = np.mgrid[r0:r1, c0:c1]
+        dy, dx = yy - cy[i], xx - cx[i]
+        ct, st = np.cos(th[i]), np.sin(th[i])
+        u = dx * ct + dy * st
+        v = -dx * st + dy * ct
+        rr = (u / maj[i]) ** 2 + (v / mnr[i]) ** 2
+        inside = rr <= 1.0
+        lab[r0:r1, c0:c1][inside] = i + 1
+        prof[r0:r1, c0:c1][inside] = (1.0 - 0.4 * rr[inside]).astype(np.float32)
+    return (lab, prof) if with_profile else lab
+
+
+def render_stack(truth, layout, ref, seed: int = 0, device="cuda", noise=0.02, bg=0.01, bg_noise=0.005,
+                 profile=None, level=0.3):
+    """(H, W, C) float32 device stack: cell pixels a*dome*ref_r/mean(ref_r)*level + N(0, noise)
+    clipped at 0, background bg + N(0, bg_noise) (clipped at 0)."""
+    import torch
+    _, _, _, _, _, bc, amp = layout
+    H, W = truth.shape
+    C = ref.shape[1]
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    t = torch.from_numpy(truth).to(device)
+    refn = ref / ref.mean(axis=1, keepdims=True) * level
+    refs = torch.from_numpy(refn.astype(np.float32)).to(device)
+    cell_spec = torch.cat([torch.zeros(1, C, device=device),
+                           torch.from_numpy(amp.astype(np.float32)).to(device)[:, None] *
+                           refs[torch.from_numpy(bc).to(device).long()]], 0)
+    stack = cell_spec[t.long()]
+    if profile is not None:
+        stack = stack * torch.from_numpy(profile).to(device)[..., None]
+    fg = (t > 0)[..., None]
+    n = torch.randn((H, W, C), generator=g, device=device, dtype=torch.float32)
+    stack = torch.where(fg, stack + noise * n, bg + bg_noise * n)
+    return stack.clamp_(min=0.0).contiguous()
+
+
+def tile(H: int = 2048, W: int = 2048, nbit: int = 10, bounds=ECOLI_BOUNDS, seed: int = 20190101, device="cuda",
+         ncells: int | None = None):
+    """Convenience: (stack, truth, layout, ref) for one synthetic tile."""
+    ref = reference_library(nbit, bounds)
+    lay = cell_layout(H, W, ncells or default_ncells(H, W), ref.shape[0], seed)
+    truth, prof = render_truth(H, W, lay, with_profile=True)
+    stack = render_stack(truth, lay, ref, seed=seed, device=device, profile=prof)
+    return stack, truth, lay, ref

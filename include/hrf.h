@@ -81,6 +81,150 @@ HRF_API hrf_status hrf_line_profile_3d_norm(const double *pad, int64_t xp, int64
 HRF_API hrf_status hrf_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t zp, int32_t patch,
                           int32_t ntheta, int32_t nphi, double *final_, hrf_stream_t stream);
 
+
+/* ==== a1-a3: stack assembly and channel reductions (stack.hip) ======================== */
+/* ecoli measurement.py:51-70 / multispecies :88-102: per-laser (H,W,C_l) f32 stacks
+ * (src_host = HOST array of DEVICE pointers) shifted by integer (dr, dc) each
+ * (shifts_host[2*i], [2*i+1]) and concatenated into dst (H,W,sum C_l); zero outside each
+ * laser's coverage; apply_mask=1 also zeroes pixels outside the coverage intersection
+ * (ecoli :69-70). */
+HRF_API hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *channels_host,
+                                         const int32_t *shifts_host, int32_t nlaser, int64_t H, int64_t W,
+                                         int32_t apply_mask, float *dst, hrf_stream_t stream);
+/* per-pixel sum over C in numpy pairwise order (== np.sum(stack, axis=2) in f64);
+ * mode 0: sum, 1: log(sum + 1e-2) (ecoli :72), 2: log10(sum + 1) (biofilm :831);
+ * mask (nullable) zeroes the sum; negate flips the sign (watershed input). */
+HRF_API hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,
+                                   int32_t negate, double *out, hrf_stream_t stream);
+HRF_API hrf_status hrf_max_f64(const double *a, int64_t n, double *max_dev, hrf_stream_t stream);
+HRF_API hrf_status hrf_div_scalar_f64(const double *a, int64_t n, const double *divisor_dev, double *out,
+                                      hrf_stream_t stream);
+/* skimage.util.pad(img, width, mode='edge') (multispecies :109) */
+HRF_API hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32_t width, double *out,
+                                    hrf_stream_t stream);
+HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out,
+                                    hrf_stream_t stream);
+
+/* ==== a8: 1-D KMeans (kmeans.hip) ======================================================
+ * sklearn KMeans(k, random_state=0).fit_predict(x.reshape(-1,1)) restated as exact-integer
+ * Lloyd iterations from a deterministic init (see oracle_kmeans_1d).  valid (nullable)
+ * excludes entries (label -1).  labels (nullable) int32; top_mask (nullable) = label of the
+ * highest centre.  centers_host[k] / iters_host receive the result (synchronises).
+ * state_ws: hrf_kmeans_state_bytes() device bytes. */
+HRF_API int64_t hrf_kmeans_state_bytes(void);
+HRF_API hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
+                                 int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host,
+                                 void *state_ws, hrf_stream_t stream);
+
+/* ==== a9/a10/a13: components, morphology, label cleanup (label.hip) ====================
+ * img dtype: 0 = uint8 mask, 1 = int32 label image (equal values connect), 2 = uint8 mask
+ * inverted.  conn 1 = 4-, 2 = 8-connectivity (skimage label default for 2-D).
+ * parent[p] = minimum raster index of p's component, -1 for background. */
+HRF_API hrf_status hrf_cc_roots(const void *img, int32_t dtype, int64_t H, int64_t W, int32_t conn, int32_t *parent,
+                                hrf_stream_t stream);
+/* raster-first numbering 1..N (skimage.measure.label / ndi.label order); blk_ws holds
+ * ceil(n/1024)+1 int32; *nlab_dev (device) = N. */
+HRF_API hrf_status hrf_cc_number(const int32_t *parent, int64_t n, int32_t *labels, int32_t *blk_ws,
+                                 int32_t *nlab_dev, hrf_stream_t stream);
+/* skimage.measure.label(img, connectivity=conn) (ecoli :97-98,109,111-112; multispecies :140) */
+HRF_API hrf_status hrf_label(const void *img, int32_t dtype, int64_t H, int64_t W, int32_t conn, int32_t *labels,
+                             int32_t *parent_ws, int32_t *blk_ws, int32_t *nlab_dev, hrf_stream_t stream);
+/* size[root] = component size (size zeroed here; n int32) */
+HRF_API hrf_status hrf_cc_sizes(const int32_t *parent, int64_t n, int32_t *size, hrf_stream_t stream);
+/* skimage.morphology.remove_small_objects on a bool image (ecoli :96,108; multispecies :137) */
+HRF_API hrf_status hrf_remove_small_objects_mask(const uint8_t *mask, int64_t H, int64_t W, int64_t min_size,
+                                                 int32_t conn, uint8_t *out, int32_t *parent_ws, int32_t *size_ws,
+                                                 hrf_stream_t stream);
+/* skimage.morphology.remove_small_holes(ar, area_threshold) (ecoli :95) */
+HRF_API hrf_status hrf_remove_small_holes(const uint8_t *mask, int64_t H, int64_t W, int64_t area_threshold,
+                                          int32_t conn, uint8_t *out, int32_t *parent_ws, int32_t *size_ws,
+                                          hrf_stream_t stream);
+/* erosion-seed freeze step (ecoli :102-106): components (conn) of mask with size < thr are
+ * OR-ed into small_or, the rest written to large (mask and large may not alias). */
+HRF_API hrf_status hrf_split_by_size(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int64_t thr,
+                                     uint8_t *small_or, uint8_t *large, int32_t *parent_ws, int32_t *size_ws,
+                                     hrf_stream_t stream);
+/* scipy.ndimage.binary_fill_holes (multispecies :138-139); flag_ws n int32 */
+HRF_API hrf_status hrf_fill_holes(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, int32_t *parent_ws,
+                                  int32_t *flag_ws, hrf_stream_t stream);
+/* skimage.segmentation.clear_border(labels) (ecoli :115, multispecies :156) */
+HRF_API hrf_status hrf_clear_border(const int32_t *labels, int64_t H, int64_t W, int32_t *out, int32_t *parent_ws,
+                                    int32_t *flag_ws, hrf_stream_t stream);
+/* remove_small_objects on an int label image (ecoli :114, multispecies :155); cnt_ws maxlab+1 */
+HRF_API hrf_status hrf_remove_small_objects_labels(const int32_t *labels, int64_t n, int32_t maxlab,
+                                                   int64_t min_size, int32_t *out, int32_t *cnt_ws,
+                                                   hrf_stream_t stream);
+/* skimage.segmentation.relabel_sequential(labels)[0] (multispecies :157); map_ws maxlab+1 */
+HRF_API hrf_status hrf_relabel_sequential(const int32_t *labels, int64_t n, int32_t maxlab, int32_t *out,
+                                          int32_t *map_ws, int32_t *nlab_dev, hrf_stream_t stream);
+/* skimage.morphology.binary_erosion / binary_dilation, cross footprint (ecoli :107,:122) */
+HRF_API hrf_status hrf_binary_erosion(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,
+                                      hrf_stream_t stream);
+HRF_API hrf_status hrf_binary_dilation(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, hrf_stream_t stream);
+HRF_API hrf_status hrf_count_nonzero_u8(const uint8_t *mask, int64_t n, int64_t *count_dev, hrf_stream_t stream);
+HRF_API hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hrf_stream_t stream);
+
+/* ==== a12: watershed (watershed.hip) =====================================================
+ * skimage.morphology.watershed(+/-image, markers, mask) (ecoli :113, multispecies :154),
+ * 4-connectivity.  state_ws: 32*H*W bytes; flag_ws: >= 4 int32.  Synchronises per 4 passes. */
+HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
+                                 int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
+                                 int32_t max_passes, int32_t *passes_host, hrf_stream_t stream);
+
+/* ==== a14-a16, a20, a21, a23: per-label reductions (stats.hip) ==========================
+ * regionprops(seg, intensity_image=stack[:,:,k]).mean_intensity for all k in ONE pass
+ * (ecoli :151-155, multispecies :167-171): sums[(maxlab+1)*C] f64, counts[maxlab+1];
+ * cal (nullable, (H*W) f32) divides channels [cal_c0, cal_c1) (flat field, ecoli :147-150). */
+HRF_API hrf_status hrf_label_sums(const float *stack, const int32_t *labels, int64_t npix, int32_t C, int32_t maxlab,
+                                  const float *cal, int32_t cal_c0, int32_t cal_c1, double *sums, int64_t *counts,
+                                  hrf_stream_t stream);
+/* rows = present labels ascending (regionprops order); avgint = sums/counts,
+ * avgint_norm = avgint / rowmax (ecoli :157, classify_spectra.py:27). */
+HRF_API hrf_status hrf_cell_table(const double *sums, const int64_t *counts, int32_t maxlab, int32_t C,
+                                  int32_t max_rows, int32_t *row_of_label, int32_t *label_of_row, double *avgint,
+                                  double *avgint_norm, int32_t *nrows_dev, hrf_stream_t stream);
+/* exact raw moments mom[(maxlab+1)*6] = {area, sum r, sum c, sum r^2, sum c^2, sum rc} */
+HRF_API hrf_status hrf_region_moments(const int32_t *labels, int64_t H, int64_t W, int32_t maxlab, int64_t *mom,
+                                      hrf_stream_t stream);
+/* regionprops area, centroid, major/minor axis, eccentricity, orientation
+ * (classify_spectra.py:38-46): props[(maxlab+1)*8] */
+HRF_API hrf_status hrf_region_props(const int64_t *mom, int32_t maxlab, double *props, hrf_stream_t stream);
+/* E. coli per-cell filter (ecoli measurement.py:116-126): cells with minor axis in
+ * [minor_lo, minor_hi] keep their 2x-cross-eroded interior, others vanish. */
+HRF_API hrf_status hrf_shape_filter(const int32_t *labels, int64_t H, int64_t W, const double *props, int32_t maxlab,
+                                    double minor_lo, double minor_hi, int32_t *out, hrf_stream_t stream);
+/* per-barcode counts (collect_measurement_results.py:92-98) */
+HRF_API hrf_status hrf_barcode_counts(const int32_t *bc, int64_t n, int32_t R, int64_t *counts, hrf_stream_t stream);
+/* identification image (image_classification.py:65-71): label L in 1..ncell -> code[L-1] */
+HRF_API hrf_status hrf_paint_ids(const int32_t *labels, int64_t n, const int32_t *code, int32_t ncell, int32_t *out,
+                                 hrf_stream_t stream);
+
+/* ==== a19: segmented-cosine classification (classify.hip) ===============================
+ * train_reference.py:223-386 (channel_cosine_intensity), :993-1072 (_7b_v2).
+ * bounds_host: nseg+1 channel offsets on the HOST (e.g. 0,32,55,75,89,95). */
+HRF_API hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t *kp_host, int32_t *rpad_host);
+/* refx (rpad x kp f32): segment-normalised references + zero-segment indicators */
+HRF_API hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host,
+                                             int32_t nseg, float *refx, hrf_stream_t stream);
+/* per pixel (north_star mode): best_idx[p] = argmin_r ungated distance, best_dist[p] */
+HRF_API hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const float *refx, int32_t R,
+                                       const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                       float *best_dist, hrf_stream_t stream);
+/* per cell (f64): variant 0 ungated, 1 channel_cosine_intensity, 2 _7b_v2; fx (N x nseg),
+ * fr (R x nseg) presence flags (needed for variants 1, 2) */
+HRF_API hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int32_t R, int32_t C,
+                                      const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
+                                      const double *fr, int32_t *arg, double *dmin, hrf_stream_t stream);
+
+/* ==== a22: label adjacency (rag.hip) ====================================================
+ * skimage.future.graph.rag_boundary edge set (biofilm :1277-1278): edge[(maxlab+1)^2] u8,
+ * edge[a*(maxlab+1)+b] = 1 for a < b. */
+HRF_API hrf_status hrf_rag_edges(const int32_t *labels, int64_t H, int64_t W, int32_t maxlab, uint8_t *edge,
+                                 hrf_stream_t stream);
+/* barcode x barcode adjacency counts (biofilm :1283-1292): adj[R*R] int64 */
+HRF_API hrf_status hrf_barcode_adjacency(const uint8_t *edge, int32_t maxlab, const int32_t *bc_of_label, int32_t R,
+                                         int64_t *adj, hrf_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -423,7 +423,9 @@ EXPORT int32_t oracle_relabel_sequential(const int32_t *l, int64_t n, int32_t *o
     int32_t mx = 0;
     for (int64_t i = 0; i < n; ++i) mx = l[i] > mx ? l[i] : mx;
     int32_t *map = (int32_t *)calloc((size_t)mx + 1, sizeof(int32_t));
-    for (int64_t i = 0; i < n; ++i) map[l[i]] = 1;
+    for (int64_t i = 0; i < n; ++i)
+        if (l[i] > 0) map[l[i]] = 1;
+    map[0] = 0;
     int32_t k = 0;
     for (int32_t v = 1; v <= mx; ++v)
         if (map[v]) map[v] = ++k;
@@ -794,4 +796,28 @@ EXPORT void oracle_paint_ids(const int32_t *lab, int64_t n, const int32_t *code,
         int32_t l = lab[i];
         out[i] = (l >= 1 && l <= ncell) ? code[l - 1] : 0;
     }
+}
+
+/* ecoli measurement.py:116-126 (per-cell shape filter + 2x binary_erosion of the cell) */
+EXPORT void oracle_shape_filter(const int32_t *lab, int64_t H, int64_t W, const double *stats, int32_t nlab,
+                                double lo, double hi, int32_t *out) {
+    for (int64_t r = 0; r < H; ++r)
+        for (int64_t c = 0; c < W; ++c) {
+            int32_t l = lab[r * W + c], o = 0;
+            if (l > 0 && l <= nlab && stats[(int64_t)l * 8 + 7] != 0.0) {
+                double mn = stats[(int64_t)l * 8 + 4];
+                if (!(mn < lo || mn > hi)) {
+                    int in = 1;
+                    for (int dr = -2; dr <= 2; ++dr)
+                        for (int dc = -2; dc <= 2; ++dc) {
+                            if (abs(dr) + abs(dc) > 2) continue;
+                            int64_t rr = r + dr, cc = c + dc;
+                            if (rr < 0 || rr >= H || cc < 0 || cc >= W) continue;
+                            in = in && lab[rr * W + cc] == l;
+                        }
+                    o = in ? l : 0;
+                }
+            }
+            out[r * W + c] = o;
+        }
 }

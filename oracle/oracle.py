@@ -291,3 +291,12 @@ def paint_ids(lab, code):
     out = np.zeros(l.shape, np.int32)
     lib().oracle_paint_ids(_p(l), I64(l.size), _p(c), ctypes.c_int32(c.size), _p(out))
     return out
+
+
+def shape_filter(lab, stats, lo=15.0, hi=35.0):
+    l = _c(lab, np.int32)
+    st = _c(stats, np.float64)
+    out = np.zeros(l.shape, np.int32)
+    lib().oracle_shape_filter(_p(l), I64(l.shape[0]), I64(l.shape[1]), _p(st), ctypes.c_int32(st.shape[0] - 1),
+                              ctypes.c_double(lo), ctypes.c_double(hi), _p(out))
+    return out

@@ -1,0 +1,294 @@
+"""Stage-by-stage parity of the libhrf.so kernels against the CPU restatement (oracle/).
+Integer outputs bit-exact; float outputs bit-exact where the restatement fixes the order,
+else within the stated tolerance."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from hiprfish_image_analysis_amd import kernels
+    return kernels
+
+
+@pytest.fixture(scope="module")
+def S():
+    from hiprfish_image_analysis_amd import synthetic
+    return synthetic
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def blobs(shape, p=0.5, seed=0, smooth=2):
+    """random binary blobs with structures spanning many 32x32 tiles"""
+    rng = np.random.default_rng(seed)
+    x = rng.random(shape)
+    for _ in range(smooth):
+        x = (x + np.roll(x, 1, 0) + np.roll(x, -1, 0) + np.roll(x, 1, 1) + np.roll(x, -1, 1)) / 5
+    return x > np.quantile(x, 1 - p)
+
+
+SHAPES = [(1, 1), (1, 70), (33, 31), (100, 77), (257, 300), (640, 512)]
+
+
+# ---- a10 connected components --------------------------------------------------------
+def test_label_golden(K, golden):
+    g = golden("label")
+    l8, n8 = K.label(dev(g["mask"]), conn=2)
+    l4, n4 = K.label(dev(g["mask"]), conn=1)
+    assert np.array_equal(host(l8), g["l8"]) and n8 == g["l8"].max()
+    assert np.array_equal(host(l4), g["l4"]) and n4 == g["l4"].max()
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("conn", [1, 2])
+def test_label_vs_oracle(K, orc, shape, conn):
+    for p in (0.3, 0.6):
+        m = blobs(shape, p, seed=shape[0] + shape[1])
+        ref, n = orc.label(m.astype(np.int32), conn)
+        got, gn = K.label(dev(m), conn=conn)
+        assert gn == n
+        assert np.array_equal(host(got), ref)
+
+
+def test_label_snake_spanning_tiles(K, orc):
+    H = W = 512
+    m = np.zeros((H, W), bool)
+    for r in range(0, H, 4):
+        m[r, :] = True
+        m[r:r + 4, 0 if (r // 4) % 2 else W - 1] = True
+    got, n = K.label(dev(m), conn=1)
+    ref, rn = orc.label(m.astype(np.int32), 1)
+    assert n == rn == 1 and np.array_equal(host(got), ref)
+
+
+def test_label_equal_value_components(K, orc, S):
+    lay = S.cell_layout(300, 280, 60, 7, seed=3)
+    truth = S.render_truth(300, 280, lay)
+    ref, n = orc.label(truth, 2)
+    got, gn = K.label(dev(truth), conn=2)
+    assert gn == n and np.array_equal(host(got), ref)
+
+
+def test_label_empty(K):
+    got, n = K.label(dev(np.zeros((50, 60), bool)))
+    assert n == 0 and not host(got).any()
+
+
+# ---- a9/a13 morphology and cleanup ------------------------------------------------------
+@pytest.mark.parametrize("shape", SHAPES[2:])
+def test_morphology(K, orc, shape):
+    m = blobs(shape, 0.45, seed=7)
+    assert np.array_equal(host(K.binary_erosion(dev(m), 1)).astype(bool), orc.erode(m, 1))
+    assert np.array_equal(host(K.binary_erosion(dev(m), 0)).astype(bool), orc.erode(m, 0))
+    assert np.array_equal(host(K.binary_dilation(dev(m))).astype(bool), orc.dilate(m))
+    assert np.array_equal(host(K.binary_opening(dev(m))).astype(bool), orc.opening(m))
+    for ms, conn in [(10, 1), (50, 2), (64, 1)]:
+        assert np.array_equal(host(K.remove_small_objects(dev(m), ms, conn)).astype(bool),
+                              orc.remove_small_objects_mask(m, ms, conn))
+    assert np.array_equal(host(K.remove_small_holes(dev(m), 64)).astype(bool), orc.remove_small_holes(m, 64))
+    assert np.array_equal(host(K.fill_holes(dev(m))).astype(bool), orc.fill_holes(m))
+    assert K.count_nonzero(dev(m)) == int(m.sum())
+
+
+def test_label_cleanup(K, orc, S):
+    H, W = 400, 360
+    lay = S.cell_layout(H, W, 90, 7, seed=11)
+    truth = S.render_truth(H, W, lay)
+    truth[truth % 7 == 0] *= 3  # non-sequential labels
+    mx = int(truth.max())
+    assert K.max_i32(dev(truth)) == mx
+    assert np.array_equal(host(K.remove_small_objects(dev(truth), 600)), orc.remove_small_objects_labels(truth, 600))
+    assert np.array_equal(host(K.clear_border(dev(truth))), orc.clear_border(truth))
+    got, n = K.relabel_sequential(dev(truth))
+    ref, rn = orc.relabel_sequential(truth)
+    assert n == rn and np.array_equal(host(got), ref)
+
+
+# ---- a8 KMeans ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["bimodal", "logsum", "trimodal"])
+def test_kmeans_golden_and_oracle(K, orc, golden, name):
+    g = golden("kmeans")
+    x = g["x_" + name]
+    k = int(g["k_" + name])
+    lab, top, cen, it = K.kmeans_1d(dev(x), k)
+    rl, rc, rit = orc.kmeans_1d(x, k)
+    assert it == rit
+    assert cen == rc.tolist()  # bitwise equal centres
+    assert np.array_equal(host(lab), rl)
+    assert np.array_equal(host(top).astype(bool), rl == int(np.argmax(rc)))
+
+
+def test_kmeans_valid_mask_and_large(K, orc):
+    rng = np.random.default_rng(4)
+    x = np.concatenate([rng.normal(0.2, 0.05, 300000), rng.normal(0.9, 0.1, 200000)])
+    valid = rng.random(x.size) > 0.2
+    for k in (2, 3):
+        lab, top, cen, it = K.kmeans_1d(dev(x), k, valid=dev(valid))
+        rl, rc, rit = orc.kmeans_1d(x, k, valid)
+        assert it == rit and cen == rc.tolist() and np.array_equal(host(lab), rl)
+
+
+# ---- a12 watershed ----------------------------------------------------------------------
+@pytest.mark.parametrize("shape", [(64, 64), (130, 97), (300, 330)])
+def test_watershed_vs_heap_flood(K, orc, shape):
+    rng = np.random.default_rng(shape[0])
+    H, W = shape
+    img = rng.random(shape)
+    for _ in range(3):  # smooth so basins span tiles
+        img = (img + np.roll(img, 1, 0) + np.roll(img, 1, 1) + np.roll(img, -1, 0) + np.roll(img, -1, 1)) / 5
+    img += rng.random(shape) * 1e-9  # distinct values
+    mask = blobs(shape, 0.8, seed=2)
+    markers = np.zeros(shape, np.int32)
+    nm = max(2, H * W // 400)
+    idx = rng.choice(H * W, nm, replace=False)
+    markers.flat[idx] = np.arange(1, nm + 1)
+    ref = orc.watershed(-img, markers, mask)
+    got = K.watershed(dev(img), dev(markers), dev(mask), negate=True)
+    assert np.array_equal(host(got), ref)
+    got2 = K.watershed(dev(-img), dev(markers), None)
+    assert np.array_equal(host(got2), orc.watershed(-img, markers, None))
+
+
+# ---- a15/a16/a20 per-label reductions ---------------------------------------------------
+def test_label_sums_and_table(K, orc, S):
+    H, W, C = 300, 256, 95
+    stack, truth, lay, ref = S.tile(H, W, seed=5, ncells=40)
+    truth[truth % 5 == 0] = 0
+    st = host(stack)
+    mx = int(truth.max())
+    sums, counts = K.label_sums(stack, dev(truth), mx)
+    rs, rcnt = orc.label_sums(st, truth, mx)
+    assert np.array_equal(host(counts), rcnt)
+    np.testing.assert_allclose(host(sums), rs, rtol=1e-12, atol=1e-12)
+    cal = (0.5 + np.random.default_rng(1).random((H, W))).astype(np.float32)
+    sums2, _ = K.label_sums(stack, dev(truth), mx, cal=dev(cal), cal_range=(0, 32))
+    st2 = st.astype(np.float64).copy()
+    st2[..., :32] /= cal[..., None].astype(np.float64)
+    mask = truth > 0
+    ref2 = np.zeros_like(rs)
+    np.add.at(ref2, truth[mask], st2[mask])
+    np.testing.assert_allclose(host(sums2), ref2, rtol=1e-12, atol=1e-12)
+    rol, lor, avg, avgn = K.cell_table(sums, counts, mx)
+    present = np.nonzero(rcnt)[0]
+    present = present[present > 0]
+    assert np.array_equal(host(lor), present)
+    ravg = rs[present] / rcnt[present][:, None]
+    np.testing.assert_allclose(host(avg), ravg, rtol=1e-12)
+    np.testing.assert_allclose(host(avgn), ravg / ravg.max(axis=1)[:, None], rtol=1e-12)
+
+
+def test_region_props(K, orc, S):
+    lay = S.cell_layout(512, 512, 120, 7, seed=9)
+    truth = S.render_truth(512, 512, lay)
+    mx = int(truth.max())
+    got = host(K.region_props(dev(truth), mx))
+    ref = orc.region_stats(truth, mx)
+    np.testing.assert_array_equal(got[:, [0, 7]], ref[:, [0, 7]])
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_counts_paint(K, orc):
+    rng = np.random.default_rng(2)
+    bc = rng.integers(-1, 1023, 5000).astype(np.int32)
+    assert np.array_equal(host(K.barcode_counts(dev(bc), 1023)), orc.barcode_counts(bc, 1023))
+    lab = rng.integers(0, 40, (100, 90)).astype(np.int32)
+    code = rng.integers(1, 1024, 30).astype(np.int32)
+    assert np.array_equal(host(K.paint_ids(dev(lab), dev(code))), orc.paint_ids(lab, code))
+
+
+# ---- a19 classification ---------------------------------------------------------------
+@pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63)), (5, (0, 32))])
+def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds):
+    ref = S.reference_library(nbit, bounds) if len(bounds) > 2 else \
+        np.abs(np.random.default_rng(0).normal(size=(31, 32))).astype(np.float32)
+    R, C = ref.shape
+    stack, truth, lay, _ = S.tile(96, 80, nbit=max(nbit, 2), bounds=bounds, seed=3, ncells=8) if len(bounds) > 2 \
+        else (None, None, None, None)
+    if stack is None:
+        stack = torch.rand((96, 80, C), device="cuda")
+    st = host(stack).reshape(-1, C)
+    st[:7] = 0.0                          # all-zero pixels
+    st[7:20, bounds[0]:bounds[1]] = 0.0   # a zero segment
+    refx = K.classify_prepare(dev(ref), bounds)
+    idx, dist = K.classify_pixels(dev(st), refx, R, bounds)
+    ra, rd = orc.classify(st.astype(np.float64), ref.astype(np.float64), bounds, 0)
+    gi, gd = host(idx), host(dist)
+    np.testing.assert_allclose(gd, rd, rtol=1e-5, atol=1e-5)
+    # argmin must agree wherever the restatement's best is separated from the runner-up
+    x64 = st.astype(np.float64)
+    d_all = np.array([[orc.segcos(x64[i], ref[r].astype(np.float64), bounds, 0) for r in range(R)]
+                      for i in range(0, len(st), 37)])
+    srt = np.sort(d_all, axis=1)
+    sep = (srt[:, 1] - srt[:, 0]) > 2e-5
+    sub = np.arange(0, len(st), 37)
+    assert np.array_equal(gi[sub][sep], ra[sub][sep])
+    assert (gi == ra).mean() > 0.99
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_classify_cells_bitexact(K, orc, S, variant):
+    bounds = (0, 32, 55, 75, 89, 95)
+    ref = S.reference_library(10, bounds).astype(np.float64)
+    rng = np.random.default_rng(variant)
+    x = ref[rng.integers(0, len(ref), 300)] * rng.uniform(0.5, 1, (300, 1)) + rng.normal(0, 0.05, (300, 95))
+    x = np.clip(x, 0, None)
+    x /= x.max(axis=1, keepdims=True)
+    fr = np.stack([(ref[:, bounds[k]:bounds[k + 1]].max(axis=1) > 0.1) for k in range(5)], 1).astype(np.float64)
+    fx = np.stack([(x[:, bounds[k]:bounds[k + 1]].max(axis=1) > 0.1) for k in range(5)], 1).astype(np.float64)
+    a, d = K.classify_cells(dev(x), dev(ref), bounds, variant, dev(fx) if variant else None,
+                            dev(fr) if variant else None)
+    ra, rd = orc.classify(x, ref, bounds, variant, fx if variant else None, fr if variant else None)
+    assert np.array_equal(host(a), ra)
+    assert np.array_equal(host(d), rd)
+
+
+# ---- a22 adjacency -----------------------------------------------------------------------
+def test_rag_and_barcode_adjacency(K, orc, S):
+    lay = S.cell_layout(300, 300, 80, 7, seed=4)
+    truth = S.render_truth(300, 300, lay)
+    mx = int(truth.max())
+    e = host(K.rag_edges(dev(truth), mx))
+    re_ = orc.rag_edges(truth, mx)
+    assert np.array_equal(e, re_)
+    bc = np.random.default_rng(0).integers(0, 127, mx + 1).astype(np.int32)
+    adj = host(K.barcode_adjacency(dev(e), dev(bc), 127))
+    assert np.array_equal(adj, orc.barcode_adjacency(re_, bc, 127))
+
+
+# ---- a1-a3 stack assembly ---------------------------------------------------------------
+def test_register_assemble_and_channel_sum(K):
+    rng = np.random.default_rng(8)
+    H = W = 70
+    chans = [32, 23, 20, 14, 6]
+    shifts = [(0, 0), (3, -2), (-5, 4), (0, 7), (-1, -1)]
+    lasers = [rng.random((H, W, c)).astype(np.float32) for c in chans]
+    out = host(K.register_assemble([dev(l) for l in lasers], shifts, apply_mask=True))
+    # restatement of ecoli measurement.py:51-70
+    reg, masks = [], []
+    for img, (sr, sc) in zip(lasers, shifts):
+        r = np.zeros_like(img)
+        m = np.zeros((H, W), bool)
+        r[max(0, sr):H + min(0, sr), max(0, sc):W + min(0, sc)] = \
+            img[-min(0, sr):H - max(0, sr), -min(0, sc):W - max(0, sc)]
+        m[max(0, sr):H + min(0, sr), max(0, sc):W + min(0, sc)] = True
+        reg.append(r)
+        masks.append(m)
+    refst = np.dstack(reg) * np.prod(masks, axis=0)[:, :, None]
+    assert np.array_equal(out, refst)
+    s0 = host(K.channel_sum(dev(out), mode=0))
+    assert np.array_equal(s0, np.sum(refst.astype(np.float64), axis=2))
+    s1 = host(K.channel_sum(dev(out), mode=1))
+    np.testing.assert_allclose(s1, np.log(np.sum(refst.astype(np.float64), axis=2) + 1e-2), rtol=4e-16, atol=0)
+    m = rng.random((H, W)) > 0.5
+    s2 = host(K.channel_sum(dev(out), mask=dev(m), mode=0, negate=True))
+    assert np.array_equal(s2, -np.sum(refst.astype(np.float64) * m[:, :, None], axis=2))
