@@ -112,7 +112,7 @@ def main():
             if timed:
                 ev.append((e0, e1))
         if world > 1:
-            dist.all_reduce(res.counts, op=dist.ReduceOp.SUM)
+            P.allreduce_counts(res.counts)
         return res
 
     for i in range(args.warmup):

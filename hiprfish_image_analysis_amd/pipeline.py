@@ -150,3 +150,20 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
     if per_pixel:
         res.pixel_idx, res.pixel_dist = classify_pixels(stack, lib)
     return res
+
+
+# --------------------------------------------------------------------------------------------
+# Multi-GPU: tiles shard round-robin; the only exchange is the per-barcode count vector
+# --------------------------------------------------------------------------------------------
+def shard(n_tiles: int, rank: int, world: int):
+    """tile indices owned by `rank` (tile_idx % world)"""
+    return list(range(rank, n_tiles, world))
+
+
+def allreduce_counts(counts: torch.Tensor, group=None) -> torch.Tensor:
+    """global per-barcode counts = SUM over ranks (collect_measurement_results.py:92-98 across
+    FOVs).  RCCL on device tensors; any torch.distributed backend works."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    return counts
