@@ -27,7 +27,8 @@ sys.path.insert(0, REPO)
 H = W = 2048
 C = 95
 NBIT = 10
-F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (mode 0)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (mode 1, default)
 
 
 def _cpu_baseline(ref, bounds):
@@ -148,9 +149,15 @@ def main():
                    "parallelism": "tile-sharded x%d" % world},
     }
     if per_pixel and ev:
+        from hiprfish_image_analysis_amd import kernels as K
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
         ach = flops / (ms * 1e-3) / 1e12
+        mode = K.CLASSIFY_MODE
+        kp, rpad = K.classify_geometry(C, len(bounds) - 1, lib.R, mode)
+        peak = F16_MFMA_PEAK_TFLOPS if mode == 1 else F32_MFMA_PEAK_TFLOPS
+        # MFMA flops the hardware executes: padded K x padded R, x3 products in split-fp16 mode
+        executed = 2.0 * H * W * rpad * kp * (3 if mode == 1 else 1) / (ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "classify_pixels_pmc.json")
         if os.path.exists(pmc):
@@ -158,10 +165,12 @@ def main():
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        out["roofline"] = {"bound": "mfma", "kernel": "classify_pixels_kernel<50>", "achieved": round(ach, 2),
-                           "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                           "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                           "kernel_ms": round(ms, 4)}
+        out["roofline"] = {"bound": "mfma",
+                           "kernel": "classify_pixels_f16_kernel<7>" if mode == 1 else "classify_pixels_kernel<50>",
+                           "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(ach / peak, 4), "traffic": traffic, "kernel_ms": round(ms, 4),
+                           "mfma_dtype": "f16 (split hi/lo, 3 MFMA per f32 product)" if mode == 1 else "f32",
+                           "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline(ref, bounds)
     if rank == 0:

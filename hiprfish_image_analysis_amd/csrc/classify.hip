@@ -33,7 +33,7 @@ struct Bounds {
   int32_t nseg;
 };
 
-constexpr int RCH = 128;  // references per LDS chunk
+constexpr int RCH = 64;  // references per LDS chunk (prefetched into registers)
 
 // refx[r][0..C) = ref / |ref_seg| (0 if the norm is 0), refx[r][C+s] = (norm_s == 0),
 // zero padding to KP columns and to Rpad rows.
@@ -121,14 +121,31 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
   int bidx[2] = {0, 0};
 
   // ---- sweep the reference library in LDS chunks ----
+  // The next chunk is prefetched into registers while the current one feeds the MFMAs, so
+  // the L2 latency of the table hides behind ~25K MFMA cycles per chunk.
+  constexpr int PF = (RCH * (KP / 2) + 255) / 256;  // float2 per thread per chunk
+  float2 pf[PF];
+  auto prefetch = [&](int r0) {
+    const float2 *gsrc = reinterpret_cast<const float2 *>(refx + (int64_t)r0 * KP);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * 256;
+      if (e < RCH * (KP / 2)) pf[q] = gsrc[e];
+    }
+  };
+  prefetch(0);
   for (int r0 = 0; r0 < Rpad; r0 += RCH) {
     __syncthreads();
-    const float2 *gsrc = reinterpret_cast<const float2 *>(refx + (int64_t)r0 * KP);
-    for (int e = tid; e < RCH * (KP / 2); e += 256) {
-      const int rr = e / (KP / 2), cc = e - rr * (KP / 2);
-      reinterpret_cast<float2 *>(lds + rr * STRIDE)[cc] = gsrc[e];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * 256;
+      if (e < RCH * (KP / 2)) {
+        const int rr = e / (KP / 2), cc = e - rr * (KP / 2);
+        reinterpret_cast<float2 *>(lds + rr * STRIDE)[cc] = pf[q];
+      }
     }
     __syncthreads();
+    if (r0 + RCH < Rpad) prefetch(r0 + RCH);
 #pragma unroll 1
     for (int rb = 0; rb < RCH; rb += 32) {
       f32x16 acc0 = {0}, acc1 = {0};
@@ -158,6 +175,193 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
     }
   }
   // merge the two lane halves holding the same pixel column
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const float ob = __shfl_xor(best[g], 32, 64);
+    const int oi = __shfl_xor(bidx[g], 32, 64);
+    if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
+      best[g] = ob;
+      bidx[g] = oi;
+    }
+    const int64_t p = pbase + g * 32 + j;
+    if (h == 0 && p < P) {
+      best_idx[p] = bidx[g];
+      best_dist[p] = ((float)bd.nseg - best[g]) / (float)bd.nseg;
+    }
+  }
+}
+
+// ---- mode 1: split-fp16 MFMA ----------------------------------------------------------------
+// Each normalised operand value v (|v| <= 1) is carried as hi = fp16(v) and lo = fp16(v - hi);
+// score = sum(hi*hi' + hi*lo' + lo*hi') in one f32 accumulator.  Per product the error is the
+// dropped lo*lo' (<= 2^-22) plus lo's fp16 rounding (<= 2^-25 absolute, subnormal spacing),
+// so a 100-term score is within ~1e-6 of the exact f32 dot product; the three products are
+// v_mfma_f32_32x32x16_f16 at 16x the f32-MFMA rate.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// refh[r] = {hi[0..KP), lo'[0..KP)} fp16, from the same normalisation as ref_prep_kernel
+__global__ void ref_prep_f16_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
+                                    int32_t Rpad, _Float16 *__restrict__ refh) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= Rpad) return;
+  _Float16 *hi = refh + r * 2 * KP;
+  _Float16 *lo = hi + KP;
+  for (int k = 0; k < KP; ++k) {
+    hi[k] = (_Float16)0.0f;
+    lo[k] = (_Float16)0.0f;
+  }
+  if (r >= R) return;
+  const float *x = ref + r * C;
+  for (int s = 0; s < bd.nseg; ++s) {
+    double nn = 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) nn += (double)x[c] * (double)x[c];
+    const double inv = nn > 0 ? 1.0 / sqrt(nn) : 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) {
+      const float v = (float)((double)x[c] * inv);
+      const _Float16 h = (_Float16)v;
+      hi[c] = h;
+      lo[c] = (_Float16)(v - (float)h);
+    }
+    hi[C + s] = (_Float16)(nn > 0 ? 0.0f : 1.0f);
+  }
+}
+
+// Stage one 32-pixel group of this wave and build its split-fp16 B operand (lane = pixel j,
+// half h holds channels 16s + 8h + q).
+template <int KS16>
+__device__ __forceinline__ void build_b_f16(const float *__restrict__ stack, int64_t P, int32_t C, const Bounds &bd,
+                                            int64_t p0, float *stg, int lane, int j, int h, h8 (&bh)[KS16],
+                                            h8 (&bl)[KS16]) {
+  const int64_t np = std::max<int64_t>(0, std::min<int64_t>(32, P - p0));
+  const int64_t nel = np * C;
+  const float *src = stack + p0 * C;
+  for (int64_t e = lane; e < 32 * C; e += 64) stg[e] = e < nel ? src[e] : 0.0f;
+  __syncthreads();
+  float inv[SMAX];
+  float zf[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    inv[s] = 0.0f;
+    zf[s] = 0.0f;
+    if (s < bd.nseg) {
+      double nn = 0.0;
+      for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) {
+        const double v = (double)stg[j * C + c];
+        nn += v * v;
+      }
+      inv[s] = nn > 0 ? (float)(1.0 / sqrt(nn)) : 0.0f;
+      zf[s] = nn > 0 ? 0.0f : 1.0f;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KS16; ++s) {
+    h8 vh, vl;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 16 * s + 8 * h + q;
+      float v = 0.0f;
+      if (k < C) {
+        float iv = inv[0];
+#pragma unroll
+        for (int t = 1; t < SMAX; ++t)
+          if (t < bd.nseg && k >= bd.b[t]) iv = inv[t];
+        v = (float)((double)stg[j * C + k] * (double)iv);
+      } else if (k < C + bd.nseg) {
+        float z = zf[0];
+#pragma unroll
+        for (int t = 1; t < SMAX; ++t)
+          if (t == k - C) z = zf[t];
+        v = z;
+      }
+      const _Float16 hv = (_Float16)v;
+      vh[q] = hv;
+      vl[q] = (_Float16)(v - (float)hv);
+    }
+    bh[s] = vh;
+    bl[s] = vl;
+  }
+  __syncthreads();
+}
+
+template <int KS16>
+__global__ __launch_bounds__(256) void classify_pixels_f16_kernel(const float *__restrict__ stack, int64_t P,
+                                                                  int32_t C, Bounds bd,
+                                                                  const _Float16 *__restrict__ refh, int32_t R,
+                                                                  int32_t Rpad, int32_t *__restrict__ best_idx,
+                                                                  float *__restrict__ best_dist) {
+  constexpr int KP = 16 * KS16;
+  constexpr int ROWB = 4 * KP;               // bytes per reference: hi | lo'
+  constexpr int STRIDE = ROWB + 16;          // 16 * odd: conflict-free ds_read_b128 over 16 rows
+  constexpr int VEC = ROWB / 16;             // u32x4 per reference row
+  constexpr int PF = RCH * VEC / 256;        // = KS16 (RCH 64, VEC 4*KS16): no tail
+  static_assert(RCH * VEC == PF * 256, "prefetch must tile the chunk exactly");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  char *ldsb = reinterpret_cast<char *>(lds);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * 256 + w * 64;
+
+  h8 bh0[KS16], bl0[KS16], bh1[KS16], bl1[KS16];
+  float *stg = lds + w * (32 * C);
+  build_b_f16<KS16>(stack, P, C, bd, pbase, stg, lane, j, h, bh0, bl0);
+  build_b_f16<KS16>(stack, P, C, bd, pbase + 32, stg, lane, j, h, bh1, bl1);
+
+  float best[2] = {-__builtin_inff(), -__builtin_inff()};
+  int bidx[2] = {0, 0};
+  u32x4 pf[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) {
+    pf[q] = reinterpret_cast<const u32x4 *>(refh)[tid + q * 256];
+  }
+  for (int r0 = 0; r0 < Rpad; r0 += RCH) {
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * 256;
+      const int rr = e / VEC, cc = e - rr * VEC;
+      *reinterpret_cast<u32x4 *>(ldsb + rr * STRIDE + cc * 16) = pf[q];
+    }
+    __syncthreads();
+    if (r0 + RCH < Rpad) {
+      const u32x4 *gsrc = reinterpret_cast<const u32x4 *>(refh + (int64_t)(r0 + RCH) * 2 * KP);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        pf[q] = gsrc[tid + q * 256];
+      }
+    }
+#pragma unroll 1
+    for (int rb = 0; rb < RCH; rb += 32) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      const char *row = ldsb + (rb + j) * STRIDE + 16 * h;
+#pragma unroll
+      for (int s = 0; s < KS16; ++s) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
+        const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 32 * s);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1[s], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1[s], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int r = r0 + rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const bool ok = r < R;
+        const float s0 = acc0[reg];
+        const float s1 = acc1[reg];
+        if (ok && s0 > best[0]) {
+          best[0] = s0;
+          bidx[0] = r;
+        }
+        if (ok && s1 > best[1]) {
+          best[1] = s1;
+          bidx[1] = r;
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const float ob = __shfl_xor(best[g], 32, 64);
@@ -270,46 +474,87 @@ hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Boun
 
 extern "C" {
 
-hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t *kp_host, int32_t *rpad_host) {
+hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mode, int32_t *kp_host,
+                                 int32_t *rpad_host) {
   HRF_REQUIRE(C >= 1 && nseg >= 1 && nseg <= SMAX && R >= 1, "classify_geometry: bad arguments");
-  const int ks = choose_ks(C + nseg);
-  HRF_REQUIRE(ks > 0, "classify: C + nseg must be <= 128");
-  *kp_host = 2 * ks;
+  HRF_REQUIRE(mode == 0 || mode == 1, "classify_geometry: mode must be 0 (f32 MFMA) or 1 (split fp16 MFMA)");
+  if (mode == 0) {
+    const int ks = choose_ks(C + nseg);
+    HRF_REQUIRE(ks > 0, "classify: C + nseg must be <= 128");
+    *kp_host = 2 * ks;
+  } else {
+    const int ks16 = (int)hrf::cdiv(C + nseg, 16);
+    HRF_REQUIRE(ks16 >= 1 && ks16 <= 8, "classify: C + nseg must be <= 128");
+    *kp_host = 16 * ks16;
+  }
   *rpad_host = (int32_t)(hrf::cdiv(R, RCH) * RCH);
   return HRF_OK;
 }
 
 hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg,
-                                     float *refx, hrf_stream_t stream) {
+                                     int32_t mode, void *refx, hrf_stream_t stream) {
   Bounds bd;
   if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
   int32_t kp = 0, rpad = 0;
-  if (hrf_status s = hrf_classify_geometry(C, nseg, R, &kp, &rpad)) return s;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, mode, &kp, &rpad)) return s;
   HRF_REQUIRE(ref && refx, "classify_prepare_refs: null buffer");
-  ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad, refx);
+  if (mode == 0)
+    ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
+                                                                                      (float *)refx);
+  else
+    ref_prep_f16_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
+                                                                                          (_Float16 *)refx);
   HRF_LAUNCHED();
   return HRF_OK;
 }
 
-hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const float *refx, int32_t R,
-                               const int32_t *bounds_host, int32_t nseg, int32_t *best_idx, float *best_dist,
-                               hrf_stream_t stream) {
+hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
+                               const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
+                               float *best_dist, hrf_stream_t stream) {
   Bounds bd;
   if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
   int32_t kp = 0, rpad = 0;
-  if (hrf_status s = hrf_classify_geometry(C, nseg, R, &kp, &rpad)) return s;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, mode, &kp, &rpad)) return s;
   if (P == 0) return HRF_OK;
   HRF_REQUIRE(stack && refx && best_idx && best_dist, "classify_pixels: null buffer");
+  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
+  hipStream_t s = (hipStream_t)stream;
+  if (mode == 1) {
+    const int ks16 = kp / 16;
+    const size_t shm = std::max<size_t>((size_t)RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * C);
+    HRF_REQUIRE(shm <= 160 * 1024, "classify_pixels: C too large for LDS staging");
+#define HRF_CP16(K)                                                                                          \
+  case K:                                                                                                    \
+    hipFuncSetAttribute((const void *)classify_pixels_f16_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                        (int)shm);                                                                           \
+    classify_pixels_f16_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, (const _Float16 *)refx, R, rpad,     \
+                                                         best_idx, best_dist);                               \
+    break;
+    switch (ks16) {
+      HRF_CP16(1)
+      HRF_CP16(2)
+      HRF_CP16(3)
+      HRF_CP16(4)
+      HRF_CP16(5)
+      HRF_CP16(6)
+      HRF_CP16(7)
+      HRF_CP16(8)
+      default:
+        HRF_REQUIRE(false, "classify_pixels: unsupported K");
+    }
+#undef HRF_CP16
+    HRF_LAUNCHED();
+    return HRF_OK;
+  }
   const int ks = kp / 2;
   const size_t shm = sizeof(float) * std::max<size_t>((size_t)RCH * (kp + 2), (size_t)4 * 32 * C);
   HRF_REQUIRE(shm <= 160 * 1024, "classify_pixels: C too large for LDS staging");
-  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
-  hipStream_t s = (hipStream_t)stream;
 #define HRF_CP(K)                                                                                          \
   case K:                                                                                                  \
     hipFuncSetAttribute((const void *)classify_pixels_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                         (int)shm);                                                                         \
-    classify_pixels_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, refx, R, rpad, best_idx, best_dist);   \
+    classify_pixels_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, (const float *)refx, R, rpad, best_idx,   \
+                                                     best_dist);                                           \
     break;
   switch (ks) {
     HRF_CP(8)

@@ -9,6 +9,8 @@
 //
 // Device-resident loop: accumulate (one streaming pass) -> update (1 thread) per iteration;
 // both early-exit once converged, so the host launches fixed batches and polls rarely.
+#include <algorithm>
+
 #include "common.hpp"
 #include "wave.hpp"
 
@@ -59,7 +61,22 @@ __global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__
     am = a2 > am ? a2 : am;
     nv += __shfl_xor(nv, o, 64);
   }
+  __shared__ unsigned long long red[4][4];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
+    red[w][0] = lo;
+    red[w][1] = hi;
+    red[w][2] = am;
+    red[w][3] = nv;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) {
+      lo = red[q][0] < lo ? red[q][0] : lo;
+      hi = red[q][1] > hi ? red[q][1] : hi;
+      am = red[q][2] > am ? red[q][2] : am;
+      nv += red[q][3];
+    }
     atomicMin(&st->lo_bits, lo);
     atomicMax(&st->hi_bits, hi);
     atomicMax(&st->amax_bits, am);
@@ -190,6 +207,7 @@ template <int K>
 hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels, uint8_t *top,
                   double *centers_host, int32_t *iters_host, KmState *st, hipStream_t s) {
   const unsigned g = hrf::stream_grid(n);
+  const unsigned gr = std::min<unsigned>(g, 512);
   KmState init{};
   for (int j = 0; j < KMAX; ++j) init.center[j] = 0;
   init.lo_bits = ~0ull;
@@ -197,7 +215,7 @@ hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter
   init.amax_bits = 0;
   init.nvalid = 0;
   HRF_HIP(hipMemcpyAsync(st, &init, sizeof(KmState), hipMemcpyHostToDevice, s));
-  if (n > 0) km_minmax_kernel<<<g, 256, 0, s>>>(x, valid, n, st);
+  if (n > 0) km_minmax_kernel<<<gr, 256, 0, s>>>(x, valid, n, st);
   km_init_kernel<<<1, 1, 0, s>>>(st, K);
   HRF_LAUNCHED();
   int done = 0;
@@ -206,7 +224,7 @@ hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter
   int conv = 0;
   while (!done) {
     for (int b = 0; b < batch && launched < max_iter; ++b, ++launched) {
-      km_accum_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st);
+      km_accum_kernel<K><<<gr, 256, 0, s>>>(x, valid, n, st);
       km_update_kernel<<<1, 1, 0, s>>>(st, max_iter);
     }
     HRF_LAUNCHED();

@@ -13,6 +13,8 @@
 //   4. numbering  : roots ranked in raster order (wave ballots + block scan), which is
 //                   exactly "first appearance" numbering -- bit-identical to skimage/scipy.
 // Morphology kernels use the cross footprint of skimage's defaults.
+#include <algorithm>
+
 #include "common.hpp"
 #include "wave.hpp"
 
@@ -396,7 +398,13 @@ __global__ void count_u8_kernel(const uint8_t *__restrict__ m, int64_t n, unsign
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     c += m[i] != 0;
   c = hrf::wave_sum(c);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+  __shared__ unsigned long long red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c = red[0] + red[1] + red[2] + red[3];
+    if (c) atomicAdd(cnt, c);
+  }
 }
 
 __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t *__restrict__ mx) {
@@ -408,7 +416,13 @@ __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t
     const int32_t u = __shfl_xor(m, o, 64);
     m = u > m ? u : m;
   }
-  if ((threadIdx.x & 63) == 0) atomicMax(mx, m);
+  __shared__ int32_t red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) m = red[q] > m ? red[q] : m;
+    atomicMax(mx, m);
+  }
 }
 
 template <class V>
@@ -590,7 +604,7 @@ hrf_status hrf_count_nonzero_u8(const uint8_t *mask, int64_t n, int64_t *count_d
   HRF_REQUIRE(count_dev, "count_nonzero: null output");
   HRF_HIP(hipMemsetAsync(count_dev, 0, sizeof(int64_t), s));
   if (n == 0) return HRF_OK;
-  count_u8_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(mask, n, (unsigned long long *)count_dev);
+  count_u8_kernel<<<std::min<unsigned>(hrf::stream_grid(n), 512), 256, 0, s>>>(mask, n, (unsigned long long *)count_dev);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -600,7 +614,7 @@ hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hrf_stream
   HRF_REQUIRE(max_dev, "max_i32: null output");
   HRF_HIP(hipMemsetAsync(max_dev, 0, sizeof(int32_t), s));
   if (n == 0) return HRF_OK;
-  max_i32_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(a, n, max_dev);
+  max_i32_kernel<<<std::min<unsigned>(hrf::stream_grid(n), 512), 256, 0, s>>>(a, n, max_dev);
   HRF_LAUNCHED();
   return HRF_OK;
 }

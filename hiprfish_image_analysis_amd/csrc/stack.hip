@@ -9,6 +9,8 @@
 //   blocks of 128) so the f64 result equals np.sum(stack, axis=2) bit for bit, then
 //   log(s + 1e-2) (ecoli :72) / log10(s + 1) (biofilm :831) / identity, optionally negated
 //   (watershed input).
+#include <algorithm>
+
 #include "common.hpp"
 
 namespace {
@@ -93,6 +95,60 @@ __global__ void channel_sum_kernel(const float *__restrict__ stack, int64_t npix
   }
 }
 
+// C <= 128: 64-pixel chunks staged through LDS with 16-byte loads (coalesced), then 8 lanes per
+// pixel: lane j accumulates numpy's r[j] (a[j] + a[j+8] + ...), the three xor-shuffle levels
+// are exactly ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), lane 0 adds the tail in order.
+constexpr int CS_P = 64;
+__global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__restrict__ stack, int64_t npix, int C,
+                                                              const uint8_t *__restrict__ mask, int mode, int negate,
+                                                              double *__restrict__ out, int vec_ok) {
+  extern __shared__ __attribute__((aligned(16))) float sb[];
+  const int tid = threadIdx.x;
+  const int64_t nchunks = (npix + CS_P - 1) / CS_P;
+  const int j = tid & 7;
+  const int main_n = C < 8 ? 0 : C - (C % 8);
+  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int64_t p0 = ch * CS_P;
+    const int np = (int)min((int64_t)CS_P, npix - p0);
+    const int64_t nel = (int64_t)np * C;
+    const float *src = stack + p0 * C;
+    if (vec_ok) {
+      const int nv = (int)(nel >> 2);
+      for (int v = tid; v < nv; v += 256) reinterpret_cast<float4 *>(sb)[v] = reinterpret_cast<const float4 *>(src)[v];
+      for (int e = (nv << 2) + tid; e < nel; e += 256) sb[e] = src[e];
+    } else {
+      for (int e = tid; e < nel; e += 256) sb[e] = src[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int pi = half * 32 + (tid >> 3);
+      const float *a = sb + pi * C;
+      double res = 0.0;
+      if (C >= 8) {
+        double r = (double)a[j];
+        for (int i = 8; i < main_n; i += 8) r += (double)a[i + j];
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        res = r;
+        if (j == 0)
+          for (int i = main_n; i < C; ++i) res += (double)a[i];
+      } else if (j == 0) {
+        for (int i = 0; i < C; ++i) res += (double)a[i];
+      }
+      if (j == 0 && pi < np) {
+        const int64_t p = p0 + pi;
+        double sv = (mask && !mask[p]) ? 0.0 : 0.0 + res;
+        if (mode == 1) sv = log(sv + 1e-2);
+        else if (mode == 2) sv = log10(sv + 1.0);
+        out[p] = negate ? -sv : sv;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void max_f64_kernel(const double *__restrict__ a, int64_t n, unsigned long long *__restrict__ mx) {
   // order-preserving encoding so atomicMax on uint64 is a max on doubles
   unsigned long long m = 0;
@@ -106,7 +162,13 @@ __global__ void max_f64_kernel(const double *__restrict__ a, int64_t n, unsigned
     const unsigned long long u = __shfl_xor(m, o, 64);
     m = u > m ? u : m;
   }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+  __shared__ unsigned long long red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) m = red[q] > m ? red[q] : m;
+    if (m) atomicMax(mx, m);
+  }
 }
 
 __global__ void decode_max_kernel(unsigned long long *mx) {
@@ -172,7 +234,15 @@ hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const ui
   HRF_REQUIRE(C >= 1 && C <= 512 && mode >= 0 && mode <= 2, "channel_sum: C must be 1..512, mode 0..2");
   if (npix == 0) return HRF_OK;
   HRF_REQUIRE(stack && out, "channel_sum: null buffer");
-  channel_sum_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out);
+  if (C <= 128) {
+    const int vec_ok = C >= 4 && (((uintptr_t)stack & 15) == 0);
+    const int64_t nch = hrf::cdiv(npix, CS_P);
+    channel_sum_lds_kernel<<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
+                             (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out, vec_ok);
+  } else {
+    channel_sum_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate,
+                                                                               out);
+  }
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -182,7 +252,7 @@ hrf_status hrf_max_f64(const double *a, int64_t n, double *max_dev, hrf_stream_t
   hipStream_t s = (hipStream_t)stream;
   HRF_REQUIRE(max_dev && n >= 1 && a, "max_f64: bad arguments");
   HRF_HIP(hipMemsetAsync(max_dev, 0, sizeof(double), s));
-  max_f64_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(a, n, (unsigned long long *)max_dev);
+  max_f64_kernel<<<std::min<unsigned>(hrf::stream_grid(n), 512), 256, 0, s>>>(a, n, (unsigned long long *)max_dev);
   decode_max_kernel<<<1, 1, 0, s>>>((unsigned long long *)max_dev);
   HRF_LAUNCHED();
   return HRF_OK;

@@ -394,31 +394,41 @@ def paint_ids(labels, code):
 
 
 # ---- a19 ------------------------------------------------------------------------------------
-def classify_geometry(C, nseg, R):
+CLASSIFY_MODE = 1   # 1: split-fp16 MFMA (default), 0: f32 MFMA
+
+
+def classify_geometry(C, nseg, R, mode=None):
     import ctypes
+    mode = CLASSIFY_MODE if mode is None else mode
     kp, rp = ctypes.c_int32(0), ctypes.c_int32(0)
-    _lib.call("hrf_classify_geometry", C, nseg, R, ctypes.addressof(kp), ctypes.addressof(rp))
+    _lib.call("hrf_classify_geometry", C, nseg, R, mode, ctypes.addressof(kp), ctypes.addressof(rp))
     return kp.value, rp.value
 
 
-def classify_prepare(ref, bounds):
+def classify_prepare(ref, bounds, mode=None):
+    """-> prepared reference table for classify_pixels (mode 0: f32, mode 1: fp16 hi/lo)"""
+    mode = CLASSIFY_MODE if mode is None else mode
     ref = _dev(ref, torch.float32, "ref")
     R, C = ref.shape
     b = _i32_host(bounds)
-    kp, rp = classify_geometry(C, len(b) - 1, R)
-    refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
-    _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, _ptr(refx), _stream())
+    kp, rp = classify_geometry(C, len(b) - 1, R, mode)
+    if mode == 0:
+        refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
+    else:
+        refx = torch.empty((rp, 2 * kp), dtype=torch.float16, device=ref.device)
+    _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, mode, _ptr(refx), _stream())
     return refx
 
 
 def classify_pixels(stack, refx, R, bounds):
     stack = _dev(stack, torch.float32, "stack")
+    mode = 0 if refx.dtype == torch.float32 else 1
     C = stack.shape[-1]
     P = stack.numel() // C
     b = _i32_host(bounds)
     idx = torch.empty(stack.shape[:-1], dtype=torch.int32, device=stack.device)
     dist = torch.empty(stack.shape[:-1], dtype=torch.float32, device=stack.device)
-    _lib.call("hrf_classify_pixels", _ptr(stack), P, C, _ptr(refx), R, b.ctypes.data, len(b) - 1, _ptr(idx),
+    _lib.call("hrf_classify_pixels", _ptr(stack), P, C, _ptr(refx), R, b.ctypes.data, len(b) - 1, mode, _ptr(idx),
               _ptr(dist), _stream())
     return idx, dist
 

@@ -202,13 +202,17 @@ HRF_API hrf_status hrf_paint_ids(const int32_t *labels, int64_t n, const int32_t
 /* ==== a19: segmented-cosine classification (classify.hip) ===============================
  * train_reference.py:223-386 (channel_cosine_intensity), :993-1072 (_7b_v2).
  * bounds_host: nseg+1 channel offsets on the HOST (e.g. 0,32,55,75,89,95). */
-HRF_API hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t *kp_host, int32_t *rpad_host);
-/* refx (rpad x kp f32): segment-normalised references + zero-segment indicators */
+/* mode 0: f32 MFMA (v_mfma_f32_32x32x2_f32); mode 1: split-fp16 MFMA (hi/lo' fp16 operands,
+ * ~2^-22 relative per product, 16x-rate v_mfma_f32_32x32x16_f16).  kp/rpad: prepared-table
+ * geometry (mode 0: rpad x kp f32; mode 1: rpad x 2*kp fp16). */
+HRF_API hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mode, int32_t *kp_host,
+                                         int32_t *rpad_host);
+/* segment-normalised references + zero-segment indicator columns, padded */
 HRF_API hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host,
-                                             int32_t nseg, float *refx, hrf_stream_t stream);
+                                             int32_t nseg, int32_t mode, void *refx, hrf_stream_t stream);
 /* per pixel (north_star mode): best_idx[p] = argmin_r ungated distance, best_dist[p] */
-HRF_API hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const float *refx, int32_t R,
-                                       const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+HRF_API hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
+                                       const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
                                        float *best_dist, hrf_stream_t stream);
 /* per cell (f64): variant 0 ungated, 1 channel_cosine_intensity, 2 _7b_v2; fx (N x nseg),
  * fr (R x nseg) presence flags (needed for variants 1, 2) */

@@ -207,8 +207,9 @@ def test_counts_paint(K, orc):
 
 
 # ---- a19 classification ---------------------------------------------------------------
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63)), (5, (0, 32))])
-def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds):
+def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
     ref = S.reference_library(nbit, bounds) if len(bounds) > 2 else \
         np.abs(np.random.default_rng(0).normal(size=(31, 32))).astype(np.float32)
     R, C = ref.shape
@@ -219,7 +220,7 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds):
     st = host(stack).reshape(-1, C)
     st[:7] = 0.0                          # all-zero pixels
     st[7:20, bounds[0]:bounds[1]] = 0.0   # a zero segment
-    refx = K.classify_prepare(dev(ref), bounds)
+    refx = K.classify_prepare(dev(ref), bounds, mode=mode)
     idx, dist = K.classify_pixels(dev(st), refx, R, bounds)
     ra, rd = orc.classify(st.astype(np.float64), ref.astype(np.float64), bounds, 0)
     gi, gd = host(idx), host(dist)
