@@ -238,14 +238,15 @@ __global__ void cc_fill_kernel(const int32_t *__restrict__ parent, int64_t n, in
   }
 }
 
-// component sizes at the root index (size[] zeroed by the caller)
+// component sizes at the root index (size[] zeroed by the caller); each wave counts RUN*64
+// consecutive pixels (wave_run_count) so a giant component is one atomic per wave
+constexpr int RUN = 32;
+constexpr int64_t RUN_PX = RUN * 64;
 __global__ void cc_sizes_kernel(const int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ size) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n_up = (n + 63) / 64 * 64;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_up; p += stride) {
-    const int32_t q = p < n ? parent[p] : -1;
-    hrf::agg_atomic_add<int32_t>(size, q < 0 ? 0 : q, 1, q >= 0);
-  }
+  const int64_t nw = (n + RUN_PX - 1) / RUN_PX;
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); w < nw; w += (int64_t)gridDim.x * wpb)
+    hrf::wave_run_count<RUN>(size, w * RUN_PX, n, [&](int64_t e) { return parent[e]; });
 }
 
 // rso / remove_small_holes finish: out = (fg && size[root] >= thr) ^ inv
@@ -305,13 +306,13 @@ __global__ void clear_border_finish_kernel(const int32_t *__restrict__ lab, cons
 // rso on an int label image: counts per label value
 __global__ void label_counts_kernel(const int32_t *__restrict__ lab, int64_t n, int32_t maxlab,
                                     int32_t *__restrict__ cnt) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n_up = (n + 63) / 64 * 64;
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_up; p += stride) {
-    const int32_t l = p < n ? lab[p] : 0;
-    const bool ok = l > 0 && l <= maxlab;
-    hrf::agg_atomic_add<int32_t>(cnt, ok ? l : 0, 1, ok);
-  }
+  const int64_t nw = (n + RUN_PX - 1) / RUN_PX;
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); w < nw; w += (int64_t)gridDim.x * wpb)
+    hrf::wave_run_count<RUN>(cnt, w * RUN_PX, n, [&](int64_t e) {
+      const int32_t l = lab[e];
+      return (l > 0 && l <= maxlab) ? l : -1;
+    });
 }
 
 __global__ void rso_labels_finish_kernel(const int32_t *__restrict__ lab, const int32_t *__restrict__ cnt,
@@ -492,7 +493,7 @@ hrf_status hrf_cc_sizes(const int32_t *parent, int64_t n, int32_t *size, hrf_str
   if (n == 0) return HRF_OK;
   HRF_REQUIRE(parent && size, "cc_sizes: null buffer");
   HRF_HIP(hipMemsetAsync(size, 0, sizeof(int32_t) * n, s));
-  cc_sizes_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent, n, size);
+  cc_sizes_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(n, RUN_PX * 4), 4096), 256, 0, s>>>(parent, n, size);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -564,7 +565,7 @@ hrf_status hrf_remove_small_objects_labels(const int32_t *labels, int64_t n, int
   if (n == 0) return HRF_OK;
   HRF_REQUIRE(labels && out && cnt_ws && maxlab >= 0, "remove_small_objects_labels: bad arguments");
   HRF_HIP(hipMemsetAsync(cnt_ws, 0, sizeof(int32_t) * ((size_t)maxlab + 1), s));
-  label_counts_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, n, maxlab, cnt_ws);
+  label_counts_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(n, RUN_PX * 4), 4096), 256, 0, s>>>(labels, n, maxlab, cnt_ws);
   rso_labels_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, cnt_ws, n, maxlab, min_size, out);
   HRF_LAUNCHED();
   return HRF_OK;

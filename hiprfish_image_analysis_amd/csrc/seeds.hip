@@ -1,0 +1,312 @@
+// seeds.hip -- the E. coli erosion-seeding loop (a11) in ONE launch.
+//
+// Reference (ecoli measurement.py:97-110): while any region is left: regions (8-connected)
+// with area < 600 become seeds and leave the mask; the rest is eroded (cross, border True);
+// 4-connected fragments < 10 px are dropped; relabel; repeat.
+// None of these steps lets information cross an 8-connected component of the starting mask:
+// a pixel's cross neighbours are 8-adjacent (same component), 4-components and 8-components
+// of a subset stay inside the component, and each component's loop ends when it is empty.
+// So every component of `cell_sm` runs the loop independently: one workgroup per component
+// keeps the component's bounding box in LDS (1 flag byte + parent + size per pixel) and
+// iterates union-find / freeze / erode / sieve until it is empty, then writes its seed
+// pixels.  Components whose box exceeds the LDS budget (large clumps of touching cells) run
+// the same loop as whole-image passes over the crop that holds all of them, padded with one
+// background row/column wherever the crop edge is not the image edge (so the erosion's
+// border_value=True applies only at the true image border).
+#include <algorithm>
+#include <vector>
+
+#include "common.hpp"
+#include "wave.hpp"
+
+namespace {
+
+// 9 B/px of LDS: boxes up to 8192 px run two workgroups per CU (72 KB); boxes up to 18176 px
+// (a clump of a few touching cells) run in a second launch using the whole 160 KB
+constexpr int SEED_LDS_PX = 8192;
+constexpr int SEED_LDS_PX_MAX = 18176;
+
+// find with path halving: a box is up to 18K px and the raster-order unions would otherwise
+// build parent chains as long as a row run (quadratic finds).  A halving store only ever
+// points a node at one of its ancestors (all links go to smaller indices, so no cycles); a
+// concurrent atomicMin it overwrites belongs to a union that saw a non-root and retries.
+__device__ __forceinline__ int sfind(int32_t *par, int x) {
+  volatile int32_t *v = par;
+  for (;;) {
+    const int y = v[x];
+    if (y == x) return x;
+    const int z = v[y];
+    if (z == y) return y;
+    v[x] = z;
+    x = z;
+  }
+}
+
+__device__ __forceinline__ void sunion(int32_t *par, int a, int b) {
+  for (;;) {
+    a = sfind(par, a);
+    b = sfind(par, b);
+    if (a == b) return;
+    if (a < b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicMin(&par[a], b);
+    if (old == a) return;
+    a = old;
+  }
+}
+
+// components of flag bit0 inside the box; par[p] = root, sz[root] = size
+__device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, bool conn8) {
+  const int n = bh * bw;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    par[p] = (fl[p] & 1) ? p : -1;
+    sz[p] = 0;
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    if (!(fl[p] & 1)) continue;
+    const int r = p / bw, c = p - r * bw;
+    if (c > 0 && (fl[p - 1] & 1)) sunion(par, p, p - 1);
+    if (r > 0) {
+      if (fl[p - bw] & 1) sunion(par, p, p - bw);
+      if (conn8) {
+        if (c > 0 && (fl[p - bw - 1] & 1)) sunion(par, p, p - bw - 1);
+        if (c + 1 < bw && (fl[p - bw + 1] & 1)) sunion(par, p, p - bw + 1);
+      }
+    }
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < n; p += blockDim.x)
+    if (fl[p] & 1) par[p] = sfind(par, p);
+  __syncthreads();
+  const int n_up = (n + 63) & ~63;  // whole waves: one LDS atomic per distinct root per wave
+  for (int p = threadIdx.x; p < n_up; p += blockDim.x) {
+    const bool in = p < n && (fl[p] & 1);
+    hrf::agg_atomic_add<int32_t>(sz, in ? par[p] : 0, 1, in);
+  }
+  __syncthreads();
+}
+
+// flags: bit0 = in play (dist_lab != 0), bit1 = seed (dist_be), bit2 = erosion result
+__global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
+                                                           const int32_t *__restrict__ box,
+                                                           const uint8_t *__restrict__ cls, int32_t want,
+                                                           int32_t area_max,
+                                                           int32_t min_obj, uint8_t *__restrict__ be_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int comp = blockIdx.x + 1;
+  const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
+  if (r1 < r0 || c1 < c0 || cls[comp] != want) return;
+  const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, n = bh * bw;
+  uint8_t *fl = reinterpret_cast<uint8_t *>(lds);
+  int32_t *par = reinterpret_cast<int32_t *>(lds + ((n + 15) & ~15));
+  int32_t *sz = par + n;
+  for (int p = threadIdx.x; p < n; p += blockDim.x) {
+    const int r = p / bw, c = p - r * bw;
+    fl[p] = labels[(int64_t)(r0 + r) * W + (c0 + c)] == comp ? 1 : 0;
+  }
+  __syncthreads();
+  for (int it = 0; it < 4 * (bh + bw) + 8; ++it) {
+    // :102-106 regions (8-connected) below area_max become seeds
+    box_cc(fl, par, sz, bh, bw, true);
+    for (int p = threadIdx.x; p < n; p += blockDim.x)
+      if ((fl[p] & 1) && sz[par[p]] < area_max) fl[p] = (uint8_t)((fl[p] & ~1) | 2);
+    __syncthreads();
+    // :107 binary_erosion (cross, border_value True at the image edge; outside the box but
+    // inside the image is another component's or background territory -> False)
+    for (int p = threadIdx.x; p < n; p += blockDim.x) {
+      const int r = p / bw, c = p - r * bw;
+      bool v = fl[p] & 1;
+      if (v) {
+        v = v && (r > 0 ? (fl[p - bw] & 1) != 0 : (r0 == 0));
+        v = v && (r + 1 < bh ? (fl[p + bw] & 1) != 0 : (r1 == H - 1));
+        v = v && (c > 0 ? (fl[p - 1] & 1) != 0 : (c0 == 0));
+        v = v && (c + 1 < bw ? (fl[p + 1] & 1) != 0 : (c1 == W - 1));
+      }
+      if (v) fl[p] |= 4;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < n; p += blockDim.x) fl[p] = (uint8_t)((fl[p] & 2) | ((fl[p] >> 2) & 1));
+    __syncthreads();
+    // :108 remove_small_objects(., min_obj), 4-connected
+    box_cc(fl, par, sz, bh, bw, false);
+    int any = 0;
+    for (int p = threadIdx.x; p < n; p += blockDim.x)
+      if (fl[p] & 1) {
+        if (sz[par[p]] < min_obj)
+          fl[p] &= (uint8_t)~1;
+        else
+          any = 1;
+      }
+    if (!__syncthreads_or(any)) break;
+  }
+  for (int p = threadIdx.x; p < n; p += blockDim.x)
+    if (fl[p] & 2) {
+      const int r = p / bw, c = p - r * bw;
+      be_out[(int64_t)(r0 + r) * W + (c0 + c)] = 1;
+    }
+}
+
+// crop (with padding) of the oversized components' pixels
+__global__ void big_crop_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W, const uint8_t *__restrict__ big,
+                                int64_t r0, int64_t c0, int64_t h, int64_t w, uint8_t *__restrict__ m) {
+  const int64_t n = h * w;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = r0 + i / w, c = c0 + i % w;
+    uint8_t v = 0;
+    if (r >= 0 && r < H && c >= 0 && c < W) {
+      const int32_t l = labels[r * W + c];
+      v = l > 0 && big[l] == 2;
+    }
+    m[i] = v;
+  }
+}
+
+__global__ void big_paste_kernel(const uint8_t *__restrict__ be_crop, int64_t H, int64_t W, int64_t r0, int64_t c0,
+                                 int64_t h, int64_t w, uint8_t *__restrict__ be_out) {
+  const int64_t n = h * w;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = r0 + i / w, c = c0 + i % w;
+    if (be_crop[i] && r >= 0 && r < H && c >= 0 && c < W) be_out[r * W + c] = 1;
+  }
+}
+
+__global__ void box_init_kernel(int32_t *box, int32_t maxlab) {
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l > maxlab) return;
+  box[l * 4 + 0] = 0x7fffffff;
+  box[l * 4 + 1] = 0x7fffffff;
+  box[l * 4 + 2] = -1;
+  box[l * 4 + 3] = -1;
+}
+
+// per-label bounding boxes; atomics aggregated per distinct label in the wave
+__global__ void box_kernel(const int32_t *__restrict__ lab, int64_t H, int64_t W, int32_t maxlab,
+                           int32_t *__restrict__ box) {
+  const int64_t n = H * W;
+  const int64_t n_up = (n + 63) / 64 * 64;
+  const int lane = hrf::lane_id();
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_up; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t l = p < n ? lab[p] : 0;
+    bool active = l > 0 && l <= maxlab;
+    const int32_t r = (int32_t)(p / W), c = (int32_t)(p - (p / W) * W);
+    unsigned long long pending = __ballot(active);
+    while (pending) {
+      const int leader = __ffsll((long long)pending) - 1;
+      const int32_t k = __shfl(l, leader, 64);
+      const bool m = active && l == k;
+      const unsigned long long same = __ballot(m);
+      int32_t rmin = m ? r : 0x7fffffff, cmin = m ? c : 0x7fffffff, rmax = m ? r : -1, cmax = m ? c : -1;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        rmin = min(rmin, __shfl_xor(rmin, o, 64));
+        cmin = min(cmin, __shfl_xor(cmin, o, 64));
+        rmax = max(rmax, __shfl_xor(rmax, o, 64));
+        cmax = max(cmax, __shfl_xor(cmax, o, 64));
+      }
+      if (lane == leader) {
+        atomicMin(&box[k * 4 + 0], rmin);
+        atomicMin(&box[k * 4 + 1], cmin);
+        atomicMax(&box[k * 4 + 2], rmax);
+        atomicMax(&box[k * 4 + 3], cmax);
+      }
+      if (m) active = false;
+      pending &= ~same;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+hrf_status hrf_label_boxes(const int32_t *labels, int64_t H, int64_t W, int32_t maxlab, int32_t *box,
+                           hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(maxlab >= 0 && box, "label_boxes: bad arguments");
+  box_init_kernel<<<(unsigned)hrf::cdiv((int64_t)maxlab + 1, 256), 256, 0, s>>>(box, maxlab);
+  if (H * W > 0) box_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(labels, H, W, maxlab, box);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+// labels: 8-connected components 1..ncomp of the starting mask (hrf_label output);
+// box: hrf_label_boxes output.  Synchronises once to read the boxes, and once per iteration
+// of the whole-image loop when oversized components exist.
+hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
+                             int32_t area_max, int32_t min_obj, uint8_t *be_out, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(ncomp >= 0 && be_out && (ncomp == 0 || (labels && box)), "erosion_seeds: bad arguments");
+  HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+  if (ncomp == 0) return HRF_OK;
+  std::vector<int32_t> hb((size_t)(ncomp + 1) * 4);
+  HRF_HIP(hipMemcpyAsync(hb.data(), box, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HRF_HIP(hipStreamSynchronize(s));
+  std::vector<uint8_t> big((size_t)ncomp + 1, 0);  // 0: LDS 72 KB, 1: LDS 160 KB, 2: whole-image loop
+  int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
+  int nmid = 0;
+  for (int c = 1; c <= ncomp; ++c) {
+    const int64_t bh = hb[c * 4 + 2] - hb[c * 4 + 0] + 1, bw = hb[c * 4 + 3] - hb[c * 4 + 1] + 1;
+    if (bh <= 0 || bw <= 0 || bh * bw <= SEED_LDS_PX) continue;
+    if (bh * bw <= SEED_LDS_PX_MAX) {
+      big[c] = 1;
+      ++nmid;
+      continue;
+    }
+    big[c] = 2;
+    br0 = std::min<int64_t>(br0, hb[c * 4 + 0]);
+    bc0 = std::min<int64_t>(bc0, hb[c * 4 + 1]);
+    br1 = std::max<int64_t>(br1, hb[c * 4 + 2]);
+    bc1 = std::max<int64_t>(bc1, hb[c * 4 + 3]);
+  }
+  uint8_t *dbig = nullptr;
+  HRF_HIP(hipMallocAsync((void **)&dbig, big.size(), s));
+  HRF_HIP(hipMemcpyAsync(dbig, big.data(), big.size(), hipMemcpyHostToDevice, s));
+  const size_t shm = ((SEED_LDS_PX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX;
+  const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
+  hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_max);
+  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm, s>>>(labels, H, W, box, dbig, 0, area_max, min_obj, be_out);
+  if (nmid)
+    erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, dbig, 1, area_max, min_obj, be_out);
+  HRF_LAUNCHED();
+  hrf_status st = HRF_OK;
+  if (br1 >= 0) {
+    // pad by one background pixel where the crop edge is interior to the image
+    const int64_t r0 = br0 > 0 ? br0 - 1 : 0, c0 = bc0 > 0 ? bc0 - 1 : 0;
+    const int64_t r1 = br1 < H - 1 ? br1 + 1 : H - 1, c1 = bc1 < W - 1 ? bc1 + 1 : W - 1;
+    const int64_t h = r1 - r0 + 1, w = c1 - c0 + 1, n = h * w;
+    char *ws = nullptr;
+    HRF_HIP(hipMallocAsync((void **)&ws, (size_t)(3 * n + 8 * n + 64), s));
+    uint8_t *m = (uint8_t *)ws, *m2 = m + n, *bec = m2 + n;
+    int32_t *par = (int32_t *)(ws + ((3 * n + 15) & ~(int64_t)15)), *sz = par + n;
+    int64_t *cnt_dev = nullptr;
+    HRF_HIP(hipMallocAsync((void **)&cnt_dev, sizeof(int64_t), s));
+    HRF_HIP(hipMemsetAsync(bec, 0, (size_t)n, s));
+    big_crop_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, H, W, dbig, r0, c0, h, w, m);
+    HRF_LAUNCHED();
+    for (int64_t it = 0; it < 4 * (h + w) + 8; ++it) {
+      int64_t cnt = 0;
+      if ((st = hrf_count_nonzero_u8(m, n, cnt_dev, s))) break;
+      HRF_HIP(hipMemcpyAsync(&cnt, cnt_dev, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      HRF_HIP(hipStreamSynchronize(s));
+      if (cnt == 0) break;
+      if ((st = hrf_split_by_size(m, h, w, 2, area_max, bec, m2, par, sz, s))) break;
+      if ((st = hrf_binary_erosion(m2, h, w, 1, m, s))) break;
+      if ((st = hrf_remove_small_objects_mask(m, h, w, min_obj, 1, m2, par, sz, s))) break;
+      std::swap(m, m2);
+    }
+    if (st == HRF_OK) {
+      big_paste_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(bec, H, W, r0, c0, h, w, be_out);
+      HRF_LAUNCHED();
+    }
+    HRF_HIP(hipFreeAsync(cnt_dev, s));
+    HRF_HIP(hipFreeAsync(ws, s));
+  }
+  HRF_HIP(hipFreeAsync(dbig, s));
+  return st;
+}
+
+}  // extern "C"

@@ -51,7 +51,9 @@ __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t b1, double
 __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__ f, int negate,
                                                       const int32_t *__restrict__ markers,
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
-                                                      WsState in, WsState out, int32_t *__restrict__ changed) {
+                                                      WsState in, WsState out, int32_t *__restrict__ changed,
+                                                      const int32_t *__restrict__ prev_tile,
+                                                      int32_t *__restrict__ cur_tile) {
   __shared__ double sl[WL * WL];
   __shared__ double sf[WL * WL];
   __shared__ int32_t sh[WL * WL];
@@ -59,6 +61,17 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   __shared__ uint8_t sm[WL * WL];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.y * WT - 1, c0 = (int64_t)blockIdx.x * WT - 1;
+  // A tile whose 3x3 tile neighbourhood did not change in the previous pass is skipped: its
+  // own state did not change either, so both ping-pong buffers already hold it.
+  if (prev_tile) {
+    int act = 0;
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ty = (int)blockIdx.y + dy, tx = (int)blockIdx.x + dx;
+        if (ty >= 0 && ty < (int)gridDim.y && tx >= 0 && tx < (int)gridDim.x) act |= prev_tile[ty * gridDim.x + tx];
+      }
+    if (!act) return;
+  }
   for (int idx = tid; idx < WL * WL; idx += 256) {
     const int lr = idx / WL, lc = idx - lr * WL;
     const int64_t gr = r0 + lr, gc = c0 + lc;
@@ -140,7 +153,10 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       out.lab[g] = sb[i];
     }
   }
-  if (__syncthreads_or(any_change) && tid == 0) *changed = 1;
+  if (__syncthreads_or(any_change) && tid == 0) {
+    *changed = 1;
+    cur_tile[blockIdx.y * gridDim.x + blockIdx.x] = 1;
+  }
 }
 
 }  // namespace
@@ -162,13 +178,19 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
   ws_init_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(image, negate, markers, mask, n, a.lam, a.hop, a.lab);
   HRF_LAUNCHED();
   dim3 grid((unsigned)hrf::cdiv(W, WT), (unsigned)hrf::cdiv(H, WT));
+  const int64_t ntiles = (int64_t)grid.x * grid.y;
+  int32_t *tf = nullptr;  // per-tile change flags, two generations
+  HRF_HIP(hipMallocAsync((void **)&tf, sizeof(int32_t) * 2 * ntiles, s));
   int passes = 0;
   const int batch = 4;
   // flag_ws[k] = change flag of pass k within a batch
   for (;;) {
     HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * batch, s));
     for (int k = 0; k < batch; ++k) {
-      ws_pass_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, flag_ws + k);
+      int32_t *cur = tf + (passes & 1) * ntiles;
+      const int32_t *prev = passes == 0 ? nullptr : tf + ((passes + 1) & 1) * ntiles;
+      HRF_HIP(hipMemsetAsync(cur, 0, sizeof(int32_t) * ntiles, s));
+      ws_pass_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, flag_ws + k, prev, cur);
       WsState t = a;
       a = b;
       b = t;
@@ -180,6 +202,7 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
     HRF_HIP(hipStreamSynchronize(s));
     if (!fl[batch - 1] || passes >= max_passes) break;
   }
+  HRF_HIP(hipFreeAsync(tf, s));
   HRF_HIP(hipMemcpyAsync(out_labels, a.lab, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
   if (passes_host) *passes_host = passes;
   return HRF_OK;

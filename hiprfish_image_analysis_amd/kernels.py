@@ -484,3 +484,21 @@ def split_by_size(mask, thr, small_or, conn=2):
     _lib.call("hrf_split_by_size", _ptr(m), H, W, conn, thr, _ptr(small_or), _ptr(large), _ptr(parent), _ptr(size),
               _stream())
     return large
+
+
+def label_boxes(labels, maxlab):
+    l = _i32(labels, "labels")
+    H, W = l.shape
+    box = torch.empty((maxlab + 1, 4), dtype=torch.int32, device=l.device)
+    _lib.call("hrf_label_boxes", _ptr(l), H, W, maxlab, _ptr(box), _stream())
+    return box
+
+
+def erosion_seeds(cell_sm, area_max=600, min_obj=10):
+    """ecoli measurement.py:97-110 in one launch (per-component workgroups) -> dist_be u8"""
+    labels, n = label(cell_sm, conn=2)
+    H, W = labels.shape
+    box = label_boxes(labels, n)
+    be = torch.empty((H, W), dtype=torch.uint8, device=labels.device)
+    _lib.call("hrf_erosion_seeds", _ptr(labels), H, W, n, _ptr(box), area_max, min_obj, _ptr(be), _stream())
+    return be

@@ -21,7 +21,14 @@ MULTI_BOUNDS = (0, 23, 43, 57, 63)
 # --------------------------------------------------------------------------------------------
 def erosion_seeds(cell_sm: torch.Tensor, area_max: int = 600, min_obj: int = 10) -> torch.Tensor:
     """ecoli measurement.py:97-110: freeze regions below `area_max` as seeds, erode the rest,
-    drop fragments < `min_obj` (4-connected), repeat until nothing is left.  -> seed mask u8"""
+    drop fragments < `min_obj` (4-connected), repeat until nothing is left.  -> seed mask u8
+    One launch, one workgroup per 8-connected component (seeds.hip)."""
+    return K.erosion_seeds(cell_sm, area_max, min_obj)
+
+
+def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: int = 10) -> torch.Tensor:
+    """The same loop as whole-image passes (one CC / erosion / sieve launch set per iteration);
+    kept as a cross-check of the per-component kernel."""
     be = torch.zeros_like(K._u8(cell_sm, "cell_sm"))
     m = K._u8(cell_sm, "cell_sm")
     while K.count_nonzero(m) > 0:                      # markers = regionprops(dist_lab) non-empty

@@ -66,9 +66,11 @@ def default_ncells(H: int, W: int) -> int:
     return max(1, int(round(1500 * H * W / (2048 * 2048))))
 
 
-def render_truth(H: int, W: int, layout, with_profile: bool = False):
-    """Ground-truth cell index map (int32, 0 = background, i+1 = cell i; later cells on top),
-    optionally with the per-pixel dome intensity profile (float32)."""
+def render_truth(H: int, W: int, layout, with_profile: bool = False, max_overlap: float = 0.05):
+    """Ground-truth cell index map (int32, 0 = background, i+1 = cell i), optionally with the
+    per-pixel dome intensity profile (float32).  Cells are placed in order and a cell that
+    would cover more than `max_overlap` of its area with earlier cells is dropped: cells in a
+    FOV touch but do not stack, so clumps stay a few cells large."""
     cy, cx, maj, mnr, th, _, _ = layout
     lab = np.zeros((H, W), np.int32)
     prof = np.zeros((H, W), np.float32)
@@ -85,6 +87,8 @@ def render_truth(H: int, W: int, layout, with_profile: bool = False):
         v = -dx * st + dy * ct
         rr = (u / maj[i]) ** 2 + (v / mnr[i]) ** 2
         inside = rr <= 1.0
+        if np.count_nonzero(lab[r0:r1, c0:c1][inside]) > max_overlap * np.count_nonzero(inside):
+            continue
         lab[r0:r1, c0:c1][inside] = i + 1
         prof[r0:r1, c0:c1][inside] = (1.0 - 0.4 * rr[inside]).astype(np.float32)
     return (lab, prof) if with_profile else lab

@@ -144,6 +144,14 @@ HRF_API hrf_status hrf_remove_small_holes(const uint8_t *mask, int64_t H, int64_
 HRF_API hrf_status hrf_split_by_size(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int64_t thr,
                                      uint8_t *small_or, uint8_t *large, int32_t *parent_ws, int32_t *size_ws,
                                      hrf_stream_t stream);
+/* per-label bounding boxes box[(maxlab+1)*4] = {r0, c0, r1, c1} (inclusive; empty: r1 < r0) */
+HRF_API hrf_status hrf_label_boxes(const int32_t *labels, int64_t H, int64_t W, int32_t maxlab, int32_t *box,
+                                   hrf_stream_t stream);
+/* the whole erosion-seeding loop (ecoli :97-110) in one launch, one workgroup per
+ * 8-connected component (labels 1..ncomp from hrf_label, box from hrf_label_boxes);
+ * be_out (H*W u8) = dist_be.  Synchronises once (sizes a scratch slab for big boxes). */
+HRF_API hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
+                                     int32_t area_max, int32_t min_obj, uint8_t *be_out, hrf_stream_t stream);
 /* scipy.ndimage.binary_fill_holes (multispecies :138-139); flag_ws n int32 */
 HRF_API hrf_status hrf_fill_holes(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, int32_t *parent_ws,
                                   int32_t *flag_ws, hrf_stream_t stream);

@@ -293,3 +293,31 @@ def test_register_assemble_and_channel_sum(K):
     m = rng.random((H, W)) > 0.5
     s2 = host(K.channel_sum(dev(out), mask=dev(m), mode=0, negate=True))
     assert np.array_equal(s2, -np.sum(refst.astype(np.float64) * m[:, :, None], axis=2))
+
+
+# ---- a11 erosion seeding (per-component single launch) ------------------------------------
+@pytest.mark.parametrize("seed", [0, 1])
+def test_erosion_seeds_vs_oracle(K, orc, S, seed):
+    import pipeline as OP
+    from hiprfish_image_analysis_amd import pipeline as P
+    H, W = 400, 420
+    lay = S.cell_layout(H, W, 70, 7, seed=seed)
+    m = S.render_truth(H, W, lay) > 0
+    m[0:3, 10:200] = True                 # touches the image border
+    m[250:395, 250:415] = True            # box > 18176 px -> whole-image loop on the crop
+    m[300:400, 0:200] = True              # a second one, on the image border
+    m[60:150, 300:410] = True             # 8192 < box <= 18176 -> 160 KB LDS launch
+    ref = OP.erosion_seeds(m)
+    got = host(K.erosion_seeds(dev(m))).astype(bool)
+    assert np.array_equal(got, ref)
+    glob = host(P.erosion_seeds_global(dev(m))).astype(bool)
+    assert np.array_equal(glob, ref)
+
+
+def test_label_boxes(K):
+    lab = np.zeros((50, 60), np.int32)
+    lab[3:9, 5:20] = 1
+    lab[40:45, 50:58] = 3
+    box = host(K.label_boxes(dev(lab), 3))
+    assert box[1].tolist() == [3, 5, 8, 19] and box[3].tolist() == [40, 50, 44, 57]
+    assert box[2][2] < box[2][0]
