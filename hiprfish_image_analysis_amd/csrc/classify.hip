@@ -197,20 +197,24 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
 // dropped lo*lo' (<= 2^-22) plus lo's fp16 rounding (<= 2^-25 absolute, subnormal spacing),
 // so a 100-term score is within ~1e-6 of the exact f32 dot product; the three products are
 // v_mfma_f32_32x32x16_f16 at 16x the f32-MFMA rate.
+//
+// Reference table rows (global AND LDS image): {hi[0..KP), lo[0..KP), 16 B pad} fp16, so the
+// row pitch 4*KP+16 is 16 x odd (conflict-free ds_read_b128 over 32 rows) and a 64-row chunk
+// is a whole number of 1 KiB LDS-DMA pieces.  Column C+nseg is a validity bias: 0 for real
+// rows, -1024 for the padding rows past R, against 1.0 on the pixel side, so padding rows
+// never win the argmax and the epilogue needs no bounds test.
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
 
-// refh[r] = {hi[0..KP), lo'[0..KP)} fp16, from the same normalisation as ref_prep_kernel
 __global__ void ref_prep_f16_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
                                     int32_t Rpad, _Float16 *__restrict__ refh) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= Rpad) return;
-  _Float16 *hi = refh + r * 2 * KP;
+  _Float16 *hi = refh + r * (2 * KP + 8);
   _Float16 *lo = hi + KP;
-  for (int k = 0; k < KP; ++k) {
-    hi[k] = (_Float16)0.0f;
-    lo[k] = (_Float16)0.0f;
-  }
+  for (int k = 0; k < 2 * KP + 8; ++k) hi[k] = (_Float16)0.0f;
+  hi[C + bd.nseg] = (_Float16)(r < R ? 0.0f : -1024.0f);
   if (r >= R) return;
   const float *x = ref + r * C;
   for (int s = 0; s < bd.nseg; ++s) {
@@ -227,56 +231,113 @@ __global__ void ref_prep_f16_kernel(const float *__restrict__ ref, int32_t R, in
   }
 }
 
-// Stage one 32-pixel group of this wave and build its split-fp16 B operand (lane = pixel j,
-// half h holds channels 16s + 8h + q).
-template <int KS16>
-__device__ __forceinline__ void build_b_f16(const float *__restrict__ stack, int64_t P, int32_t C, const Bounds &bd,
-                                            int64_t p0, float *stg, int lane, int j, int h, h8 (&bh)[KS16],
-                                            h8 (&bl)[KS16]) {
+// Raw spectra of one 32-pixel group: 32*C floats = 8*C float4, at most 16 per lane (C <= 128).
+// All loads of both groups are issued before any is consumed, so a wave pays the HBM latency
+// once per tile instead of once per element.
+constexpr int LDV = 16;
+__device__ __forceinline__ void load_group(const float *__restrict__ stack, int64_t P, int32_t C, int64_t p0, int lane,
+                                           float4 (&v)[LDV]) {
   const int64_t np = std::max<int64_t>(0, std::min<int64_t>(32, P - p0));
-  const int64_t nel = np * C;
+  const int64_t nel = np * C;  // valid floats of this group
   const float *src = stack + p0 * C;
-  for (int64_t e = lane; e < 32 * C; e += 64) stg[e] = e < nel ? src[e] : 0.0f;
+  const int nv = 8 * C;
+#pragma unroll
+  for (int i = 0; i < LDV; ++i) {
+    const int e4 = lane + 64 * i;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (e4 < nv) {
+      const int64_t e = 4 * (int64_t)e4;
+      if (e + 4 <= nel) {
+        x = *reinterpret_cast<const float4 *>(src + e);
+      } else {
+        x.x = e + 0 < nel ? src[e + 0] : 0.f;
+        x.y = e + 1 < nel ? src[e + 1] : 0.f;
+        x.z = e + 2 < nel ? src[e + 2] : 0.f;
+        x.w = e + 3 < nel ? src[e + 3] : 0.f;
+      }
+    }
+    v[i] = x;
+  }
+}
+
+// Per-workgroup column map for the B operand: segk[k] = the slot of column k in a pixel's
+// 24-float multiplier row {1/norm_s (0..7), zero-indicator_s (8..15), bias 1.0 (16), 0 (17)}.
+constexpr int MROW = 24;
+__device__ __forceinline__ void build_segk(const Bounds &bd, int32_t C, int KP, uint8_t *segk) {
+  for (int k = threadIdx.x; k < KP; k += blockDim.x) {
+    int v = 17;
+    if (k < C) {
+      v = 0;
+      for (int t = 1; t < bd.nseg; ++t) v += k >= bd.b[t];
+    } else if (k < C + bd.nseg) {
+      v = 8 + (k - C);
+    } else if (k == C + bd.nseg) {
+      v = 16;
+    }
+    segk[k] = (uint8_t)v;
+  }
+}
+
+// Stage one loaded group in LDS and build its split-fp16 B operand (lane = pixel j, half h
+// holds columns 16s + 8h + q): column k = raw[k] * mult[segk[k]] (raw = 1 past C), i.e. the
+// channel scaled by its segment's 1/norm, then the zero-segment indicators, the bias column
+// 1.0 and zeros.  The two half-waves of a pixel split each segment's channels for the norm.
+template <int KS16>
+__device__ __forceinline__ void build_b_f16(const float4 (&v)[LDV], int32_t C, const Bounds &bd, float *stg,
+                                            float *mult, const uint8_t *segk, int lane, int j, int h,
+                                            h8 (&bh)[KS16], h8 (&bl)[KS16]) {
+  const int nv = 8 * C;
+#pragma unroll
+  for (int i = 0; i < LDV; ++i) {
+    const int e4 = lane + 64 * i;
+    if (e4 < nv) reinterpret_cast<float4 *>(stg)[e4] = v[i];
+  }
   __syncthreads();
-  float inv[SMAX];
-  float zf[SMAX];
+  const float *px = stg + j * C;
+  float *mj = mult + j * MROW;
 #pragma unroll
   for (int s = 0; s < SMAX; ++s) {
-    inv[s] = 0.0f;
-    zf[s] = 0.0f;
     if (s < bd.nseg) {
-      double nn = 0.0;
-      for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) {
-        const double v = (double)stg[j * C + c];
-        nn += v * v;
+      double n0 = 0.0, n1 = 0.0;
+      const int c1 = bd.b[s + 1];
+      int c = bd.b[s] + h;
+      for (; c + 2 < c1; c += 4) {
+        const double x0 = (double)px[c], x1 = (double)px[c + 2];
+        n0 += x0 * x0;
+        n1 += x1 * x1;
       }
-      inv[s] = nn > 0 ? (float)(1.0 / sqrt(nn)) : 0.0f;
-      zf[s] = nn > 0 ? 0.0f : 1.0f;
+      if (c < c1) {
+        const double x0 = (double)px[c];
+        n0 += x0 * x0;
+      }
+      double nn = n0 + n1;
+      nn += __shfl_xor(nn, 32, 64);
+      if (h == 0) {
+        mj[s] = nn > 0 ? (float)(1.0 / sqrt(nn)) : 0.0f;
+        mj[8 + s] = nn > 0 ? 0.0f : 1.0f;
+      }
     }
   }
+  if (h == 0) {
+    mj[16] = 1.0f;
+    mj[17] = 0.0f;
+  }
+  __syncthreads();
+  // per-lane bases + immediate offsets; the raw read past C lands in LDS and is discarded
+  const float *pc = px + 8 * h;
+  const uint8_t *sk = segk + 8 * h;
 #pragma unroll
   for (int s = 0; s < KS16; ++s) {
     h8 vh, vl;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = 16 * s + 8 * h + q;
-      float v = 0.0f;
-      if (k < C) {
-        float iv = inv[0];
-#pragma unroll
-        for (int t = 1; t < SMAX; ++t)
-          if (t < bd.nseg && k >= bd.b[t]) iv = inv[t];
-        v = (float)((double)stg[j * C + k] * (double)iv);
-      } else if (k < C + bd.nseg) {
-        float z = zf[0];
-#pragma unroll
-        for (int t = 1; t < SMAX; ++t)
-          if (t == k - C) z = zf[t];
-        v = z;
-      }
-      const _Float16 hv = (_Float16)v;
+      const float raw = k < C ? pc[16 * s + q] : 1.0f;
+      float x = raw * mj[sk[16 * s + q]];
+      asm volatile("" : "+v"(x));  // round to f32 first: no fused multiply-to-f16
+      const _Float16 hv = (_Float16)x;
       vh[q] = hv;
-      vl[q] = (_Float16)(v - (float)hv);
+      vl[q] = (_Float16)(x - (float)hv);
     }
     bh[s] = vh;
     bl[s] = vl;
@@ -284,18 +345,21 @@ __device__ __forceinline__ void build_b_f16(const float *__restrict__ stack, int
   __syncthreads();
 }
 
+// One workgroup = 4 waves x 64 pixels, held as split-fp16 B operands in VGPRs for the whole
+// sweep.  The library streams through two LDS chunk buffers by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR staging): chunk c+1 is in flight while chunk c feeds the
+// MFMAs, one barrier per chunk.  The argmax is fused (lane = pixel column, 16 rows per tile).
 template <int KS16>
-__global__ __launch_bounds__(256) void classify_pixels_f16_kernel(const float *__restrict__ stack, int64_t P,
-                                                                  int32_t C, Bounds bd,
-                                                                  const _Float16 *__restrict__ refh, int32_t R,
-                                                                  int32_t Rpad, int32_t *__restrict__ best_idx,
-                                                                  float *__restrict__ best_dist) {
+__global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float *__restrict__ stack, int64_t P,
+                                                                     int32_t C, Bounds bd,
+                                                                     const _Float16 *__restrict__ refh, int32_t R,
+                                                                     int32_t Rpad, int32_t *__restrict__ best_idx,
+                                                                     float *__restrict__ best_dist) {
   constexpr int KP = 16 * KS16;
-  constexpr int ROWB = 4 * KP;               // bytes per reference: hi | lo'
-  constexpr int STRIDE = ROWB + 16;          // 16 * odd: conflict-free ds_read_b128 over 16 rows
-  constexpr int VEC = ROWB / 16;             // u32x4 per reference row
-  constexpr int PF = RCH * VEC / 256;        // = KS16 (RCH 64, VEC 4*KS16): no tail
-  static_assert(RCH * VEC == PF * 256, "prefetch must tile the chunk exactly");
+  constexpr int ROWB = 4 * KP + 16;
+  constexpr int CHB = RCH * ROWB;
+  constexpr int NPC = CHB / 1024;  // LDS-DMA pieces per chunk
+  static_assert(CHB % 1024 == 0, "chunk must be whole 1 KiB pieces");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   char *ldsb = reinterpret_cast<char *>(lds);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -303,37 +367,40 @@ __global__ __launch_bounds__(256) void classify_pixels_f16_kernel(const float *_
   const int64_t pbase = (int64_t)blockIdx.x * 256 + w * 64;
 
   h8 bh0[KS16], bl0[KS16], bh1[KS16], bl1[KS16];
+  // staging aliases the chunk buffers (done before the first DMA): raw rows, multiplier rows,
+  // column map
   float *stg = lds + w * (32 * C);
-  build_b_f16<KS16>(stack, P, C, bd, pbase, stg, lane, j, h, bh0, bl0);
-  build_b_f16<KS16>(stack, P, C, bd, pbase + 32, stg, lane, j, h, bh1, bl1);
-
-  float best[2] = {-__builtin_inff(), -__builtin_inff()};
-  int bidx[2] = {0, 0};
-  u32x4 pf[PF];
-#pragma unroll
-  for (int q = 0; q < PF; ++q) {
-    pf[q] = reinterpret_cast<const u32x4 *>(refh)[tid + q * 256];
+  float *mult = lds + 4 * 32 * C + w * (32 * MROW);
+  uint8_t *segk = reinterpret_cast<uint8_t *>(lds + 4 * 32 * (C + MROW));
+  build_segk(bd, C, KP, segk);
+  {
+    float4 v0[LDV], v1[LDV];
+    load_group(stack, P, C, pbase, lane, v0);
+    load_group(stack, P, C, pbase + 32, lane, v1);
+    build_b_f16<KS16>(v0, C, bd, stg, mult, segk, lane, j, h, bh0, bl0);
+    build_b_f16<KS16>(v1, C, bd, stg, mult, segk, lane, j, h, bh1, bl1);
   }
-  for (int r0 = 0; r0 < Rpad; r0 += RCH) {
-    __syncthreads();
+
+  const char *gref = reinterpret_cast<const char *>(refh);
+  auto issue = [&](int c) {
+    const char *g = gref + (int64_t)c * CHB + lane * 16;
+    char *l = ldsb + (c & 1) * CHB;
+    for (int q = w; q < NPC; q += 4)
+      __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
+  };
+  issue(0);
+
+  float best0 = -__builtin_inff(), best1 = -__builtin_inff();
+  int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
+  const int nch = Rpad / RCH;
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // chunk c landed (vmcnt(0) + barrier); everyone is past chunk c-1
+    if (c + 1 < nch) issue(c + 1);
+    const char *buf = ldsb + (c & 1) * CHB;
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      const int e = tid + q * 256;
-      const int rr = e / VEC, cc = e - rr * VEC;
-      *reinterpret_cast<u32x4 *>(ldsb + rr * STRIDE + cc * 16) = pf[q];
-    }
-    __syncthreads();
-    if (r0 + RCH < Rpad) {
-      const u32x4 *gsrc = reinterpret_cast<const u32x4 *>(refh + (int64_t)(r0 + RCH) * 2 * KP);
-#pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        pf[q] = gsrc[tid + q * 256];
-      }
-    }
-#pragma unroll 1
     for (int rb = 0; rb < RCH; rb += 32) {
       f32x16 acc0 = {0}, acc1 = {0};
-      const char *row = ldsb + (rb + j) * STRIDE + 16 * h;
+      const char *row = buf + (rb + j) * ROWB + 16 * h;
 #pragma unroll
       for (int s = 0; s < KS16; ++s) {
         const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
@@ -345,23 +412,24 @@ __global__ __launch_bounds__(256) void classify_pixels_f16_kernel(const float *_
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
       }
+      const int rbase = c * RCH + rb;
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
-        const int r = r0 + rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const bool ok = r < R;
-        const float s0 = acc0[reg];
-        const float s1 = acc1[reg];
-        if (ok && s0 > best[0]) {
-          best[0] = s0;
-          bidx[0] = r;
+        const int r = rbase + (reg & 3) + 8 * (reg >> 2);
+        const float s0 = acc0[reg], s1 = acc1[reg];
+        if (s0 > best0) {
+          best0 = s0;
+          bi0 = r;
         }
-        if (ok && s1 > best[1]) {
-          best[1] = s1;
-          bidx[1] = r;
+        if (s1 > best1) {
+          best1 = s1;
+          bi1 = r;
         }
       }
     }
   }
+  float best[2] = {best0, best1};
+  int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const float ob = __shfl_xor(best[g], 32, 64);
@@ -483,8 +551,8 @@ hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mod
     HRF_REQUIRE(ks > 0, "classify: C + nseg must be <= 128");
     *kp_host = 2 * ks;
   } else {
-    const int ks16 = (int)hrf::cdiv(C + nseg, 16);
-    HRF_REQUIRE(ks16 >= 1 && ks16 <= 8, "classify: C + nseg must be <= 128");
+    const int ks16 = (int)hrf::cdiv(C + nseg + 1, 16);  // + the validity-bias column
+    HRF_REQUIRE(ks16 >= 1 && ks16 <= 8, "classify: C + nseg must be <= 127");
     *kp_host = 16 * ks16;
   }
   *rpad_host = (int32_t)(hrf::cdiv(R, RCH) * RCH);
@@ -521,7 +589,7 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
   hipStream_t s = (hipStream_t)stream;
   if (mode == 1) {
     const int ks16 = kp / 16;
-    const size_t shm = std::max<size_t>((size_t)RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * C);
+    const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * (C + MROW) + 128);
     HRF_REQUIRE(shm <= 160 * 1024, "classify_pixels: C too large for LDS staging");
 #define HRF_CP16(K)                                                                                          \
   case K:                                                                                                    \

@@ -415,7 +415,7 @@ def classify_prepare(ref, bounds, mode=None):
     if mode == 0:
         refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
     else:
-        refx = torch.empty((rp, 2 * kp), dtype=torch.float16, device=ref.device)
+        refx = torch.empty((rp, 2 * kp + 8), dtype=torch.float16, device=ref.device)  # hi | lo | pad
     _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, mode, _ptr(refx), _stream())
     return refx
 

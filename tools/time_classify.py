@@ -1,0 +1,38 @@
+"""Time hrf_classify_pixels on a resident 2048x2048x95 stack for several library sizes
+(separates the per-workgroup prologue from the per-reference sweep)."""
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from hiprfish_image_analysis_amd import kernels as K  # noqa: E402
+from hiprfish_image_analysis_amd import synthetic as S  # noqa: E402
+
+
+def main():
+    H = W = 2048
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    stack = torch.rand((H, W, 95), generator=g, device="cuda")
+    for R in [int(a) for a in (sys.argv[1:] or ["64", "256", "1023"])]:
+        ref = torch.rand((R, 95), generator=g, device="cuda")
+        refx = K.classify_prepare(ref, S.ECOLI_BOUNDS)
+        for _ in range(2):
+            K.classify_pixels(stack, refx, R, S.ECOLI_BOUNDS)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = 5
+        e0.record()
+        for _ in range(n):
+            K.classify_pixels(stack, refx, R, S.ECOLI_BOUNDS)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / n
+        tf = 2.0 * H * W * R * 95 / ms / 1e9
+        print("R=%5d  %.3f ms  %.1f TF/s algorithmic  %.1f TF/s executed" % (R, ms, tf, 3 * tf * 112 / 95))
+
+
+if __name__ == "__main__":
+    t = time.time()
+    main()
