@@ -7,8 +7,10 @@
 // integer atomics, so the centres -- and therefore every label -- are independent of the
 // reduction order and identical to the CPU restatement bit for bit.
 //
-// Device-resident loop: accumulate (one streaming pass) -> update (1 thread) per iteration;
-// both early-exit once converged, so the host launches fixed batches and polls rarely.
+// Device-resident loop: ONE launch per Lloyd iteration.  Launch `it` first applies update
+// number `it` (every block derives the same centres from the previous launch's integer sums),
+// then streams the data once accumulating into a rotating sum buffer; it exits at once when
+// converged, so the host launches batches and polls rarely.
 #include <algorithm>
 
 #include "common.hpp"
@@ -19,9 +21,10 @@ namespace {
 constexpr int KMAX = 8;
 
 struct KmState {
-  double center[KMAX];
-  long long sum[KMAX];
-  unsigned long long cnt[KMAX];
+  double center[KMAX];         // final centres (read by the host and km_label_kernel)
+  double cen[2][KMAX];         // centres used by launch it live in cen[it & 1]
+  long long sum[3][KMAX];      // launch it accumulates into sum[it % 3]
+  unsigned long long cnt[3][KMAX];
   unsigned long long lo_bits, hi_bits;  // order-preserving encodings of min / max
   unsigned long long amax_bits;         // |x| max (non-negative doubles order as uint64)
   unsigned long long nvalid;
@@ -95,8 +98,9 @@ __global__ void km_init_kernel(KmState *st, int k) {
   st->scale = 61 - ln - e;
   for (int j = 0; j < KMAX; ++j) {
     st->center[j] = j < k ? mn + ((double)j + 0.5) * (mx - mn) / (double)k : 0.0;
-    st->sum[j] = 0;
-    st->cnt[j] = 0;
+    st->cen[0][j] = st->cen[1][j] = st->center[j];  // launch 0 reads cen[1]
+    st->sum[0][j] = 0;
+    st->cnt[0][j] = 0;
   }
   st->k = k;
   st->converged = nv == 0;
@@ -119,13 +123,40 @@ __device__ __forceinline__ int km_assign(double v, const double *c) {
 }
 
 template <int K>
-__global__ __launch_bounds__(256) void km_accum_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid,
-                                                      int64_t n, KmState *st) {
+__global__ __launch_bounds__(256) void km_step_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid,
+                                                     int64_t n, KmState *st, int it, int max_iter) {
   if (st->converged) return;
+  const int s = st->scale;
   double c[K];
 #pragma unroll
-  for (int j = 0; j < K; ++j) c[j] = st->center[j];
-  const int s = st->scale;
+  for (int j = 0; j < K; ++j) c[j] = st->cen[(it + 1) & 1][j];
+  if (it > 0) {
+    // update number `it` (the former km_update_kernel), identical in every block
+    const int pb = (it + 2) % 3;
+    int changed = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const unsigned long long cn = st->cnt[pb][j];
+      if (cn) {
+        const double cj = ldexp((double)st->sum[pb][j] / (double)cn, -s);
+        if (cj != c[j]) changed = 1;
+        c[j] = cj;
+      }
+    }
+    if (!changed || it >= max_iter) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int j = 0; j < K; ++j) st->center[j] = c[j];
+        st->iters = it;
+        st->converged = 1;
+      }
+      return;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < K) {
+    st->cen[it & 1][threadIdx.x] = c[threadIdx.x];
+    st->sum[(it + 1) % 3][threadIdx.x] = 0;
+    st->cnt[(it + 1) % 3][threadIdx.x] = 0;
+  }
   long long sum[K];
   unsigned long long cnt[K];
 #pragma unroll
@@ -162,27 +193,10 @@ __global__ __launch_bounds__(256) void km_accum_kernel(const double *__restrict_
     const long long a = ssum[0][j] + ssum[1][j] + ssum[2][j] + ssum[3][j];
     const unsigned long long b = scnt[0][j] + scnt[1][j] + scnt[2][j] + scnt[3][j];
     if (b) {
-      atomicAdd((unsigned long long *)&st->sum[j], (unsigned long long)a);
-      atomicAdd(&st->cnt[j], b);
+      atomicAdd((unsigned long long *)&st->sum[it % 3][j], (unsigned long long)a);
+      atomicAdd(&st->cnt[it % 3][j], b);
     }
   }
-}
-
-__global__ void km_update_kernel(KmState *st, int max_iter) {
-  if (st->converged) return;
-  int changed = 0;
-  const int s = st->scale;
-  for (int j = 0; j < st->k; ++j) {
-    if (st->cnt[j]) {
-      const double c = ldexp((double)st->sum[j] / (double)st->cnt[j], -s);
-      if (c != st->center[j]) changed = 1;
-      st->center[j] = c;
-    }
-    st->sum[j] = 0;
-    st->cnt[j] = 0;
-  }
-  st->iters += 1;
-  if (!changed || st->iters >= max_iter) st->converged = 1;
 }
 
 template <int K>
@@ -223,14 +237,13 @@ hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter
   int batch = 4;
   int conv = 0;
   while (!done) {
-    for (int b = 0; b < batch && launched < max_iter; ++b, ++launched) {
-      km_accum_kernel<K><<<gr, 256, 0, s>>>(x, valid, n, st);
-      km_update_kernel<<<1, 1, 0, s>>>(st, max_iter);
-    }
+    // launch `it` applies update `it`; update max_iter ends the fit, so at most max_iter + 1
+    for (int b = 0; b < batch && launched <= max_iter; ++b, ++launched)
+      km_step_kernel<K><<<gr, 256, 0, s>>>(x, valid, n, st, launched, max_iter);
     HRF_LAUNCHED();
     HRF_HIP(hipMemcpyAsync(&conv, &st->converged, sizeof(int), hipMemcpyDeviceToHost, s));
     HRF_HIP(hipStreamSynchronize(s));
-    done = conv || launched >= max_iter;
+    done = conv || launched > max_iter;
     batch = batch < 16 ? batch * 2 : 16;
   }
   if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
