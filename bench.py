@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--tiles", type=int, default=2, help="distinct resident tiles per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-pixel", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the per-pixel classification after the segmentation on one stream")
     args = ap.parse_args()
 
     import torch
@@ -98,20 +100,12 @@ def main():
     torch.cuda.synchronize()
 
     per_pixel = not args.no_per_pixel
-    stream = torch.cuda.current_stream()
     ev = []
 
     def step(i, timed):
         stack = tiles[i % len(tiles)]
-        res = P.process_tile(stack, lib, per_pixel=False)
-        if per_pixel:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            res.pixel_idx, res.pixel_dist = P.classify_pixels(stack, lib)
-            e1.record(stream)
-            if timed:
-                ev.append((e0, e1))
+        res = P.process_tile(stack, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
+                             pixel_events=ev if timed else None)
         if world > 1:
             P.allreduce_counts(res.counts)
         return res
@@ -146,11 +140,23 @@ def main():
                                "E. coli segmentation + per-cell spectra + per-cell and per-pixel segmented-cosine "
                                "classification + barcode counts" + (" (RCCL all-reduce of counts)" if world > 1 else ""),
                    "H": H, "W": W, "C": C, "R": lib.R, "per_pixel": per_pixel, "cells_last_tile": ncells,
-                   "parallelism": "tile-sharded x%d" % world},
+                   "parallelism": "tile-sharded x%d" % world,
+                   "per_pixel_overlap": per_pixel and not args.no_overlap},
     }
     if per_pixel and ev:
         from hiprfish_image_analysis_amd import kernels as K
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        # the same kernel alone on the GPU (after the timed region): with the overlap the
+        # timed-region duration includes the compute units it shares with the segmentation
+        iso = []
+        for i in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            P.classify_pixels(tiles[i % len(tiles)], lib)
+            b.record()
+            iso.append((a, b))
+        torch.cuda.synchronize()
+        ms_iso = float(np.mean([a.elapsed_time(b) for a, b in iso]))
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
         ach = flops / (ms * 1e-3) / 1e12
         mode = K.CLASSIFY_MODE
@@ -170,7 +176,11 @@ def main():
                            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(ach / peak, 4), "traffic": traffic, "kernel_ms": round(ms, 4),
                            "mfma_dtype": "f16 (split hi/lo, 3 MFMA per f32 product)" if mode == 1 else "f32",
-                           "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4)}
+                           "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4),
+                           "overlapped_with_segmentation": not args.no_overlap,
+                           "isolated_kernel_ms": round(ms_iso, 4),
+                           "isolated_achieved": round(flops / (ms_iso * 1e-3) / 1e12, 2),
+                           "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline(ref, bounds)
     if rank == 0:

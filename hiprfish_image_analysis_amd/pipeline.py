@@ -147,15 +147,55 @@ class TileResult:
     pixel_dist: torch.Tensor | None = None
 
 
-def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0):
-    """One tile of the hot path: measure (segment + per-cell spectra) + classify + count."""
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(device)
+    if s is None:
+        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0,
+                 overlap: bool = True, pixel_events: list | None = None):
+    """One tile of the hot path: measure (segment + per-cell spectra) + classify + count.
+
+    The per-pixel classification does not depend on the segmentation, so with `overlap` it
+    runs on a side stream concurrently with the segmentation chain (many small, latency-bound
+    launches and a few host synchronisations) and fills the compute units that chain leaves
+    idle; the caller's stream joins it before returning.  `pixel_events`, if given, receives
+    the (start, end) events recorded around the classification on the stream it ran on."""
+    main = torch.cuda.current_stream(stack.device)
+    pix = None
+    if per_pixel:
+        refx = lib.refx()                                     # prepared on the caller's stream
+        side = _side_stream(stack.device) if overlap else main
+        if overlap:
+            side.wait_stream(main)                            # stack (and refx) ready
+        with torch.cuda.stream(side):
+            e0 = e1 = None
+            if pixel_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(side)
+            pix = K.classify_pixels(stack, refx, lib.R, lib.bounds)
+            if pixel_events is not None:
+                e1.record(side)
+                pixel_events.append((e0, e1))
+        if overlap:
+            stack.record_stream(side)
+            refx.record_stream(side)
     meas = measure_ecoli(stack, calibration)
     idx, dist = classify_cells(meas.avgint_norm, lib, variant)
     counts = K.barcode_counts(idx, lib.R)                       # collect_measurement_results.py:92-98
     ident = K.paint_ids(meas.segmentation, idx + 1)             # image_classification.py:65-71
     res = TileResult(meas, idx, dist, counts, ident)
     if per_pixel:
-        res.pixel_idx, res.pixel_dist = classify_pixels(stack, lib)
+        if overlap:
+            main.wait_stream(side)
+            for t in pix:
+                t.record_stream(main)
+        res.pixel_idx, res.pixel_dist = pix
     return res
 
 
