@@ -63,9 +63,10 @@ def _cpu_baseline(ref, bounds):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--tiles", type=int, default=2, help="distinct resident tiles per rank")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--tiles", type=int, default=0, help="distinct resident tiles per rank (default 2*concurrent)")
+    ap.add_argument("--concurrent", type=int, default=2, help="tiles processed concurrently per step per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-pixel", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
@@ -92,6 +93,8 @@ def main():
     lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), bounds, NBIT)
     lib.refx()
     tiles = []
+    if args.tiles <= 0:
+        args.tiles = 2 * max(1, args.concurrent)
     for t in range(args.tiles):
         seed = 20190101 + rank * 1000 + t
         lay = S.cell_layout(H, W, S.default_ncells(H, W), lib.R, seed)
@@ -102,13 +105,30 @@ def main():
     per_pixel = not args.no_per_pixel
     ev = []
 
+    T = max(1, args.concurrent)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(T)] if T > 1 else [torch.cuda.current_stream(dev)]
+    pool = None
+    if T > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(T)
+
+    def tile_job(j, stack, timed):
+        with torch.cuda.stream(streams[j]):
+            return P.process_tile(stack, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
+                                  pixel_events=ev if timed else None)
+
     def step(i, timed):
-        stack = tiles[i % len(tiles)]
-        res = P.process_tile(stack, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
-                             pixel_events=ev if timed else None)
+        # T tiles per step, each on its own stream driven by its own host thread (the
+        # segmentation chain of one tile is latency-bound and synchronises with the host)
+        stacks = [tiles[(i * T + j) % len(tiles)] for j in range(T)]
+        if pool is None:
+            res = [tile_job(0, stacks[0], timed)]
+        else:
+            res = [f.result() for f in [pool.submit(tile_job, j, stacks[j], timed) for j in range(T)]]
         if world > 1:
-            P.allreduce_counts(res.counts)
-        return res
+            for r in res:
+                P.allreduce_counts(r.counts)
+        return res[-1]
 
     for i in range(args.warmup):
         step(i, False)
@@ -129,7 +149,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    pixels = H * W * args.steps * world
+    pixels = H * W * args.steps * world * T
     value = pixels / elapsed / 1e6
     out = {
         "metric": "Mpixel-spectra/s (segment+classify) on 2048²×95 vs 1023 refs; 1/2/4/8 GPU",
@@ -140,7 +160,8 @@ def main():
                                "E. coli segmentation + per-cell spectra + per-cell and per-pixel segmented-cosine "
                                "classification + barcode counts" + (" (RCCL all-reduce of counts)" if world > 1 else ""),
                    "H": H, "W": W, "C": C, "R": lib.R, "per_pixel": per_pixel, "cells_last_tile": ncells,
-                   "parallelism": "tile-sharded x%d" % world,
+                   "parallelism": "tile-sharded x%d" % world, "tiles_per_step_per_gpu": T,
+                   "global_batch": T * world,
                    "per_pixel_overlap": per_pixel and not args.no_overlap},
     }
     if per_pixel and ev:

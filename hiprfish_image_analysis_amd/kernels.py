@@ -177,11 +177,12 @@ def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True):
     x = _dev(x, torch.float64, "x")
     n = x.numel()
     dev = x.device
-    st = _KM_STATE.get(dev)
+    key = (dev, _stream())        # one workspace per stream: concurrent tiles must not share it
+    st = _KM_STATE.get(key)
     if st is None:
         nb = _lib.lib().hrf_kmeans_state_bytes()
         st = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
-        _KM_STATE[dev] = st
+        _KM_STATE[key] = st
     v = _u8(valid, "valid") if valid is not None else None
     labels = torch.empty(x.shape, dtype=torch.int32, device=dev) if want_labels else None
     top = torch.empty(x.shape, dtype=torch.uint8, device=dev)

@@ -150,10 +150,13 @@ class TileResult:
 _SIDE_STREAMS: dict = {}
 
 
-def _side_stream(device) -> torch.cuda.Stream:
-    s = _SIDE_STREAMS.get(device)
+def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
+    """the side stream paired with `main` (one per caller stream, so concurrent tiles on
+    different streams do not serialise on a shared one)"""
+    key = (main.device, main.cuda_stream)
+    s = _SIDE_STREAMS.get(key)
     if s is None:
-        s = _SIDE_STREAMS[device] = torch.cuda.Stream(device=device)
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=main.device)
     return s
 
 
@@ -170,7 +173,7 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
     pix = None
     if per_pixel:
         refx = lib.refx()                                     # prepared on the caller's stream
-        side = _side_stream(stack.device) if overlap else main
+        side = _side_stream(main) if overlap else main
         if overlap:
             side.wait_stream(main)                            # stack (and refx) ready
         with torch.cuda.stream(side):
