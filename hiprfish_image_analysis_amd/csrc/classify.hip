@@ -20,6 +20,7 @@
 // Per cell (reference semantics, gated by presence flags): f64, exact channel order of the
 // restatement, one workgroup per cell -- bit-identical to oracle_segcos.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -265,14 +266,14 @@ __device__ __forceinline__ void load_group(const float *__restrict__ stack, int6
 constexpr int MROW = 24;
 __device__ __forceinline__ void build_segk(const Bounds &bd, int32_t C, int KP, uint8_t *segk) {
   for (int k = threadIdx.x; k < KP; k += blockDim.x) {
-    int v = 17;
+    int v = 0x80 | 17;  // bit 7: not a channel (the value is the multiplier slot itself)
     if (k < C) {
       v = 0;
       for (int t = 1; t < bd.nseg; ++t) v += k >= bd.b[t];
     } else if (k < C + bd.nseg) {
-      v = 8 + (k - C);
+      v = 0x80 | (8 + (k - C));
     } else if (k == C + bd.nseg) {
-      v = 16;
+      v = 0x80 | 16;
     }
     segk[k] = (uint8_t)v;
   }
@@ -331,9 +332,11 @@ __device__ __forceinline__ void build_b_f16(const float4 (&v)[LDV], int32_t C, c
     h8 vh, vl;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int k = 16 * s + 8 * h + q;
-      const float raw = k < C ? pc[16 * s + q] : 1.0f;
-      float x = raw * mj[sk[16 * s + q]];
+      // the channel test comes from the column map (a load), not from k < C, which the
+      // compiler would hoist out of the tile loop as 56 live masks
+      const int code = sk[16 * s + q];
+      const float m = mj[code & 31];
+      float x = (code & 0x80) ? m : pc[16 * s + q] * m;
       asm volatile("" : "+v"(x));  // round to f32 first: no fused multiply-to-f16
       const _Float16 hv = (_Float16)x;
       vh[q] = hv;
@@ -392,6 +395,28 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
 
   float best0 = -__builtin_inff(), best1 = -__builtin_inff();
   int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
+  // Software-pipelined argmax: the scores of block b are compared while block b+1's MFMAs
+  // run (a slice of the 16 registers after each k-step), so the epilogue's VALU fills the MFMA
+  // issue gaps instead of following them.  Blocks are still consumed in increasing row order.
+  f32x16 pv0, pv1;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) pv0[reg] = pv1[reg] = -__builtin_inff();
+  int pr = 0;  // first row of the pending block
+  auto epi = [&](int lo, int hi) {
+#pragma unroll
+    for (int reg = lo; reg < hi; ++reg) {
+      const int r = pr + (reg & 3) + 8 * (reg >> 2);
+      const float s0 = pv0[reg], s1 = pv1[reg];
+      if (s0 > best0) {
+        best0 = s0;
+        bi0 = r;
+      }
+      if (s1 > best1) {
+        best1 = s1;
+        bi1 = r;
+      }
+    }
+  };
   const int nch = Rpad / RCH;
   for (int c = 0; c < nch; ++c) {
     __syncthreads();  // chunk c landed (vmcnt(0) + barrier); everyone is past chunk c-1
@@ -411,23 +436,14 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1[s], acc1, 0, 0, 0);
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
+        epi((16 * s) / KS16, (16 * (s + 1)) / KS16);  // previous block, slice s
       }
-      const int rbase = c * RCH + rb;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int r = rbase + (reg & 3) + 8 * (reg >> 2);
-        const float s0 = acc0[reg], s1 = acc1[reg];
-        if (s0 > best0) {
-          best0 = s0;
-          bi0 = r;
-        }
-        if (s1 > best1) {
-          best1 = s1;
-          bi1 = r;
-        }
-      }
+      pv0 = acc0;
+      pv1 = acc1;
+      pr = c * RCH + rb;
     }
   }
+  epi(0, 16);  // the last block
   float best[2] = {best0, best1};
   int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
 #pragma unroll
