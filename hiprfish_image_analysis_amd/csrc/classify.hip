@@ -462,6 +462,275 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
   }
 }
 
+// ---- mode 2: split-fp16 MFMA on the reference channel layouts ---------------------------------
+// The E. coli (95 channels, lasers 405/488/514/561/633: train_reference.py:1401) and
+// synthetic-community (63 channels, 488/514/561/633: :1488) layouts as compile-time segment
+// maps.  Every B-operand column's segment is then known at compile time, so the operand build
+// is straight-line code (a select only where the two lane halves straddle a segment bound)
+// with no LDS table lookups, and K = C + 1 (channels + the validity-bias column) instead of
+// C + nseg + 1: the zero-segment indicator terms (+1 for a segment that is zero in both the
+// pixel and the reference row) are added in the argmax epilogue, and only by a wave holding a
+// pixel with an all-zero segment (wave-uniform branch to a second copy of the sweep; each
+// prepared row carries its zero-segment mask in its pad bytes).  95 -> 96 columns: 6 k-steps
+// per 32-row block instead of 7.
+struct LayEcoli {
+  static constexpr int C = 95, NSEG = 5;
+  __host__ __device__ static constexpr int b(int s) {
+    return s <= 0 ? 0 : s == 1 ? 32 : s == 2 ? 55 : s == 3 ? 75 : s == 4 ? 89 : 95;
+  }
+};
+struct LayMulti {
+  static constexpr int C = 63, NSEG = 4;
+  __host__ __device__ static constexpr int b(int s) { return s <= 0 ? 0 : s == 1 ? 23 : s == 2 ? 43 : s == 3 ? 57 : 63; }
+};
+
+// segment of B-operand column k: 0..NSEG-1 for a channel, -1 for the bias column (k == C),
+// -2 for zero padding
+template <class L>
+__host__ __device__ constexpr int col_seg(int k) {
+  if (k > L::C) return -2;
+  if (k == L::C) return -1;
+  int s = 0;
+  for (int t = 1; t < L::NSEG; ++t) s += k >= L::b(t) ? 1 : 0;
+  return s;
+}
+template <class L>
+constexpr int lay_ks16() {
+  return (L::C + 1 + 15) / 16;
+}
+
+// Stage one loaded group in LDS and build its split-fp16 B operand (lane = pixel j, half h
+// holds columns 16s + 8h + q).  Segment norms in f64 from the lane's own columns plus the
+// other half's (one shuffle), as the restatement; zx = the pixel's all-zero segments.
+template <class L, int KS>
+__device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, int lane, int j, int h,
+                                            h8 (&bh)[KS], h8 (&bl)[KS], uint32_t &zx) {
+  const int nv = 8 * L::C;
+#pragma unroll
+  for (int i = 0; i < LDV; ++i) {
+    const int e4 = lane + 64 * i;
+    if (e4 < nv) reinterpret_cast<float4 *>(stg)[e4] = v[i];
+  }
+  __syncthreads();
+  const float *pc = stg + j * L::C + 8 * h;
+  float raw[KS][8];
+  double nn[L::NSEG];
+#pragma unroll
+  for (int s = 0; s < L::NSEG; ++s) nn[s] = 0.0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int sa = col_seg<L>(16 * s + q), sb = col_seg<L>(16 * s + 8 + q);
+      const float r = pc[16 * s + q];  // past the row end: another pixel's value, masked here
+      const float x = h ? (sb >= 0 ? r : 0.0f) : (sa >= 0 ? r : 0.0f);
+      raw[s][q] = x;
+      const double x2 = (double)x * (double)x;
+      if (sa == sb) {
+        if (sa >= 0) nn[sa >= 0 ? sa : 0] += x2;
+      } else {
+        if (sa >= 0) nn[sa >= 0 ? sa : 0] += h ? 0.0 : x2;
+        if (sb >= 0) nn[sb >= 0 ? sb : 0] += h ? x2 : 0.0;
+      }
+    }
+  float inv[L::NSEG];
+  zx = 0;
+#pragma unroll
+  for (int s = 0; s < L::NSEG; ++s) {
+    const double t = nn[s] + __shfl_xor(nn[s], 32, 64);
+    inv[s] = t > 0.0 ? (float)(1.0 / sqrt(t)) : 0.0f;
+    zx |= (t > 0.0 ? 0u : 1u) << s;
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    h8 vh, vl;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int sa = col_seg<L>(16 * s + q), sb = col_seg<L>(16 * s + 8 + q);
+      const float ma = sa >= 0 ? inv[sa >= 0 ? sa : 0] : (sa == -1 ? 1.0f : 0.0f);
+      const float mb = sb >= 0 ? inv[sb >= 0 ? sb : 0] : (sb == -1 ? 1.0f : 0.0f);
+      float x;
+      if (sa >= 0 && sb >= 0)
+        x = raw[s][q] * (h ? mb : ma);
+      else
+        x = h ? (sb >= 0 ? raw[s][q] * mb : mb) : (sa >= 0 ? raw[s][q] * ma : ma);
+      asm volatile("" : "+v"(x));  // round to f32 first: no fused multiply-to-f16
+      const _Float16 hv = (_Float16)x;
+      vh[q] = hv;
+      vl[q] = (_Float16)(x - (float)hv);
+    }
+    bh[s] = vh;
+    bl[s] = vl;
+  }
+  __syncthreads();
+}
+
+// The library sweep of one workgroup (see classify_pixels_f16_kernel); ZS adds the
+// zero-segment indicator terms popcount(zx & zr) to every score.
+template <int KS16, int ROWB, bool ZS>
+__device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w, int h,
+                                          const h8 (&bh0)[KS16], const h8 (&bl0)[KS16], const h8 (&bh1)[KS16],
+                                          const h8 (&bl1)[KS16], uint32_t zx0, uint32_t zx1, float &best0,
+                                          float &best1, int &bi0, int &bi1) {
+  constexpr int KP = 16 * KS16;
+  constexpr int CHB = RCH * ROWB;
+  constexpr int NPC = CHB / 1024;
+  const int j = lane & 31;
+  auto issue = [&](int c) {
+    const char *g = gref + (int64_t)c * CHB + lane * 16;
+    char *l = ldsb + (c & 1) * CHB;
+    for (int q = w; q < NPC; q += 4)
+      __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
+  };
+  issue(0);
+  f32x16 pv0, pv1;
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) pv0[reg] = pv1[reg] = -__builtin_inff();
+  int pr = 0;  // first row of the pending block
+  const unsigned char *zrow = reinterpret_cast<const unsigned char *>(gref) + 4 * KP + (int64_t)(4 * h) * ROWB;
+  auto epi = [&](int lo, int hi) {
+#pragma unroll
+    for (int reg = lo; reg < hi; ++reg) {
+      const int r = pr + (reg & 3) + 8 * (reg >> 2);
+      float s0 = pv0[reg], s1 = pv1[reg];
+      if (ZS) {
+        const uint32_t zr = zrow[(int64_t)r * ROWB];
+        s0 += (float)__popc(zx0 & zr);
+        s1 += (float)__popc(zx1 & zr);
+      }
+      if (s0 > best0) {
+        best0 = s0;
+        bi0 = r;
+      }
+      if (s1 > best1) {
+        best1 = s1;
+        bi1 = r;
+      }
+    }
+  };
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();  // chunk c landed (vmcnt(0) + barrier); everyone is past chunk c-1
+    if (c + 1 < nch) issue(c + 1);
+    const char *buf = ldsb + (c & 1) * CHB;
+#pragma unroll
+    for (int rb = 0; rb < RCH; rb += 32) {
+      f32x16 acc0 = {0}, acc1 = {0};
+      const char *row = buf + (rb + j) * ROWB + 16 * h;
+#pragma unroll
+      for (int s = 0; s < KS16; ++s) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
+        const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 32 * s);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1[s], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1[s], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
+        epi((16 * s) / KS16, (16 * (s + 1)) / KS16);  // previous block, slice s
+      }
+      pv0 = acc0;
+      pv1 = acc1;
+      pr = c * RCH + rb;
+    }
+  }
+  epi(0, 16);  // the last block
+}
+
+template <class L>
+__global__ __launch_bounds__(256, 2) void classify_pixels_lay_kernel(const float *__restrict__ stack, int64_t P,
+                                                                     const _Float16 *__restrict__ refh, int32_t R,
+                                                                     int32_t Rpad, int32_t *__restrict__ best_idx,
+                                                                     float *__restrict__ best_dist) {
+  constexpr int KS16 = lay_ks16<L>();
+  constexpr int KP = 16 * KS16;
+  constexpr int ROWB = 4 * KP + 16;
+  static_assert((RCH * ROWB) % 1024 == 0, "chunk must be whole 1 KiB pieces");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * 256 + w * 64;
+
+  h8 bh0[KS16], bl0[KS16], bh1[KS16], bl1[KS16];
+  uint32_t zx0 = 0, zx1 = 0;
+  float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
+  {
+    float4 v0[LDV], v1[LDV];
+    load_group(stack, P, L::C, pbase, lane, v0);
+    load_group(stack, P, L::C, pbase + 32, lane, v1);
+    build_b_lay<L, KS16>(v0, stg, lane, j, h, bh0, bl0, zx0);
+    build_b_lay<L, KS16>(v1, stg, lane, j, h, bh1, bl1, zx1);
+  }
+  float best0 = -__builtin_inff(), best1 = -__builtin_inff();
+  int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
+  const char *gref = reinterpret_cast<const char *>(refh);
+  char *ldsb = reinterpret_cast<char *>(lds);
+  const int nch = Rpad / RCH;
+  // every wave of the workgroup takes the same branch (the chunk barriers are shared)
+  if (__syncthreads_or((zx0 | zx1) != 0))
+    lay_sweep<KS16, ROWB, true>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1);
+  else
+    lay_sweep<KS16, ROWB, false>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1);
+  float best[2] = {best0, best1};
+  int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const float ob = __shfl_xor(best[g], 32, 64);
+    const int oi = __shfl_xor(bidx[g], 32, 64);
+    if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
+      best[g] = ob;
+      bidx[g] = oi;
+    }
+    const int64_t p = pbase + g * 32 + j;
+    if (h == 0 && p < P) {
+      best_idx[p] = bidx[g];
+      best_dist[p] = ((float)L::NSEG - best[g]) / (float)L::NSEG;
+    }
+  }
+}
+
+// mode-2 table: {hi[KP], lo[KP], pad 16 B} fp16 per row, KP = 16 * ceil((C + 1) / 16); column C
+// is the validity bias (0 real rows, -1024 padding rows); byte 4*KP of the row holds the row's
+// zero-segment mask.
+__global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
+                                    int32_t Rpad, _Float16 *__restrict__ refh) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= Rpad) return;
+  _Float16 *hi = refh + r * (2 * KP + 8);
+  _Float16 *lo = hi + KP;
+  for (int k = 0; k < 2 * KP + 8; ++k) hi[k] = (_Float16)0.0f;
+  hi[C] = (_Float16)(r < R ? 0.0f : -1024.0f);
+  if (r >= R) return;
+  const float *x = ref + r * C;
+  uint8_t zr = 0;
+  for (int s = 0; s < bd.nseg; ++s) {
+    double nn = 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) nn += (double)x[c] * (double)x[c];
+    const double inv = nn > 0 ? 1.0 / sqrt(nn) : 0.0;
+    for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) {
+      const float v = (float)((double)x[c] * inv);
+      const _Float16 h = (_Float16)v;
+      hi[c] = h;
+      lo[c] = (_Float16)(v - (float)h);
+    }
+    if (!(nn > 0)) zr |= (uint8_t)(1u << s);
+  }
+  reinterpret_cast<uint8_t *>(hi + 2 * KP)[0] = zr;
+}
+
+// 1 = E. coli layout, 2 = synthetic-community layout, 0 = other
+template <class L>
+bool is_layout(const Bounds &bd, int C) {
+  if (C != L::C || bd.nseg != L::NSEG) return false;
+  for (int s = 0; s <= L::NSEG; ++s)
+    if (bd.b[s] != L::b(s)) return false;
+  return true;
+}
+int layout_id(const Bounds &bd, int C) {
+  if (is_layout<LayEcoli>(bd, C)) return 1;
+  if (is_layout<LayMulti>(bd, C)) return 2;
+  return 0;
+}
+
 // ---- per cell, f64, gated variants; one workgroup per cell ----
 __device__ double seg_dist(const double *x, const double *y, int lo, int hi) {
   double d = 0, nx = 0, ny = 0;
@@ -561,8 +830,11 @@ extern "C" {
 hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mode, int32_t *kp_host,
                                  int32_t *rpad_host) {
   HRF_REQUIRE(C >= 1 && nseg >= 1 && nseg <= SMAX && R >= 1, "classify_geometry: bad arguments");
-  HRF_REQUIRE(mode == 0 || mode == 1, "classify_geometry: mode must be 0 (f32 MFMA) or 1 (split fp16 MFMA)");
-  if (mode == 0) {
+  HRF_REQUIRE(mode >= 0 && mode <= 2,
+              "classify_geometry: mode must be 0 (f32 MFMA), 1 (split fp16 MFMA) or 2 (split fp16, reference layouts)");
+  if (mode == 2) {
+    *kp_host = 16 * (int32_t)hrf::cdiv(C + 1, 16);
+  } else if (mode == 0) {
     const int ks = choose_ks(C + nseg);
     HRF_REQUIRE(ks > 0, "classify: C + nseg must be <= 128");
     *kp_host = 2 * ks;
@@ -582,7 +854,12 @@ hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, con
   int32_t kp = 0, rpad = 0;
   if (hrf_status s = hrf_classify_geometry(C, nseg, R, mode, &kp, &rpad)) return s;
   HRF_REQUIRE(ref && refx, "classify_prepare_refs: null buffer");
-  if (mode == 0)
+  HRF_REQUIRE(mode != 2 || layout_id(bd, C) != 0,
+              "classify: mode 2 needs the E. coli (0,32,55,75,89,95) or multispecies (0,23,43,57,63) layout");
+  if (mode == 2)
+    ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
+                                                                                          (_Float16 *)refx);
+  else if (mode == 0)
     ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
                                                                                       (float *)refx);
   else
@@ -603,6 +880,24 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
   HRF_REQUIRE(stack && refx && best_idx && best_dist, "classify_pixels: null buffer");
   const unsigned grid = (unsigned)hrf::cdiv(P, 256);
   hipStream_t s = (hipStream_t)stream;
+  if (mode == 2) {
+    const int lay = layout_id(bd, C);
+    HRF_REQUIRE(lay != 0, "classify: mode 2 needs the E. coli or multispecies channel layout");
+    const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * C);
+    if (lay == 1) {
+      hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayEcoli>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      classify_pixels_lay_kernel<LayEcoli><<<grid, 256, shm, s>>>(stack, P, (const _Float16 *)refx, R, rpad, best_idx,
+                                                                  best_dist);
+    } else {
+      hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayMulti>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+      classify_pixels_lay_kernel<LayMulti><<<grid, 256, shm, s>>>(stack, P, (const _Float16 *)refx, R, rpad, best_idx,
+                                                                  best_dist);
+    }
+    HRF_LAUNCHED();
+    return HRF_OK;
+  }
   if (mode == 1) {
     const int ks16 = kp / 16;
     const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * (C + MROW) + 128);

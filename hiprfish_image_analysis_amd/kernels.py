@@ -166,6 +166,20 @@ def mask_mul(a, mask):
     return out
 
 
+# ---- a4 -------------------------------------------------------------------------------------
+def nl_means_2d(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
+    """skimage.restoration.denoise_nl_means(img, patch_size, patch_distance, h, sigma=sigma)
+    on a 2-D f64 image (multispecies measurement.py:108)"""
+    img = _dev(img, torch.float64, "image")
+    if img.dim() != 2:
+        raise ValueError("nl_means_2d: 2-D image expected")
+    H, W = img.shape
+    out = torch.empty_like(img)
+    _lib.call("hrf_nl_means_2d", _ptr(img), H, W, int(patch_size), int(patch_distance), float(h), float(sigma),
+              _ptr(out), _stream())
+    return out
+
+
 # ---- a8 -------------------------------------------------------------------------------------
 _KM_STATE = {}
 

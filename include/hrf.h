@@ -105,6 +105,14 @@ HRF_API hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32
 HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out,
                                     hrf_stream_t stream);
 
+/* ==== a4: non-local means (nlmeans.hip) ==================================================
+ * skimage.restoration.denoise_nl_means(img, patch_size, patch_distance, h, fast_mode=True,
+ * sigma) on a 2-D f64 image (multispecies :108 h=0.02, biofilm :350): reflect padding,
+ * out (H, W) f64.  Built for the reference's defaults patch_size 7, patch_distance 11
+ * (others -> HRF_EINVAL). */
+HRF_API hrf_status hrf_nl_means_2d(const double *img, int64_t H, int64_t W, int32_t patch_size, int32_t patch_distance,
+                                   double h, double sigma, double *out, hrf_stream_t stream);
+
 /* ==== a8: 1-D KMeans (kmeans.hip) ======================================================
  * sklearn KMeans(k, random_state=0).fit_predict(x.reshape(-1,1)) restated as exact-integer
  * Lloyd iterations from a deterministic init (see oracle_kmeans_1d).  valid (nullable)

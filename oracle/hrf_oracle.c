@@ -798,6 +798,127 @@ EXPORT void oracle_paint_ids(const int32_t *lab, int64_t n, const int32_t *code,
     }
 }
 
+/* ------------------------------------------------------------------------------------
+ * a4 non-local means: skimage.restoration.denoise_nl_means(image, patch_size=7,
+ * patch_distance=11, h, fast_mode=True, sigma) on a 2-D image (multispecies :108 h=0.02,
+ * biofilm :350).  skimage is not installed here and the reference pins no version: the
+ * algorithm below is skimage's published fast 2-D path (_nl_means_denoising.pyx,
+ * _fast_nl_means_denoising_2d), parity against skimage itself is unpinned.
+ * ---------------------------------------------------------------------------------- */
+/* numpy.pad(mode='reflect') source index: mirror without repeating the edge */
+static int64_t reflect_idx(int64_t i, int64_t n) {
+    if (n == 1) return 0;
+    int64_t per = 2 * (n - 1), m = i % per;
+    if (m < 0) m += per;
+    return m < n ? m : per - m;
+}
+
+static double *reflect_pad(const double *img, int64_t H, int64_t W, int64_t pw) {
+    int64_t hp = H + 2 * pw, wp = W + 2 * pw;
+    double *p = (double *)malloc(sizeof(double) * hp * wp);
+    for (int64_t r = 0; r < hp; ++r)
+        for (int64_t c = 0; c < wp; ++c) p[r * wp + c] = img[reflect_idx(r - pw, H) * W + reflect_idx(c - pw, W)];
+    return p;
+}
+
+/* The algorithm as skimage runs it: reflect padding by offset + d + 1; for each shift
+ * t = (t_row in [-d, d], t_col in [0, d]) the integral image of the per-pixel squared
+ * differences between the image and its t-shifted copy (minus var) gives every patch
+ * distance in four lookups; a pair within the cutoff (distance / (h^2 s^2) <= 5) adds
+ * alpha * exp(-distance) to the weights of BOTH pixels and the other pixel's value to each
+ * result (alpha = 0.5 for t_col == 0, t_row != 0, whose pairs are visited twice; the zero
+ * shift credits its pixel twice); result / weights, padding cropped.  Rows and columns
+ * within offset of the padded border (they only reach cropped pixels) are skipped. */
+EXPORT void oracle_nl_means_skimage(const double *img, int64_t H, int64_t W, int patch, int dist, double h,
+                                    double sigma, double *out) {
+    const int s = patch % 2 == 0 ? patch + 1 : patch;
+    const int off = s / 2;
+    const int64_t pw = off + dist + 1, nr = H + 2 * pw, nc = W + 2 * pw;
+    double *P = reflect_pad(img, H, W, pw);
+    double *res = (double *)calloc((size_t)(nr * nc), sizeof(double));
+    double *wt = (double *)calloc((size_t)(nr * nc), sizeof(double));
+    double *I = (double *)malloc(sizeof(double) * nr * nc);
+    const double h2 = h * h, s2 = (double)s * (double)s, h2s2 = 1.0 * h2 * s2, var = sigma * sigma;
+    for (int tr = -dist; tr <= dist; ++tr)
+        for (int tc = 0; tc <= dist; ++tc) {
+            const double alpha = (tc == 0 && tr != 0) ? 0.5 : 1.0;
+            memset(I, 0, sizeof(double) * nr * nc);
+            const int64_t rs = tr < 0 ? -tr : 1, re = tr > 0 ? nr - tr : nr;
+            for (int64_t r = (rs > 1 ? rs : 1); r < re; ++r)
+                for (int64_t c = 1; c < nc - tc; ++c) {
+                    double t = P[r * nc + c] - P[(r + tr) * nc + c + tc];
+                    double d = t * t;
+                    d -= 1.0 * var;
+                    I[r * nc + c] = d + I[(r - 1) * nc + c] + I[r * nc + c - 1] - I[(r - 1) * nc + c - 1];
+                }
+            const int64_t r_lo = (off + 1 > off - tr) ? off + 1 : off - tr;
+            const int64_t r_hi = (nr - off < nr - off - tr) ? nr - off : nr - off - tr;
+            for (int64_t r = r_lo; r < r_hi; ++r)
+                for (int64_t c = off + 1; c < nc - off - tc; ++c) {
+                    double D = I[(r + off) * nc + c + off] + I[(r - off - 1) * nc + c - off - 1] -
+                               I[(r - off - 1) * nc + c + off] - I[(r + off) * nc + c - off - 1];
+                    D = (D > 0.0 ? D : 0.0) / h2s2;
+                    if (D > 5.0) continue;
+                    const double w = alpha * exp(-D);
+                    const int64_t q = (r + tr) * nc + c + tc;
+                    wt[r * nc + c] += w;
+                    wt[q] += w;
+                    res[r * nc + c] += w * P[q];
+                    res[q] += w * P[r * nc + c];
+                }
+        }
+    for (int64_t r = 0; r < H; ++r)
+        for (int64_t c = 0; c < W; ++c) {
+            const int64_t i = (r + pw) * nc + c + pw;
+            out[r * W + c] = res[i] / wt[i];
+        }
+    free(P);
+    free(res);
+    free(wt);
+    free(I);
+}
+
+/* The same weights per pixel, in the summation order of libhrf's nl_means_kernel:
+ * out[p] = (2 P[p] + sum_s w_s P[p+s]) / (2 + sum_s w_s) over the full (2d+1)^2 window
+ * (s != 0) in raster order of s; patch distance = sum over 7 rows (top to bottom) of the
+ * row's 7 squared differences (left to right); w = exp(-max(D,0)/h2s2) if <= 5 else 0. */
+EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, int dist, double h, double sigma,
+                            double *out) {
+    const int s = patch % 2 == 0 ? patch + 1 : patch;
+    const int off = s / 2;
+    const int64_t pw = off + dist, wp = W + 2 * pw;
+    double *P = reflect_pad(img, H, W, pw);
+    const double h2 = h * h, s2 = (double)s * (double)s, h2s2 = 1.0 * h2 * s2, var = sigma * sigma;
+    for (int64_t r = 0; r < H; ++r)
+        for (int64_t c = 0; c < W; ++c) {
+            const double *p = P + (r + pw) * wp + (c + pw);
+            double acc = p[0] + p[0], ws = 2.0;
+            for (int sr = -dist; sr <= dist; ++sr)
+                for (int sc = -dist; sc <= dist; ++sc) {
+                    if (sr == 0 && sc == 0) continue;
+                    const double *q = p + sr * wp + sc;
+                    double D = 0.0;
+                    for (int du = -off; du <= off; ++du) {
+                        double hs = 0.0;
+                        for (int dv = -off; dv <= off; ++dv) {
+                            const double t = p[du * wp + dv] - q[du * wp + dv];
+                            const double sq = t * t - var;
+                            hs = dv == -off ? sq : hs + sq;
+                        }
+                        D = du == -off ? hs : D + hs;
+                    }
+                    const double d = (D > 0.0 ? D : 0.0) / h2s2;
+                    if (d <= 5.0) {
+                        const double w = exp(-d);
+                        ws += w;
+                        acc += w * q[0];
+                    }
+                }
+            out[r * W + c] = acc / ws;
+        }
+    free(P);
+}
+
 /* ecoli measurement.py:116-126 (per-cell shape filter + 2x binary_erosion of the cell) */
 EXPORT void oracle_shape_filter(const int32_t *lab, int64_t H, int64_t W, const double *stats, int32_t nlab,
                                 double lo, double hi, int32_t *out) {

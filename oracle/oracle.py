@@ -112,6 +112,39 @@ def enhance_3d(pad, patch=11, ntheta=9, nphi=9):
     return out
 
 
+# ---- a4 -------------------------------------------------------------------------------
+def nl_means(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
+    """skimage.restoration.denoise_nl_means (fast 2-D) in libhrf's summation order"""
+    im = _c(img, np.float64)
+    out = np.zeros(im.shape, np.float64)
+    lib().oracle_nl_means(_p(im), I64(im.shape[0]), I64(im.shape[1]), patch_size, patch_distance,
+                          ctypes.c_double(h), ctypes.c_double(sigma), _p(out))
+    return out
+
+
+def nl_means_skimage(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
+    """skimage's fast 2-D NL-means algorithm itself (integral images, symmetric pair credit)"""
+    im = _c(img, np.float64)
+    out = np.zeros(im.shape, np.float64)
+    lib().oracle_nl_means_skimage(_p(im), I64(im.shape[0]), I64(im.shape[1]), patch_size, patch_distance,
+                                  ctypes.c_double(h), ctypes.c_double(sigma), _p(out))
+    return out
+
+
+def register_translation(src, target):
+    """skimage.feature.register_translation(src, target)[0] with its defaults (upsample_factor 1):
+    argmax |ifft(F(src) conj(F(target)))|, wrapped to (-n/2, n/2] per axis (numpy FFT)."""
+    src = np.asarray(src, np.float64)
+    target = np.asarray(target, np.float64)
+    cc = np.fft.ifftn(np.fft.fftn(src) * np.fft.fftn(target).conj())
+    maxima = np.unravel_index(np.argmax(np.abs(cc)), cc.shape)
+    shifts = np.array(maxima, dtype=np.float64)
+    mid = np.array([np.fix(n / 2) for n in cc.shape])
+    big = shifts > mid
+    shifts[big] -= np.array(cc.shape)[big]
+    return shifts
+
+
 # ---- a9/a10/a12/a13 ------------------------------------------------------------------
 def label(img, conn=2):
     """skimage.measure.label(img, connectivity=conn) (background 0, equal-value components)"""

@@ -86,6 +86,30 @@ def test_label_raster_numbering(orc, golden):
     assert np.array_equal(l4, g["l4"])
 
 
+@pytest.mark.parametrize("shape,h,sigma", [((40, 52), 0.02, 0.0), ((33, 29), 0.1, 0.0), ((7, 5), 0.05, 0.01),
+                                           ((1, 9), 0.05, 0.0)])
+def test_nl_means_restatement_equals_integral_image_algorithm(orc, shape, h, sigma):
+    """a4: the per-pixel formulation libhrf computes (oracle_nl_means) equals skimage's
+    integral-image / symmetric-pair algorithm (oracle_nl_means_skimage) to rounding.
+    skimage itself is absent: parity to skimage is unpinned."""
+    rng = np.random.default_rng(sum(shape))
+    yy, xx = np.mgrid[0:shape[0], 0:shape[1]]
+    img = 0.5 + 0.3 * np.sin(yy / 6.0) * np.cos(xx / 5.0) + 0.01 * rng.standard_normal(shape)
+    a = orc.nl_means(img, 7, 11, h, sigma)
+    b = orc.nl_means_skimage(img, 7, 11, h, sigma)
+    np.testing.assert_allclose(a, b, rtol=1e-11, atol=0)
+    assert np.abs(a - img).max() > 1e-4          # it actually denoises
+
+
+def test_register_translation_restatement(orc):
+    """f1: numpy restatement of skimage.feature.register_translation recovers known shifts"""
+    rng = np.random.default_rng(1)
+    img = rng.random((64, 80))
+    for dr, dc in [(3, -5), (-7, 2), (0, 0), (15, 15)]:
+        moved = np.roll(img, (dr, dc), axis=(0, 1))
+        assert tuple(orc.register_translation(img, moved)) == (-dr, -dc)
+
+
 def _same_partition(a, b):
     pairs = set(zip(a.tolist(), b.tolist()))
     return len(pairs) == len(set(a.tolist())) == len(set(b.tolist()))

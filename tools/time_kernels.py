@@ -1,0 +1,50 @@
+"""Time individual libhrf kernels on resident 2048x2048 inputs (HIP events, mean of 5).
+
+python tools/time_kernels.py [nlmeans] [classify] [register]
+"""
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from hiprfish_image_analysis_amd import kernels as K  # noqa: E402
+from hiprfish_image_analysis_amd import synthetic as S  # noqa: E402
+
+
+def timed(fn, n=5):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def main():
+    what = sys.argv[1:] or ["nlmeans", "classify"]
+    H = W = 2048
+    if "nlmeans" in what:
+        stack, _, _, _ = S.tile(H, W, nbit=7, bounds=S.MULTI_BOUNDS, seed=1)
+        s = K.channel_sum(stack)
+        s = K.div_scalar(s, K.max_f64(s))
+        ms = timed(lambda: K.nl_means_2d(s, h=0.02))
+        print("nl_means_2d 2048^2: %.3f ms  (%.1f Mpix/s, %.2f G pixel-shifts/s)" % (ms, H * W / ms / 1e3,
+                                                                                  H * W * 528 / ms / 1e6))
+    if "classify" in what:
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0)
+        for C, bounds, R in [(95, S.ECOLI_BOUNDS, 1023), (63, S.MULTI_BOUNDS, 127)]:
+            stack = torch.rand((H, W, C), generator=g, device="cuda")
+            ref = torch.rand((R, C), generator=g, device="cuda")
+            for mode in K.classify_modes(bounds):
+                refx = K.classify_prepare(ref, bounds, mode)
+                ms = timed(lambda: K.classify_pixels(stack, refx, R, bounds, mode))
+                tf = 2.0 * H * W * R * C / ms / 1e9
+                print("classify C=%d R=%d mode %d: %.3f ms  %.1f TF/s algorithmic" % (C, R, mode, ms, tf))
+
+
+if __name__ == "__main__":
+    main()
