@@ -28,13 +28,16 @@ H = W = 2048
 C = 95
 NBIT = 10
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (mode 0)
-F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (mode 1, default)
+F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (modes 1, 2)
+KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
+               2: "classify_pixels_lay_kernel<LayEcoli>"}
 
 
 def _cpu_baseline(ref, bounds):
     """Oracle restatement (oracle/pipeline.py, single-threaded C + numpy) on a bounded sample of
-    the same workload: segment+measure+per-cell classify of a 1024x1024x95 tile, and per-pixel
-    classification of 4096 pixels; scaled to Mpixel-spectra/s of the full step."""
+    the same workload: segment+measure+per-cell classify of one whole 2048x2048x95 tile, and per-pixel
+    classification of 131072 of its pixels (~10 s of CPU); per-pixel costs summed into
+    Mpixel-spectra/s of the full step."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     import pipeline as OP
@@ -42,20 +45,20 @@ def _cpu_baseline(ref, bounds):
     from hiprfish_image_analysis_amd import synthetic as S
     O.build()
     os.environ.setdefault("OMP_NUM_THREADS", "1")
-    hs = 1024
+    hs = 2048
     lay = S.cell_layout(hs, hs, S.default_ncells(hs, hs), ref.shape[0], seed=99)
     truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
     st = S.render_stack(truth, lay, ref, seed=99, device="cpu", profile=prof).numpy()
     t0 = time.perf_counter()
     OP.process_tile(st, ref, bounds)
     t_seg = (time.perf_counter() - t0) / (hs * hs)
-    npx = 4096
+    npx = 1 << 17
     x = st.reshape(-1, C)[:npx].astype(np.float64)
     t0 = time.perf_counter()
     O.classify(x, ref.astype(np.float64), bounds, 0)
     t_pix = (time.perf_counter() - t0) / npx
     return {"value": round(1e-6 / (t_seg + t_pix), 4), "unit": "Mpixel-spectra/s", "cores": 1, "kind": "port",
-            "sample": "oracle/pipeline.py process_tile on a 1024x1024x95 tile (%.1f s) + per-pixel classify of "
+            "sample": "oracle/pipeline.py process_tile on a 2048x2048x95 tile (%.1f s) + per-pixel classify of "
                       "%d pixels vs 1023 refs (%.1f s), 1 thread; per-pixel costs summed" %
                       (t_seg * hs * hs, npx, t_pix * npx)}
 
@@ -180,23 +183,26 @@ def main():
         ms_iso = float(np.mean([a.elapsed_time(b) for a, b in iso]))
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
         ach = flops / (ms * 1e-3) / 1e12
-        mode = K.CLASSIFY_MODE
+        mode = K.refx_mode(lib.refx(), C, bounds)
         kp, rpad = K.classify_geometry(C, len(bounds) - 1, lib.R, mode)
-        peak = F16_MFMA_PEAK_TFLOPS if mode == 1 else F32_MFMA_PEAK_TFLOPS
-        # MFMA flops the hardware executes: padded K x padded R, x3 products in split-fp16 mode
-        executed = 2.0 * H * W * rpad * kp * (3 if mode == 1 else 1) / (ms * 1e-3) / 1e12
+        peak = F16_MFMA_PEAK_TFLOPS if mode else F32_MFMA_PEAK_TFLOPS
+        # MFMA flops the hardware executes: padded K x padded R, x3 products in split-fp16 modes
+        executed = 2.0 * H * W * rpad * kp * (3 if mode else 1) / (ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "classify_pixels_pmc.json")
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                rec = json.load(open(pmc))
+                # only a PMC record of the kernel this run used counts
+                if KERNEL_NAME[mode].split("<")[0] in rec.get("kernel", ""):
+                    traffic = rec.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         out["roofline"] = {"bound": "mfma",
-                           "kernel": "classify_pixels_f16_kernel<7>" if mode == 1 else "classify_pixels_kernel<50>",
+                           "kernel": KERNEL_NAME[mode],
                            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(ach / peak, 4), "traffic": traffic, "kernel_ms": round(ms, 4),
-                           "mfma_dtype": "f16 (split hi/lo, 3 MFMA per f32 product)" if mode == 1 else "f32",
+                           "mfma_dtype": "f16 (split hi/lo, 3 MFMA per f32 product)" if mode else "f32",
                            "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4),
                            "overlapped_with_segmentation": not args.no_overlap,
                            "isolated_kernel_ms": round(ms_iso, 4),

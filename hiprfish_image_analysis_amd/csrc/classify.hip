@@ -419,7 +419,11 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
   };
   const int nch = Rpad / RCH;
   for (int c = 0; c < nch; ++c) {
-    __syncthreads();  // chunk c landed (vmcnt(0) + barrier); everyone is past chunk c-1
+    // chunk c landed: this wave's LDS-DMA retired (hipcc does not count global_load_lds for the
+    // barrier's wait, so the vmcnt(0) is explicit), then the barrier covers every wave's pieces;
+    // everyone is past chunk c-1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (c + 1 < nch) issue(c + 1);
     const char *buf = ldsb + (c & 1) * CHB;
 #pragma unroll
@@ -500,11 +504,14 @@ constexpr int lay_ks16() {
 }
 
 // Stage one loaded group in LDS and build its split-fp16 B operand (lane = pixel j, half h
-// holds columns 16s + 8h + q).  Segment norms in f64 from the lane's own columns plus the
-// other half's (one shuffle), as the restatement; zx = the pixel's all-zero segments.
+// holds columns 16s + 8h + q).  Segment norms: f32 sums of the lane's own columns plus the
+// other half's (one shuffle), 1/sqrt by v_rsq (both within ~1e-7 of the restatement's f64,
+// far inside the classifier's 1e-5); a segment is zero when all its values are +-0 (exact,
+// from the bit patterns), and a sum that underflows f32 is redone in f64.  zx = the pixel's
+// all-zero segments; neg = some value is negative.
 template <class L, int KS>
 __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, int lane, int j, int h,
-                                            h8 (&bh)[KS], h8 (&bl)[KS], uint32_t &zx) {
+                                            h8 (&bh)[KS], h8 (&bl)[KS], uint32_t &zx, uint32_t &neg) {
   const int nv = 8 * L::C;
 #pragma unroll
   for (int i = 0; i < LDV; ++i) {
@@ -514,9 +521,14 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
   __syncthreads();
   const float *pc = stg + j * L::C + 8 * h;
   float raw[KS][8];
-  double nn[L::NSEG];
+  float nn[L::NSEG];
+  uint32_t nzs[L::NSEG];
+  uint32_t sgn = 0;
 #pragma unroll
-  for (int s = 0; s < L::NSEG; ++s) nn[s] = 0.0;
+  for (int s = 0; s < L::NSEG; ++s) {
+    nn[s] = 0.0f;
+    nzs[s] = 0u;
+  }
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -525,21 +537,48 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
       const float r = pc[16 * s + q];  // past the row end: another pixel's value, masked here
       const float x = h ? (sb >= 0 ? r : 0.0f) : (sa >= 0 ? r : 0.0f);
       raw[s][q] = x;
-      const double x2 = (double)x * (double)x;
+      const uint32_t xb = __float_as_uint(x);
+      sgn |= xb;
+      const uint32_t mag = xb << 1;  // non-zero iff |x| != 0
       if (sa == sb) {
-        if (sa >= 0) nn[sa >= 0 ? sa : 0] += x2;
+        if (sa >= 0) {
+          nn[sa >= 0 ? sa : 0] = __builtin_fmaf(x, x, nn[sa >= 0 ? sa : 0]);
+          nzs[sa >= 0 ? sa : 0] |= mag;
+        }
       } else {
-        if (sa >= 0) nn[sa >= 0 ? sa : 0] += h ? 0.0 : x2;
-        if (sb >= 0) nn[sb >= 0 ? sb : 0] += h ? x2 : 0.0;
+        const float x2 = x * x;
+        if (sa >= 0) {
+          nn[sa >= 0 ? sa : 0] += h ? 0.0f : x2;
+          nzs[sa >= 0 ? sa : 0] |= h ? 0u : mag;
+        }
+        if (sb >= 0) {
+          nn[sb >= 0 ? sb : 0] += h ? x2 : 0.0f;
+          nzs[sb >= 0 ? sb : 0] |= h ? mag : 0u;
+        }
       }
     }
+  neg = sgn >> 31;
   float inv[L::NSEG];
   zx = 0;
 #pragma unroll
   for (int s = 0; s < L::NSEG; ++s) {
-    const double t = nn[s] + __shfl_xor(nn[s], 32, 64);
-    inv[s] = t > 0.0 ? (float)(1.0 / sqrt(t)) : 0.0f;
-    zx |= (t > 0.0 ? 0u : 1u) << s;
+    const float t = nn[s] + __shfl_xor(nn[s], 32, 64);
+    const uint32_t nz = nzs[s] | __shfl_xor(nzs[s], 32, 64);
+    inv[s] = nz ? rsqrtf(t) : 0.0f;
+    zx |= (nz ? 0u : 1u) << s;
+    if (nz && !(t >= 1e-30f)) {  // f32 underflow (|x| < ~1e-19 throughout): redo in f64
+      double td = 0.0;
+#pragma unroll
+      for (int ss = 0; ss < KS; ++ss)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int sa = col_seg<L>(16 * ss + q), sb = col_seg<L>(16 * ss + 8 + q);
+          const double x = (double)raw[ss][q];
+          if ((h ? sb : sa) == s) td += x * x;
+        }
+      td += __shfl_xor(td, 32, 64);
+      inv[s] = (float)(1.0 / sqrt(td));
+    }
   }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -565,9 +604,14 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
   __syncthreads();
 }
 
-// The library sweep of one workgroup (see classify_pixels_f16_kernel); ZS adds the
-// zero-segment indicator terms popcount(zx & zr) to every score.
-template <int KS16, int ROWB, bool ZS>
+// The library sweep of one workgroup (see classify_pixels_f16_kernel).  ZS adds the
+// zero-segment indicator terms popcount(zx & zr) to every score.  KEYED (all scores >= 0:
+// no negative value in the workgroup's pixels or the library) runs the argmax on integer
+// keys: score bits with the low 4 mantissa bits replaced by 15 - register (so the max also
+// names the register, lower rows winning ties), a max tree per block and one compare per
+// block -- about half the VALU of a compare-and-select per score.  The 4 dropped bits are
+// <= 2^-19 relative (< 1e-5 of a distance); blocks still compete in row order.
+template <int KS16, int ROWB, int NW, bool ZS, bool KEYED>
 __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w, int h,
                                           const h8 (&bh0)[KS16], const h8 (&bl0)[KS16], const h8 (&bh1)[KS16],
                                           const h8 (&bl1)[KS16], uint32_t zx0, uint32_t zx1, float &best0,
@@ -579,7 +623,7 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
   auto issue = [&](int c) {
     const char *g = gref + (int64_t)c * CHB + lane * 16;
     char *l = ldsb + (c & 1) * CHB;
-    for (int q = w; q < NPC; q += 4)
+    for (int q = w; q < NPC; q += NW)
       __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
   };
   issue(0);
@@ -588,6 +632,8 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
   for (int reg = 0; reg < 16; ++reg) pv0[reg] = pv1[reg] = -__builtin_inff();
   int pr = 0;  // first row of the pending block
   const unsigned char *zrow = reinterpret_cast<const unsigned char *>(gref) + 4 * KP + (int64_t)(4 * h) * ROWB;
+  int bk0 = INT32_MIN, bk1 = INT32_MIN;        // KEYED: the pending block's keys
+  int key0 = INT32_MIN, key1 = INT32_MIN;      // KEYED: best keys so far
   auto epi = [&](int lo, int hi) {
 #pragma unroll
     for (int reg = lo; reg < hi; ++reg) {
@@ -598,18 +644,38 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
         s0 += (float)__popc(zx0 & zr);
         s1 += (float)__popc(zx1 & zr);
       }
-      if (s0 > best0) {
-        best0 = s0;
-        bi0 = r;
+      if (KEYED) {
+        bk0 = max(bk0, (__float_as_int(s0) & -16) | (15 - reg));
+        bk1 = max(bk1, (__float_as_int(s1) & -16) | (15 - reg));
+      } else {
+        if (s0 > best0) {
+          best0 = s0;
+          bi0 = r;
+        }
+        if (s1 > best1) {
+          best1 = s1;
+          bi1 = r;
+        }
       }
-      if (s1 > best1) {
-        best1 = s1;
-        bi1 = r;
+    }
+    if (KEYED && hi == 16) {  // the pending block is complete
+      if (bk0 > key0) {
+        key0 = bk0;
+        bi0 = pr;
       }
+      if (bk1 > key1) {
+        key1 = bk1;
+        bi1 = pr;
+      }
+      bk0 = bk1 = INT32_MIN;
     }
   };
   for (int c = 0; c < nch; ++c) {
-    __syncthreads();  // chunk c landed (vmcnt(0) + barrier); everyone is past chunk c-1
+    // chunk c landed: this wave's LDS-DMA retired (hipcc does not count global_load_lds for the
+    // barrier's wait, so the vmcnt(0) is explicit), then the barrier covers every wave's pieces;
+    // everyone is past chunk c-1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (c + 1 < nch) issue(c + 1);
     const char *buf = ldsb + (c & 1) * CHB;
 #pragma unroll
@@ -634,10 +700,17 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
     }
   }
   epi(0, 16);  // the last block
+  if (KEYED) {
+    const int g0 = 15 - (key0 & 15), g1 = 15 - (key1 & 15);
+    bi0 += (g0 & 3) + 8 * (g0 >> 2);
+    bi1 += (g1 & 3) + 8 * (g1 >> 2);
+    best0 = __int_as_float(key0 & -16);
+    best1 = __int_as_float(key1 & -16);
+  }
 }
 
-template <class L>
-__global__ __launch_bounds__(256, 2) void classify_pixels_lay_kernel(const float *__restrict__ stack, int64_t P,
+template <class L, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(const float *__restrict__ stack, int64_t P,
                                                                      const _Float16 *__restrict__ refh, int32_t R,
                                                                      int32_t Rpad, int32_t *__restrict__ best_idx,
                                                                      float *__restrict__ best_dist) {
@@ -648,28 +721,38 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_lay_kernel(const float
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * 256 + w * 64;
+  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
 
   h8 bh0[KS16], bl0[KS16], bh1[KS16], bl1[KS16];
-  uint32_t zx0 = 0, zx1 = 0;
+  uint32_t zx0 = 0, zx1 = 0, ng0 = 0, ng1 = 0;
   float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
   {
     float4 v0[LDV], v1[LDV];
     load_group(stack, P, L::C, pbase, lane, v0);
     load_group(stack, P, L::C, pbase + 32, lane, v1);
-    build_b_lay<L, KS16>(v0, stg, lane, j, h, bh0, bl0, zx0);
-    build_b_lay<L, KS16>(v1, stg, lane, j, h, bh1, bl1, zx1);
+    build_b_lay<L, KS16>(v0, stg, lane, j, h, bh0, bl0, zx0, ng0);
+    build_b_lay<L, KS16>(v1, stg, lane, j, h, bh1, bl1, zx1, ng1);
   }
+  // the library's "has a negative value" flag sits in row 0's pad (ref_negflag_kernel)
+  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 4);
   float best0 = -__builtin_inff(), best1 = -__builtin_inff();
   int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
   const char *gref = reinterpret_cast<const char *>(refh);
   char *ldsb = reinterpret_cast<char *>(lds);
   const int nch = Rpad / RCH;
   // every wave of the workgroup takes the same branch (the chunk barriers are shared)
-  if (__syncthreads_or((zx0 | zx1) != 0))
-    lay_sweep<KS16, ROWB, true>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1);
-  else
-    lay_sweep<KS16, ROWB, false>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1);
+  const bool zs = __syncthreads_or((zx0 | zx1) != 0);
+  const bool keyed = !libneg && !__syncthreads_or((ng0 | ng1) != 0);
+#define HRF_SWEEP(Z, K) \
+  lay_sweep<KS16, ROWB, NW, Z, K>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1)
+  if (keyed) {
+    if (zs) HRF_SWEEP(true, true);
+    else HRF_SWEEP(false, true);
+  } else {
+    if (zs) HRF_SWEEP(true, false);
+    else HRF_SWEEP(false, false);
+  }
+#undef HRF_SWEEP
   float best[2] = {best0, best1};
   int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
 #pragma unroll
@@ -715,6 +798,16 @@ __global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, in
     if (!(nn > 0)) zr |= (uint8_t)(1u << s);
   }
   reinterpret_cast<uint8_t *>(hi + 2 * KP)[0] = zr;
+}
+
+// row 0's pad word (byte 4*KP + 4) = 1 when any library value is negative (the keyed argmax
+// needs every score >= 0); one workgroup, after ref_prep_lay_kernel
+__global__ __launch_bounds__(256) void ref_negflag_kernel(const float *__restrict__ ref, int64_t n, int32_t KP,
+                                                          _Float16 *__restrict__ refh) {
+  int neg = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) neg |= ref[i] < 0.0f;
+  neg = __syncthreads_or(neg);
+  if (threadIdx.x == 0) *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(refh) + 4 * KP + 4) = (uint32_t)neg;
 }
 
 // 1 = E. coli layout, 2 = synthetic-community layout, 0 = other
@@ -856,10 +949,11 @@ hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, con
   HRF_REQUIRE(ref && refx, "classify_prepare_refs: null buffer");
   HRF_REQUIRE(mode != 2 || layout_id(bd, C) != 0,
               "classify: mode 2 needs the E. coli (0,32,55,75,89,95) or multispecies (0,23,43,57,63) layout");
-  if (mode == 2)
+  if (mode == 2) {
     ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
                                                                                           (_Float16 *)refx);
-  else if (mode == 0)
+    ref_negflag_kernel<<<1, 256, 0, (hipStream_t)stream>>>(ref, (int64_t)R * C, kp, (_Float16 *)refx);
+  } else if (mode == 0)
     ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
                                                                                       (float *)refx);
   else
@@ -883,18 +977,29 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
   if (mode == 2) {
     const int lay = layout_id(bd, C);
     HRF_REQUIRE(lay != 0, "classify: mode 2 needs the E. coli or multispecies channel layout");
-    const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * 4 * 32 * C);
+    // waves per workgroup: the library chunks streamed through LDS are shared by NW*64 pixels
+    static const int nw = getenv("HRF_CLASSIFY_NW") ? atoi(getenv("HRF_CLASSIFY_NW")) : 4;
+    const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * nw * 32 * C);
+#define HRF_LAY(LAY, NWV)                                                                                      \
+  (void)hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LAY, NWV>,                                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize,                                       \
+                            (int)shm);                                                                        \
+  classify_pixels_lay_kernel<LAY, NWV><<<(unsigned)hrf::cdiv(P, 64 * NWV), 64 * NWV, shm, s>>>(                 \
+      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
     if (lay == 1) {
-      hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayEcoli>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      classify_pixels_lay_kernel<LayEcoli><<<grid, 256, shm, s>>>(stack, P, (const _Float16 *)refx, R, rpad, best_idx,
-                                                                  best_dist);
+      if (nw == 8) {
+        HRF_LAY(LayEcoli, 8);
+      } else {
+        HRF_LAY(LayEcoli, 4);
+      }
     } else {
-      hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayMulti>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-      classify_pixels_lay_kernel<LayMulti><<<grid, 256, shm, s>>>(stack, P, (const _Float16 *)refx, R, rpad, best_idx,
-                                                                  best_dist);
+      if (nw == 8) {
+        HRF_LAY(LayMulti, 8);
+      } else {
+        HRF_LAY(LayMulti, 4);
+      }
     }
+#undef HRF_LAY
     HRF_LAUNCHED();
     return HRF_OK;
   }

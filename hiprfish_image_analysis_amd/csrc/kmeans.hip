@@ -46,15 +46,27 @@ __device__ __forceinline__ double ord_dec(unsigned long long e) {
 __global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
                                  KmState *st) {
   unsigned long long lo = ~0ull, hi = 0ull, am = 0ull, nv = 0ull;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) continue;
-    const double v = x[i];
-    const unsigned long long e = ord_enc(v);
-    lo = e < lo ? e : lo;
-    hi = e > hi ? e : hi;
-    const unsigned long long a = (unsigned long long)__double_as_longlong(fabs(v));
-    am = a > am ? a : am;
-    nv += 1;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += T * 8) {
+    double vv[8];
+    bool ok[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t k = i + e * T;
+      ok[e] = k < n;
+      vv[e] = ok[e] ? x[k] : 0.0;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (!ok[e] || (valid && !valid[i + e * T])) continue;
+      const double v = vv[e];
+      const unsigned long long en = ord_enc(v);
+      lo = en < lo ? en : lo;
+      hi = en > hi ? en : hi;
+      const unsigned long long a = (unsigned long long)__double_as_longlong(fabs(v));
+      am = a > am ? a : am;
+      nv += 1;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -106,6 +118,8 @@ __global__ void km_init_kernel(KmState *st, int k) {
   st->converged = nv == 0;
   st->iters = 0;
 }
+
+constexpr int KM_E = 8;  // elements in flight per thread
 
 template <int K>
 __device__ __forceinline__ int km_assign(double v, const double *c) {
@@ -164,15 +178,32 @@ __global__ __launch_bounds__(256) void km_step_kernel(const double *__restrict__
     sum[j] = 0;
     cnt[j] = 0;
   }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !valid[i]) continue;
-    const double v = x[i];
-    const int bj = km_assign<K>(v, c);
-    const long long q = (long long)rint(ldexp(v, s));
+  // KM_E strided elements per thread per round, all loads issued before any is used: the pass
+  // is bound by memory-level parallelism, not arithmetic
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += T * KM_E) {
+    double v[KM_E];
+    bool ok[KM_E];
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      sum[j] += bj == j ? q : 0;
-      cnt[j] += bj == j;
+    for (int e = 0; e < KM_E; ++e) {
+      const int64_t k = i + e * T;
+      ok[e] = k < n;
+      v[e] = ok[e] ? x[k] : 0.0;
+    }
+    if (valid) {
+#pragma unroll
+      for (int e = 0; e < KM_E; ++e) ok[e] = ok[e] && valid[i + e * T];
+    }
+#pragma unroll
+    for (int e = 0; e < KM_E; ++e) {
+      if (!ok[e]) continue;
+      const int bj = km_assign<K>(v[e], c);
+      const long long q = (long long)rint(ldexp(v[e], s));
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        sum[j] += bj == j ? q : 0;
+        cnt[j] += bj == j;
+      }
     }
   }
   __shared__ long long ssum[4][K];

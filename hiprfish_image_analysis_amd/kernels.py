@@ -409,20 +409,32 @@ def paint_ids(labels, code):
 
 
 # ---- a19 ------------------------------------------------------------------------------------
-CLASSIFY_MODE = 1   # 1: split-fp16 MFMA (default), 0: f32 MFMA
+CLASSIFY_MODE = None   # None: 2 on the reference layouts, else 1; 1: split-fp16 MFMA; 0: f32 MFMA
+REFERENCE_LAYOUTS = ((0, 32, 55, 75, 89, 95), (0, 23, 43, 57, 63))   # train_reference.py:1401, :1488
 
 
-def classify_geometry(C, nseg, R, mode=None):
+def classify_modes(bounds):
+    """the per-pixel classifier modes available for a channel layout, fastest first"""
+    return (2, 1, 0) if tuple(int(b) for b in bounds) in REFERENCE_LAYOUTS else (1, 0)
+
+
+def _mode(bounds, mode):
+    if mode is None:
+        mode = CLASSIFY_MODE
+    return classify_modes(bounds)[0] if mode is None else mode
+
+
+def classify_geometry(C, nseg, R, mode=1):
     import ctypes
-    mode = CLASSIFY_MODE if mode is None else mode
     kp, rp = ctypes.c_int32(0), ctypes.c_int32(0)
     _lib.call("hrf_classify_geometry", C, nseg, R, mode, ctypes.addressof(kp), ctypes.addressof(rp))
     return kp.value, rp.value
 
 
 def classify_prepare(ref, bounds, mode=None):
-    """-> prepared reference table for classify_pixels (mode 0: f32, mode 1: fp16 hi/lo)"""
-    mode = CLASSIFY_MODE if mode is None else mode
+    """-> prepared reference table for classify_pixels (mode 0: f32; 1: fp16 hi/lo with
+    zero-segment indicator columns; 2: fp16 hi/lo, reference layouts, indicators in the epilogue)"""
+    mode = _mode(bounds, mode)
     ref = _dev(ref, torch.float32, "ref")
     R, C = ref.shape
     b = _i32_host(bounds)
@@ -435,10 +447,22 @@ def classify_prepare(ref, bounds, mode=None):
     return refx
 
 
-def classify_pixels(stack, refx, R, bounds):
+def refx_mode(refx, C, bounds):
+    """which mode a prepared table was built for (its dtype and row width tell)"""
+    if refx.dtype == torch.float32:
+        return 0
+    if 2 in classify_modes(bounds):
+        kp2, _ = classify_geometry(C, len(bounds) - 1, 1, 2)
+        if refx.shape[1] == 2 * kp2 + 8:
+            return 2
+    return 1
+
+
+def classify_pixels(stack, refx, R, bounds, mode=None):
     stack = _dev(stack, torch.float32, "stack")
-    mode = 0 if refx.dtype == torch.float32 else 1
     C = stack.shape[-1]
+    if mode is None:
+        mode = refx_mode(refx, C, bounds)
     P = stack.numel() // C
     b = _i32_host(bounds)
     idx = torch.empty(stack.shape[:-1], dtype=torch.int32, device=stack.device)

@@ -207,9 +207,11 @@ def test_counts_paint(K, orc):
 
 
 # ---- a19 classification ---------------------------------------------------------------
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63)), (5, (0, 32))])
 def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
+    if mode not in K.classify_modes(bounds):
+        pytest.skip("mode 2 is built for the reference channel layouts only")
     ref = S.reference_library(nbit, bounds) if len(bounds) > 2 else \
         np.abs(np.random.default_rng(0).normal(size=(31, 32))).astype(np.float32)
     R, C = ref.shape
@@ -234,6 +236,48 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
     sub = np.arange(0, len(st), 37)
     assert np.array_equal(gi[sub][sep], ra[sub][sep])
     assert (gi == ra).mean() > 0.99
+
+
+@pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
+def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
+    """mode 2 (indicator terms in the epilogue) vs mode 1 (indicator columns) on a 512x384
+    tile whose first rows carry zero segments; spot-checked against the restatement"""
+    stack, truth, lay, ref = S.tile(512, 384, nbit=nbit, bounds=bounds, seed=21)
+    R, C = ref.shape
+    st = stack.clone()
+    st[0:3] = 0.0                                   # whole rows of all-zero pixels
+    st[3:9, :, bounds[1]:bounds[2]] = 0.0           # a zero segment
+    st[100:102, :, bounds[-2]:bounds[-1]] = 0.0     # another, far from the first
+    out = {}
+    for mode in (1, 2):
+        refx = K.classify_prepare(dev(ref), bounds, mode=mode)
+        out[mode] = [host(t).ravel() for t in K.classify_pixels(st, refx, R, bounds)]
+    np.testing.assert_allclose(out[2][1], out[1][1], rtol=0, atol=2e-6)
+    assert (out[2][0] == out[1][0]).mean() > 0.999
+    sel = np.concatenate([np.arange(0, 9 * 384, 17), 100 * 384 + np.arange(0, 768, 13),
+                          np.random.default_rng(0).choice(512 * 384, 300, replace=False)])
+    x = host(st).reshape(-1, C)[sel].astype(np.float64)
+    ri, rd = orc.classify(x, ref.astype(np.float64), bounds, 0)
+    np.testing.assert_allclose(out[2][1][sel], rd, rtol=1e-5, atol=1e-5)
+    assert (out[2][0][sel] == ri).mean() > 0.98
+
+
+def test_classify_pixels_mode2_negative_values(K, orc, S):
+    """workgroups holding a negative value (or a library with one) take the exact
+    compare-and-select argmax instead of the keyed one"""
+    bounds = (0, 32, 55, 75, 89, 95)
+    stack, truth, lay, ref = S.tile(256, 128, nbit=10, bounds=bounds, seed=5)
+    R, C = ref.shape
+    st = stack.clone()
+    st[0:4] -= 0.02                                 # some pixels (first 2 workgroups) go negative
+    sel = np.concatenate([np.arange(0, 4 * 128, 3), np.random.default_rng(1).choice(256 * 128, 200, replace=False)])
+    x = host(st).reshape(-1, C)[sel].astype(np.float64)
+    for lib in (ref, ref - 0.01):                   # then a library with negative entries
+        refx = K.classify_prepare(dev(lib.astype(np.float32)), bounds, mode=2)
+        gi, gd = [host(t).ravel()[sel] for t in K.classify_pixels(st, refx, R, bounds)]
+        ri, rd = orc.classify(x, lib.astype(np.float64), bounds, 0)
+        np.testing.assert_allclose(gd, rd, rtol=1e-5, atol=1e-5)
+        assert (gi == ri).mean() > 0.98
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])

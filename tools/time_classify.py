@@ -1,5 +1,8 @@
 """Time hrf_classify_pixels on a resident 2048x2048x95 stack for several library sizes
-(separates the per-workgroup prologue from the per-reference sweep)."""
+(separates the per-workgroup prologue from the per-reference sweep).
+
+python tools/time_classify.py [mode] [R ...]     (mode default: the fastest for the layout)
+"""
 import sys
 import time
 
@@ -11,13 +14,17 @@ from hiprfish_image_analysis_amd import synthetic as S  # noqa: E402
 
 
 def main():
+    args = sys.argv[1:]
+    mode = int(args.pop(0)) if args else None
     H = W = 2048
     g = torch.Generator(device="cuda")
     g.manual_seed(0)
     stack = torch.rand((H, W, 95), generator=g, device="cuda")
-    for R in [int(a) for a in (sys.argv[1:] or ["64", "256", "1023"])]:
+    for R in [int(a) for a in (args or ["64", "256", "1023"])]:
         ref = torch.rand((R, 95), generator=g, device="cuda")
-        refx = K.classify_prepare(ref, S.ECOLI_BOUNDS)
+        refx = K.classify_prepare(ref, S.ECOLI_BOUNDS, mode)
+        m = K.refx_mode(refx, 95, S.ECOLI_BOUNDS)
+        kp, _ = K.classify_geometry(95, 5, R, m)
         for _ in range(2):
             K.classify_pixels(stack, refx, R, S.ECOLI_BOUNDS)
         torch.cuda.synchronize()
@@ -30,7 +37,8 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / n
         tf = 2.0 * H * W * R * 95 / ms / 1e9
-        print("R=%5d  %.3f ms  %.1f TF/s algorithmic  %.1f TF/s executed" % (R, ms, tf, 3 * tf * 112 / 95))
+        print("mode %d R=%5d  %.3f ms  %.1f TF/s algorithmic  %.1f TF/s executed" % (m, R, ms, tf,
+                                                                                   3 * tf * kp / 95 if m else tf))
 
 
 if __name__ == "__main__":
