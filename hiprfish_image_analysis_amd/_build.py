@@ -56,7 +56,8 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
         res = list(ex.map(_compile, srcs))
     objs = [o for o, _ in res]
     if any(ch for _, ch in res) or not os.path.exists(LIB) or force:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
+               "-L/opt/rocm/lib", "-lhipfft", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s" % r.stderr[-4000:])

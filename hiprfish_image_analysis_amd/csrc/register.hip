@@ -1,0 +1,166 @@
+// register.hip -- integer registration shift estimate.
+//
+// skimage.feature.register_translation(src, target) with its defaults (upsample_factor 1,
+// space 'real'), as the reference calls it before stack assembly: ecoli
+// measurement.py:45-46 (per-laser channel max images), multispecies :82-83 (channel sums),
+// biofilm :326-327 (log channel sums).  The cross-correlation ifft(F(src) * conj(F(target)))
+// is formed with two real-to-complex f64 FFTs (hipFFT), a pointwise conjugate product over
+// the half spectrum and one complex-to-real inverse; the shift is the location of max |cc|
+// (first in raster order), wrapped per axis to (-n/2, n/2] (shift > fix(n/2) -> shift - n).
+// The argmax is a two-level reduction on (value, index) pairs, deterministic.
+#include <hipfft/hipfft.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
+
+#include "common.hpp"
+
+namespace {
+
+struct Plans {
+  hipfftHandle fwd, inv;
+};
+std::mutex g_plan_mu;
+std::map<std::tuple<int, int64_t, int64_t>, Plans> g_plans;
+
+#define HRF_FFT(expr)                                                               \
+  do {                                                                              \
+    hipfftResult r_ = (expr);                                                       \
+    if (r_ != HIPFFT_SUCCESS) {                                                     \
+      ::hrf::set_error("%s failed: hipfft status %d (%s:%d)", #expr, (int)r_,      \
+                       __FILE__, __LINE__);                                         \
+      return HRF_EHIP;                                                              \
+    }                                                                               \
+  } while (0)
+
+hrf_status get_plans(int64_t H, int64_t W, Plans *out) {
+  int dev = 0;
+  HRF_HIP(hipGetDevice(&dev));
+  auto key = std::make_tuple(dev, H, W);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) {
+    *out = it->second;
+    return HRF_OK;
+  }
+  Plans p{};
+  HRF_FFT(hipfftPlan2d(&p.fwd, (int)H, (int)W, HIPFFT_D2Z));
+  HRF_FFT(hipfftPlan2d(&p.inv, (int)H, (int)W, HIPFFT_Z2D));
+  g_plans[key] = p;
+  *out = p;
+  return HRF_OK;
+}
+
+// o = a * conj(b) (numpy: src_freq * target_freq.conj())
+__global__ void xcorr_product_kernel(const hipfftDoubleComplex *__restrict__ a, const hipfftDoubleComplex *__restrict__ b,
+                                     int64_t n, hipfftDoubleComplex *__restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const hipfftDoubleComplex x = a[i], y = b[i];
+    o[i] = make_hipDoubleComplex(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);
+  }
+}
+
+struct Best {
+  double v;
+  int64_t i;
+};
+__device__ __forceinline__ Best better(Best a, Best b) {
+  // larger |cc| wins, equal values -> smaller raster index (numpy argmax: first occurrence)
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+
+constexpr int AM_BLOCKS = 1024;
+
+__global__ __launch_bounds__(256) void abs_argmax_partial_kernel(const double *__restrict__ cc, int64_t n,
+                                                                 Best *__restrict__ part) {
+  Best b{-1.0, INT64_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = fabs(cc[i]);
+    if (v > b.v) b = Best{v, i};  // increasing i per thread: first occurrence kept
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best c{__shfl_xor(b.v, o, 64), (int64_t)__shfl_xor((long long)b.i, o, 64)};
+    b = better(b, c);
+  }
+  __shared__ Best red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) b = better(b, red[q]);
+    part[blockIdx.x] = b;
+  }
+}
+
+__global__ __launch_bounds__(256) void abs_argmax_final_kernel(const Best *__restrict__ part, int nparts,
+                                                               int64_t *__restrict__ best_idx) {
+  Best b{-1.0, INT64_MAX};
+  for (int i = threadIdx.x; i < nparts; i += 256) b = better(b, part[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best c{__shfl_xor(b.v, o, 64), (int64_t)__shfl_xor((long long)b.i, o, 64)};
+    b = better(b, c);
+  }
+  __shared__ Best red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) b = better(b, red[q]);
+    *best_idx = b.i;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrf_register_workspace_bytes(int64_t H, int64_t W) {
+  const int64_t nc = H * (W / 2 + 1);
+  return 3 * nc * (int64_t)sizeof(hipfftDoubleComplex) + H * W * (int64_t)sizeof(double) +
+         AM_BLOCKS * (int64_t)sizeof(Best) + 64;
+}
+
+hrf_status hrf_register_translation(const double *src, const double *target, int64_t H, int64_t W, void *work,
+                                    int32_t *shift_host, hrf_stream_t stream) {
+  HRF_REQUIRE(H >= 1 && W >= 1 && H <= (1 << 20) && W <= (1 << 20), "register_translation: bad image size");
+  HRF_REQUIRE(src && target && work && shift_host, "register_translation: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nc = H * (W / 2 + 1);
+  char *w = (char *)work;
+  hipfftDoubleComplex *fa = (hipfftDoubleComplex *)w;
+  hipfftDoubleComplex *fb = fa + nc;
+  hipfftDoubleComplex *fp = fb + nc;
+  double *cc = (double *)(fp + nc);
+  Best *part = (Best *)(cc + H * W);
+  int64_t *bidx = (int64_t *)(part + AM_BLOCKS);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);  // plan handles are shared; bind the stream and run
+    Plans p{};
+    if (hrf_status st = get_plans(H, W, &p)) return st;
+    HRF_FFT(hipfftSetStream(p.fwd, s));
+    HRF_FFT(hipfftSetStream(p.inv, s));
+    // hipFFT's real-to-complex transform does not modify its input
+    HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(src), fa));
+    HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(target), fb));
+    xcorr_product_kernel<<<hrf::stream_grid(nc), 256, 0, s>>>(fa, fb, nc, fp);
+    HRF_LAUNCHED();
+    HRF_FFT(hipfftExecZ2D(p.inv, fp, cc));  // unnormalised: a positive scale leaves the argmax
+  }
+  const unsigned nb = (unsigned)std::min<int64_t>(AM_BLOCKS, hrf::cdiv(H * W, 256));
+  abs_argmax_partial_kernel<<<nb, 256, 0, s>>>(cc, H * W, part);
+  abs_argmax_final_kernel<<<1, 256, 0, s>>>(part, (int)nb, bidx);
+  HRF_LAUNCHED();
+  int64_t best = 0;
+  HRF_HIP(hipMemcpyAsync(&best, bidx, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HRF_HIP(hipStreamSynchronize(s));
+  int64_t r = best / W, c = best % W;
+  if (r > H / 2) r -= H;  // midpoints = fix(n / 2)
+  if (c > W / 2) c -= W;
+  shift_host[0] = (int32_t)r;
+  shift_host[1] = (int32_t)c;
+  return HRF_OK;
+}
+
+}  // extern "C"

@@ -95,13 +95,26 @@ __global__ void channel_sum_kernel(const float *__restrict__ stack, int64_t npix
   }
 }
 
+// Flat-field calibration folded into a reduction: channels [c0, c1) of pixel p are divided by
+// cal[p * sp + c * sc] in f64 (numpy's stack / calibration_image broadcasting: sp = 1, sc = 0
+// for an (H, W) plane; sp = 0, sc = 1 for a (C,) vector; sp = C, sc = 1 for (H, W, C)).
+struct Cal {
+  const float *p;
+  int64_t sp;
+  int32_t sc, c0, c1;
+  __device__ __forceinline__ double apply(double x, int64_t pix, int c) const {
+    return (p && c >= c0 && c < c1) ? x / (double)p[pix * sp + (int64_t)c * sc] : x;
+  }
+};
+
 // C <= 128: 64-pixel chunks staged through LDS with 16-byte loads (coalesced), then 8 lanes per
 // pixel: lane j accumulates numpy's r[j] (a[j] + a[j+8] + ...), the three xor-shuffle levels
 // are exactly ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), lane 0 adds the tail in order.
 constexpr int CS_P = 64;
+template <bool CAL>
 __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__restrict__ stack, int64_t npix, int C,
                                                               const uint8_t *__restrict__ mask, int mode, int negate,
-                                                              double *__restrict__ out, int vec_ok) {
+                                                              double *__restrict__ out, int vec_ok, Cal cal) {
   extern __shared__ __attribute__((aligned(16))) float sb[];
   const int tid = threadIdx.x;
   const int64_t nchunks = (npix + CS_P - 1) / CS_P;
@@ -124,18 +137,20 @@ __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__res
     for (int half = 0; half < 2; ++half) {
       const int pi = half * 32 + (tid >> 3);
       const float *a = sb + pi * C;
+      const int64_t pix = p0 + (pi < np ? pi : 0);
+      auto val = [&](int i) { return CAL ? cal.apply((double)a[i], pix, i) : (double)a[i]; };
       double res = 0.0;
       if (C >= 8) {
-        double r = (double)a[j];
-        for (int i = 8; i < main_n; i += 8) r += (double)a[i + j];
+        double r = val(j);
+        for (int i = 8; i < main_n; i += 8) r += val(i + j);
         r = r + __shfl_xor(r, 1, 64);
         r = r + __shfl_xor(r, 2, 64);
         r = r + __shfl_xor(r, 4, 64);
         res = r;
         if (j == 0)
-          for (int i = main_n; i < C; ++i) res += (double)a[i];
+          for (int i = main_n; i < C; ++i) res += val(i);
       } else if (j == 0) {
-        for (int i = 0; i < C; ++i) res += (double)a[i];
+        for (int i = 0; i < C; ++i) res += val(i);
       }
       if (j == 0 && pi < np) {
         const int64_t p = p0 + pi;
@@ -202,6 +217,38 @@ __global__ void mask_mul_kernel(const double *__restrict__ a, const uint8_t *__r
     o[i] = a[i] * (double)(m[i] != 0);
 }
 
+// np.max(stack, axis=2) as f64 (ecoli measurement.py:45, the registration images)
+__global__ void channel_max_kernel(const float *__restrict__ stack, int64_t npix, int C, double *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    const float *a = stack + p * C;
+    float m = a[0];
+    for (int c = 1; c < C; ++c) m = (a[c] > m || a[c] != a[c]) ? a[c] : m;  // numpy max propagates NaN
+    out[p] = (double)m;
+  }
+}
+
+__global__ void and_u8_kernel(const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, int64_t n,
+                              uint8_t *__restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = (uint8_t)(a[i] != 0 && b[i] != 0);
+}
+
+__global__ void mask_labels_kernel(const int32_t *__restrict__ l, const uint8_t *__restrict__ m, int64_t n,
+                                   int32_t *__restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = m[i] ? l[i] : 0;
+}
+
+// the calibrated stack as f64 (multispecies :104 image_channel, written as _registered.npy :166)
+__global__ void calibrate_kernel(const float *__restrict__ stack, int64_t npix, int C, Cal cal,
+                                 double *__restrict__ out) {
+  const int64_t n = npix * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = e / C;
+    out[e] = cal.apply((double)stack[e], p, (int)(e - p * C));
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -237,12 +284,66 @@ hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const ui
   if (C <= 128) {
     const int vec_ok = C >= 4 && (((uintptr_t)stack & 15) == 0);
     const int64_t nch = hrf::cdiv(npix, CS_P);
-    channel_sum_lds_kernel<<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
-                             (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out, vec_ok);
+    channel_sum_lds_kernel<false><<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
+                                    (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out, vec_ok, Cal{});
   } else {
     channel_sum_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate,
                                                                                out);
   }
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_channel_sum_cal(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
+                               int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, int32_t mode, double *out,
+                               hrf_stream_t stream) {
+  if (!cal) return hrf_channel_sum(stack, npix, C, nullptr, mode, 0, out, stream);
+  HRF_REQUIRE(C >= 1 && C <= 128 && mode >= 0 && mode <= 2, "channel_sum_cal: C must be 1..128, mode 0..2");
+  HRF_REQUIRE(cal_sp >= 0 && cal_sc >= 0 && cal_c0 >= 0 && cal_c1 <= C, "channel_sum_cal: bad calibration layout");
+  if (npix == 0) return HRF_OK;
+  HRF_REQUIRE(stack && out, "channel_sum_cal: null buffer");
+  const int vec_ok = C >= 4 && (((uintptr_t)stack & 15) == 0);
+  const int64_t nch = hrf::cdiv(npix, CS_P);
+  channel_sum_lds_kernel<true><<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
+                                 (hipStream_t)stream>>>(stack, npix, C, nullptr, mode, 0, out, vec_ok,
+                                                        Cal{cal, cal_sp, cal_sc, cal_c0, cal_c1});
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *out, hrf_stream_t stream) {
+  HRF_REQUIRE(C >= 1, "channel_max: C must be >= 1");
+  if (npix == 0) return HRF_OK;
+  HRF_REQUIRE(stack && out, "channel_max: null buffer");
+  channel_max_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_calibrate_f64(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
+                             int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, double *out, hrf_stream_t stream) {
+  HRF_REQUIRE(C >= 1 && cal_sp >= 0 && cal_sc >= 0 && cal_c0 >= 0 && cal_c1 <= C, "calibrate: bad arguments");
+  if (npix == 0) return HRF_OK;
+  HRF_REQUIRE(stack && out, "calibrate: null buffer");
+  calibrate_kernel<<<hrf::stream_grid(npix * C), 256, 0, (hipStream_t)stream>>>(stack, npix, C,
+                                                                             Cal{cal, cal_sp, cal_sc, cal_c0, cal_c1},
+                                                                             out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_and_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint8_t *out, hrf_stream_t stream) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(a && b && out, "and_u8: null buffer");
+  and_u8_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(a, b, n, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_mask_labels(const int32_t *labels, const uint8_t *mask, int64_t n, int32_t *out, hrf_stream_t stream) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(labels && mask && out, "mask_labels: null buffer");
+  mask_labels_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(labels, mask, n, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -18,8 +18,8 @@ constexpr int LS_P = 64;  // pixels per chunk
 
 __global__ __launch_bounds__(256) void label_sums_kernel(const float *__restrict__ stack,
                                                          const int32_t *__restrict__ lab, int64_t npix, int C,
-                                                         int32_t maxlab, const float *__restrict__ cal, int cal0,
-                                                         int cal1, double *__restrict__ sums,
+                                                         int32_t maxlab, const float *__restrict__ cal, int64_t cal_sp,
+                                                         int cal_sc, int cal0, int cal1, double *__restrict__ sums,
                                                          unsigned long long *__restrict__ counts, int vec_ok) {
   extern __shared__ __attribute__((aligned(16))) float sbuf[];
   __shared__ int32_t slab[LS_P];
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void label_sums_kernel(const float *__restrict
       int32_t l = tid < np ? lab[p0 + tid] : 0;
       if (l < 0 || l > maxlab) l = 0;
       slab[tid] = l;
-      scal[tid] = (cal && tid < np) ? (double)cal[p0 + tid] : 1.0;
+      scal[tid] = (cal && tid < np && cal_sc == 0) ? (double)cal[(p0 + tid) * cal_sp] : 1.0;
       mine = l != 0;
     }
     if (!__syncthreads_or(mine)) continue;
@@ -68,7 +68,8 @@ __global__ __launch_bounds__(256) void label_sums_kernel(const float *__restrict
         }
         if (l) {
           const double x = (double)sbuf[i * C + c];
-          acc += calc ? x / scal[i] : x;
+          // a plane calibration is staged per pixel; per-channel / full ones are read directly
+          acc += calc ? x / (cal_sc == 0 ? scal[i] : (double)cal[(p0 + i) * cal_sp + (int64_t)c * cal_sc]) : x;
         }
       }
       if (run) atomicAdd(&sums[(int64_t)run * C + c], acc);
@@ -286,6 +287,13 @@ extern "C" {
 hrf_status hrf_label_sums(const float *stack, const int32_t *labels, int64_t npix, int32_t C, int32_t maxlab,
                           const float *cal, int32_t cal_c0, int32_t cal_c1, double *sums, int64_t *counts,
                           hrf_stream_t stream) {
+  return hrf_label_sums_cal(stack, labels, npix, C, maxlab, cal, 1, 0, cal_c0, cal_c1, sums, counts, stream);
+}
+
+hrf_status hrf_label_sums_cal(const float *stack, const int32_t *labels, int64_t npix, int32_t C, int32_t maxlab,
+                              const float *cal, int64_t cal_sp, int32_t cal_sc, int32_t cal_c0, int32_t cal_c1,
+                              double *sums, int64_t *counts, hrf_stream_t stream) {
+  HRF_REQUIRE(cal_sp >= 0 && cal_sc >= 0, "label_sums: bad calibration layout");
   hipStream_t s = (hipStream_t)stream;
   HRF_REQUIRE(C >= 1 && C <= 512 && maxlab >= 0 && npix >= 0, "label_sums: C must be 1..512");
   HRF_REQUIRE(sums && counts, "label_sums: null output");
@@ -297,7 +305,7 @@ hrf_status hrf_label_sums(const float *stack, const int32_t *labels, int64_t npi
   const size_t shm = sizeof(float) * LS_P * C;
   const int64_t nchunks = hrf::cdiv(npix, LS_P);
   const unsigned grid = (unsigned)std::min<int64_t>(nchunks, 256 * 16);
-  label_sums_kernel<<<grid, 256, shm, s>>>(stack, labels, npix, C, maxlab, cal, cal_c0, cal_c1, sums,
+  label_sums_kernel<<<grid, 256, shm, s>>>(stack, labels, npix, C, maxlab, cal, cal_sp, cal_sc, cal_c0, cal_c1, sums,
                                            (unsigned long long *)counts, vec_ok);
   HRF_LAUNCHED();
   return HRF_OK;

@@ -126,14 +126,76 @@ def register_assemble(srcs, shifts, apply_mask=True):
     return out
 
 
-def channel_sum(stack, mask=None, mode=0, negate=False):
-    """np.sum(stack, axis=2) (f64, numpy pairwise order); mode 1 -> log(s+1e-2), 2 -> log10(s+1)"""
+def _cal_layout(cal, H, W, C, cal_range=None):
+    """calibration tensor -> (f32 tensor, pixel stride, channel stride, c0, c1) following numpy
+    broadcasting of stack (H, W, C) / cal: (H, W) or (H, W, 1) per pixel, (C,) or (1, 1, C) per
+    channel, (H, W, C) full; cal_range limits the divided channels (ecoli: 0..32)."""
+    c = _dev(cal, torch.float32, "calibration")
+    c0, c1 = cal_range if cal_range is not None else (0, C)
+    if c.shape in ((H, W), (H, W, 1)):
+        return c, 1, 0, c0, c1
+    if c.shape in ((C,), (1, C), (1, 1, C)):
+        return c, 0, 1, c0, c1
+    if c.shape == (H, W, C):
+        return c, C, 1, c0, c1
+    raise ValueError("calibration of shape %s does not broadcast against the (%d, %d, %d) stack"
+                     % (tuple(c.shape), H, W, C))
+
+
+def channel_sum(stack, mask=None, mode=0, negate=False, cal=None, cal_range=None):
+    """np.sum(stack, axis=2) (f64, numpy pairwise order); mode 1 -> log(s+1e-2), 2 -> log10(s+1);
+    cal: np.sum(stack / cal, axis=2) (multispecies measurement.py:104-105)"""
     stack = _dev(stack, torch.float32, "stack")
     H, W, C = stack.shape
-    m = _u8(mask, "mask") if mask is not None else None
     out = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    if cal is not None:
+        if mask is not None or negate:
+            raise ValueError("channel_sum: calibration with mask/negate is not supported")
+        c, sp, sc, c0, c1 = _cal_layout(cal, H, W, C, cal_range)
+        _lib.call("hrf_channel_sum_cal", _ptr(stack), H * W, C, _ptr(c), sp, sc, c0, c1, mode, _ptr(out), _stream())
+        return out
+    m = _u8(mask, "mask") if mask is not None else None
     _lib.call("hrf_channel_sum", _ptr(stack), H * W, C, _ptr(m), mode, int(negate), _ptr(out), _stream())
     return out
+
+
+def channel_max(stack):
+    """np.max(stack, axis=2) as f64 (ecoli measurement.py:45)"""
+    stack = _dev(stack, torch.float32, "stack")
+    H, W, C = stack.shape
+    out = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    _lib.call("hrf_channel_max", _ptr(stack), H * W, C, _ptr(out), _stream())
+    return out
+
+
+def calibrate(stack, cal, cal_range=None):
+    """stack / cal as f64 (multispecies measurement.py:104, saved as _registered.npy :166)"""
+    stack = _dev(stack, torch.float32, "stack")
+    H, W, C = stack.shape
+    out = torch.empty((H, W, C), dtype=torch.float64, device=stack.device)
+    if cal is None:
+        _lib.call("hrf_calibrate_f64", _ptr(stack), H * W, C, None, 0, 0, 0, 0, _ptr(out), _stream())
+        return out
+    c, sp, sc, c0, c1 = _cal_layout(cal, H, W, C, cal_range)
+    _lib.call("hrf_calibrate_f64", _ptr(stack), H * W, C, _ptr(c), sp, sc, c0, c1, _ptr(out), _stream())
+    return out
+
+
+def register_translation(src, target):
+    """skimage.feature.register_translation(src, target)[0] (upsample_factor 1): integer
+    (row, col) shift, via hipFFT (ecoli measurement.py:45-46, multispecies :82-83)"""
+    import ctypes
+    import numpy as np
+    src = _dev(src, torch.float64, "src")
+    target = _dev(target, torch.float64, "target")
+    if src.shape != target.shape or src.dim() != 2:
+        raise ValueError("register_translation: two equal-shape 2-D images expected")
+    H, W = src.shape
+    nb = int(_lib.lib().hrf_register_workspace_bytes(H, W))
+    work = torch.empty(nb, dtype=torch.uint8, device=src.device)
+    sh = np.zeros(2, np.int32)
+    _lib.call("hrf_register_translation", _ptr(src), _ptr(target), H, W, _ptr(work), sh.ctypes.data, _stream())
+    return int(sh[0]), int(sh[1])
 
 
 def max_f64(a):
@@ -155,6 +217,23 @@ def pad_edge(a, width=5):
     H, W = a.shape
     out = torch.empty((H + 2 * width, W + 2 * width), dtype=torch.float64, device=a.device)
     _lib.call("hrf_pad_edge_f64", _ptr(a), H, W, width, _ptr(out), _stream())
+    return out
+
+
+def and_mask(a, b):
+    """a AND b on masks -> u8 (multispecies measurement.py:140, :153)"""
+    x, y = _u8(a, "a"), _u8(b, "b")
+    out = torch.empty_like(x)
+    _lib.call("hrf_and_u8", _ptr(x), _ptr(y), x.numel(), _ptr(out), _stream())
+    return out
+
+
+def mask_labels(labels, mask):
+    """labels * mask (multispecies measurement.py:152)"""
+    l = _i32(labels, "labels")
+    m = _u8(mask, "mask")
+    out = torch.empty_like(l)
+    _lib.call("hrf_mask_labels", _ptr(l), _ptr(m), l.numel(), _ptr(out), _stream())
     return out
 
 
@@ -354,16 +433,19 @@ def watershed(image, markers, mask=None, negate=False, max_passes=100000):
 
 # ---- a14-a16, a20, a21, a23 -----------------------------------------------------------------
 def label_sums(stack, labels, maxlab, cal=None, cal_range=None):
+    """per-label channel sums of stack (/ cal) and pixel counts (ecoli measurement.py:147-155)"""
     stack = _dev(stack, torch.float32, "stack")
     l = _i32(labels, "labels")
-    C = stack.shape[-1]
+    H, W, C = stack.shape
     npix = l.numel()
     sums = torch.empty((maxlab + 1, C), dtype=torch.float64, device=stack.device)
     counts = torch.empty(maxlab + 1, dtype=torch.int64, device=stack.device)
-    c0, c1 = cal_range if cal_range is not None else (0, C)
-    calp = _ptr(_dev(cal, torch.float32, "cal")) if cal is not None else None
-    _lib.call("hrf_label_sums", _ptr(stack), _ptr(l), npix, C, maxlab, calp, c0, c1, _ptr(sums), _ptr(counts),
-              _stream())
+    calp, sp, sc, c0, c1 = None, 1, 0, 0, C
+    if cal is not None:
+        c, sp, sc, c0, c1 = _cal_layout(cal, H, W, C, cal_range)
+        calp = _ptr(c)
+    _lib.call("hrf_label_sums_cal", _ptr(stack), _ptr(l), npix, C, maxlab, calp, sp, sc, c0, c1, _ptr(sums),
+              _ptr(counts), _stream())
     return sums, counts
 
 

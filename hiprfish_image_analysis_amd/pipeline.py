@@ -80,6 +80,67 @@ def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, 
 
 
 # --------------------------------------------------------------------------------------------
+# Registration shift estimate
+# --------------------------------------------------------------------------------------------
+def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15):
+    """Integer shift of every laser stack against the first, skimage register_translation
+    (upsample 1) on a per-laser projection:
+    * reduce "max": np.max(image, axis=2), |shift| > clamp -> 0 (ecoli measurement.py:45-57);
+    * reduce "sum": np.sum(image, axis=2), no clamp (multispecies measurement.py:82-84).
+    -> [(0, 0), (dr_1, dc_1), ...] ready for kernels.register_assemble."""
+    proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
+    shifts = [(0, 0)]
+    for img in proj[1:]:
+        r, c = K.register_translation(proj[0], img)
+        if clamp is not None:
+            r = 0 if abs(r) > clamp else r
+            c = 0 if abs(c) > clamp else c
+        shifts.append((r, c))
+    return shifts
+
+
+# --------------------------------------------------------------------------------------------
+# Synthetic-community measurement (hiprfish_imaging_multispecies_spectral_image_measurement.py)
+# --------------------------------------------------------------------------------------------
+def segment_multispecies(stack: torch.Tensor, calibration: torch.Tensor | None = None, keep: dict | None = None):
+    """multispecies measurement.py:102-157 on the registered (H, W, C) stack.
+    -> (segmentation int32 relabelled 1..n, n, registered sum f64, final_bkg_filtered f64)
+
+    The two KMeans(2) cluster choices (:125-135, :141-149) take the cluster whose positive
+    values have the larger mean; for a 1-D partition into intervals that is the cluster with
+    the larger centre (kernels.kmeans_1d's top mask)."""
+    s = K.channel_sum(stack, cal=calibration)                    # :104-105 sum(stack / cal)
+    norm = K.div_scalar(s, K.max_f64(s))                         # :106
+    nl = K.nl_means_2d(norm, 7, 11, 0.02, 0.0)                   # :108 (estimate_sigma :107 unused)
+    final = K.enhance_2d(K.pad_edge(nl, 5))                      # :109-124
+    _, rough, _, _ = K.kmeans_1d(final, 2, want_labels=False)    # :125-135
+    opened = K.remove_small_objects(K.binary_opening(rough), 10, conn=1)   # :136-137
+    seeds_mask = K.and_mask(K.fill_holes(opened), K.fill_holes(rough))     # :138-140
+    seeds, nseeds = K.label(seeds_mask, conn=2)                  # :140 measure.label (8-conn)
+    _, bkg, _, _ = K.kmeans_1d(nl, 2, want_labels=False)         # :141-149
+    final_bkg = K.mask_mul(final, bkg)                           # :150
+    seeds_bkg = K.mask_labels(seeds, bkg)                        # :152
+    wmask = K.and_mask(rough, bkg)                               # :153
+    seg = K.watershed(final_bkg, seeds_bkg, wmask, negate=True)  # :154 watershed(-final_bkg)
+    seg = K.remove_small_objects(seg, 60, maxlab=nseeds)         # :155
+    seg = K.clear_border(seg)                                    # :156
+    seg, n = K.relabel_sequential(seg, nseeds)                   # :157
+    if keep is not None:
+        keep.update(image_sum=s, nl=nl, final=final, rough_mask=rough, seeds=seeds, bkg_mask=bkg,
+                    watershed=seg)
+    return seg, n, s, final_bkg
+
+
+def measure_multispecies(stack: torch.Tensor, calibration: torch.Tensor | None = None, keep: dict | None = None):
+    """multispecies measurement.py:161-174: segment, per-cell mean of the calibrated stack
+    (regionprops mean_intensity per channel, :167-171), row-max normalisation (:172)."""
+    seg, n, s, final_bkg = segment_multispecies(stack, calibration, keep)
+    sums, counts = K.label_sums(stack, seg, n, cal=calibration)
+    _, lor, avgint, avgint_norm = K.cell_table(sums, counts, n)
+    return Measurement(seg, n, lor, avgint, avgint_norm, extras=dict(image_sum=s, final_bkg=final_bkg))
+
+
+# --------------------------------------------------------------------------------------------
 # Classification (segmented cosine against a reference library; see DESIGN.md §classify)
 # --------------------------------------------------------------------------------------------
 @dataclass

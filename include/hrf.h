@@ -96,6 +96,24 @@ HRF_API hrf_status hrf_register_assemble(const float *const *src_host, const int
  * mask (nullable) zeroes the sum; negate flips the sign (watershed input). */
 HRF_API hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,
                                    int32_t negate, double *out, hrf_stream_t stream);
+/* the same sum over the flat-field corrected stack (multispecies :103-105): channels
+ * [cal_c0, cal_c1) of pixel p divided by cal[p*cal_sp + c*cal_sc] in f64 first -- numpy's
+ * stack / calibration broadcasting for an (H,W) plane (sp 1, sc 0), a (C,) vector (sp 0,
+ * sc 1) or a full (H,W,C) array (sp C, sc 1).  C <= 128.  cal NULL: plain sum. */
+HRF_API hrf_status hrf_channel_sum_cal(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
+                                       int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, int32_t mode, double *out,
+                                       hrf_stream_t stream);
+/* np.max(stack, axis=2) as f64 (ecoli :45, the per-laser registration images) */
+HRF_API hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *out, hrf_stream_t stream);
+/* the calibrated stack as f64, out (npix, C) (multispecies :104 image_channel / :166 _registered.npy) */
+HRF_API hrf_status hrf_calibrate_f64(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
+                                     int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, double *out,
+                                     hrf_stream_t stream);
+/* out = a AND b on u8 masks (multispecies :140, :153) */
+HRF_API hrf_status hrf_and_u8(const uint8_t *a, const uint8_t *b, int64_t n, uint8_t *out, hrf_stream_t stream);
+/* out = labels where mask, else 0 (multispecies :152 seeds * bkg) */
+HRF_API hrf_status hrf_mask_labels(const int32_t *labels, const uint8_t *mask, int64_t n, int32_t *out,
+                                   hrf_stream_t stream);
 HRF_API hrf_status hrf_max_f64(const double *a, int64_t n, double *max_dev, hrf_stream_t stream);
 HRF_API hrf_status hrf_div_scalar_f64(const double *a, int64_t n, const double *divisor_dev, double *out,
                                       hrf_stream_t stream);
@@ -104,6 +122,15 @@ HRF_API hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32
                                     hrf_stream_t stream);
 HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out,
                                     hrf_stream_t stream);
+
+/* ==== f1: registration shift estimate (register.hip) ====================================
+ * skimage.feature.register_translation(src, target)[0] (upsample_factor 1; ecoli :45-46,
+ * multispecies :82-83): argmax |ifft(F(src) conj(F(target)))| wrapped to (-n/2, n/2] per
+ * axis, via hipFFT (f64).  src/target (H, W) f64; work: hrf_register_workspace_bytes(H, W)
+ * device bytes; shift_host[2] = (row, col) integer shift.  Synchronises the stream. */
+HRF_API int64_t hrf_register_workspace_bytes(int64_t H, int64_t W);
+HRF_API hrf_status hrf_register_translation(const double *src, const double *target, int64_t H, int64_t W,
+                                            void *work, int32_t *shift_host, hrf_stream_t stream);
 
 /* ==== a4: non-local means (nlmeans.hip) ==================================================
  * skimage.restoration.denoise_nl_means(img, patch_size, patch_distance, h, fast_mode=True,
@@ -194,6 +221,11 @@ HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int3
 HRF_API hrf_status hrf_label_sums(const float *stack, const int32_t *labels, int64_t npix, int32_t C, int32_t maxlab,
                                   const float *cal, int32_t cal_c0, int32_t cal_c1, double *sums, int64_t *counts,
                                   hrf_stream_t stream);
+/* the same with a strided calibration: channels [c0, c1) of pixel p divided by
+ * cal[p*cal_sp + c*cal_sc] (plane: sp 1, sc 0; per channel: sp 0, sc 1; full: sp C, sc 1) */
+HRF_API hrf_status hrf_label_sums_cal(const float *stack, const int32_t *labels, int64_t npix, int32_t C,
+                                      int32_t maxlab, const float *cal, int64_t cal_sp, int32_t cal_sc, int32_t cal_c0,
+                                      int32_t cal_c1, double *sums, int64_t *counts, hrf_stream_t stream);
 /* rows = present labels ascending (regionprops order); avgint = sums/counts,
  * avgint_norm = avgint / rowmax (ecoli :157, classify_spectra.py:27). */
 HRF_API hrf_status hrf_cell_table(const double *sums, const int64_t *counts, int32_t maxlab, int32_t C,

@@ -2,8 +2,10 @@
 
 TEST INFRASTRUCTURE ONLY (the checker for tests/, smoke() and bench.py's cpu_baseline).
 Mirrors hiprfish-image-analysis-ecoli/hiprfish_imaging_spectral_image_measurement.py
-segment_images (:44-127) and measure_reference_images (:142-162), and the restated
-classification (train_reference.py metrics), step for step.
+segment_images (:44-127) and measure_reference_images (:142-162),
+hiprfish-image-analysis-synthetic-community/hiprfish_imaging_multispecies_spectral_image_measurement.py
+generate_2d_segmentation (:78-159) and measure_biofilm_images_no_reference (:161-174), and the
+restated classification (train_reference.py metrics), step for step.
 """
 from __future__ import annotations
 
@@ -74,3 +76,99 @@ def process_tile(stack, library, bounds, calibration=None):
     counts = O.barcode_counts(idx, library.shape[0])
     return dict(segmentation=seg, labels=labs, avgint=avgint, avgint_norm=avgint_norm, cell_idx=idx,
                 cell_dist=dist, counts=counts)
+
+
+# ---- multispecies measurement (synthetic-community) -------------------------------------
+def register_stacks(lasers, shifts, apply_mask):
+    """ecoli :51-70 / multispecies :85-102: dst[r, c] = src[r - dr, c - dc] inside the
+    shifted frame, 0 outside; apply_mask multiplies by the intersection of all frames."""
+    H, W = lasers[0].shape[:2]
+    reg = []
+    frame = np.ones((H, W), bool)
+    for img, (dr, dc) in zip(lasers, shifts):
+        out = np.zeros(img.shape, np.float64)
+        m = np.zeros((H, W), bool)
+        out[max(0, dr):H + min(0, dr), max(0, dc):W + min(0, dc)] = \
+            img[-min(0, dr):H - max(0, dr), -min(0, dc):W - max(0, dc)]
+        m[max(0, dr):H + min(0, dr), max(0, dc):W + min(0, dc)] = True
+        frame &= m
+        reg.append(out)
+    st = np.dstack(reg)
+    return st * frame[:, :, None] if apply_mask else st
+
+
+def estimate_shifts(lasers, reduce="max", clamp=15):
+    """ecoli :45-57 (channel max, |shift| > 15 -> 0) / multispecies :82-84 (channel sum)"""
+    proj = [np.max(l, axis=2).astype(np.float64) if reduce == "max" else np.sum(l.astype(np.float64), axis=2)
+            for l in lasers]
+    out = [(0, 0)]
+    for p in proj[1:]:
+        r, c = (int(v) for v in O.register_translation(proj[0], p))
+        if clamp is not None:
+            r = 0 if abs(r) > clamp else r
+            c = 0 if abs(c) > clamp else c
+        out.append((r, c))
+    return out
+
+
+def _calibrated(stack, calibration):
+    """stack / calibration in f64; an (H, W) plane applies to every channel (as libhrf's
+    per-pixel layout), any other shape broadcasts as numpy does"""
+    st = stack.astype(np.float64)
+    if calibration is None:
+        return st
+    c = calibration.astype(np.float64)
+    if c.shape == st.shape[:2]:
+        c = c[..., None]
+    return st / c
+
+
+def _brighter_cluster(img, lab, cen):
+    """multispecies :126-135 / :142-149: the cluster whose positive values have the larger mean
+    (i0 < i1 -> cluster 1).  When one cluster has no positive value the reference's choice
+    follows sklearn's arbitrary label order; the larger centre is taken then."""
+    i = []
+    for j in (0, 1):
+        v = img * (lab == j)
+        v = v[v > 0]
+        i.append(np.average(v) if v.size else np.nan)
+    if np.isnan(i[0]) or np.isnan(i[1]):
+        return lab == int(np.argmax(cen))
+    return lab == 1 if i[0] < i[1] else lab == 0
+
+
+def segment_multispecies(stack, calibration=None, keep=None, nl=None):
+    """multispecies :102-157 on the registered stack -> (segmentation, n, image_sum, final_bkg).
+    `nl` injects the NL-means image (a float step compared separately within tolerance) so the
+    discrete steps after it can be compared exactly."""
+    st = _calibrated(stack, calibration)                                          # :103-104
+    s = np.sum(st, axis=2)                                                        # :105
+    norm = s / np.max(s)                                                          # :106
+    if nl is None:
+        nl = O.nl_means_skimage(norm, 7, 11, 0.02, 0.0)                           # :108
+    final = O.enhance_2d(np.pad(nl, 5, mode='edge'))                              # :109-124
+    l2, c2, _ = O.kmeans_1d(final, 2)                                             # :125
+    rough = _brighter_cluster(final, l2, c2)                                      # :126-135
+    opened = O.remove_small_objects_mask(O.opening(rough), 10, 1)                 # :136-137
+    seeds, nseeds = O.label((O.fill_holes(opened) & O.fill_holes(rough)).astype(np.int32), 2)   # :138-140
+    lb, cb, _ = O.kmeans_1d(nl, 2)                                                # :141
+    bkg = _brighter_cluster(nl, lb, cb)                                           # :142-149
+    final_bkg = final * bkg                                                       # :150
+    seg = O.watershed(-final_bkg, seeds * bkg, rough & bkg)                       # :152-154
+    seg = O.remove_small_objects_labels(seg, 60)                                  # :155
+    seg = O.clear_border(seg)                                                     # :156
+    seg, n = O.relabel_sequential(seg)                                            # :157
+    if keep is not None:
+        keep.update(image_sum=s, norm=norm, nl=nl, final=final, rough_mask=rough, seeds=seeds, bkg_mask=bkg)
+    return seg, n, s, final_bkg
+
+
+def measure_multispecies(stack, calibration=None, keep=None, nl=None):
+    """multispecies :161-174 -> (segmentation, labels, avgint, avgint_norm)"""
+    seg, n, s, final_bkg = segment_multispecies(stack, calibration, keep, nl)
+    st = _calibrated(stack, calibration)
+    labs = np.arange(1, n + 1, dtype=np.int32)
+    labs = labs[np.bincount(seg.ravel(), minlength=n + 1)[1:] > 0]
+    avgint = np.stack([st[seg == l].mean(axis=0) for l in labs]) if len(labs) else np.zeros((0, st.shape[2]))
+    avgint_norm = avgint / avgint.max(axis=1, keepdims=True) if len(labs) else avgint
+    return seg, labs, avgint, avgint_norm

@@ -72,3 +72,38 @@ def test_process_tile_classification_and_counts(mods, orc):
     pi, pd = host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel]
     np.testing.assert_allclose(pd, rd, rtol=1e-5, atol=1e-5)
     assert (pi == ri).mean() > 0.97
+
+
+# ---- synthetic-community measurement (multispecies measurement.py:78-174) ------------------
+@pytest.mark.parametrize("H,W,seed,cal_kind", [(256, 256, 11, "channel"), (320, 384, 12, "full"),
+                                              (256, 256, 13, None)])
+def test_measure_multispecies_parity(mods, orc, H, W, seed, cal_kind):
+    P, S, OP = mods
+    stack, truth, lay, ref = S.tile(H, W, bounds=P.MULTI_BOUNDS, seed=seed)
+    C = stack.shape[2]
+    rng = np.random.default_rng(seed)
+    cal = None
+    if cal_kind == "channel":
+        cal = (0.5 + rng.random(C)).astype(np.float32)
+    elif cal_kind == "full":
+        cal = (0.5 + rng.random((H, W, C))).astype(np.float32)
+    keep = {}
+    m = P.measure_multispecies(stack, None if cal is None else torch.from_numpy(cal).cuda(), keep=keep)
+    # float stages: channel sum of the calibrated stack bit-exact, NL-means within 1e-12
+    okeep = {}
+    st64 = OP._calibrated(host(stack), cal)
+    s = np.sum(st64, axis=2)
+    assert np.array_equal(host(keep["image_sum"]), s)
+    np.testing.assert_allclose(host(keep["nl"]), orc.nl_means_skimage(s / s.max(), 7, 11, 0.02, 0.0),
+                               rtol=0, atol=1e-12)
+    # discrete stages exact once the NL-means image is shared
+    oseg, olabs, oavg, oavgn = OP.measure_multispecies(host(stack), cal, keep=okeep, nl=host(keep["nl"]))
+    np.testing.assert_allclose(host(keep["final"]), okeep["final"], rtol=1e-12, atol=1e-15)
+    for k in ("rough_mask", "bkg_mask"):
+        assert np.array_equal(host(keep[k]).astype(bool), okeep[k]), k
+    assert np.array_equal(host(keep["seeds"]), okeep["seeds"])
+    assert np.array_equal(host(m.segmentation), oseg)
+    assert m.maxlab == len(olabs) and len(olabs) >= 1
+    assert np.array_equal(host(m.labels), olabs)
+    np.testing.assert_allclose(host(m.avgint), oavg, rtol=1e-12)
+    np.testing.assert_allclose(host(m.avgint_norm), oavgn, rtol=1e-12)
