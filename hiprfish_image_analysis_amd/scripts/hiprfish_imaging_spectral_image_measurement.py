@@ -6,8 +6,8 @@ same flags (main :164-169), same outputs ({s}_avgint.csv, {s}_avgint_norm.csv, {
   -i/--image_name FILE...   per-laser images in 405, 488, 514, 561, 633 nm order
   -c/--calibration T|F       flat-field correction (default T)
   -cf/--calibration_images_filename  (H, W) calibration .npy applied to channels 0-31
-  --shifts dr,dc ...         per-laser registration shifts (default: all 0; the FFT shift
-                             estimate of :45-46 is not part of this build)
+  --shifts dr,dc ...         per-laser registration shifts overriding the estimate of
+                             :45-57 (register_translation of the channel-max images)
 """
 import argparse
 import os
@@ -36,9 +36,10 @@ def main(argv=None):
     print('Analyzing sample {}...'.format(sample))
     dev = torch.device("cuda", 0)
     lasers = [torch.from_numpy(io.load_laser_stack(f)).to(dev) for f in args.image_name]
-    shifts = [(0, 0)] * len(lasers)
     if args.shifts:
         shifts = [tuple(int(v) for v in s.split(',')) for s in args.shifts]
+    else:
+        shifts = P.estimate_shifts(lasers, reduce="max", clamp=15)               # :45-47
     # ecoli :54-57: shifts beyond 15 px are discarded
     shifts = [(r if abs(r) <= 15 else 0, c if abs(c) <= 15 else 0) for r, c in shifts]
     stack = K.register_assemble(lasers, shifts, apply_mask=True)          # :51-70

@@ -1,0 +1,102 @@
+"""The drop-in stage scripts (hiprfish_image_analysis_amd/scripts/) end to end on synthetic
+per-laser images written as {stem}.npy: registration estimate -> measurement -> files, then
+classification of the written spectra; outputs checked against the oracle restatement."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hiprfish_image_analysis_amd", "scripts"))
+
+
+def split_lasers(stack, bounds, shifts):
+    """(H, W, C) -> per-laser stacks, laser i displaced so that the reference registration
+    (dst[r] = src[r - shift]) undoes it"""
+    out = []
+    for i, (dr, dc) in enumerate(shifts):
+        out.append(np.ascontiguousarray(np.roll(stack[:, :, bounds[i]:bounds[i + 1]], (-dr, -dc), axis=(0, 1))))
+    return out
+
+
+def test_ecoli_measurement_cli(tmp_path, orc):
+    import pipeline as OP
+    import hiprfish_imaging_spectral_image_measurement as cli
+
+    from hiprfish_image_analysis_amd import synthetic as S
+    stack, _, _, _ = S.tile(256, 256, seed=31)
+    lasers = split_lasers(stack.cpu().numpy(), S.ECOLI_BOUNDS, [(0, 0), (2, -1), (0, 3), (-1, 0), (1, 1)])
+    files = []
+    for i, l in enumerate(lasers):
+        np.save(tmp_path / ("s_%d.npy" % (i + 1)), l)
+        files.append(str(tmp_path / ("s_%d.czi" % (i + 1))))
+    cal = (0.7 + 0.3 * np.random.default_rng(1).random((256, 256))).astype(np.float32)
+    np.save(tmp_path / "cal.npy", cal)
+    cli.main(['-i'] + files + ['-c', 'T', '-cf', str(tmp_path / "cal.npy")])
+    sample = str(tmp_path / "s")
+    shifts = OP.estimate_shifts(lasers, "max", 15)
+    reg = OP.register_stacks(lasers, shifts, True).astype(np.float32)
+    oseg, olabs, oavg, oavgn = OP.measure_ecoli(reg, calibration=cal)
+    assert np.array_equal(np.load(sample + "_seg.npy"), oseg)
+    np.testing.assert_allclose(np.loadtxt(sample + "_avgint.csv", delimiter=',', ndmin=2), oavg, rtol=1e-12)
+    np.testing.assert_allclose(np.loadtxt(sample + "_avgint_norm.csv", delimiter=',', ndmin=2), oavgn, rtol=1e-12)
+
+
+def test_multispecies_measure_and_classify_cli(tmp_path, orc):
+    import pandas as pd
+    import pipeline as OP
+    import hiprfish_imaging_classify_spectra as ccli
+    import hiprfish_imaging_multispecies_spectral_image_measurement as mcli
+
+    from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    stack, _, _, ref = S.tile(256, 256, nbit=7, bounds=S.MULTI_BOUNDS, seed=32)
+    lasers = split_lasers(stack.cpu().numpy(), S.MULTI_BOUNDS, [(0, 0), (3, 2), (-2, 0), (1, -4)])
+    for x, l in zip(mcli.EXCITATIONS, lasers):
+        np.save(tmp_path / ("m_%s.npy" % x), l)
+    C = stack.shape[2]
+    cal = (0.5 + np.random.default_rng(2).random(C)).astype(np.float32)
+    np.save(tmp_path / "cal.npy", cal)
+    m = mcli.main(['-i', str(tmp_path / "m_488.czi"), '-c', str(tmp_path / "cal.npy")])
+    sample = str(tmp_path / "m")
+    shifts = OP.estimate_shifts(lasers, "sum", None)
+    reg = OP.register_stacks(lasers, shifts, False).astype(np.float32)
+    # the script's measurement equals the pipeline on the oracle-registered stack ...
+    dreg = torch.from_numpy(reg).cuda()
+    dcal = torch.from_numpy(cal).cuda()
+    keep = {}
+    m2 = P.measure_multispecies(dreg, dcal, keep=keep)
+    seg = np.load(sample + "_seg.npy")
+    assert np.array_equal(seg, m2.segmentation.cpu().numpy())
+    # ... and the oracle restatement once the NL-means image is shared
+    oseg, olabs, oavg, oavgn = OP.measure_multispecies(reg, cal, nl=keep["nl"].cpu().numpy())
+    assert np.array_equal(seg, oseg) and len(olabs) >= 1
+    csv = pd.read_csv(sample + "_avgint_norm.csv")
+    assert list(csv.columns) == [str(i) for i in range(C)]
+    np.testing.assert_allclose(csv.values, oavgn, rtol=1e-12)
+    np.testing.assert_array_equal(np.load(sample + "_registered.npy"), reg.astype(np.float64) / cal.astype(np.float64))
+    # classification of the written spectra
+    np.save(tmp_path / "lib.npy", ref)
+    info = ccli.main(['-i', sample + "_avgint_norm.csv", '-r', str(tmp_path / "lib.npy")])
+    out = pd.read_csv(sample + "_cell_information.csv", header=None)
+    assert out.shape == (len(olabs), 77)
+    x = csv.values / csv.values.max(axis=1)[:, None]
+    lib = ref.astype(np.float64) / ref.astype(np.float64).max(axis=1, keepdims=True)
+    b = S.MULTI_BOUNDS
+    fx = np.stack([x[:, b[k]:b[k + 1]].max(axis=1) > 0.1 for k in range(4)], 1).astype(np.float64)
+    fr = np.stack([lib[:, b[k]:b[k + 1]].max(axis=1) > 0.1 for k in range(4)], 1).astype(np.float64)
+    idx, _ = orc.classify(x, lib, b, 2, fx, fr)
+    assert [str(v).zfill(7) for v in out[67]] == [format(i + 1, "07b") for i in idx]
+    np.testing.assert_allclose(out.iloc[:, 63:67].values.astype(np.float64), fx)
+    assert (out[68] == sample).all()
+    assert np.array_equal(out[69].values, olabs)
+    stats = orc.region_stats(oseg)
+    np.testing.assert_allclose(out.iloc[:, 70:76].values.astype(np.float64), stats[olabs][:, 1:7], rtol=1e-9, atol=1e-9)
+    assert np.array_equal(out[76].values, stats[olabs][:, 0].astype(np.int64))
+    assert info is not None and m is not None
+    del K
