@@ -5,6 +5,8 @@ No CPU fallback exists: a CPU tensor or a missing libhrf.so raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -263,26 +265,47 @@ def nl_means_2d(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
 _KM_STATE = {}
 
 
-def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True):
-    """-> labels int32 (or None), top-cluster mask u8, centres (list), iterations"""
+# "sorted" (one sort + step searches) or "stream" (one pass per Lloyd iteration); same results
+KMEANS_PATH = os.environ.get("HRF_KMEANS_PATH", "sorted")
+
+
+def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, path=None, share=None):
+    """1-D KMeans (sklearn KMeans(k, random_state=0) restated, see kmeans.hip)
+    -> labels int32 (or None), top-cluster mask u8, centres (list), iterations.
+    share: a dict passed to successive calls on the SAME x / valid so the sorted path sorts once."""
     import ctypes
     import numpy as np
     x = _dev(x, torch.float64, "x")
     n = x.numel()
     dev = x.device
-    key = (dev, _stream())        # one workspace per stream: concurrent tiles must not share it
-    st = _KM_STATE.get(key)
-    if st is None:
-        nb = _lib.lib().hrf_kmeans_state_bytes()
-        st = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
-        _KM_STATE[key] = st
     v = _u8(valid, "valid") if valid is not None else None
     labels = torch.empty(x.shape, dtype=torch.int32, device=dev) if want_labels else None
     top = torch.empty(x.shape, dtype=torch.uint8, device=dev)
     cen = np.zeros(k, np.float64)
     it = ctypes.c_int32(0)
-    _lib.call("hrf_kmeans_1d", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
-              ctypes.addressof(it), _ptr(st), _stream())
+    if (path or KMEANS_PATH) == "stream":
+        key = (dev, _stream())        # one workspace per stream: concurrent tiles must not share it
+        st = _KM_STATE.get(key)
+        if st is None:
+            nb = _lib.lib().hrf_kmeans_state_bytes()
+            st = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
+            _KM_STATE[key] = st
+        _lib.call("hrf_kmeans_1d", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
+                  ctypes.addressof(it), _ptr(st), _stream())
+        return labels, top, cen.tolist(), it.value
+    ident = (x.data_ptr(), n, v.data_ptr() if v is not None else 0)
+    reuse = share is not None and share.get("ident") == ident
+    if reuse:
+        ws = share["ws"]
+    else:
+        nb = int(_lib.lib().hrf_kmeans_sorted_workspace_bytes(n))
+        if nb <= 0:
+            raise _lib.HrfError("hrf_kmeans_sorted_workspace_bytes failed")
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        if share is not None:
+            share.update(ident=ident, ws=ws, x=x, valid=v)   # keep the inputs alive with the sort
+    _lib.call("hrf_kmeans_1d_sorted", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
+              ctypes.addressof(it), _ptr(ws), ws.numel(), int(reuse), _stream())
     return labels, top, cen.tolist(), it.value
 
 

@@ -41,8 +41,9 @@ def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: in
 def segment_ecoli(stack: torch.Tensor, keep: dict | None = None):
     """ecoli measurement.py:44-127 on the registered stack.  -> (segmentation int32, max label)"""
     image_cn = K.channel_sum(stack, mode=1)                              # :71-72 log(sum + 1e-2)
-    _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False)    # :73-84 brighter cluster
-    _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False)      # :85-94 brightest layer
+    share = {}                                                           # one sort for both fits
+    _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False, share=share)   # :73-84 brighter cluster
+    _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False, share=share)     # :85-94 brightest layer
     opened = K.binary_opening(K.remove_small_holes(interior, 64, 1))      # :95
     cell_sm = K.remove_small_objects(opened, 50, conn=1)                 # :96
     be = erosion_seeds(cell_sm)                                          # :97-110

@@ -150,6 +150,17 @@ HRF_API int64_t hrf_kmeans_state_bytes(void);
 HRF_API hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
                                  int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host,
                                  void *state_ws, hrf_stream_t stream);
+/* Same result (bit for bit: centres, labels, iteration count) from one radix sort of the
+ * values plus a prefix sum of their fixed-point encodings; all Lloyd iterations run in one
+ * launch as step searches on the sorted array.  work: hrf_kmeans_sorted_workspace_bytes(n)
+ * device bytes.  reuse_sort != 0: `work` already holds the sort of this very x / valid from
+ * a previous call (e.g. k = 2 then k = 3 on ecoli image_cn, :73 and :85).  Falls back to
+ * the streaming path by itself when its premise fails (NaN input, coincident centres). */
+HRF_API int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n);
+HRF_API hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
+                                        int32_t *labels, uint8_t *top_mask, double *centers_host,
+                                        int32_t *iters_host, void *work, int64_t work_bytes, int32_t reuse_sort,
+                                        hrf_stream_t stream);
 
 /* ==== a9/a10/a13: components, morphology, label cleanup (label.hip) ====================
  * img dtype: 0 = uint8 mask, 1 = int32 label image (equal values connect), 2 = uint8 mask

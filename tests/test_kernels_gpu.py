@@ -138,6 +138,44 @@ def test_kmeans_valid_mask_and_large(K, orc):
         assert it == rit and cen == rc.tolist() and np.array_equal(host(lab), rl)
 
 
+@pytest.mark.parametrize("n,k", [(1, 1), (2, 2), (4097, 3), (1 << 20, 2), (3 * (1 << 20) + 17, 3), (200000, 5),
+                                 (100000, 8), (4096 * 4096 + 5, 3)])
+def test_kmeans_sorted_matches_streaming_and_oracle(K, orc, n, k):
+    """the sorted path (one sort + step searches) equals the streaming pass and the restatement"""
+    rng = np.random.default_rng(n + k)
+    x = np.log(rng.gamma(2.0, 1.0, n) + 1e-2) if n > 10 else rng.random(n)
+    x[rng.random(n) < 0.01] = x[0]          # repeated values
+    d = dev(x)
+    a = K.kmeans_1d(d, k, path="sorted")
+    b = K.kmeans_1d(d, k, path="stream")
+    assert a[3] == b[3] and a[2] == b[2] and torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    if n <= (1 << 20):
+        rl, rc, rit = orc.kmeans_1d(x, k)
+        assert a[3] == rit and a[2] == rc.tolist() and np.array_equal(host(a[0]), rl)
+
+
+def test_kmeans_sorted_share_valid_and_fallbacks(K, orc):
+    rng = np.random.default_rng(8)
+    x = np.concatenate([rng.normal(0.2, 0.05, 300000), rng.normal(0.9, 0.1, 200000), rng.normal(3, 0.2, 50000)])
+    valid = rng.random(x.size) > 0.2
+    share = {}
+    for k in (2, 3, 2):   # second and third calls reuse the sort
+        lab, top, cen, it = K.kmeans_1d(dev(x), k, valid=dev(valid), share=share)
+        rl, rc, rit = orc.kmeans_1d(x, k, valid)
+        assert it == rit and cen == rc.tolist() and np.array_equal(host(lab), rl)
+        assert np.array_equal(host(top).astype(bool), (rl == int(np.argmax(rc))) & valid)
+    # constant input (coincident centres) and NaN input take the streaming path inside
+    for y in (np.full(10000, 0.5), np.where(rng.random(20000) < 0.001, np.nan, rng.random(20000))):
+        for k in (2, 3):
+            a = K.kmeans_1d(dev(y), k, path="sorted")
+            b = K.kmeans_1d(dev(y), k, path="stream")
+            assert a[3] == b[3] and np.array_equal(np.array(a[2]), np.array(b[2]), equal_nan=True)
+            assert torch.equal(a[0], b[0])
+    # empty
+    lab, top, cen, it = K.kmeans_1d(dev(np.zeros(0)), 2)
+    assert lab.numel() == 0 and it == 0
+
+
 # ---- a12 watershed ----------------------------------------------------------------------
 @pytest.mark.parametrize("shape", [(64, 64), (130, 97), (300, 330)])
 def test_watershed_vs_heap_flood(K, orc, shape):
