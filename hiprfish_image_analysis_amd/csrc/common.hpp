@@ -58,6 +58,31 @@ inline unsigned stream_grid(int64_t n, int block = 256) {
   return (unsigned)g;
 }
 
+// Grid for a persistent chunk loop: exactly the blocks that are resident at once (occupancy
+// x CUs), so every CU runs the same number of chunk iterations and no partial second wave of
+// blocks trails the launch.  The CU count is cached per device.
+inline int cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+template <class Kern>
+inline unsigned resident_grid(Kern kernel, int block, size_t shm, int64_t nwork) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, shm) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  int64_t g = (int64_t)per_cu * cu_count();
+  if (g > nwork) g = nwork;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
 // Line-profile sampling tables (neighbor2d.pyx:32-55, neighbor.pyx:209-243), computed on
 // the host and uploaded per call.  tables.cpp.
 int lp_table_2d(int patch, int nphi, int32_t *off /*[nphi][patch][2]*/);

@@ -12,12 +12,13 @@
 // then streams the data once accumulating into a rotating sum buffer; it exits at once when
 // converged, so the host launches batches and polls rarely.
 //
-// Sorted path (hrf_kmeans_1d_sorted, the one the pipelines use): the valid values are radix
-// sorted once (rocPRIM, on order-preserving uint64 encodings) and the fixed-point values
-// prefix-summed in that order.  With ascending, well separated centres the label
+// Sorted path (hrf_kmeans_1d_sorted, the one the pipelines use): the valid values are sorted
+// once by value bucket (2^20 equal-width buckets, rocPRIM radix sort of 20-bit keys with the
+// values as payload) and their fixed-point values prefix-summed in that order.  With ascending, well separated centres the label
 // argmin_j (x - c_j)^2 (first minimum) is a non-decreasing step function of x, so one Lloyd
-// iteration reduces to locating the k - 1 label steps in the sorted array (a 4096-ary search
-// by one 1024-thread workgroup) and reading cluster sums and counts off the prefix array:
+// iteration reduces to locating the k - 1 label steps in the bucket-ordered array (a 4096-ary
+// search by one 1024-thread workgroup that narrows to whole buckets, then counts the few
+// values of the straddling bucket) and reading cluster sums and counts off the prefix array:
 // the same integer sums, hence the same centres, as the streaming pass -- with all iterations
 // in ONE launch and no per-iteration pass over the data.  A sort can serve several k on the
 // same input (E. coli :73 and :85 both cluster image_cn).  Whenever the step-function premise
@@ -312,101 +313,158 @@ hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter
 }
 
 
-// ---- sorted path -------------------------------------------------------------------------
-__global__ void km_encode_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
-                                 unsigned long long *__restrict__ keys) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    keys[i] = (!valid || valid[i]) ? ord_enc(x[i]) : ~0ull;  // invalid entries sort past every value
+// ---- sorted path: sort by value bucket ------------------------------------------------------
+// NB value buckets of equal width over [min, max]; bucket(x) is a non-decreasing function of
+// x, so every value of bucket b is below every value of bucket b' > b.  The valid values are
+// radix sorted by their 20-bit bucket index (rocPRIM pairs, 3 digit passes instead of 8 for
+// full 64-bit keys; invalid entries get key NB and land past them), in no particular order
+// inside a bucket -- only integer sums are read off the result, so that order never shows.
+// off[b] = first position of bucket b, then the fixed-point encodings are prefix-summed.
+constexpr int KM_NB = 1 << 20;
+constexpr int KM_NB_BITS = 21;  // keys 0..NB inclusive
+
+__device__ __forceinline__ int km_bucket(double x, double mn, double inv) {
+  const double t = (x - mn) * inv;
+  return t >= 0.0 ? (t < (double)(KM_NB - 1) ? (int)t : KM_NB - 1) : 0;  // NaN -> 0
 }
 
-// q[i] = fixed-point value of the i-th smallest valid value (0 past the valid ones)
-__global__ void km_fixed_kernel(const unsigned long long *__restrict__ keys, int64_t n, const KmState *st,
-                                long long *__restrict__ q, long long *__restrict__ prefix0) {
-  const int s = st->scale;
-  const int64_t nv = (int64_t)st->nvalid;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *prefix0 = 0;
+// bucket geometry from the min / max found by km_minmax_kernel
+__global__ void km_bucket_init_kernel(KmState *st, double *geo) {
+  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
+  geo[0] = mn;
+  geo[1] = mx > mn ? (double)KM_NB / (mx - mn) : 0.0;
+}
+
+__global__ void km_bucket_key_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
+                                     const double *__restrict__ geo, uint32_t *__restrict__ key) {
+  const double mn = geo[0], inv = geo[1];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    q[i] = i < nv ? (long long)rint(ldexp(ord_dec(keys[i]), s)) : 0;
+    key[i] = (!valid || valid[i]) ? (uint32_t)km_bucket(x[i], mn, inv) : (uint32_t)KM_NB;
+}
+
+// off[b] = first sorted position whose key is >= b (b = 0..NB, a binary search each, so empty
+// stretches of buckets cost nothing extra); q = fixed-point values in sorted order
+__global__ void km_bucket_bounds_kernel(const uint32_t *__restrict__ key, const double *__restrict__ xs, int64_t n,
+                                        const KmState *st, unsigned long long *__restrict__ off,
+                                        long long *__restrict__ q, long long *__restrict__ prefix0) {
+  const int s = st->scale;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t0 == 0) *prefix0 = 0;
+  for (int64_t b = t0; b <= KM_NB; b += T) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)key[mid] < b) lo = mid + 1;
+      else hi = mid;
+    }
+    off[b] = (unsigned long long)lo;
+  }
+  for (int64_t i = t0; i < n; i += T) q[i] = (long long)rint(ldexp(xs[i], s));
 }
 
 constexpr int KS_T = 1024;           // threads of the iteration workgroup
 constexpr int KS_P = 4;              // probes per thread per round -> 4096-ary search
 static_assert(KS_T * KS_P == 4096, "index arithmetic below shifts by 12");
 
-// First index in [lo, hi) of the sorted values whose label exceeds j (hi when none), for all
-// boundaries j < K - 1 at once; pos[j] receives the answer.
+// For label step j (labels <= j versus > j): the number of bucket-ordered values with label
+// <= j and the sum of their fixed-point encodings.  Invariant: the range [lo, hi) starts and
+// ends on bucket boundaries, every value before it has label <= j and every value after it
+// label > j (labels are non-decreasing in the value, buckets are ordered by value).  A round
+// probes 4096 evenly spaced values: the range shrinks to [start of the last bucket holding a
+// "<= j" probe, end of the first bucket holding a "> j" probe).  A range of <= 4096 values, or
+// one that a round could not halve, is counted exhaustively.
 template <int K>
-__device__ void km_find_steps(const unsigned long long *__restrict__ keys, int64_t nv, const double *c,
-                              int64_t *pos, int *cnt_sh) {
+__device__ void km_bucket_step(const double *__restrict__ xs, const long long *__restrict__ q,
+                               const long long *__restrict__ prefix, const unsigned long long *__restrict__ off,
+                               int64_t nv, double mn, double inv, const double *c, int j, int64_t *cnt_le,
+                               long long *sum_le) {
   const int t = threadIdx.x;
-  __shared__ int64_t lo_sh[KMAX], hi_sh[KMAX];
-  if (t < K - 1) {
-    lo_sh[t] = 0;
-    hi_sh[t] = nv;
+  __shared__ int64_t lo_sh, hi_sh;
+  __shared__ int bf_sh, bt_sh, exh_sh;
+  __shared__ unsigned long long nf_sh;
+  __shared__ long long sf_sh;
+  if (t == 0) {
+    lo_sh = 0;
+    hi_sh = nv;
+    exh_sh = 0;
   }
   __syncthreads();
-  for (int j = 0; j < K - 1; ++j) {
-    // every boundary is searched with the whole workgroup; its range shrinks 4096-fold per round
-    while (true) {
-      const int64_t lo = lo_sh[j], hi = hi_sh[j];
-      const int64_t len = hi - lo;
-      if (len <= 0) break;
-      if (t == 0) *cnt_sh = 0;
-      __syncthreads();
-      const bool exact = len <= (int64_t)KS_T * KS_P;
-      int nf = 0;  // probes of this thread whose label is <= j
-#pragma unroll
-      for (int p = 0; p < KS_P; ++p) {
-        const int m = t * KS_P + p;
-        int64_t idx;
-        if (exact) {
-          idx = lo + m;
-          if (idx >= hi) continue;
-        } else {
-          idx = lo + ((len * m) >> 12);  // KS_T * KS_P = 4096; len < 2^51
-        }
-        nf += km_assign<K>(ord_dec(keys[idx]), c) <= j;
-      }
-      const int wsum = hrf::wave_sum(nf);
-      if ((t & 63) == 0 && wsum) atomicAdd(cnt_sh, wsum);
-      __syncthreads();
-      const int F = *cnt_sh;
-      __syncthreads();
-      if (exact) {
-        if (t == 0) {
-          lo_sh[j] = lo + F;
-          hi_sh[j] = lo + F;
-        }
-        __syncthreads();
-        break;
-      }
-      // probes are a non-decreasing sample: the first F say "<= j", the rest "> j"
+  while (true) {
+    const int64_t lo = lo_sh, hi = hi_sh;
+    const int64_t len = hi - lo;
+    if (exh_sh || len <= (int64_t)KS_T * KS_P) {
+      // count the range exhaustively: values with label <= j and the sum of their encodings
       if (t == 0) {
-        const int64_t nlo = F == 0 ? lo : lo + ((len * (F - 1)) >> 12) + 1;
-        const int64_t nhi = F == KS_T * KS_P ? hi : lo + ((len * F) >> 12);
-        lo_sh[j] = nlo;
-        hi_sh[j] = nhi;
+        nf_sh = 0;
+        sf_sh = 0;
       }
       __syncthreads();
+      unsigned long long nf = 0;
+      long long sf = 0;
+      for (int64_t idx = lo + t; idx < hi; idx += KS_T)
+        if (km_assign<K>(xs[idx], c) <= j) {
+          nf += 1;
+          sf += q[idx];
+        }
+      nf = hrf::wave_sum(nf);
+      sf = hrf::wave_sum(sf);
+      if ((t & 63) == 0 && nf) {
+        atomicAdd(&nf_sh, nf);
+        atomicAdd((unsigned long long *)&sf_sh, (unsigned long long)sf);
+      }
+      __syncthreads();
+      if (t == 0) {
+        *cnt_le = lo + (int64_t)nf_sh;
+        *sum_le = prefix[lo] + sf_sh;
+      }
+      __syncthreads();
+      return;
     }
-    // the next boundary lies at or after this one
-    if (t == 0 && j + 1 < K - 1) lo_sh[j + 1] = lo_sh[j];
+    if (t == 0) {
+      bf_sh = -1;
+      bt_sh = KM_NB;
+    }
+    __syncthreads();
+    int bf = -1, bt = KM_NB;
+#pragma unroll
+    for (int p = 0; p < KS_P; ++p) {
+      const int64_t idx = lo + ((len * (t * KS_P + p)) >> 12);  // KS_T * KS_P = 4096; len < 2^51
+      const double v = xs[idx];
+      const int b = km_bucket(v, mn, inv);
+      if (km_assign<K>(v, c) <= j) bf = b > bf ? b : bf;
+      else bt = b < bt ? b : bt;
+    }
+    if (bf >= 0) atomicMax(&bf_sh, bf);
+    if (bt < KM_NB) atomicMin(&bt_sh, bt);
+    __syncthreads();
+    if (t == 0) {
+      const int64_t nlo = bf_sh >= 0 ? (int64_t)off[bf_sh] : lo;
+      const int64_t nhi = bt_sh < KM_NB ? (int64_t)off[bt_sh + 1] : hi;
+      const int64_t clo = nlo > lo ? nlo : lo, chi = nhi < hi ? nhi : hi;
+      exh_sh = 2 * (chi - clo) > len;  // few buckets hold the range: no real progress
+      lo_sh = clo;
+      hi_sh = chi;
+    }
     __syncthreads();
   }
-  if (t < K - 1) pos[t] = lo_sh[t];
-  __syncthreads();
 }
 
 template <int K>
-__global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const unsigned long long *__restrict__ keys,
-                                                              const long long *__restrict__ prefix, KmState *st,
+__global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const double *__restrict__ xs,
+                                                              const long long *__restrict__ q,
+                                                              const long long *__restrict__ prefix,
+                                                              const unsigned long long *__restrict__ off,
+                                                              const double *__restrict__ geo, KmState *st,
                                                               int max_iter) {
   __shared__ double c[KMAX];
-  __shared__ int64_t pos[KMAX];
-  __shared__ int cnt_sh, stop;
+  __shared__ int64_t cle[KMAX];
+  __shared__ long long sle[KMAX];
+  __shared__ int stop;
   const int t = threadIdx.x;
   const int64_t nv = (int64_t)st->nvalid;
   const int s = st->scale;
+  const double mn = geo[0], inv = geo[1];
   if (t < K) c[t] = st->center[t];
   if (t == 0) stop = 0;
   __syncthreads();
@@ -428,20 +486,22 @@ __global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const unsigned lon
     }
     __syncthreads();
     if (stop) break;
-    km_find_steps<K>(keys, nv, c, pos, &cnt_sh);
+    for (int j = 0; j + 1 < K; ++j) km_bucket_step<K>(xs, q, prefix, off, nv, mn, inv, c, j, &cle[j], &sle[j]);
     if (t == 0) {
       int changed = 0;
-      int64_t p0 = 0;
+      int64_t c0 = 0;
+      long long s0 = 0;
       for (int j = 0; j < K; ++j) {
-        const int64_t p1 = j < K - 1 ? pos[j] : nv;
-        const int64_t cn = p1 - p0;
+        const int64_t c1 = j < K - 1 ? cle[j] : nv;
+        const long long s1 = j < K - 1 ? sle[j] : prefix[nv];
+        const int64_t cn = c1 - c0;
         if (cn) {
-          const long long sm = prefix[p1] - prefix[p0];
-          const double cj = ldexp((double)sm / (double)cn, -s);
+          const double cj = ldexp((double)(s1 - s0) / (double)cn, -s);
           if (cj != c[j]) changed = 1;
           c[j] = cj;
         }
-        p0 = p1;
+        c0 = c1;
+        s0 = s1;
       }
       if (!changed) stop = 1;
     }
@@ -461,7 +521,10 @@ __global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const unsigned lon
 
 struct SortWs {
   KmState *st;
-  unsigned long long *keys_in, *keys;
+  double *geo;
+  uint32_t *key_in, *key;
+  unsigned long long *off;
+  double *xs;
   long long *q, *prefix;
   void *tmp;
   size_t tmp_bytes;
@@ -471,28 +534,42 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 hrf_status sort_tmp_bytes(int64_t n, size_t *bytes) {
   size_t a = 0, b = 0;
-  HRF_HIP(rocprim::radix_sort_keys(nullptr, a, (unsigned long long *)nullptr, (unsigned long long *)nullptr,
-                                   (size_t)std::max<int64_t>(n, 1), 0, 64, (hipStream_t)0));
-  HRF_HIP(rocprim::inclusive_scan(nullptr, b, (long long *)nullptr, (long long *)nullptr,
-                                  (size_t)std::max<int64_t>(n, 1), rocprim::plus<long long>(), (hipStream_t)0));
+  const size_t m = (size_t)std::max<int64_t>(n, 1);
+  HRF_HIP(rocprim::radix_sort_pairs(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr, (const double *)nullptr,
+                                    (double *)nullptr, m, 0, KM_NB_BITS, (hipStream_t)0));
+  HRF_HIP(rocprim::inclusive_scan(nullptr, b, (const unsigned long long *)nullptr, (unsigned long long *)nullptr, m,
+                                  rocprim::plus<unsigned long long>(), (hipStream_t)0));
   *bytes = std::max(a, b);
   return HRF_OK;
 }
 
+int64_t sort_ws_bytes(int64_t n, size_t tmp_bytes) {
+  const size_t m = (size_t)std::max<int64_t>(n, 1);
+  return (int64_t)(align256(sizeof(KmState)) + 256 + 2 * align256(sizeof(uint32_t) * m) +
+                   align256(sizeof(unsigned long long) * (KM_NB + 1)) + 2 * align256(sizeof(double) * m) +
+                   align256(sizeof(long long) * (m + 1)) + align256(tmp_bytes));
+}
+
 SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   char *w = (char *)work;
+  const size_t m = (size_t)std::max<int64_t>(n, 1);
   SortWs ws{};
-  const size_t nb = align256(sizeof(unsigned long long) * (size_t)std::max<int64_t>(n, 1));
   ws.st = (KmState *)w;
   w += align256(sizeof(KmState));
-  ws.keys_in = (unsigned long long *)w;
-  w += nb;
-  ws.keys = (unsigned long long *)w;
-  w += nb;
+  ws.geo = (double *)w;
+  w += 256;
+  ws.key_in = (uint32_t *)w;
+  w += align256(sizeof(uint32_t) * m);
+  ws.key = (uint32_t *)w;
+  w += align256(sizeof(uint32_t) * m);
+  ws.off = (unsigned long long *)w;
+  w += align256(sizeof(unsigned long long) * (KM_NB + 1));
+  ws.xs = (double *)w;
+  w += align256(sizeof(double) * m);
   ws.q = (long long *)w;
-  w += nb;
+  w += align256(sizeof(double) * m);
   ws.prefix = (long long *)w;
-  w += align256(sizeof(long long) * (size_t)(std::max<int64_t>(n, 1) + 1));
+  w += align256(sizeof(long long) * (m + 1));
   ws.tmp = w;
   ws.tmp_bytes = tmp_bytes;
   return ws;
@@ -514,16 +591,20 @@ hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int m
   km_init_kernel<<<1, 1, 0, s>>>(st, K);
   HRF_LAUNCHED();
   if (!reuse && n > 0) {
-    km_encode_kernel<<<g, 256, 0, s>>>(x, valid, n, ws.keys_in);
+    km_bucket_init_kernel<<<1, 1, 0, s>>>(st, ws.geo);
+    km_bucket_key_kernel<<<g, 256, 0, s>>>(x, valid, n, ws.geo, ws.key_in);
     HRF_LAUNCHED();
     size_t tb = ws.tmp_bytes;
-    HRF_HIP(rocprim::radix_sort_keys(ws.tmp, tb, ws.keys_in, ws.keys, (size_t)n, 0, 64, s));
-    km_fixed_kernel<<<g, 256, 0, s>>>(ws.keys, n, st, ws.q, ws.prefix);
+    HRF_HIP(rocprim::radix_sort_pairs(ws.tmp, tb, ws.key_in, ws.key, x, ws.xs, (size_t)n, 0, KM_NB_BITS, s));
+    km_bucket_bounds_kernel<<<hrf::stream_grid(std::max<int64_t>(n, KM_NB + 1)), 256, 0, s>>>(ws.key, ws.xs, n, st, ws.off, ws.q, ws.prefix);
     HRF_LAUNCHED();
     tb = ws.tmp_bytes;
-    HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, ws.q, ws.prefix + 1, (size_t)n, rocprim::plus<long long>(), s));
+    // entries past the valid values (invalid ones, sorted last) are never read back: the scan
+    // covers all n in unsigned (wrapping) arithmetic; prefixes up to nvalid are the exact sums
+    HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, (const unsigned long long *)ws.q, (unsigned long long *)ws.prefix + 1,
+                                    (size_t)n, rocprim::plus<unsigned long long>(), s));
   }
-  km_sorted_iter_kernel<K><<<1, KS_T, 0, s>>>(ws.keys, ws.prefix, st, max_iter);
+  km_sorted_iter_kernel<K><<<1, KS_T, 0, s>>>(ws.xs, ws.q, ws.prefix, ws.off, ws.geo, st, max_iter);
   HRF_LAUNCHED();
   if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
   HRF_LAUNCHED();
@@ -570,9 +651,7 @@ hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32
 int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n) {
   size_t tb = 0;
   if (sort_tmp_bytes(n, &tb) != HRF_OK) return -1;
-  const size_t nb = align256(sizeof(unsigned long long) * (size_t)std::max<int64_t>(n, 1));
-  return (int64_t)(align256(sizeof(KmState)) + 3 * nb + align256(sizeof(long long) * (size_t)(std::max<int64_t>(n, 1) + 1)) +
-                   align256(tb));
+  return sort_ws_bytes(n, tb);
 }
 
 hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,

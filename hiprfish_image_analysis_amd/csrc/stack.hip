@@ -284,7 +284,8 @@ hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const ui
   if (C <= 128) {
     const int vec_ok = C >= 4 && (((uintptr_t)stack & 15) == 0);
     const int64_t nch = hrf::cdiv(npix, CS_P);
-    channel_sum_lds_kernel<false><<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
+    const size_t shm = sizeof(float) * CS_P * C;
+    channel_sum_lds_kernel<false><<<hrf::resident_grid(channel_sum_lds_kernel<false>, 256, shm, nch), 256, shm,
                                     (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate, out, vec_ok, Cal{});
   } else {
     channel_sum_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, mask, mode, negate,
@@ -304,7 +305,8 @@ hrf_status hrf_channel_sum_cal(const float *stack, int64_t npix, int32_t C, cons
   HRF_REQUIRE(stack && out, "channel_sum_cal: null buffer");
   const int vec_ok = C >= 4 && (((uintptr_t)stack & 15) == 0);
   const int64_t nch = hrf::cdiv(npix, CS_P);
-  channel_sum_lds_kernel<true><<<(unsigned)std::min<int64_t>(nch, 256 * 8), 256, sizeof(float) * CS_P * C,
+  const size_t shm = sizeof(float) * CS_P * C;
+  channel_sum_lds_kernel<true><<<hrf::resident_grid(channel_sum_lds_kernel<true>, 256, shm, nch), 256, shm,
                                  (hipStream_t)stream>>>(stack, npix, C, nullptr, mode, 0, out, vec_ok,
                                                         Cal{cal, cal_sp, cal_sc, cal_c0, cal_c1});
   HRF_LAUNCHED();

@@ -304,7 +304,7 @@ hrf_status hrf_label_sums_cal(const float *stack, const int32_t *labels, int64_t
   const int vec_ok = C >= 4 && ((C * LS_P) % 4 == 0) && (((uintptr_t)stack & 15) == 0);
   const size_t shm = sizeof(float) * LS_P * C;
   const int64_t nchunks = hrf::cdiv(npix, LS_P);
-  const unsigned grid = (unsigned)std::min<int64_t>(nchunks, 256 * 16);
+  const unsigned grid = hrf::resident_grid(label_sums_kernel, 256, shm, nchunks);
   label_sums_kernel<<<grid, 256, shm, s>>>(stack, labels, npix, C, maxlab, cal, cal_sp, cal_sc, cal_c0, cal_c1, sums,
                                            (unsigned long long *)counts, vec_ok);
   HRF_LAUNCHED();

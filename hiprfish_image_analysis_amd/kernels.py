@@ -646,3 +646,51 @@ def erosion_seeds(cell_sm, area_max=600, min_obj=10):
     be = torch.empty((H, W), dtype=torch.uint8, device=labels.device)
     _lib.call("hrf_erosion_seeds", _ptr(labels), H, W, n, _ptr(box), area_max, min_obj, _ptr(be), _stream())
     return be
+
+
+# ---- native segmentation drivers (segment.hip) ------------------------------------------------
+_SEG_CTX = {}
+
+
+def _seg_ctx(dev, H, W):
+    """one driver context per (device, stream, tile size): concurrent tiles on different streams
+    never share buffers"""
+    import ctypes
+    key = (dev, _stream(), H, W)
+    h = _SEG_CTX.get(key)
+    if h is None:
+        h = ctypes.c_void_p()
+        _lib.call("hrf_seg_ctx_create", H, W, ctypes.addressof(h))
+        _SEG_CTX[key] = h
+    return h
+
+
+def segment_ecoli_native(stack):
+    """ecoli measurement.py:44-127 in one native call -> (segmentation int32, max label)"""
+    import ctypes
+    stack = _dev(stack, torch.float32, "stack")
+    H, W, C = stack.shape
+    seg = torch.empty((H, W), dtype=torch.int32, device=stack.device)
+    mx = ctypes.c_int32(0)
+    _lib.call("hrf_segment_ecoli", _seg_ctx(stack.device, H, W), _ptr(stack), C, _ptr(seg), ctypes.addressof(mx),
+              _stream())
+    return seg, mx.value
+
+
+def segment_multispecies_native(stack, cal=None):
+    """multispecies measurement.py:102-157 in one native call
+    -> (segmentation relabelled 1..n, n, image_sum f64, final_bkg f64)"""
+    import ctypes
+    stack = _dev(stack, torch.float32, "stack")
+    H, W, C = stack.shape
+    calp, sp, sc, c0, c1 = None, 1, 0, 0, C
+    if cal is not None:
+        cal_t, sp, sc, c0, c1 = _cal_layout(cal, H, W, C)
+        calp = _ptr(cal_t)
+    seg = torch.empty((H, W), dtype=torch.int32, device=stack.device)
+    s = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    fb = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    n = ctypes.c_int32(0)
+    _lib.call("hrf_segment_multispecies", _seg_ctx(stack.device, H, W), _ptr(stack), C, calp, sp, sc, c0, c1,
+              _ptr(seg), ctypes.addressof(n), _ptr(s), _ptr(fb), _stream())
+    return seg, n.value, s, fb

@@ -6,6 +6,7 @@ Each function cites the reference lines it stands in for.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -38,8 +39,15 @@ def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: in
     return be
 
 
+# The segmentation chains run as one native call (segment.hip, same calls in the same order)
+# unless intermediates are requested (`keep`) or HRF_NATIVE_SEG=0.
+NATIVE_SEG = os.environ.get("HRF_NATIVE_SEG", "1") != "0"
+
+
 def segment_ecoli(stack: torch.Tensor, keep: dict | None = None):
     """ecoli measurement.py:44-127 on the registered stack.  -> (segmentation int32, max label)"""
+    if keep is None and NATIVE_SEG:
+        return K.segment_ecoli_native(stack)
     image_cn = K.channel_sum(stack, mode=1)                              # :71-72 log(sum + 1e-2)
     share = {}                                                           # one sort for both fits
     _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False, share=share)   # :73-84 brighter cluster
@@ -110,6 +118,8 @@ def segment_multispecies(stack: torch.Tensor, calibration: torch.Tensor | None =
     The two KMeans(2) cluster choices (:125-135, :141-149) take the cluster whose positive
     values have the larger mean; for a 1-D partition into intervals that is the cluster with
     the larger centre (kernels.kmeans_1d's top mask)."""
+    if keep is None and NATIVE_SEG:
+        return K.segment_multispecies_native(stack, calibration)
     s = K.channel_sum(stack, cal=calibration)                    # :104-105 sum(stack / cal)
     norm = K.div_scalar(s, K.max_f64(s))                         # :106
     nl = K.nl_means_2d(norm, 7, 11, 0.02, 0.0)                   # :108 (estimate_sigma :107 unused)

@@ -225,6 +225,25 @@ HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int3
                                  int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
                                  int32_t max_passes, int32_t *passes_host, hrf_stream_t stream);
 
+/* ==== native segmentation drivers (segment.hip) ==========================================
+ * One call runs a whole segmentation chain -- the same library calls, in the same order, as
+ * pipeline.segment_ecoli / segment_multispecies -- with device buffers owned by a context
+ * sized for one H x W tile (create once per tile size and per concurrently used stream; a
+ * context serves one call at a time).  Outputs are caller-owned device buffers. */
+typedef struct hrf_seg_ctx hrf_seg_ctx;
+HRF_API hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out);
+HRF_API hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *ctx);
+/* ecoli measurement.py:44-127: seg_out (H*W int32, labels not re-sequenced), *maxlab_host */
+HRF_API hrf_status hrf_segment_ecoli(hrf_seg_ctx *ctx, const float *stack, int32_t C, int32_t *seg_out,
+                                     int32_t *maxlab_host, hrf_stream_t stream);
+/* multispecies measurement.py:102-157 (calibration as hrf_channel_sum_cal, cal may be NULL):
+ * seg_out relabelled 1..*nlab_host; image_sum_out / final_bkg_out (nullable, H*W f64) receive
+ * the calibrated channel sum (:105) and the background-filtered enhanced image (:150). */
+HRF_API hrf_status hrf_segment_multispecies(hrf_seg_ctx *ctx, const float *stack, int32_t C, const float *cal,
+                                            int64_t cal_sp, int32_t cal_sc, int32_t cal_c0, int32_t cal_c1,
+                                            int32_t *seg_out, int32_t *nlab_host, double *image_sum_out,
+                                            double *final_bkg_out, hrf_stream_t stream);
+
 /* ==== a14-a16, a20, a21, a23: per-label reductions (stats.hip) ==========================
  * regionprops(seg, intensity_image=stack[:,:,k]).mean_intensity for all k in ONE pass
  * (ecoli :151-155, multispecies :167-171): sums[(maxlab+1)*C] f64, counts[maxlab+1];

@@ -107,3 +107,22 @@ def test_measure_multispecies_parity(mods, orc, H, W, seed, cal_kind):
     assert np.array_equal(host(m.labels), olabs)
     np.testing.assert_allclose(host(m.avgint), oavg, rtol=1e-12)
     np.testing.assert_allclose(host(m.avgint_norm), oavgn, rtol=1e-12)
+
+
+# ---- native drivers (segment.hip) == the Python composition of the same calls --------------
+@pytest.mark.parametrize("H,W,seed", [(256, 256, 21), (384, 640, 22), (1024, 1024, 23)])
+def test_native_segmentation_equals_composed(mods, H, W, seed):
+    P, S, OP = mods
+    stack, _, _, _ = S.tile(H, W, seed=seed)
+    seg_n, mx_n = P.segment_ecoli(stack)                 # one native call
+    seg_c, mx_c = P.segment_ecoli(stack, keep={})        # composed from Python
+    assert mx_n == mx_c and torch.equal(seg_n, seg_c)
+    ms, _, _, _ = S.tile(H, W, nbit=7, bounds=P.MULTI_BOUNDS, seed=seed)
+    cal = torch.rand(ms.shape[2], device="cuda") + 0.5
+    a = P.segment_multispecies(ms, cal)
+    b = P.segment_multispecies(ms, cal, keep={})
+    assert a[1] == b[1] and torch.equal(a[0], b[0])
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    # repeated calls reuse the context
+    seg_n2, _ = P.segment_ecoli(stack)
+    assert torch.equal(seg_n2, seg_n)

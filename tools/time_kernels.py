@@ -1,6 +1,6 @@
 """Time individual libhrf kernels on resident 2048x2048 inputs (HIP events, mean of 5).
 
-python tools/time_kernels.py [nlmeans] [classify] [register]
+python tools/time_kernels.py [nlmeans] [classify] [stream]
 """
 import sys
 
@@ -44,6 +44,23 @@ def main():
                 ms = timed(lambda: K.classify_pixels(stack, refx, R, bounds, mode))
                 tf = 2.0 * H * W * R * C / ms / 1e9
                 print("classify C=%d R=%d mode %d: %.3f ms  %.1f TF/s algorithmic" % (C, R, mode, ms, tf))
+
+    if "stream" in what:
+        from hiprfish_image_analysis_amd import pipeline as P
+        stack, truth, _, _ = S.tile(H, W, seed=3)
+        C = stack.shape[2]
+        nb = H * W * (4 * C + 8)
+        ms = timed(lambda: K.channel_sum(stack, mode=1))
+        print("channel_sum (log) 2048^2x95: %.3f ms  %.0f GB/s (%.1f %% of 8 TB/s)" % (ms, nb / ms / 1e6, nb / ms / 8e10))
+        cal = torch.rand(C, device="cuda") + 0.5
+        ms = timed(lambda: K.channel_sum(stack, cal=cal))
+        print("channel_sum cal(C) 2048^2x95: %.3f ms  %.0f GB/s" % (ms, nb / ms / 1e6))
+        seg, maxlab = P.segment_ecoli(stack)
+        fg = int(K.count_nonzero(seg))
+        nb2 = fg * 4 * C + H * W * 4
+        ms = timed(lambda: K.label_sums(stack, seg, maxlab))
+        print("label_sums (%d labels, %.0f %% fg): %.3f ms  %.0f GB/s algorithmic" % (maxlab, 100.0 * fg / H / W, ms,
+                                                                                      nb2 / ms / 1e6))
 
 
 if __name__ == "__main__":
