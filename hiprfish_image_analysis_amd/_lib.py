@@ -10,7 +10,7 @@ import os
 import re
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libhrf.so")
+LIB_PATH = os.environ.get("HRF_LIB") or os.path.join(_PKG, "libhrf.so")   # HRF_LIB: A/B builds
 HEADER = os.path.join(os.path.dirname(_PKG), "include", "hrf.h")
 
 _lib = None
