@@ -109,7 +109,11 @@ def main():
     ev = []
 
     T = max(1, args.concurrent)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(T)] if T > 1 else [torch.cuda.current_stream(dev)]
+    # the segmentation chains (short, latency-bound launches) run on high-priority streams so
+    # their workgroups are dispatched ahead of the pending ones of the long classifier grid,
+    # which process_tile puts on a default-priority side stream
+    prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("HRF_PRIORITY", "1") != "0" else 0
+    streams = [torch.cuda.Stream(device=dev, priority=prio) for _ in range(T)]
     pool = None
     if T > 1:
         from concurrent.futures import ThreadPoolExecutor
