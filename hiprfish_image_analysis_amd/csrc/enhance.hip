@@ -174,6 +174,58 @@ __global__ __launch_bounds__(256) void enhance3d_kernel(const double *__restrict
 }
 
 // ------------------------------------------------------------------------------------
+// neighbor.line_profile_memory_efficient_v3 (neighbor.pyx:268-349): its own sampling table
+// (LP3D_V3: reaches up to 18 voxels along x and z, past the patch), read the way the
+// reference's unchecked memoryview reads it -- flat address (i+a)*yp*zp + (j+b)*zp + (k+c)
+// into the padded array, 0 past its end (undefined in the reference) -- the 72 normalised
+// centre taps, their mean in loop order, p25 / p75 and mean*(p25-p75)/(p25+p75+1e-8).
+// One thread per voxel straight from global memory (L2-resident windows): the reference
+// imports this function but never calls it.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void enhance3d_v3_kernel(const double *__restrict__ pad, int64_t xp, int64_t yp,
+                                                           int64_t zp, double *__restrict__ out, int64_t X, int64_t Y,
+                                                           int64_t Z) {
+  const int64_t total = xp * yp * zp, n = X * Y * Z;
+  for (int64_t vox = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; vox < n; vox += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = vox / (Y * Z), rem = vox - i * (Y * Z), j = rem / Z, k = rem - j * Z;
+    double v[72];
+    double avg = 0.0;
+#pragma unroll
+    for (int t = 0; t < 72; ++t) {
+      double mn = 0.0, mx = 0.0, c = 0.0;
+#pragma unroll
+      for (int l = 0; l < 11; ++l) {
+        const int64_t a = (i + LP3D_V3_11_9_9[t][l][0]) * yp * zp + (j + LP3D_V3_11_9_9[t][l][1]) * zp +
+                          (k + LP3D_V3_11_9_9[t][l][2]);
+        const double q = a < total ? pad[a] : 0.0;
+        if (l == 0) {
+          mn = q;
+          mx = q;
+        } else {
+          mn = q < mn ? q : mn;
+          mx = q > mx ? q : mx;
+        }
+        if (l == 5) c = q;
+      }
+      double r = mx - mn;
+      if (1e-8 > r) r = 1e-8;
+      v[t] = (c - mn) / r;
+      avg += v[t];  // :341-343, in loop order
+    }
+    avg /= 72.0;
+#pragma unroll
+    for (int q = 0; q < SEL72_N; ++q) {
+      const double a = v[SEL72[q][0]], bb = v[SEL72[q][1]];
+      v[SEL72[q][0]] = a < bb ? a : bb;
+      v[SEL72[q][1]] = a < bb ? bb : a;
+    }
+    const double p25 = v[18] - (v[18] - v[17]) * 0.25;
+    const double p75 = v[53] + (v[54] - v[53]) * 0.25;
+    out[vox] = avg * (p25 - p75) / (p25 + p75 + 1e-8);
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Unfused gathers for the drop-in API (outputs the full profile arrays).
 // ------------------------------------------------------------------------------------
 __global__ void lp2d_gather_kernel(const double *__restrict__ pad, int64_t ld, const int32_t *__restrict__ tab,
@@ -340,6 +392,19 @@ hrf_status hrf_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t zp,
   dim3 grid((unsigned)hrf::cdiv(Z, E3_TZ), (unsigned)hrf::cdiv(Y, E3_TY), (unsigned)hrf::cdiv(X, E3_TX));
   HRF_REQUIRE(grid.y <= 65535 && grid.z <= 65535, "enhance_3d: volume too large");
   enhance3d_kernel<0><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_enhance_3d_v3(const double *pad, int64_t xp, int64_t yp, int64_t zp, int32_t patch, int32_t ntheta,
+                             int32_t nphi, double *out, hrf_stream_t stream) {
+  HRF_REQUIRE(patch == 11 && ntheta == 9 && nphi == 9,
+              "line_profile_memory_efficient_v3: only the reference parameters (11, 9, 9) are built");
+  HRF_REQUIRE(xp >= 10 && yp >= 10 && zp >= 10, "line_profile_memory_efficient_v3: padded volume smaller than patch");
+  const int64_t X = xp - 10, Y = yp - 10, Z = zp - 10;
+  if (X == 0 || Y == 0 || Z == 0) return HRF_OK;
+  HRF_REQUIRE(pad && out, "line_profile_memory_efficient_v3: null buffer");
+  enhance3d_v3_kernel<<<hrf::stream_grid(X * Y * Z), 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, out, X, Y, Z);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -2,7 +2,8 @@
 
 * LP2D_11_9[9][11][2], LP3D_11_9_9[72][11][3]: line-profile sampling offsets for the
   reference's fixed parameters (neighbor2d.pyx:32-55 with patch 11 / phi 9; neighbor.pyx
-  :209-243 with patch 11 / theta 9 / phi 9).  Computed by an independent restatement of
+  :209-243 with patch 11 / theta 9 / phi 9); LP3D_V3_11_9_9 the variant table of
+  line_profile_memory_efficient_v3 (neighbor.pyx:293-311).  Computed by an independent restatement of
   the table construction; tests/test_tables.py checks them against the reference-derived
   golden tables and against hrf_lp_table_2d/3d.
 * SEL9 / SEL72: comparator lists of Knuth's merge-exchange sort (TAOCP 5.2.2 Algorithm M)
@@ -58,6 +59,47 @@ def table_3d(patch=11, ntheta=9, nphi=9):
     return out
 
 
+def sample_line_v3(patch, iv):
+    """neighbor.pyx:293-311 (line_profile_memory_efficient_v3): like sample_line but
+    np.round on the short-line branch and np.floor of s*li*(2*iv+1)/line_n (signed iv) on
+    the full-length one"""
+    inc = (patch - 1) // 2
+    ndim = len(iv)
+    arg = max(range(ndim), key=lambda k: (abs(iv[k]), -k))
+    line_n = 2 * abs(iv[arg]) + 1
+    off = [[0] * ndim for _ in range(patch)]
+    if line_n < patch:
+        base = (patch - line_n) // 2
+        for li in range(line_n):
+            for k in range(ndim):
+                s = (iv[k] > 0) - (iv[k] < 0)
+                h = float(s * li) * float(2 * abs(iv[k]) + 1) / float(line_n)
+                off[li + base][k] = int(round(h) + inc - iv[k])
+        for li in range(base):
+            off[li] = list(off[base])
+            off[li + line_n + base] = list(off[line_n + base - 1])
+    else:
+        for li in range(line_n):
+            for k in range(ndim):
+                s = (iv[k] > 0) - (iv[k] < 0)
+                h = float(s * li) * float(2 * iv[k] + 1) / float(line_n)
+                off[li][k] = int(math.floor(h) + inc - iv[k])
+    return off
+
+
+def table_3d_v3(patch=11, ntheta=9, nphi=9):
+    inc = (patch - 1) // 2
+    out = []
+    for th in range(1, ntheta):
+        for phi in range(nphi):
+            ap = phi * math.pi / nphi
+            at = th * math.pi / ntheta
+            out.append(sample_line_v3(patch, [round(inc * math.cos(ap) * math.sin(at)),
+                                              round(inc * math.sin(ap) * math.sin(at)),
+                                              round(inc * math.cos(at))]))
+    return out
+
+
 def merge_exchange(n):
     """Knuth Algorithm M: comparator list sorting any n inputs ascending."""
     comps = []
@@ -102,6 +144,7 @@ def check(comps, n, outputs, trials=3000):
 def main():
     t2 = table_2d()
     t3 = table_3d()
+    t3v3 = table_3d_v3()
     sel9 = prune(merge_exchange(9), [2, 3, 6, 7])
     sel72 = prune(merge_exchange(72), [17, 18, 53, 54])
     check(sel9, 9, [2, 3, 6, 7])
@@ -111,10 +154,11 @@ def main():
     for d in t2:
         lines.append("  {" + ", ".join("{%d, %d}" % tuple(o) for o in d) + "},")
     lines.append("};")
-    lines.append("constexpr int8_t LP3D_11_9_9[72][11][3] = {")
-    for d in t3:
-        lines.append("  {" + ", ".join("{%d, %d, %d}" % tuple(o) for o in d) + "},")
-    lines.append("};")
+    for name, tab in [("LP3D_11_9_9", t3), ("LP3D_V3_11_9_9", t3v3)]:
+        lines.append("constexpr int8_t %s[72][11][3] = {" % name)
+        for d in tab:
+            lines.append("  {" + ", ".join("{%d, %d, %d}" % tuple(o) for o in d) + "},")
+        lines.append("};")
     for name, sel in [("SEL9", sel9), ("SEL72", sel72)]:
         lines.append("constexpr int %s_N = %d;" % (name, len(sel)))
         lines.append("constexpr uint8_t %s[%d][2] = {" % (name, len(sel)))

@@ -87,6 +87,17 @@ def enhance_3d(pad: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def enhance_3d_v3(pad: torch.Tensor) -> torch.Tensor:
+    """neighbor.line_profile_memory_efficient_v3(pad, 11, 9, 9) (neighbor.pyx:268-349)"""
+    pad = _dev(pad, torch.float64, "image_padded")
+    xp, yp, zp = pad.shape
+    if min(xp, yp, zp) < 10:
+        raise ValueError("negative dimensions are not allowed")
+    out = torch.empty((xp - 10, yp - 10, zp - 10), dtype=torch.float64, device=pad.device)
+    _lib.call("hrf_enhance_3d_v3", _ptr(pad), xp, yp, zp, 11, 9, 9, _ptr(out), _stream())
+    return out
+
+
 # ---- helpers --------------------------------------------------------------------------------
 def _u8(t: torch.Tensor, name: str) -> torch.Tensor:
     if not isinstance(t, torch.Tensor) or not t.is_cuda:

@@ -80,6 +80,12 @@ HRF_API hrf_status hrf_line_profile_3d_norm(const double *pad, int64_t xp, int64
  * materialises the (X,Y,Z,72) intermediate.  patch 11, ntheta 9, nphi 9 only. */
 HRF_API hrf_status hrf_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t zp, int32_t patch,
                           int32_t ntheta, int32_t nphi, double *final_, hrf_stream_t stream);
+/* neighbor.line_profile_memory_efficient_v3(pad, 11, 9, 9) (neighbor.pyx:268-349; imported
+ * by biofilm :40): its own table, flat-address reads as the reference's unchecked memoryview
+ * makes them (0 past the array's end, where the reference is undefined),
+ * out (X,Y,Z) = mean * (p25 - p75) / (p25 + p75 + 1e-8). */
+HRF_API hrf_status hrf_enhance_3d_v3(const double *pad, int64_t xp, int64_t yp, int64_t zp, int32_t patch,
+                                     int32_t ntheta, int32_t nphi, double *out, hrf_stream_t stream);
 
 
 /* ==== a1-a3: stack assembly and channel reductions (stack.hip) ======================== */

@@ -256,6 +256,113 @@ EXPORT void oracle_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t
 }
 
 /* ------------------------------------------------------------------------------------
+ * neighbor.line_profile_memory_efficient_v3 (neighbor.pyx:268-349).  Table (:293-311): as
+ * v2 but the short-line branch rounds (np.round, half to even: no exact halves occur) and
+ * the full-length branch floors s*li*(2*iv+1)/line_n with the SIGNED interval.  Per voxel:
+ * the 72 min/max-normalised centre taps (range clamped to 1e-8), their mean accumulated in
+ * order (:341-343), p25 and p75 (np.percentile, linear), and
+ * final = mean * (p25 - p75) / (p25 + p75 + 1e-8) (:344-347: "uq" is the 25th percentile).
+ * The table reaches past the patch (offsets up to 18 along x and z); the reference reads
+ * image_patch[vli, vlj, vlk] unchecked, i.e. pad[(i+vli)*yp*zp + (j+vlj)*zp + (k+vlk)] as a
+ * flat address (z overflow wraps into the next row), and beyond the end of the array for
+ * voxels near the far x face, where its result is undefined.  Restated with the same flat
+ * addressing; reads past the end of the array give 0.
+ * ---------------------------------------------------------------------------------- */
+static void build_line_v3(int patch, const int64_t *iv, int32_t *off /*[patch][3]*/) {
+    int inc = (patch - 1) / 2;
+    int arg = 0;
+    for (int k = 1; k < 3; ++k)
+        if (llabs(iv[k]) > llabs(iv[arg])) arg = k;
+    int line_n = (int)(2 * llabs(iv[arg]) + 1);
+    for (int i = 0; i < patch * 3; ++i) off[i] = 0;
+    if (line_n < patch) {
+        int base = (patch - line_n) / 2;
+        for (int li = 0; li < line_n; ++li)
+            for (int k = 0; k < 3; ++k) {
+                double h = (double)(sgn_i(iv[k]) * (int64_t)li) * (double)(2 * llabs(iv[k]) + 1) / (double)line_n;
+                off[(li + base) * 3 + k] = (int32_t)(nearbyint(h) + (double)inc - (double)iv[k]);
+            }
+        for (int li = 0; li < base; ++li)
+            for (int k = 0; k < 3; ++k) off[li * 3 + k] = off[base * 3 + k];
+        for (int li = 0; li < base; ++li)
+            for (int k = 0; k < 3; ++k) off[(li + line_n + base) * 3 + k] = off[(line_n + base - 1) * 3 + k];
+    } else {
+        for (int li = 0; li < line_n; ++li)
+            for (int k = 0; k < 3; ++k) {
+                double h = (double)(sgn_i(iv[k]) * (int64_t)li) * (double)(2 * iv[k] + 1) / (double)line_n;
+                off[li * 3 + k] = (int32_t)(floor(h) + (double)inc - (double)iv[k]);
+            }
+    }
+}
+
+EXPORT void oracle_lp_table_3d_v3(int patch, int ntheta, int nphi, int32_t *off) {
+    int inc = (patch - 1) / 2;
+    for (int th = 1; th < ntheta; ++th)
+        for (int phi = 0; phi < nphi; ++phi) {
+            double ap = (double)phi * M_PI / (double)nphi;
+            double at = (double)th * M_PI / (double)ntheta;
+            int64_t iv[3] = {(int64_t)nearbyint((double)inc * cos(ap) * sin(at)),
+                             (int64_t)nearbyint((double)inc * sin(ap) * sin(at)),
+                             (int64_t)nearbyint((double)inc * cos(at))};
+            build_line_v3(patch, iv, off + (int64_t)((th - 1) * nphi + phi) * patch * 3);
+        }
+}
+
+/* 1 where every read of voxel (i, j, k) stays inside the padded array (the defined part) */
+EXPORT void oracle_v3_defined(int64_t xp, int64_t yp, int64_t zp, int patch, int ntheta, int nphi, uint8_t *ok) {
+    int ndir = (ntheta - 1) * nphi;
+    int32_t *off = (int32_t *)malloc(sizeof(int32_t) * ndir * patch * 3);
+    oracle_lp_table_3d_v3(patch, ntheta, nphi, off);
+    int64_t X = xp - (patch - 1), Y = yp - (patch - 1), Z = zp - (patch - 1), total = xp * yp * zp;
+    for (int64_t i = 0; i < X; ++i)
+        for (int64_t j = 0; j < Y; ++j)
+            for (int64_t k = 0; k < Z; ++k) {
+                int good = 1;
+                for (int e = 0; e < ndir * patch && good; ++e)
+                    if ((i + off[e * 3]) * yp * zp + (j + off[e * 3 + 1]) * zp + (k + off[e * 3 + 2]) >= total) good = 0;
+                ok[(i * Y + j) * Z + k] = (uint8_t)good;
+            }
+    free(off);
+}
+
+EXPORT void oracle_enhance_3d_v3(const double *pad, int64_t xp, int64_t yp, int64_t zp, int patch, int ntheta,
+                                 int nphi, double *final_) {
+    int ndir = (ntheta - 1) * nphi;
+    int32_t *off = (int32_t *)malloc(sizeof(int32_t) * ndir * patch * 3);
+    oracle_lp_table_3d_v3(patch, ntheta, nphi, off);
+    double *v = (double *)malloc(sizeof(double) * ndir);
+    int64_t X = xp - (patch - 1), Y = yp - (patch - 1), Z = zp - (patch - 1);
+    for (int64_t i = 0; i < X; ++i)
+        for (int64_t j = 0; j < Y; ++j)
+            for (int64_t k = 0; k < Z; ++k) {
+                double avg = 0.0;
+                const int64_t total = xp * yp * zp;
+                for (int t = 0; t < ndir; ++t) {
+                    const int32_t *o = off + t * patch * 3;
+                    double mn = 0, mx = 0, c = 0;
+                    for (int l = 0; l < patch; ++l) {
+                        const int64_t a = (i + o[l * 3]) * yp * zp + (j + o[l * 3 + 1]) * zp + (k + o[l * 3 + 2]);
+                        const double q = a < total ? pad[a] : 0.0;
+                        if (l == 0) { mn = q; mx = q; }
+                        else { mn = q < mn ? q : mn; mx = q > mx ? q : mx; }
+                        if (l == (patch - 1) / 2) c = q;
+                    }
+                    double r = mx - mn;
+                    if (1e-8 > r) r = 1e-8;
+                    v[t] = (c - mn) / r;
+                    avg += v[t];
+                }
+                avg /= (double)ndir;
+                qsort(v, ndir, sizeof(double), cmp_double);
+                double p25 = np_percentile_sorted(v, ndir, 25.0);
+                double p75 = np_percentile_sorted(v, ndir, 75.0);
+                final_[(i * Y + j) * Z + k] = avg * (p25 - p75) / (p25 + p75 + 1e-8);
+            }
+    free(off);
+    free(v);
+}
+
+/* ------------------------------------------------------------------------------------
  * a10 connected components: skimage.measure.label / morphology.label semantics
  * (ecoli measurement.py:97-98,109,111-112; multispecies :140).  Pixels connect when both
  * are non-zero and EQUAL (label of an int image), 4- (conn=1) or 8-connectivity

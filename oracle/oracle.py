@@ -112,6 +112,29 @@ def enhance_3d(pad, patch=11, ntheta=9, nphi=9):
     return out
 
 
+def lp_table_3d_v3(patch=11, ntheta=9, nphi=9):
+    off = np.zeros(((ntheta - 1) * nphi, patch, 3), np.int32)
+    lib().oracle_lp_table_3d_v3(patch, ntheta, nphi, _p(off))
+    return off
+
+
+def enhance_3d_v3(pad, patch=11, ntheta=9, nphi=9):
+    """neighbor.line_profile_memory_efficient_v3 (neighbor.pyx:268-349)"""
+    pad = _c(pad, np.float64)
+    xp, yp, zp = pad.shape
+    out = np.zeros((xp - patch + 1, yp - patch + 1, zp - patch + 1), np.float64)
+    lib().oracle_enhance_3d_v3(_p(pad), I64(xp), I64(yp), I64(zp), patch, ntheta, nphi, _p(out))
+    return out
+
+
+def v3_defined(shape, patch=11, ntheta=9, nphi=9):
+    """voxels of line_profile_memory_efficient_v3 whose reads stay inside the padded array"""
+    xp, yp, zp = shape
+    ok = np.zeros((xp - patch + 1, yp - patch + 1, zp - patch + 1), np.uint8)
+    lib().oracle_v3_defined(I64(xp), I64(yp), I64(zp), patch, ntheta, nphi, _p(ok))
+    return ok.astype(bool)
+
+
 # ---- a4 -------------------------------------------------------------------------------
 def nl_means(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
     """skimage.restoration.denoise_nl_means (fast 2-D) in libhrf's summation order"""

@@ -55,6 +55,29 @@ def edge_pad(img, w=5):
     return np.pad(img, w, mode="edge")
 
 
+def main_v3():
+    """neighbor3d_v3.npz: the reference's line_profile_memory_efficient_v3 (neighbor.pyx:268-349)
+    on small edge-padded volumes (kept separate so the other fixtures are not regenerated)."""
+    subprocess.check_call([os.path.join(REPO, "oracle", "build_ref.sh")])
+    sys.path.insert(0, os.path.join(REPO, "oracle", "_ref"))
+    import neighbor
+    rng = np.random.default_rng(20190102)
+    out = {}
+    # the reference's v3 table reaches up to 18 voxels along x and z (neighbor.pyx:304-307
+    # floor with the signed interval), i.e. past the 11-voxel patch: its reads are flat-address
+    # arithmetic on the padded array and leave the buffer for voxels near the far x face.
+    # Volumes here are long in x so that the first X-9 slices only read inside the array.
+    for name, vol in [("a", rng.random((14, 5, 4))), ("b", rng.random((12, 6, 2)) ** 3),
+                      ("c", np.full((11, 4, 3), 0.5))]:
+        if name == "c":
+            vol[1:3, 1:3, 1] = rng.random((2, 2))
+        pad = edge_pad(vol)
+        out["pad_" + name] = pad
+        with np.errstate(all="ignore"):
+            out["final_" + name] = neighbor.line_profile_memory_efficient_v3(pad, 11, 9, 9)
+    np.savez_compressed(os.path.join(HERE, "neighbor3d_v3.npz"), **out)
+
+
 def main():
     subprocess.check_call([os.path.join(REPO, "oracle", "build_ref.sh")])
     sys.path.insert(0, os.path.join(REPO, "oracle", "_ref"))
@@ -164,4 +187,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["v3"]:
+        main_v3()
+    else:
+        main()

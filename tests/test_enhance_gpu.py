@@ -87,6 +87,28 @@ def test_enhance_3d_flat_volume(K, orc):
     same(K.enhance_3d(dev(pad)).cpu().numpy(), orc.enhance_3d(pad))
 
 
+@pytest.mark.parametrize("case", ["a", "b", "c"])
+def test_memory_efficient_v3(K, orc, golden, case):
+    g = golden("neighbor3d_v3")
+    pad = g["pad_" + case]
+    got = K.enhance_3d_v3(dev(pad)).cpu().numpy()
+    same(got, orc.enhance_3d_v3(pad))                  # everywhere, incl. the flat-address tail
+    ok = orc.v3_defined(pad.shape)
+    same(got[ok], g["final_" + case][ok])              # the reference itself where defined
+
+
+def test_memory_efficient_v3_dropin(K, orc):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "hiprfish_image_analysis_amd", "scripts"))
+    import neighbor
+    pad = np.random.default_rng(3).random((22, 13, 17))
+    same(neighbor.line_profile_memory_efficient_v3(pad, 11, 9, 9), orc.enhance_3d_v3(pad))
+    with pytest.raises(ValueError):
+        neighbor.line_profile_memory_efficient_v3(pad.astype(np.float32), 11, 9, 9)
+
+
 def test_empty_and_too_small(K):
     pad = torch.zeros((10, 12), dtype=torch.float64, device="cuda")
     assert K.enhance_2d(pad).shape == (0, 2)

@@ -42,6 +42,26 @@ def test_enhance_3d_bitexact(orc, golden):
     assert np.array_equal(orc.enhance_3d(g["pad"]), g["final"])
 
 
+@pytest.mark.parametrize("case", ["a", "b", "c"])
+def test_memory_efficient_v3_on_defined_voxels(orc, golden, case):
+    """neighbor.line_profile_memory_efficient_v3 (reference Cython output): bit-exact wherever
+    the reference's unchecked reads stay inside the padded array"""
+    g = golden("neighbor3d_v3")
+    pad, want = g["pad_" + case], g["final_" + case]
+    ok = orc.v3_defined(pad.shape)
+    assert ok.any()
+    assert np.array_equal(orc.enhance_3d_v3(pad)[ok], want[ok])
+
+
+def test_v3_table_matches_generated_constants(orc):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "hiprfish_image_analysis_amd", "csrc"))
+    import gen_tables
+    assert np.array_equal(orc.lp_table_3d_v3(), np.array(gen_tables.table_3d_v3()))
+
+
 def test_metric_channel_cosine_intensity(orc, golden):
     g = golden("metrics")
     b = [0, 32, 55, 75, 89, 95]
