@@ -100,3 +100,51 @@ def test_multispecies_measure_and_classify_cli(tmp_path, orc):
     assert np.array_equal(out[76].values, stats[olabs][:, 0].astype(np.int64))
     assert info is not None and m is not None
     del K
+
+
+def test_collect_measurement_results_cli(tmp_path):
+    """collect_measurement_results.py -t R / -t M on hand-made result folders"""
+    import pandas as pd
+    import hiprfish_imaging_collect_measurement_results as cli
+    rng = np.random.default_rng(4)
+    rows = []
+    for s, img, enc in [("S1", "08_18_2018_enc_5_fov_1", 5), ("S1", "08_18_2018_enc_5_fov_2", 5),
+                        ("S2", "09_01_2018_enc_1023_fov_3", 1023)]:
+        d = tmp_path / s
+        d.mkdir(exist_ok=True)
+        n = int(rng.integers(5, 40))
+        np.savetxt(d / (img + "_avgint.csv"), rng.random((n, 4)), delimiter=",")
+        codes = [format(enc, "010b")] * n
+        for j in rng.choice(n, 4, replace=False):     # 1-, 2- and 3-bit errors
+            flip = rng.choice(10, int(rng.integers(1, 4)), replace=False)
+            c = list(codes[j])
+            for f in flip:
+                c[f] = "1" if c[f] == "0" else "0"
+            codes[j] = "".join(c)
+        (d / (img + "_cell_ids.txt")).write_text("\n".join(codes) + "\n")
+        rows.append((s, img, codes, n, enc))
+    pd.DataFrame({"SAMPLE": [r[0] for r in rows], "IMAGES": [r[1] for r in rows]}).to_csv(tmp_path / "tab.csv",
+                                                                                       index=False)
+    out = str(tmp_path / "res.csv")
+    cli.main([str(tmp_path), str(tmp_path / "tab.csv"), out, "-t", "R"])
+    r = pd.read_csv(out, float_precision="round_trip")
+    for i, (_, _, codes, n, enc) in enumerate(rows):
+        ref = format(enc, "010b")
+        nb = [sum(a != b for a, b in zip(c, ref)) for c in codes]
+        assert r.NCells[i] == n and r.Barcodes[i] == enc and r.BarcodeComplexity[i] == ref.count("1")
+        wrong = sum(x > 0 for x in nb)
+        assert r.ErrorRate[i] == (1 - (n - wrong) / n if wrong else 1 / n)
+        assert r.OneBitError[i] == sum(x == 1 for x in nb) / n
+        assert r.TwoBitError[i] == sum(x == 2 for x in nb) / n
+        assert r.MultipleBitError[i] == sum(x > 2 for x in nb) / n
+    cli.main([str(tmp_path), str(tmp_path / "tab.csv"), out, "-t", "M"])
+    a = pd.read_csv(str(tmp_path / "res_abundance.csv"))
+    assert list(a.columns) == ["Barcodes", "FOV1", "FOV2", "FOV3"] and a.shape[0] == 1023
+    for i, (_, _, codes, n, enc) in enumerate(rows):
+        want = np.zeros(1023)
+        for c in codes:
+            if int(c, 2) >= 1:
+                want[int(c, 2) - 1] += 1
+        assert np.array_equal(a["FOV%d" % (i + 1)].values, want)
+    m = pd.read_csv(out)
+    assert list(m.FOV) == [1, 2, 3] and list(m.NCells) == [r[3] for r in rows]
