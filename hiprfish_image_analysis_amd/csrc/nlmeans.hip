@@ -24,6 +24,8 @@
 // (pixel, shift) before the weight.  Sums run in a fixed order (7 columns, then 7 rows) with
 // -ffp-contract=off, so the patch distances equal the oracle's bit for bit; exp() may differ
 // in the last ulp.  HBM traffic is 16 B per pixel: the kernel is f64-VALU bound (exp).
+#include <cmath>
+
 #include "common.hpp"
 
 namespace {
@@ -38,6 +40,32 @@ constexpr int NL_LW = NL_TW + 2 * NL_HALO;         // 92 doubles: even, rows sta
 constexpr int NL_LH = NL_TH + 2 * NL_HALO;
 constexpr int NL_ROWS = NL_R + 2 * NL_OFF;         // 14 rows of squared differences
 constexpr double NL_CUTOFF = 5.0;
+
+// exp(x) for x in [-5.0001, 0] (the weights that pass skimage's cut): Cody-Waite reduction
+// x = k ln2 + r, |r| <= ln2/2, then the degree-13 Taylor polynomial of e^r in Horner form
+// (truncation < 5e-18) and an exact scale by 2^k -- 16 FMAs and no range handling, against
+// the library exp's special-case paths.  Within a few ulp of exp(); the weights enter a
+// normalised average, so the result moves by ~1e-15 relative.
+__device__ __forceinline__ double exp_neg_small(double x) {
+  const double k = rint(x * 1.4426950408889634);
+  double r = __builtin_fma(-k, 6.93147180369123816490e-01, x);  // ln2 hi (Cody-Waite)
+  r = __builtin_fma(-k, 1.90821492927058770002e-10, r);         // ln2 lo
+  double p = 1.0 / 6227020800.0;                                // 1/13!
+  p = __builtin_fma(p, r, 1.0 / 479001600.0);
+  p = __builtin_fma(p, r, 1.0 / 39916800.0);
+  p = __builtin_fma(p, r, 1.0 / 3628800.0);
+  p = __builtin_fma(p, r, 1.0 / 362880.0);
+  p = __builtin_fma(p, r, 1.0 / 40320.0);
+  p = __builtin_fma(p, r, 1.0 / 5040.0);
+  p = __builtin_fma(p, r, 1.0 / 720.0);
+  p = __builtin_fma(p, r, 1.0 / 120.0);
+  p = __builtin_fma(p, r, 1.0 / 24.0);
+  p = __builtin_fma(p, r, 1.0 / 6.0);
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return __builtin_ldexp(p, (int)k);
+}
 
 // numpy.pad(mode='reflect') index: mirror without repeating the edge, period 2(n-1)
 __device__ __forceinline__ int64_t reflect_idx(int64_t i, int64_t n) {
@@ -64,7 +92,7 @@ __device__ __forceinline__ void read10(const double *p, double (&v)[10]) {
 // (entries 1..8); the shifted window starts at lc-3+sc, aligned when sc is odd (entries
 // 0..7), one entry later in the run that starts before it when sc is even (entries 1..8).
 template <int ODD>
-__device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, int lc, int sr, int sc, double h2s2,
+__device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, int lc, int sr, int sc, double inv,
                                          double lim, double var, double (&acc)[NL_R][NL_K],
                                          double (&wsum)[NL_R][NL_K]) {
   constexpr int SB = ODD ? 0 : 1;  // first used entry of the shifted run
@@ -102,16 +130,12 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
 #pragma unroll
       for (int k = 0; k < NL_K; ++k) {
         const double Dv = D[i][k];
-        // lim = 5.0001 h2s2 >= every D whose rounded D/h2s2 is <= 5: the division and the exp
-        // run only for pairs that can pass the cutoff
+        // lim = the largest D with fl(D / h2s2) <= 5 (host): exactly skimage's cut, no division
         if (Dv <= lim) {
-          const double d = (Dv > 0.0 ? Dv : 0.0) / h2s2;
-          if (d <= NL_CUTOFF) {
-            const double w = exp(-d);
-            wsum[i][k] += w;
-            const double t = w * ctr[i][k];
-            acc[i][k] += t;
-          }
+          const double w = exp_neg_small(-(Dv > 0.0 ? Dv : 0.0) * inv);
+          wsum[i][k] += w;
+          const double t = w * ctr[i][k];
+          acc[i][k] += t;
         }
       }
     }
@@ -120,7 +144,8 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
 }
 
 __global__ __launch_bounds__(NL_THREADS, 2) void nl_means_kernel(const double *__restrict__ img, int64_t H, int64_t W,
-                                                                 double h2s2, double var, double *__restrict__ out) {
+                                                                 double inv, double lim, double var,
+                                                                 double *__restrict__ out) {
   __shared__ __attribute__((aligned(16))) double P[NL_LH * NL_LW];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.y * NL_TH, c0 = (int64_t)blockIdx.x * NL_TW;
@@ -135,7 +160,6 @@ __global__ __launch_bounds__(NL_THREADS, 2) void nl_means_kernel(const double *_
   const int g = tid & 31, strip = tid >> 5;
   const int lc = NL_HALO + NL_K * g;          // LDS column of the pair's first pixel (even)
   const int br = NL_HALO + NL_R * strip;      // LDS row of the block's first pixel
-  const double lim = 5.0001 * h2s2;
 
   double acc[NL_R][NL_K], wsum[NL_R][NL_K];
 #pragma unroll
@@ -152,9 +176,9 @@ __global__ __launch_bounds__(NL_THREADS, 2) void nl_means_kernel(const double *_
 #pragma unroll 1
     for (int sc = -NL_DIST; sc <= NL_DIST; ++sc) {
       if (sc & 1)
-        nl_shift<1>(P, br, lc, sr, sc, h2s2, lim, var, acc, wsum);
+        nl_shift<1>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
       else if (sr != 0 || sc != 0)
-        nl_shift<0>(P, br, lc, sr, sc, h2s2, lim, var, acc, wsum);
+        nl_shift<0>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
     }
   }
 #pragma unroll
@@ -185,9 +209,15 @@ hrf_status hrf_nl_means_2d(const double *img, int64_t H, int64_t W, int32_t patc
   const double h2 = h * h, s2 = (double)s * (double)s;
   const double h2s2 = 1.0 * h2 * s2;
   const double var = sigma * sigma;
+  // the cut d = max(D, 0) / h2s2 <= 5 as a threshold on D: fl(D / h2s2) is non-decreasing in D,
+  // so walk from 5 h2s2 to the last double whose quotient still rounds to <= 5
+  double lim = NL_CUTOFF * h2s2;
+  while (lim / h2s2 > NL_CUTOFF) lim = std::nextafter(lim, -1.0);
+  while (std::nextafter(lim, 2.0 * lim + 1.0) / h2s2 <= NL_CUTOFF) lim = std::nextafter(lim, 2.0 * lim + 1.0);
+  const double inv = 1.0 / h2s2;
   dim3 grid((unsigned)hrf::cdiv(W, NL_TW), (unsigned)hrf::cdiv(H, NL_TH));
   HRF_REQUIRE(grid.y <= 65535, "nl_means_2d: image too tall");
-  nl_means_kernel<<<grid, NL_THREADS, 0, (hipStream_t)stream>>>(img, H, W, h2s2, var, out);
+  nl_means_kernel<<<grid, NL_THREADS, 0, (hipStream_t)stream>>>(img, H, W, inv, lim, var, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }
