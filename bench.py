@@ -3,12 +3,15 @@
 A step = one pass of the hot path over one synthetic 2048x2048x95 tile per rank, inputs
 resident in HBM: E. coli measurement (log-sum -> KMeans -> morphology -> erosion seeds ->
 watershed -> cleanup -> shape filter -> per-cell mean spectra), per-cell segmented-cosine
-classification against the 1023-barcode library, per-pixel classification (fused f32-MFMA
-GEMM + argmax), per-barcode counts and the identification map.  With N ranks every rank
+classification against the 1023-barcode library, per-pixel classification (split-fp16 MFMA
+GEMM + fused argmax), per-barcode counts and the identification map.  With N ranks every rank
 processes its own tiles (weak scaling) and the per-barcode counts are all-reduced over RCCL
 each step -- the path's only exchange (collect_measurement_results.py:92-98 across FOVs).
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-extras]
+At N=1 the line also carries "extras": the other GPU configurations of BASELINE.json measured
+the same way (cfg2: 2048x2048x63 synthetic-community tiles against the 127-barcode library;
+cfg4: the fused 3-D enhancement of a 1024x1024x64 volume).
 (for N > 1 launch with torch.distributed.run, one process per GPU)
 """
 from __future__ import annotations
@@ -63,6 +66,70 @@ def _cpu_baseline(ref, bounds):
                       (t_seg * hs * hs, npx, t_pix * npx)}
 
 
+def _timed_tiles(job, tiles, T, streams, pool, steps, warmup):
+    """steps x T tiles, T concurrent (own stream + host thread each) -> seconds"""
+    import torch
+
+    def one(j, st):
+        with torch.cuda.stream(streams[j]):
+            return job(st)
+
+    def step(i):
+        sts = [tiles[(i * T + j) % len(tiles)] for j in range(T)]
+        if pool is None:
+            return [one(0, sts[0])]
+        return [f.result() for f in [pool.submit(one, j, sts[j]) for j in range(T)]]
+    for i in range(warmup):
+        step(i)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def _extras(dev, T, streams, pool):
+    """BASELINE.json configs 2 and 4 on this GPU (inputs resident, synthetic data)."""
+    import torch
+
+    from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    out = {}
+    b = S.MULTI_BOUNDS
+    ref = S.reference_library(7, b)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), b, 7)
+    lib.refx()
+    tiles = [S.tile(H, W, nbit=7, bounds=b, seed=20190201 + t, device=dev)[0] for t in range(2 * T)]
+    steps = 6
+    sec = _timed_tiles(lambda st: P.process_tile(st, lib, measure=P.measure_multispecies, variant=2), tiles, T,
+                       streams, pool, steps, 2)
+    out["cfg2"] = {"workload": "2048x2048x63 synthetic-community tiles, 127-barcode (7-bit) library: calibrated "
+                               "sum, NL-means, 2-D enhancement, segmentation, per-cell means, per-cell (_7b_v2) "
+                               "and per-pixel classification, counts", "concurrent": T,
+                   "value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
+                   "ms_per_tile": round(sec / (steps * T) * 1e3, 3)}
+    del tiles
+    X, Y, Z = 1024, 1024, 64
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    pad = torch.rand((X + 10, Y + 10, Z + 10), dtype=torch.float64, device=dev, generator=g)
+    K.enhance_3d(pad)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        K.enhance_3d(pad)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    out["cfg4"] = {"workload": "1024x1024x64 volume (edge-padded), fused line_profile_memory_efficient_v2 + "
+                               "biofilm :812-817 post-chain (72 directions x 11 taps per voxel)",
+                   "value": round(X * Y * Z / ms / 1e3, 3), "unit": "Mvoxel/s", "ms": round(ms, 3)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -72,6 +139,7 @@ def main():
     ap.add_argument("--concurrent", type=int, default=2, help="tiles processed concurrently per step per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-pixel", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the cfg2 / cfg4 measurements (N=1 only)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the per-pixel classification after the segmentation on one stream")
     args = ap.parse_args()
@@ -212,6 +280,8 @@ def main():
                            "isolated_kernel_ms": round(ms_iso, 4),
                            "isolated_achieved": round(flops / (ms_iso * 1e-3) / 1e12, 2),
                            "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4)}
+    if world == 1 and not args.no_extras:
+        out["extras"] = _extras(dev, T, streams, pool)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline(ref, bounds)
     if rank == 0:

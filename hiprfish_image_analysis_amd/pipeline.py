@@ -233,14 +233,16 @@ def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
 
 
 def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0,
-                 overlap: bool = True, pixel_events: list | None = None):
+                 overlap: bool = True, pixel_events: list | None = None, measure=None):
     """One tile of the hot path: measure (segment + per-cell spectra) + classify + count.
 
     The per-pixel classification does not depend on the segmentation, so with `overlap` it
     runs on a side stream concurrently with the segmentation chain (many small, latency-bound
     launches and a few host synchronisations) and fills the compute units that chain leaves
     idle; the caller's stream joins it before returning.  `pixel_events`, if given, receives
-    the (start, end) events recorded around the classification on the stream it ran on."""
+    the (start, end) events recorded around the classification on the stream it ran on.
+    `measure` selects the measurement chain (default measure_ecoli; measure_multispecies for
+    the synthetic-community pipeline)."""
     main = torch.cuda.current_stream(stack.device)
     pix = None
     if per_pixel:
@@ -260,7 +262,7 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
         if overlap:
             stack.record_stream(side)
             refx.record_stream(side)
-    meas = measure_ecoli(stack, calibration)
+    meas = (measure or measure_ecoli)(stack, calibration)
     idx, dist = classify_cells(meas.avgint_norm, lib, variant)
     counts = K.barcode_counts(idx, lib.R)                       # collect_measurement_results.py:92-98
     ident = K.paint_ids(meas.segmentation, idx + 1)             # image_classification.py:65-71

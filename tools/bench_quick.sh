@@ -5,6 +5,6 @@ mkdir -p gpurun_out
 out=gpurun_out/quick.log
 : > $out
 for args in "" "--no-per-pixel"; do
-  r=$(timeout -k 10 240 python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 $args 2>/dev/null) || exit 1
+  r=$(timeout -k 10 240 python3 bench.py --no-cpu-baseline --no-extras --steps 20 --warmup 5 $args 2>/dev/null) || exit 1
   echo "[$args] $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" >> $out
 done
