@@ -15,10 +15,15 @@ import oracle as O
 
 
 def erosion_seeds(cell_sm, area_max=600, min_obj=10):
-    """ecoli measurement.py:97-110"""
+    """ecoli measurement.py:97-110.  The reference loops while anything is left; a region that
+    covers the image edge wall to wall never erodes (border_value=True) and never shrinks below
+    area_max, so there it does not terminate.  Capped, as libhrf's per-component loop is, at
+    4 (H + W) + 8 rounds -- more than any region that can vanish needs."""
     m = cell_sm.astype(bool).copy()
     be = np.zeros_like(m)
-    while m.any():
+    cap = 4 * (m.shape[0] + m.shape[1]) + 8
+    while m.any() and cap > 0:
+        cap -= 1
         lab, n = O.label(m.astype(np.int32), 2)
         area = np.bincount(lab.ravel(), minlength=n + 1)
         small = (lab > 0) & (area[lab] < area_max)

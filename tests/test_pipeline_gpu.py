@@ -126,3 +126,44 @@ def test_native_segmentation_equals_composed(mods, H, W, seed):
     # repeated calls reuse the context
     seg_n2, _ = P.segment_ecoli(stack)
     assert torch.equal(seg_n2, seg_n)
+
+
+# ---- degenerate tiles: empty, constant, tiny, ragged -----------------------------------------
+def _degenerate_tiles(S, C):
+    rng = np.random.default_rng(40)
+    out = {"zeros": np.zeros((64, 80, C), np.float32),
+           "constant": np.full((48, 48, C), 0.25, np.float32),
+           "noise_only": (0.01 + 0.005 * rng.standard_normal((96, 64, C))).clip(0).astype(np.float32),
+           "tiny": rng.random((12, 17, C)).astype(np.float32)}
+    st, _, _, _ = S.tile(160, 96, seed=41, ncells=3)
+    out["few_cells_ragged"] = st.cpu().numpy()[:, :, :C] if st.shape[2] >= C else None
+    return out
+
+
+def test_ecoli_degenerate_tiles(mods):
+    P, S, OP = mods
+    for name, st in _degenerate_tiles(S, 95).items():
+        if st is None:
+            continue
+        d = torch.from_numpy(np.ascontiguousarray(st)).cuda()
+        seg_n, mx_n = P.segment_ecoli(d)
+        seg_c, mx_c = P.segment_ecoli(d, keep={})
+        assert mx_n == mx_c and torch.equal(seg_n, seg_c), name
+        oseg, _ = OP.segment_ecoli(st)
+        assert np.array_equal(host(seg_n), oseg), name
+        m = P.measure_ecoli(d)
+        assert m.avgint.shape[1] == 95 and m.avgint.shape[0] == len(np.setdiff1d(np.unique(oseg), [0])), name
+
+
+def test_multispecies_degenerate_tiles(mods, orc):
+    P, S, OP = mods
+    for name, st in _degenerate_tiles(S, 63).items():
+        if st is None or name == "zeros":
+            continue   # an all-zero stack divides 0 by 0 in the reference's sum / max (:106)
+        d = torch.from_numpy(np.ascontiguousarray(st)).cuda()
+        a = P.segment_multispecies(d)
+        keep = {}
+        b = P.segment_multispecies(d, keep=keep)
+        assert a[1] == b[1] and torch.equal(a[0], b[0]), name
+        oseg, on, _, _ = OP.segment_multispecies(st, nl=host(keep["nl"]))
+        assert np.array_equal(host(a[0]), oseg) and a[1] == on, name
