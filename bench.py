@@ -177,10 +177,11 @@ def main():
     ev = []
 
     T = max(1, args.concurrent)
-    # the segmentation chains (short, latency-bound launches) run on high-priority streams so
-    # their workgroups are dispatched ahead of the pending ones of the long classifier grid,
-    # which process_tile puts on a default-priority side stream
-    prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("HRF_PRIORITY", "1") != "0" else 0
+    # HRF_PRIORITY=1 puts the segmentation chains on high-priority streams (their workgroups
+    # dispatched ahead of the pending ones of the long classifier grid on its default-priority
+    # side stream): measured neutral on throughput (915.6 vs 912.9 Mpix/s, 5 interleaved runs
+    # each), so off by default -- it stretches the classifier's in-bench launch duration
+    prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("HRF_PRIORITY", "0") == "1" else 0
     streams = [torch.cuda.Stream(device=dev, priority=prio) for _ in range(T)]
     pool = None
     if T > 1:
