@@ -91,13 +91,12 @@ __device__ __forceinline__ void read10(const double *p, double (&v)[10]) {
 // covers LDS columns lc-3 .. lc+4 (lc = 14 + 2g, even), read as the aligned run lc-4 .. lc+5
 // (entries 1..8); the shifted window starts at lc-3+sc, aligned when sc is odd (entries
 // 0..7), one entry later in the run that starts before it when sc is even (entries 1..8).
-template <int ODD>
+template <int ODD, bool VAR>
 __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, int lc, int sr, int sc, double inv,
                                          double lim, double var, double (&acc)[NL_R][NL_K],
                                          double (&wsum)[NL_R][NL_K]) {
   constexpr int SB = ODD ? 0 : 1;  // first used entry of the shifted run
   double D[NL_R][NL_K];            // running patch distances of the block's rows
-  double ctr[NL_R][NL_K];          // P[p + s] of the block's pixels
   const double *pa = P + (br - NL_OFF) * NL_LW + lc - 4;
   // shifted run start lc-3+sc-SB: written as an even offset so the reads stay ds_read_b128
   const double *pb = pa + sr * NL_LW + (ODD ? 2 * ((sc + 1) >> 1) : 2 * (sc >> 1));
@@ -110,7 +109,7 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
 #pragma unroll
     for (int j = 0; j < NL_K + 2 * NL_OFF; ++j) {
       const double t = a[1 + j] - b[SB + j];
-      sq[j] = t * t - var;
+      sq[j] = VAR ? t * t - var : t * t;  // sigma = 0 (the reference's call): var is exactly 0
     }
 #pragma unroll
     for (int k = 0; k < NL_K; ++k) {
@@ -123,10 +122,12 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
         if (i == x) D[i][k] = s;
         else if (i < x && x <= i + 2 * NL_OFF) D[i][k] += s;
       }
-      if (x >= NL_OFF && x < NL_OFF + NL_R) ctr[x - NL_OFF][k] = b[SB + NL_OFF + k];
     }
     if (x >= 2 * NL_OFF) {  // output row x-6 is complete
       const int i = x - 2 * NL_OFF;
+      // P[p + s] of the row's two pixels, re-read from LDS rather than held in registers
+      const double *pc = P + (br + i + sr) * NL_LW + lc + sc;
+      const double ctr[NL_K] = {pc[0], pc[1]};
 #pragma unroll
       for (int k = 0; k < NL_K; ++k) {
         const double Dv = D[i][k];
@@ -134,7 +135,7 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
         if (Dv <= lim) {
           const double w = exp_neg_small(-(Dv > 0.0 ? Dv : 0.0) * inv);
           wsum[i][k] += w;
-          const double t = w * ctr[i][k];
+          const double t = w * ctr[k];
           acc[i][k] += t;
         }
       }
@@ -143,6 +144,7 @@ __device__ __forceinline__ void nl_shift(const double *__restrict__ P, int br, i
   }
 }
 
+template <bool VAR>
 __global__ __launch_bounds__(NL_THREADS, 2) void nl_means_kernel(const double *__restrict__ img, int64_t H, int64_t W,
                                                                  double inv, double lim, double var,
                                                                  double *__restrict__ out) {
@@ -176,9 +178,9 @@ __global__ __launch_bounds__(NL_THREADS, 2) void nl_means_kernel(const double *_
 #pragma unroll 1
     for (int sc = -NL_DIST; sc <= NL_DIST; ++sc) {
       if (sc & 1)
-        nl_shift<1>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
+        nl_shift<1, VAR>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
       else if (sr != 0 || sc != 0)
-        nl_shift<0>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
+        nl_shift<0, VAR>(P, br, lc, sr, sc, inv, lim, var, acc, wsum);
     }
   }
 #pragma unroll
@@ -217,7 +219,10 @@ hrf_status hrf_nl_means_2d(const double *img, int64_t H, int64_t W, int32_t patc
   const double inv = 1.0 / h2s2;
   dim3 grid((unsigned)hrf::cdiv(W, NL_TW), (unsigned)hrf::cdiv(H, NL_TH));
   HRF_REQUIRE(grid.y <= 65535, "nl_means_2d: image too tall");
-  nl_means_kernel<<<grid, NL_THREADS, 0, (hipStream_t)stream>>>(img, H, W, inv, lim, var, out);
+  if (var == 0.0)
+    nl_means_kernel<false><<<grid, NL_THREADS, 0, (hipStream_t)stream>>>(img, H, W, inv, lim, var, out);
+  else
+    nl_means_kernel<true><<<grid, NL_THREADS, 0, (hipStream_t)stream>>>(img, H, W, inv, lim, var, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }
