@@ -89,6 +89,50 @@ def _timed_tiles(job, tiles, T, streams, pool, steps, warmup):
     return time.perf_counter() - t0
 
 
+def _hbm_kernels(dev):
+    """The streaming (HBM-bound) kernels of the path on one resident cfg3 tile, isolated:
+    algorithmic bytes per launch / mean launch time (HIP events) against the 8 TB/s peak."""
+    import torch
+
+    from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    stack, _, _, _ = S.tile(H, W, seed=20190301, device=dev)
+    seg, maxlab = P.segment_ecoli(stack)
+    fg = int(K.count_nonzero(seg))
+    lasers, c0 = [], 0
+    for c1 in S.ECOLI_BOUNDS[1:]:
+        lasers.append(stack[:, :, c0:c1].contiguous())
+        c0 = c1
+    shifts = [(0, 0), (2, -1), (0, 3), (-1, 0), (1, 1)]
+
+    def timed(fn, n=10):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(n):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / n
+    rows = {
+        # bytes: stack read + f64 image written
+        "channel_sum": (lambda: K.channel_sum(stack, mode=1), H * W * (4 * C + 8)),
+        # bytes: per-laser stacks read + assembled stack written
+        "register_assemble": (lambda: K.register_assemble(lasers, shifts, apply_mask=True), H * W * 8 * C),
+        # bytes: label map read + the spectra of labelled pixels read (background is skipped)
+        "label_sums": (lambda: K.label_sums(stack, seg, maxlab), H * W * 4 + fg * 4 * C),
+    }
+    out = {}
+    for name, (fn, nbytes) in rows.items():
+        ms = timed(fn)
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {"ms": round(ms, 4), "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
+                     "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4)}
+    return out
+
+
 def _extras(dev, T, streams, pool):
     """BASELINE.json configs 2 and 4 on this GPU (inputs resident, synthetic data)."""
     import torch
@@ -124,6 +168,8 @@ def _extras(dev, T, streams, pool):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 3
+    del pad
+    out["hbm_kernels"] = _hbm_kernels(dev)
     out["cfg4"] = {"workload": "1024x1024x64 volume (edge-padded), fused line_profile_memory_efficient_v2 + "
                                "biofilm :812-817 post-chain (72 directions x 11 taps per voxel)",
                    "value": round(X * Y * Z / ms / 1e3, 3), "unit": "Mvoxel/s", "ms": round(ms, 3)}

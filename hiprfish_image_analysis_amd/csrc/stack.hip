@@ -54,6 +54,61 @@ __global__ void assemble_kernel(Lasers L, int64_t H, int64_t W, int apply_mask, 
   }
 }
 
+// LDS-staged form for C <= 128: one workgroup = 64 consecutive pixels of one row.  Each laser's
+// 64 x C_l source block is one contiguous run (a shift moves whole rows and columns), read
+// coalesced and scattered into the pixel-major LDS tile at its channel offset; the tile is
+// then written out as one contiguous 64 x C run with 16-byte stores.  32-bit index math only.
+constexpr int AS_P = 64;
+__global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+                                                           float *__restrict__ dst, int vec_ok) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  __shared__ uint8_t okp[AS_P];
+  const int C = L.c0[L.n];
+  const int tid = threadIdx.x;
+  const int64_t r = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * AS_P;
+  const int np = (int)min((int64_t)AS_P, W - c0);
+  if (tid < AS_P) {
+    bool ok = tid < np;
+    if (apply_mask)
+      for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, L.dr[q], L.dc[q]);
+    okp[tid] = (uint8_t)ok;
+  }
+  for (int q = 0; q < L.n; ++q) {
+    const int cl = L.c0[q + 1] - L.c0[q], off = L.c0[q];
+    const int64_t rs = r - L.dr[q];
+    const bool row_ok = r >= (L.dr[q] > 0 ? L.dr[q] : 0) && r < H + (L.dr[q] < 0 ? L.dr[q] : 0);
+    const float *src = L.src[q] + (rs * W + (c0 - L.dc[q])) * (int64_t)cl;  // pixel c0's source (may be off-row)
+    const int cmin = L.dc[q] > 0 ? L.dc[q] : 0, cmax = (int)W + (L.dc[q] < 0 ? L.dc[q] : 0);
+    const int n = np * cl;
+    for (int i = tid; i < n; i += 256) {
+      const int p = i / cl, ch = i - p * cl;
+      const int64_t c = c0 + p;
+      const bool cov = row_ok && c >= cmin && c < cmax;
+      tile[p * C + off + ch] = cov ? src[i] : 0.0f;
+    }
+  }
+  __syncthreads();
+  float *out = dst + (r * W + c0) * (int64_t)C;
+  const int n = np * C;
+  if (vec_ok) {
+    for (int v = tid; v < (n >> 2); v += 256) {
+      const int e = v << 2;
+      float4 x = reinterpret_cast<const float4 *>(tile)[v];
+      if (apply_mask) {
+        x.x = okp[e / C] ? x.x : 0.0f;
+        x.y = okp[(e + 1) / C] ? x.y : 0.0f;
+        x.z = okp[(e + 2) / C] ? x.z : 0.0f;
+        x.w = okp[(e + 3) / C] ? x.w : 0.0f;
+      }
+      reinterpret_cast<float4 *>(out)[v] = x;
+    }
+    for (int e = ((n >> 2) << 2) + tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
+  } else {
+    for (int e = tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
+  }
+}
+
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
 __device__ double pw_block(const float *a, int n) {
   if (n < 8) {
@@ -271,7 +326,15 @@ hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *ch
   const int64_t n = H * W * L.c0[nlaser];
   if (n == 0) return HRF_OK;
   HRF_REQUIRE(dst, "register_assemble: null output");
-  assemble_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst);
+  const int C = L.c0[nlaser];
+  if (C <= 128 && H <= 65535) {
+    // row runs start at pixel (r, 64 k): 16-byte aligned when W * C is a multiple of 4 floats
+    const int vec_ok = ((W * C) % 4 == 0) && (((uintptr_t)dst & 15) == 0);
+    dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
+    assemble_lds_kernel<<<grid, 256, sizeof(float) * AS_P * C, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, vec_ok);
+  } else {
+    assemble_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst);
+  }
   HRF_LAUNCHED();
   return HRF_OK;
 }
