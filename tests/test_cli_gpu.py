@@ -148,3 +148,40 @@ def test_collect_measurement_results_cli(tmp_path):
         assert np.array_equal(a["FOV%d" % (i + 1)].values, want)
     m = pd.read_csv(out)
     assert list(m.FOV) == [1, 2, 3] and list(m.NCells) == [r[3] for r in rows]
+
+
+def test_ecoli_image_classification_cli(tmp_path, orc):
+    """image_classification.py drop-in on measured spectra: barcodes (gated metric) against the
+    restated classifier, the _avgint_ids.csv column layout and the identification image"""
+    import pandas as pd
+    import hiprfish_imaging_image_classification as ccli
+    import hiprfish_imaging_spectral_image_measurement as mcli
+
+    from hiprfish_image_analysis_amd import synthetic as S
+    stack, _, _, ref = S.tile(256, 256, seed=33)
+    lasers = split_lasers(stack.cpu().numpy(), S.ECOLI_BOUNDS, [(0, 0)] * 5)
+    files = []
+    for i, l in enumerate(lasers):
+        np.save(tmp_path / ("e_%d.npy" % (i + 1)), l)
+        files.append(str(tmp_path / ("e_%d.czi" % (i + 1))))
+    mcli.main(['-i'] + files + ['-c', 'F'])
+    sample = str(tmp_path / "e")
+    np.save(tmp_path / "lib.npy", ref)
+    codes = ccli.main([sample + "_avgint.csv", "-rf", str(tmp_path / "lib.npy")])
+    avg = np.loadtxt(sample + "_avgint.csv", delimiter=",", ndmin=2)
+    x = avg / avg.max(axis=1)[:, None]
+    lib = ref.astype(np.float64) / ref.astype(np.float64).max(axis=1, keepdims=True)
+    b = S.ECOLI_BOUNDS
+    fx = np.stack([x[:, b[k]:b[k + 1]].max(axis=1) > 0.1 for k in range(5)], 1).astype(np.float64)
+    fr = np.stack([lib[:, b[k]:b[k + 1]].max(axis=1) > 0.1 for k in range(5)], 1).astype(np.float64)
+    idx, _ = orc.classify(x, lib, b, 1, fx, fr)
+    want = [format(i + 1, "010b") for i in idx]
+    assert list(codes) == want
+    assert [l.strip() for l in open(sample + "_cell_ids.txt")] == want
+    ids = pd.read_csv(sample + "_avgint_ids.csv", header=None, dtype=str)
+    assert ids.shape == (len(want), 135)
+    assert list(ids[132]) == want and (ids[133] == sample).all()
+    np.testing.assert_allclose(ids.iloc[:, 95:126].values.astype(np.float64), np.diff(x[:, :32], axis=1),
+                               rtol=1e-15, atol=1e-15)
+    seg = np.load(sample + "_seg.npy")
+    assert list(ids[134].astype(int)) == sorted(set(np.unique(seg)) - {0})
