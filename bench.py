@@ -239,33 +239,45 @@ def main():
             return P.process_tile(stack, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
                                   pixel_events=ev if timed else None)
 
-    def step(i, timed):
-        # T tiles per step, each on its own stream driven by its own host thread (the
-        # segmentation chain of one tile is latency-bound and synchronises with the host)
-        stacks = [tiles[(i * T + j) % len(tiles)] for j in range(T)]
-        if pool is None:
-            res = [tile_job(0, stacks[0], timed)]
-        else:
-            res = [f.result() for f in [pool.submit(tile_job, j, stacks[j], timed) for j in range(T)]]
-        if world > 1:
-            for r in res:
-                P.allreduce_counts(r.counts)
-        return res[-1]
+    def worker(j, first, nsteps, timed):
+        # worker j drives tiles first*T + j, (first+1)*T + j, ... on its own stream, with no
+        # barrier between steps: a tile's segmentation chain starts while the previous tile's
+        # classifier still runs, so the GPU never drains at a step boundary.  Counts are
+        # summed on the worker's stream (one all-reduce per job, after the join).
+        acc = None
+        res = None
+        for i in range(first, first + nsteps):
+            res = tile_job(j, tiles[(i * T + j) % len(tiles)], timed)
+            with torch.cuda.stream(streams[j]):
+                acc = res.counts.clone() if acc is None else acc.add_(res.counts)
+        return res, acc
 
-    for i in range(args.warmup):
-        step(i, False)
+    def run(first, nsteps, timed):
+        if pool is None:
+            outs = [worker(0, first, nsteps, timed)]
+        else:
+            outs = [f.result() for f in [pool.submit(worker, j, first, nsteps, timed) for j in range(T)]]
+        for j in range(T):
+            torch.cuda.current_stream().wait_stream(streams[j])
+        counts = outs[0][1]
+        for _, a in outs[1:]:
+            counts = counts + a
+        if world > 1:
+            P.allreduce_counts(counts)          # global per-barcode counts of the whole batch
+        return outs[-1][0], counts
+
+    run(0, args.warmup, False)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ncells = 0
-    for i in range(args.steps):
-        res = step(i, True)
+    res, counts = run(args.warmup, args.steps, True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ncells = int(res.cell_idx.numel())
+    total_cells = int(counts.sum().item())
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -282,6 +294,7 @@ def main():
                                "E. coli segmentation + per-cell spectra + per-cell and per-pixel segmented-cosine "
                                "classification + barcode counts" + (" (RCCL all-reduce of counts)" if world > 1 else ""),
                    "H": H, "W": W, "C": C, "R": lib.R, "per_pixel": per_pixel, "cells_last_tile": ncells,
+                   "cells_counted": total_cells,
                    "parallelism": "tile-sharded x%d" % world, "tiles_per_step_per_gpu": T,
                    "global_batch": T * world,
                    "per_pixel_overlap": per_pixel and not args.no_overlap},
