@@ -70,21 +70,21 @@ def _timed_tiles(job, tiles, T, streams, pool, steps, warmup):
     """steps x T tiles, T concurrent (own stream + host thread each) -> seconds"""
     import torch
 
-    def one(j, st):
+    def worker(j, first, n):
+        # as in the main loop: each worker runs its tile sequence without a step barrier
         with torch.cuda.stream(streams[j]):
-            return job(st)
+            for i in range(first, first + n):
+                job(tiles[(i * T + j) % len(tiles)])
 
-    def step(i):
-        sts = [tiles[(i * T + j) % len(tiles)] for j in range(T)]
+    def run(first, n):
         if pool is None:
-            return [one(0, sts[0])]
-        return [f.result() for f in [pool.submit(one, j, sts[j]) for j in range(T)]]
-    for i in range(warmup):
-        step(i)
+            worker(0, first, n)
+        else:
+            [f.result() for f in [pool.submit(worker, j, first, n) for j in range(T)]]
+    run(0, warmup)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        step(i)
+    run(warmup, steps)
     torch.cuda.synchronize()
     return time.perf_counter() - t0
 
@@ -146,7 +146,7 @@ def _extras(dev, T, streams, pool):
     lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), b, 7)
     lib.refx()
     tiles = [S.tile(H, W, nbit=7, bounds=b, seed=20190201 + t, device=dev)[0] for t in range(2 * T)]
-    steps = 6
+    steps = 10
     sec = _timed_tiles(lambda st: P.process_tile(st, lib, measure=P.measure_multispecies, variant=2), tiles, T,
                        streams, pool, steps, 2)
     out["cfg2"] = {"workload": "2048x2048x63 synthetic-community tiles, 127-barcode (7-bit) library: calibrated "
