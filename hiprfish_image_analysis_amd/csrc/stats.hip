@@ -2,15 +2,17 @@
 //
 // a15 hrf_label_sums: the reference computes the per-cell mean spectrum with one skimage
 // regionprops pass per channel (ecoli measurement.py:151-155, multispecies :167-171) --
-// C passes over the image.  Here one streaming pass: each workgroup stages a chunk of 64
-// raster pixels x C channels (contiguous in HBM) into LDS with 16-byte loads, skipping
-// vectors whose pixels are all background, then reduces runs of equal labels per channel
-// in f64 and flushes one atomic per (run, channel).  Flat-field division
+// C passes over the image.  Here one streaming pass that fetches only labelled pixels and
+// reduces runs of equal labels per channel in f64, one atomic per (run, channel):
+// label_sums_wave_kernel (C <= 128, default) works per wave without LDS or barriers;
+// label_sums_kernel (any C) stages 64-pixel chunks through LDS.  Flat-field division
 // (ecoli :147-150) is folded into the reduction so the calibrated stack never exists.
 // a20 hrf_region_moments/props: exact int64 raw moments (agg. atomics) -> regionprops
 // area/centroid/axes/eccentricity/orientation with exact integer central moments.
 #include "common.hpp"
 #include "wave.hpp"
+
+#include <cstdlib>
 
 namespace {
 
@@ -89,6 +91,107 @@ __global__ __launch_bounds__(256) void label_sums_kernel(const float *__restrict
       if (run) atomicAdd(&counts[run], n);
     }
     __syncthreads();
+  }
+}
+
+// Wave-per-chunk variant (default): each wave owns a 64-pixel raster chunk at a time, lane =
+// pixel for the label read (next chunk's labels prefetched while this one reduces), lane =
+// channel (c, c + 64) for the spectra.  Only foreground pixels are fetched, LS_B of them per
+// round with every load in flight (each pixel's C floats are contiguous, so a round is LS_B
+// coalesced row reads); runs of equal labels accumulate in f64 registers and flush one atomic
+// per (run, channel).  No LDS, no workgroup barriers: background chunks cost one ballot.
+constexpr int LS_B = 16;
+
+template <int CAL>  // 0 none, 1 per-pixel plane (cal_sc == 0), 2 per-channel / full array
+__global__ __launch_bounds__(256) void label_sums_wave_kernel(const float *__restrict__ stack,
+                                                              const int32_t *__restrict__ lab, int64_t npix, int C,
+                                                              int32_t maxlab, const float *__restrict__ cal,
+                                                              int64_t cal_sp, int cal_sc, int cal0, int cal1,
+                                                              double *__restrict__ sums,
+                                                              unsigned long long *__restrict__ counts) {
+  const int lane = hrf::lane_id();
+  const int64_t nchunks = (npix + 63) >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t ch = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int c0 = lane, c1 = lane + 64;
+  const bool v0 = c0 < C, v1 = c1 < C;
+  const bool k0 = CAL != 0 && c0 >= cal0 && c0 < cal1, k1 = CAL != 0 && c1 >= cal0 && c1 < cal1;
+  auto load_label = [&](int64_t c) -> int32_t {
+    const int64_t p = (c << 6) + lane;
+    int32_t l = (c < nchunks && p < npix) ? __builtin_nontemporal_load(lab + p) : 0;
+    return (l < 0 || l > maxlab) ? 0 : l;
+  };
+  int32_t lnext = load_label(ch);
+  for (; ch < nchunks; ch += nwaves) {
+    const int32_t l = lnext;
+    lnext = load_label(ch + nwaves);
+    unsigned long long fg = __ballot(l != 0);
+    if (!fg) continue;
+    const int64_t p0 = ch << 6;
+    float pcal = 1.0f;
+    if (CAL == 1) pcal = (p0 + lane < npix) ? cal[(p0 + lane) * cal_sp] : 1.0f;
+    int32_t run = 0;  // wave-uniform
+    unsigned long long n = 0;
+    double a0 = 0.0, a1 = 0.0;
+    while (fg) {
+      int idx[LS_B];
+      int nb = 0;
+#pragma unroll
+      for (int j = 0; j < LS_B; ++j) {
+        idx[j] = fg ? __ffsll((long long)fg) - 1 : -1;
+        if (fg) { fg &= fg - 1; ++nb; }
+      }
+      float x0[LS_B], x1[LS_B], q0[LS_B], q1[LS_B];
+#pragma unroll
+      for (int j = 0; j < LS_B; ++j) {
+        x0[j] = x1[j] = 0.0f;
+        q0[j] = q1[j] = 1.0f;
+        if (j < nb) {
+          const int64_t p = p0 + idx[j];
+          const float *src = stack + p * C;
+          if (v0) x0[j] = __builtin_nontemporal_load(src + c0);
+          if (v1) x1[j] = __builtin_nontemporal_load(src + c1);
+          if (CAL == 2) {
+            if (k0) q0[j] = cal[p * cal_sp + (int64_t)c0 * cal_sc];
+            if (k1) q1[j] = cal[p * cal_sp + (int64_t)c1 * cal_sc];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LS_B; ++j) {
+        if (j < nb) {
+          const int32_t lj = __builtin_amdgcn_readlane(l, idx[j]);
+          if (lj != run) {
+            if (run) {
+              double *row = sums + (int64_t)run * C;
+              if (v0) atomicAdd(row + c0, a0);
+              if (v1) atomicAdd(row + c1, a1);
+              if (lane == 0) atomicAdd(counts + run, n);
+            }
+            run = lj;
+            a0 = a1 = 0.0;
+            n = 0;
+          }
+          ++n;
+          if (CAL == 1) {
+            const double d = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                 __builtin_bit_cast(int, pcal), idx[j]));
+            a0 += k0 ? (double)x0[j] / d : (double)x0[j];
+            a1 += k1 ? (double)x1[j] / d : (double)x1[j];
+          } else if (CAL == 2) {
+            a0 += k0 ? (double)x0[j] / (double)q0[j] : (double)x0[j];
+            a1 += k1 ? (double)x1[j] / (double)q1[j] : (double)x1[j];
+          } else {
+            a0 += (double)x0[j];
+            a1 += (double)x1[j];
+          }
+        }
+      }
+    }
+    double *row = sums + (int64_t)run * C;
+    if (v0) atomicAdd(row + c0, a0);
+    if (v1) atomicAdd(row + c1, a1);
+    if (lane == 0) atomicAdd(counts + run, n);
   }
 }
 
@@ -301,6 +404,22 @@ hrf_status hrf_label_sums_cal(const float *stack, const int32_t *labels, int64_t
   HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * ((size_t)maxlab + 1), s));
   if (npix == 0) return HRF_OK;
   HRF_REQUIRE(stack && labels, "label_sums: null input");
+  static const bool lds_variant = getenv("HRF_LS_LDS") != nullptr;  // A/B switch
+  if (C <= 128 && !lds_variant) {
+    const int64_t nchunks = hrf::cdiv(npix, 64);
+    const int mode = cal == nullptr ? 0 : (cal_sc == 0 ? 1 : 2);
+    const int64_t nblk = hrf::cdiv(nchunks, 4);
+#define HRF_LSW(M)                                                                                                 \
+  {                                                                                                                \
+    const unsigned grid = hrf::resident_grid(label_sums_wave_kernel<M>, 256, 0, nblk);                             \
+    label_sums_wave_kernel<M><<<grid, 256, 0, s>>>(stack, labels, npix, C, maxlab, cal, cal_sp, cal_sc, cal_c0,     \
+                                                   cal_c1, sums, (unsigned long long *)counts);                   \
+  }
+    if (mode == 0) HRF_LSW(0) else if (mode == 1) HRF_LSW(1) else HRF_LSW(2)
+#undef HRF_LSW
+    HRF_LAUNCHED();
+    return HRF_OK;
+  }
   const int vec_ok = C >= 4 && ((C * LS_P) % 4 == 0) && (((uintptr_t)stack & 15) == 0);
   const size_t shm = sizeof(float) * LS_P * C;
   const int64_t nchunks = hrf::cdiv(npix, LS_P);

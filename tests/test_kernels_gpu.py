@@ -225,6 +225,31 @@ def test_label_sums_and_table(K, orc, S):
     np.testing.assert_allclose(host(avgn), ravg / ravg.max(axis=1)[:, None], rtol=1e-12)
 
 
+@pytest.mark.parametrize("C", [1, 7, 64, 128, 150])
+def test_label_sums_channel_counts(K, C):
+    """wave kernel (C <= 128: one or two channels per lane) and the LDS kernel (C > 128);
+    ragged pixel count, labels past maxlab and negative labels count as background"""
+    rng = np.random.default_rng(C)
+    H, W = 37, 91
+    st = rng.random((H, W, C)).astype(np.float32)
+    lab = rng.integers(-2, 9, size=(H, W)).astype(np.int32)
+    lab[5:9] = 3  # long runs
+    mx = 6
+    sums, counts = K.label_sums(dev(st), dev(lab), mx)
+    ok = (lab > 0) & (lab <= mx)
+    rs = np.zeros((mx + 1, C))
+    np.add.at(rs, lab[ok], st[ok].astype(np.float64))
+    assert np.array_equal(host(counts), np.bincount(lab[ok], minlength=mx + 1))
+    np.testing.assert_allclose(host(sums), rs, rtol=1e-12, atol=1e-12)
+    cal = (0.5 + rng.random(C)).astype(np.float32)
+    sums2, _ = K.label_sums(dev(st), dev(lab), mx, cal=dev(cal), cal_range=(0, min(C, 5)))
+    st2 = st.astype(np.float64)
+    st2[..., :5] /= cal[:5].astype(np.float64)
+    rs2 = np.zeros((mx + 1, C))
+    np.add.at(rs2, lab[ok], st2[ok])
+    np.testing.assert_allclose(host(sums2), rs2, rtol=1e-12, atol=1e-12)
+
+
 def test_region_props(K, orc, S):
     lay = S.cell_layout(512, 512, 120, 7, seed=9)
     truth = S.render_truth(512, 512, lay)

@@ -61,6 +61,9 @@ def main():
         ms = timed(lambda: K.label_sums(stack, seg, maxlab))
         print("label_sums (%d labels, %.0f %% fg): %.3f ms  %.0f GB/s algorithmic" % (maxlab, 100.0 * fg / H / W, ms,
                                                                                       nb2 / ms / 1e6))
+        calp = (0.5 + torch.rand((H, W), device="cuda"))
+        ms = timed(lambda: K.label_sums(stack, seg, maxlab, cal=calp, cal_range=(0, 32)))
+        print("label_sums plane cal: %.3f ms  %.0f GB/s algorithmic" % (ms, nb2 / ms / 1e6))
 
 
 if __name__ == "__main__":
