@@ -377,16 +377,25 @@ static_assert(KS_T * KS_P == 4096, "index arithmetic below shifts by 12");
 template <int K>
 __device__ void km_bucket_step(const double *__restrict__ xs, const long long *__restrict__ q,
                                const long long *__restrict__ prefix, const unsigned long long *__restrict__ off,
-                               int64_t nv, double mn, double inv, const double *c, int j, int64_t *cnt_le,
-                               long long *sum_le) {
+                               int64_t nv, double mn, double inv, double range, const double *c, int j,
+                               int64_t *cnt_le, long long *sum_le) {
   const int t = threadIdx.x;
   __shared__ int64_t lo_sh, hi_sh;
   __shared__ int bf_sh, bt_sh, exh_sh;
   __shared__ unsigned long long nf_sh;
   __shared__ long long sf_sh;
   if (t == 0) {
-    lo_sh = 0;
-    hi_sh = nv;
+    // Direct bracket: the label step lies within delta of the midpoint m (the comparison's
+    // rounding moves it by ~2^-53 of the centre gap; delta is 2^-40 of the magnitudes), and
+    // km_bucket is monotone in the value, so every value in a bucket below bucket(m - delta)
+    // has label <= j and every value in a bucket above bucket(m + delta) label > j.  The
+    // range then starts on those bucket boundaries instead of [0, nv).
+    const double m = 0.5 * c[j] + 0.5 * c[j + 1];
+    const double delta = (fabs(c[j]) + fabs(c[j + 1]) + range) * 0x1p-40;
+    const int blo = km_bucket(m - delta, mn, inv), bhi = km_bucket(m + delta, mn, inv);
+    const int64_t lo = (int64_t)off[blo], hi = (int64_t)off[bhi + 1];
+    lo_sh = lo < 0 ? 0 : (lo > nv ? nv : lo);
+    hi_sh = hi < lo_sh ? lo_sh : (hi > nv ? nv : hi);
     exh_sh = 0;
   }
   __syncthreads();
@@ -402,6 +411,7 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       __syncthreads();
       unsigned long long nf = 0;
       long long sf = 0;
+      const long long plo = t == 0 ? prefix[lo] : 0;  // issued before the scan's loads
       for (int64_t idx = lo + t; idx < hi; idx += KS_T)
         if (km_assign<K>(xs[idx], c) <= j) {
           nf += 1;
@@ -416,7 +426,7 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       __syncthreads();
       if (t == 0) {
         *cnt_le = lo + (int64_t)nf_sh;
-        *sum_le = prefix[lo] + sf_sh;
+        *sum_le = plo + sf_sh;
       }
       __syncthreads();
       return;
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const double *__re
     }
     __syncthreads();
     if (stop) break;
-    for (int j = 0; j + 1 < K; ++j) km_bucket_step<K>(xs, q, prefix, off, nv, mn, inv, c, j, &cle[j], &sle[j]);
+    for (int j = 0; j + 1 < K; ++j) km_bucket_step<K>(xs, q, prefix, off, nv, mn, inv, range, c, j, &cle[j], &sle[j]);
     if (t == 0) {
       int changed = 0;
       int64_t c0 = 0;
