@@ -66,7 +66,11 @@ def lib():
             raise HrfError("libhrf.so not built (%s); run `python -m hiprfish_image_analysis_amd._build`" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in declared_functions().items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None)
+            if fn is None:
+                if os.environ.get("HRF_LIB"):   # an older A/B build may predate newer entries
+                    continue
+                raise HrfError("%s does not export %s (declared in include/hrf.h)" % (LIB_PATH, name))
             fn.restype = res
             fn.argtypes = args
         _lib = L

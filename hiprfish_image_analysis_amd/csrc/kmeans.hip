@@ -585,10 +585,11 @@ SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   return ws;
 }
 
+// Enqueue the sorted path (sort unless `reuse`, iterations, labels) and the read-back of its
+// final state into *fin (host); the caller synchronises before km_sorted_finish reads it.
 template <int K>
-hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
-                         uint8_t *top, double *centers_host, int32_t *iters_host, const SortWs &ws, int reuse,
-                         hipStream_t s) {
+hrf_status km_sorted_launch(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
+                            uint8_t *top, const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
   KmState *st = ws.st;
   const unsigned g = hrf::stream_grid(n);
   if (!reuse) {
@@ -618,9 +619,17 @@ hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int m
   HRF_LAUNCHED();
   if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
   HRF_LAUNCHED();
-  KmState fin;
-  HRF_HIP(hipMemcpyAsync(&fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
-  HRF_HIP(hipStreamSynchronize(s));
+  HRF_HIP(hipMemcpyAsync(fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
+  return HRF_OK;
+}
+
+// After the synchronisation: NaN input or merging centres send the call to the streaming
+// path, which recomputes everything (labels, top mask) in the workspace's state block.
+template <int K>
+hrf_status km_sorted_finish(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
+                            uint8_t *top, double *centers_host, int32_t *iters_host, const SortWs &ws,
+                            hipStream_t s, const KmState &fin) {
+  KmState *st = ws.st;
   if (fin.fallback) {
     // the streaming path recomputes everything from scratch in its own state block
     if (hrf_status r = km_run<K>(x, valid, n, max_iter, labels, top, centers_host, iters_host, st, s)) return r;
@@ -630,6 +639,38 @@ hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int m
     for (int j = 0; j < K; ++j) centers_host[j] = fin.center[j];
   if (iters_host) *iters_host = fin.iters;
   return HRF_OK;
+}
+
+template <int K>
+hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
+                         uint8_t *top, double *centers_host, int32_t *iters_host, const SortWs &ws, int reuse,
+                         hipStream_t s) {
+  KmState fin;
+  if (hrf_status r = km_sorted_launch<K>(x, valid, n, max_iter, labels, top, ws, reuse, s, &fin)) return r;
+  HRF_HIP(hipStreamSynchronize(s));
+  return km_sorted_finish<K>(x, valid, n, max_iter, labels, top, centers_host, iters_host, ws, s, fin);
+}
+
+hrf_status km_launch_k(int k, const double *x, const uint8_t *valid, int64_t n, int max_iter, uint8_t *top,
+                       const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
+  switch (k) {
+#define HRF_KML(KK) \
+  case KK: return km_sorted_launch<KK>(x, valid, n, max_iter, nullptr, top, ws, reuse, s, fin);
+    HRF_KML(1) HRF_KML(2) HRF_KML(3) HRF_KML(4) HRF_KML(5) HRF_KML(6) HRF_KML(7)
+#undef HRF_KML
+    default: return km_sorted_launch<8>(x, valid, n, max_iter, nullptr, top, ws, reuse, s, fin);
+  }
+}
+
+hrf_status km_finish_k(int k, const double *x, const uint8_t *valid, int64_t n, int max_iter, uint8_t *top,
+                       const SortWs &ws, hipStream_t s, const KmState &fin) {
+  switch (k) {
+#define HRF_KMF(KK) \
+  case KK: return km_sorted_finish<KK>(x, valid, n, max_iter, nullptr, top, nullptr, nullptr, ws, s, fin);
+    HRF_KMF(1) HRF_KMF(2) HRF_KMF(3) HRF_KMF(4) HRF_KMF(5) HRF_KMF(6) HRF_KMF(7)
+#undef HRF_KMF
+    default: return km_sorted_finish<8>(x, valid, n, max_iter, nullptr, top, nullptr, nullptr, ws, s, fin);
+  }
 }
 
 }  // namespace
@@ -687,6 +728,36 @@ hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n
 #undef HRF_KMS
     default: return km_run_sorted<8>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, ws, reuse_sort, s);
   }
+}
+
+hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int64_t n, int32_t k1, int32_t k2,
+                                     int32_t max_iter, uint8_t *top1, uint8_t *top2, void *work, int64_t work_bytes,
+                                     hrf_stream_t stream) {
+  HRF_REQUIRE(k1 >= 1 && k1 <= KMAX && k2 >= 1 && k2 <= KMAX, "kmeans_1d_pair: k must be 1..8");
+  HRF_REQUIRE(n >= 0 && max_iter >= 1 && work, "kmeans_1d_pair: bad arguments");
+  HRF_REQUIRE(n == 0 || x, "kmeans_1d_pair: null input");
+  const int64_t need = hrf_kmeans_sorted_workspace_bytes(n);
+  HRF_REQUIRE(need > 0, "kmeans_1d_pair: workspace size query failed");
+  if (work_bytes < need) {
+    ::hrf::set_error("kmeans_1d_pair: workspace of %lld bytes, %lld needed", (long long)work_bytes, (long long)need);
+    return HRF_ENOMEM;
+  }
+  size_t tb = 0;
+  if (hrf_status r = sort_tmp_bytes(n, &tb)) return r;
+  const SortWs ws = carve(work, n, tb);
+  hipStream_t s = (hipStream_t)stream;
+  // both runs enqueued before the one synchronisation; the second reuses the sort.  A
+  // fallback of either (rare) then reruns that k on the streaming path, after both.
+  // pinned read-back slots (one pair per host thread, kept for the thread's lifetime), so the
+  // first state copy does not block the host before the second run is enqueued
+  static thread_local KmState *fin = nullptr;
+  if (!fin) HRF_HIP(hipHostMalloc((void **)&fin, 2 * sizeof(KmState), hipHostMallocDefault));
+  if (hrf_status r = km_launch_k(k1, x, valid, n, max_iter, top1, ws, 0, s, &fin[0])) return r;
+  if (hrf_status r = km_launch_k(k2, x, valid, n, max_iter, top2, ws, 1, s, &fin[1])) return r;
+  HRF_HIP(hipStreamSynchronize(s));
+  const KmState f1 = fin[0], f2 = fin[1];
+  if (hrf_status r = km_finish_k(k1, x, valid, n, max_iter, top1, ws, s, f1)) return r;
+  return km_finish_k(k2, x, valid, n, max_iter, top2, ws, s, f2);
 }
 
 }  // extern "C"

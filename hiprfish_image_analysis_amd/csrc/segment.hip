@@ -152,8 +152,8 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   uint8_t *rough = c->m[0], *interior = c->m[1], *a = c->m[2], *b = c->m[3], *d = c->m[4];
   int32_t *lab1 = c->l[0], *seeds = c->l[1], *ws = c->l[2], *lab3 = c->l[3];
   HRF_TRY(hrf_channel_sum(stack, n, C, nullptr, 1, 0, c->cn, s));               // :71-72
-  HRF_TRY(kmeans_top(c, c->cn, 2, 0, rough, s));                                // :73-84
-  HRF_TRY(kmeans_top(c, c->cn, 3, 1, interior, s));                             // :85-94
+  HRF_TRY(hrf_kmeans_1d_sorted_pair(c->cn, nullptr, c->n, 2, 3, 300, rough, interior, c->km, c->km_bytes,
+                                    s));                                        // :73-94
   HRF_TRY(hrf_remove_small_holes(interior, H, W, 64, 1, a, c->parent, c->size, s));   // :95
   HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
   HRF_TRY(hrf_binary_dilation(b, H, W, d, s));

@@ -182,25 +182,28 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
   int32_t *tf = nullptr;  // per-tile change flags, two generations
   HRF_HIP(hipMallocAsync((void **)&tf, sizeof(int32_t) * 2 * ntiles, s));
   int passes = 0;
-  const int batch = 4;
-  // flag_ws[k] = change flag of pass k within a batch
-  for (;;) {
-    HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * batch, s));
+  // Passes run in batches with one host read per batch: the first batch of 8 covers the
+  // typical tile (~7 passes) with a single synchronisation, later batches 4.  Passes after
+  // convergence change nothing (unique fixed point) and skip every tile (no tile changed).
+  // flag_ws[0] = change flag of the batch's last pass, flag_ws[1] = scratch for the others.
+  for (int batch = 8;; batch = 4) {
+    HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 2, s));
     for (int k = 0; k < batch; ++k) {
       int32_t *cur = tf + (passes & 1) * ntiles;
       const int32_t *prev = passes == 0 ? nullptr : tf + ((passes + 1) & 1) * ntiles;
       HRF_HIP(hipMemsetAsync(cur, 0, sizeof(int32_t) * ntiles, s));
-      ws_pass_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, flag_ws + k, prev, cur);
+      ws_pass_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, flag_ws + (k == batch - 1 ? 0 : 1),
+                                          prev, cur);
       WsState t = a;
       a = b;
       b = t;
       ++passes;
     }
     HRF_LAUNCHED();
-    int32_t fl[batch];
-    HRF_HIP(hipMemcpyAsync(fl, flag_ws, sizeof(fl), hipMemcpyDeviceToHost, s));
+    int32_t fl = 0;
+    HRF_HIP(hipMemcpyAsync(&fl, flag_ws, sizeof(fl), hipMemcpyDeviceToHost, s));
     HRF_HIP(hipStreamSynchronize(s));
-    if (!fl[batch - 1] || passes >= max_passes) break;
+    if (!fl || passes >= max_passes) break;
   }
   HRF_HIP(hipFreeAsync(tf, s));
   HRF_HIP(hipMemcpyAsync(out_labels, a.lab, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));

@@ -320,6 +320,23 @@ def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, path=None, share
     return labels, top, cen.tolist(), it.value
 
 
+def kmeans_1d_pair(x, k1, k2, valid=None, max_iter=300):
+    """top-cluster masks of KMeans(k1) and KMeans(k2) on the same x with one sort and one host
+    synchronisation (ecoli measurement.py:73-94: k = 2 and k = 3 on image_cn)"""
+    x = _dev(x, torch.float64, "x")
+    n = x.numel()
+    v = _u8(valid, "valid") if valid is not None else None
+    top1 = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    top2 = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    nb = int(_lib.lib().hrf_kmeans_sorted_workspace_bytes(n))
+    if nb <= 0:
+        raise _lib.HrfError("hrf_kmeans_sorted_workspace_bytes failed")
+    ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
+    _lib.call("hrf_kmeans_1d_sorted_pair", _ptr(x), _ptr(v), n, k1, k2, max_iter, _ptr(top1), _ptr(top2), _ptr(ws),
+              ws.numel(), _stream())
+    return top1, top2
+
+
 # ---- a9/a10/a13 -----------------------------------------------------------------------------
 def _img(img):
     if img.dtype == torch.int32:

@@ -167,6 +167,13 @@ HRF_API hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, i
                                         int32_t *labels, uint8_t *top_mask, double *centers_host,
                                         int32_t *iters_host, void *work, int64_t work_bytes, int32_t reuse_sort,
                                         hrf_stream_t stream);
+/* Two KMeans runs (k1, then k2 reusing the sort) on the same x with ONE host
+ * synchronisation: ecoli measurement.py:73-84 (k = 2, top cluster -> top1) and :85-94
+ * (k = 3 -> top2).  Top masks equal two hrf_kmeans_1d_sorted calls'; each run falls back to
+ * the streaming path by itself after the synchronisation. */
+HRF_API hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int64_t n, int32_t k1, int32_t k2,
+                                             int32_t max_iter, uint8_t *top1, uint8_t *top2, void *work,
+                                             int64_t work_bytes, hrf_stream_t stream);
 
 /* ==== a9/a10/a13: components, morphology, label cleanup (label.hip) ====================
  * img dtype: 0 = uint8 mask, 1 = int32 label image (equal values connect), 2 = uint8 mask
@@ -226,7 +233,7 @@ HRF_API hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hr
 
 /* ==== a12: watershed (watershed.hip) =====================================================
  * skimage.morphology.watershed(+/-image, markers, mask) (ecoli :113, multispecies :154),
- * 4-connectivity.  state_ws: 32*H*W bytes; flag_ws: >= 4 int32.  Synchronises per 4 passes. */
+ * 4-connectivity.  state_ws: 32*H*W bytes; flag_ws: >= 4 int32.  Synchronises after 8 passes, then per 4. */
 HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
                                  int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
                                  int32_t max_passes, int32_t *passes_host, hrf_stream_t stream);

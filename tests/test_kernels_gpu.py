@@ -176,6 +176,29 @@ def test_kmeans_sorted_share_valid_and_fallbacks(K, orc):
     assert lab.numel() == 0 and it == 0
 
 
+@pytest.mark.parametrize("case", ["mixture", "valid", "constant", "nan", "empty"])
+def test_kmeans_pair_equals_two_calls(K, case):
+    """hrf_kmeans_1d_sorted_pair (one sort, one synchronisation) gives the top masks of two
+    separate sorted calls, including the inputs that send a run to the streaming fallback"""
+    rng = np.random.default_rng(11)
+    x = np.concatenate([rng.normal(0.2, 0.05, 30000), rng.normal(0.9, 0.1, 20000), rng.normal(3, 0.2, 5000)])
+    valid = None
+    if case == "valid":
+        valid = dev(rng.random(x.size) > 0.2)
+    elif case == "constant":
+        x = np.full(10000, 0.5)
+    elif case == "nan":
+        x = np.where(rng.random(20000) < 0.001, np.nan, rng.random(20000))
+    elif case == "empty":
+        x = np.zeros(0)
+    d = dev(x)
+    t1, t2 = K.kmeans_1d_pair(d, 2, 3, valid=valid)
+    share = {}
+    a = K.kmeans_1d(d, 2, valid=valid, share=share, want_labels=False)
+    b = K.kmeans_1d(d, 3, valid=valid, share=share, want_labels=False)
+    assert torch.equal(t1, a[1]) and torch.equal(t2, b[1])
+
+
 # ---- a12 watershed ----------------------------------------------------------------------
 @pytest.mark.parametrize("shape", [(64, 64), (130, 97), (300, 330)])
 def test_watershed_vs_heap_flood(K, orc, shape):
