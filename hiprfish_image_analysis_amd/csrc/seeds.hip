@@ -240,11 +240,26 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
                              int32_t area_max, int32_t min_obj, uint8_t *be_out, hrf_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   HRF_REQUIRE(ncomp >= 0 && be_out && (ncomp == 0 || (labels && box)), "erosion_seeds: bad arguments");
-  HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
-  if (ncomp == 0) return HRF_OK;
+  if (ncomp == 0) {
+    HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+    return HRF_OK;
+  }
   std::vector<int32_t> hb((size_t)(ncomp + 1) * 4);
   HRF_HIP(hipMemcpyAsync(hb.data(), box, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));
+  return ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s);
+}
+
+}  // extern "C"
+
+// The same with the boxes already on the host (hb: (ncomp + 1) x 4, as hrf_label_boxes
+// writes them): the native E. coli driver reads them back at its component-count
+// synchronisation instead of a second one here.
+hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
+                                      const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
+                                      hipStream_t s) {
+  HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+  if (ncomp == 0) return HRF_OK;
   std::vector<uint8_t> big((size_t)ncomp + 1, 0);  // 0: LDS 72 KB, 1: LDS 160 KB, 2: whole-image loop
   int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
   int nmid = 0;
@@ -308,5 +323,3 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   HRF_HIP(hipFreeAsync(dbig, s));
   return st;
 }
-
-}  // extern "C"

@@ -26,11 +26,13 @@ struct hrf_seg_ctx {
   int32_t *parent = nullptr, *size = nullptr, *blk = nullptr, *dint = nullptr;
   void *ws_state = nullptr;
   int32_t *ws_flag = nullptr;
+  int32_t *hpin = nullptr;  // pinned host slots for counts read back at a later synchronisation
   void *km = nullptr;
   int64_t km_bytes = 0;
   // per-label scratch, grown on demand
   int64_t lab_cap = 0;
   int32_t *box = nullptr, *cnt = nullptr;
+  int32_t *hbox = nullptr;  // pinned host copy of box (4 * lab_cap)
   int64_t *mom = nullptr;
   double *props = nullptr;
 };
@@ -50,12 +52,20 @@ hrf_status ensure_labels(hrf_seg_ctx *c, int64_t maxlab, hipStream_t s) {
   hipFree(c->cnt);
   hipFree(c->mom);
   hipFree(c->props);
+  if (c->hbox) hipHostFree(c->hbox);
+  c->hbox = nullptr;
   int64_t cap = 1024;
   while (cap < maxlab + 1) cap *= 2;
   if (hrf_status r = dalloc(&c->box, 4 * cap)) return r;
   if (hrf_status r = dalloc(&c->cnt, cap)) return r;
   if (hrf_status r = dalloc(&c->mom, 6 * cap)) return r;
   if (hrf_status r = dalloc(&c->props, 8 * cap)) return r;
+  if (hipHostMalloc((void **)&c->hbox, sizeof(int32_t) * 4 * cap, hipHostMallocDefault) != hipSuccess) {
+    c->hbox = nullptr;
+    c->lab_cap = 0;
+    ::hrf::set_error("seg_ctx: pinned host allocation failed");
+    return HRF_EHIP;
+  }
   c->lab_cap = cap;
   return HRF_OK;
 }
@@ -75,6 +85,14 @@ hrf_status read_i32(const int32_t *dev, int32_t *host, hipStream_t s) {
 hrf_status label_conn2(hrf_seg_ctx *c, const uint8_t *mask, int32_t *labels, int32_t *nlab, hipStream_t s) {
   HRF_TRY(hrf_label(mask, 0, c->H, c->W, 2, labels, c->parent, c->blk, c->dint, s));
   return read_i32(c->dint, nlab, s);
+}
+
+// skimage.measure.label(mask, connectivity=2) with the count's read-back only enqueued: it
+// lands in c->hpin[0] at the caller's next synchronisation (saves one host round trip)
+hrf_status label_conn2_deferred(hrf_seg_ctx *c, const uint8_t *mask, int32_t *labels, hipStream_t s) {
+  HRF_TRY(hrf_label(mask, 0, c->H, c->W, 2, labels, c->parent, c->blk, c->dint, s));
+  HRF_HIP(hipMemcpyAsync(c->hpin, c->dint, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  return HRF_OK;
 }
 
 // KMeans(k) top-cluster mask; `reuse` when the previous call sorted the same x
@@ -112,6 +130,11 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
       (r = dalloc(&c->dint, 16)) || (r = dalloc(&c->ws_flag, 8)))
     return fail(r);
   if ((r = dalloc((char **)&c->ws_state, 32 * n))) return fail(r);
+  if (hipHostMalloc((void **)&c->hpin, 16 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
+    c->hpin = nullptr;
+    ::hrf::set_error("seg_ctx: pinned host allocation failed");
+    return fail(HRF_EHIP);
+  }
   c->km_bytes = hrf_kmeans_sorted_workspace_bytes(c->n);
   if (c->km_bytes <= 0) return fail(HRF_EHIP);
   if ((r = dalloc((char **)&c->km, (size_t)c->km_bytes))) return fail(r);
@@ -135,6 +158,8 @@ hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *c) {
   hipFree(c->dint);
   hipFree(c->ws_state);
   hipFree(c->ws_flag);
+  if (c->hpin) hipHostFree(c->hpin);
+  if (c->hbox) hipHostFree(c->hbox);
   hipFree(c->km);
   hipFree(c->box);
   hipFree(c->cnt);
@@ -158,16 +183,29 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
   HRF_TRY(hrf_binary_dilation(b, H, W, d, s));
   HRF_TRY(hrf_remove_small_objects_mask(d, H, W, 50, 1, a, c->parent, c->size, s));  // :96 cell_sm = a
-  int32_t ncomp = 0;                                                            // :97-110
-  HRF_TRY(label_conn2(c, a, lab1, &ncomp, s));
-  HRF_TRY(ensure_labels(c, ncomp, s));
-  HRF_TRY(hrf_label_boxes(lab1, H, W, ncomp, c->box, s));
-  HRF_TRY(hrf_erosion_seeds(lab1, H, W, ncomp, c->box, 600, 10, b, s));
+  // :97-110.  Components, their count and their boxes come back in ONE synchronisation: the
+  // boxes are computed for every label the current capacity holds (labels above it are
+  // ignored by the box kernel) and redone in the rare case the count exceeds it.
+  HRF_TRY(hrf_label(a, 0, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
+  HRF_HIP(hipMemcpyAsync(c->hpin + 1, c->dint, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HRF_TRY(ensure_labels(c, 1, s));
+  int32_t guess = (int32_t)(c->lab_cap - 1);
+  HRF_TRY(hrf_label_boxes(lab1, H, W, guess, c->box, s));
+  HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)guess + 1), hipMemcpyDeviceToHost, s));
+  HRF_HIP(hipStreamSynchronize(s));
+  const int32_t ncomp = c->hpin[1];
+  if (ncomp > guess) {
+    HRF_TRY(ensure_labels(c, ncomp, s));
+    HRF_TRY(hrf_label_boxes(lab1, H, W, ncomp, c->box, s));
+    HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)ncomp + 1), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+  }
+  HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s));
   HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
-  int32_t nseeds = 0;
-  HRF_TRY(label_conn2(c, d, seeds, &nseeds, s));                                // :111-112
+  HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
   int32_t passes = 0;
   HRF_TRY(hrf_watershed(c->cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
+  const int32_t nseeds = c->hpin[0];  // read back by the watershed's synchronisation
   HRF_TRY(ensure_labels(c, nseeds, s));
   HRF_TRY(hrf_remove_small_objects_labels(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114
   HRF_TRY(hrf_clear_border(lab1, H, W, lab3, c->parent, c->size, s));          // :115
@@ -203,9 +241,9 @@ hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t 
   HRF_TRY(hrf_fill_holes(a, H, W, b, c->parent, c->size, s));                  // :138
   HRF_TRY(hrf_fill_holes(rough, H, W, d, c->parent, c->size, s));              // :139
   HRF_TRY(hrf_and_u8(b, d, n, e, s));                                          // :140
-  int32_t nseeds = 0;
-  HRF_TRY(label_conn2(c, e, seeds, &nseeds, s));
+  HRF_TRY(label_conn2_deferred(c, e, seeds, s));
   HRF_TRY(kmeans_top(c, nl, 2, 0, bkg, s));                                     // :141-149
+  const int32_t nseeds = c->hpin[0];  // read back by the KMeans synchronisation
   double *final_bkg = final_bkg_out ? final_bkg_out : c->cn;
   HRF_TRY(hrf_mask_mul_f64(fin, bkg, n, final_bkg, s));                         // :150
   HRF_TRY(hrf_mask_labels(seeds, bkg, n, seeds_b, s));                          // :152
