@@ -53,7 +53,8 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
                                                       WsState in, WsState out, int32_t *__restrict__ changed,
                                                       const int32_t *__restrict__ prev_tile,
-                                                      int32_t *__restrict__ cur_tile) {
+                                                      int32_t *__restrict__ cur_tile,
+                                                      int32_t *__restrict__ next_tile) {
   __shared__ double sl[WL * WL];
   __shared__ double sf[WL * WL];
   __shared__ int32_t sh[WL * WL];
@@ -61,6 +62,10 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   __shared__ uint8_t sm[WL * WL];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.y * WT - 1, c0 = (int64_t)blockIdx.x * WT - 1;
+  // Tile flags rotate through three generations: this pass reads prev, sets cur, and clears
+  // next for the following pass (last read as prev by the pass before this one, which has
+  // finished), so no memset is needed between passes.
+  if (tid == 0) next_tile[blockIdx.y * gridDim.x + blockIdx.x] = 0;
   // A tile whose 3x3 tile neighbourhood did not change in the previous pass is skipped: its
   // own state did not change either, so both ping-pong buffers already hold it.
   if (prev_tile) {
@@ -179,8 +184,9 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
   HRF_LAUNCHED();
   dim3 grid((unsigned)hrf::cdiv(W, WT), (unsigned)hrf::cdiv(H, WT));
   const int64_t ntiles = (int64_t)grid.x * grid.y;
-  int32_t *tf = nullptr;  // per-tile change flags, two generations
-  HRF_HIP(hipMallocAsync((void **)&tf, sizeof(int32_t) * 2 * ntiles, s));
+  int32_t *tf = nullptr;  // per-tile change flags, three rotating generations
+  HRF_HIP(hipMallocAsync((void **)&tf, sizeof(int32_t) * 3 * ntiles, s));
+  HRF_HIP(hipMemsetAsync(tf, 0, sizeof(int32_t) * 2 * ntiles, s));  // generations of passes 0 and 1
   int passes = 0;
   // Passes run in batches with one host read per batch: the first batch of 8 covers the
   // typical tile (~7 passes) with a single synchronisation, later batches 4.  Passes after
@@ -189,11 +195,11 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
   for (int batch = 8;; batch = 4) {
     HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 2, s));
     for (int k = 0; k < batch; ++k) {
-      int32_t *cur = tf + (passes & 1) * ntiles;
-      const int32_t *prev = passes == 0 ? nullptr : tf + ((passes + 1) & 1) * ntiles;
-      HRF_HIP(hipMemsetAsync(cur, 0, sizeof(int32_t) * ntiles, s));
+      int32_t *cur = tf + (passes % 3) * ntiles;
+      const int32_t *prev = passes == 0 ? nullptr : tf + ((passes + 2) % 3) * ntiles;
+      int32_t *next = tf + ((passes + 1) % 3) * ntiles;
       ws_pass_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, flag_ws + (k == batch - 1 ? 0 : 1),
-                                          prev, cur);
+                                          prev, cur, next);
       WsState t = a;
       a = b;
       b = t;
