@@ -164,8 +164,41 @@ struct Cal {
 
 // C <= 128: 64-pixel chunks staged through LDS with 16-byte loads (coalesced), then 8 lanes per
 // pixel: lane j accumulates numpy's r[j] (a[j] + a[j+8] + ...), the three xor-shuffle levels
-// are exactly ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), lane 0 adds the tail in order.
+// are exactly ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), lane 0 adds the tail in order.  The next
+// chunk's loads are issued into registers right after this chunk lands in LDS, so they are in
+// flight while it is reduced (0.364 -> 0.337 ms at 2048^2 x 95, 56 -> 60 % of HBM peak).
 constexpr int CS_P = 64;
+
+// The 16-byte loads of chunk c into eight named registers (an indexed array is not promoted
+// out of scratch here), nothing past the last chunk; CS_PUT stores them into LDS.
+#define CS_FETCH(c)                                                                                  \
+  {                                                                                                  \
+    const int64_t q0 = (c) * CS_P;                                                                   \
+    const int nvq = (c) < nchunks ? (int)(((int64_t)min((int64_t)CS_P, npix - q0) * C) >> 2) : 0;   \
+    const float4 *g = reinterpret_cast<const float4 *>(stack + q0 * C);                             \
+    if (tid < nvq) r0 = g[tid];                                                                      \
+    if (tid + 256 < nvq) r1 = g[tid + 256];                                                          \
+    if (tid + 512 < nvq) r2 = g[tid + 512];                                                          \
+    if (tid + 768 < nvq) r3 = g[tid + 768];                                                          \
+    if (tid + 1024 < nvq) r4 = g[tid + 1024];                                                        \
+    if (tid + 1280 < nvq) r5 = g[tid + 1280];                                                        \
+    if (tid + 1536 < nvq) r6 = g[tid + 1536];                                                        \
+    if (tid + 1792 < nvq) r7 = g[tid + 1792];                                                        \
+  }
+#define CS_PUT(nv)                                                                                   \
+  {                                                                                                  \
+    float4 *d = reinterpret_cast<float4 *>(sb);                                                      \
+    if (tid < (nv)) d[tid] = r0;                                                                     \
+    if (tid + 256 < (nv)) d[tid + 256] = r1;                                                         \
+    if (tid + 512 < (nv)) d[tid + 512] = r2;                                                         \
+    if (tid + 768 < (nv)) d[tid + 768] = r3;                                                         \
+    if (tid + 1024 < (nv)) d[tid + 1024] = r4;                                                       \
+    if (tid + 1280 < (nv)) d[tid + 1280] = r5;                                                       \
+    if (tid + 1536 < (nv)) d[tid + 1536] = r6;                                                       \
+    if (tid + 1792 < (nv)) d[tid + 1792] = r7;                                                       \
+  }
+static_assert(CS_P * 128 / 4 == 8 * 256, "CS_FETCH covers 8 float4 per thread");
+
 template <bool CAL>
 __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__restrict__ stack, int64_t npix, int C,
                                                               const uint8_t *__restrict__ mask, int mode, int negate,
@@ -175,6 +208,10 @@ __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__res
   const int64_t nchunks = (npix + CS_P - 1) / CS_P;
   const int j = tid & 7;
   const int main_n = C < 8 ? 0 : C - (C % 8);
+  // Vector path, software-pipelined: the next chunk's 16-byte loads are in flight in
+  // registers while this chunk is reduced from LDS (C <= 128: at most 8 per thread).
+  float4 r0, r1, r2, r3, r4, r5, r6, r7;
+  if (vec_ok) CS_FETCH((int64_t)blockIdx.x)
   for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const int64_t p0 = ch * CS_P;
     const int np = (int)min((int64_t)CS_P, npix - p0);
@@ -182,12 +219,13 @@ __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__res
     const float *src = stack + p0 * C;
     if (vec_ok) {
       const int nv = (int)(nel >> 2);
-      for (int v = tid; v < nv; v += 256) reinterpret_cast<float4 *>(sb)[v] = reinterpret_cast<const float4 *>(src)[v];
+      CS_PUT(nv)
       for (int e = (nv << 2) + tid; e < nel; e += 256) sb[e] = src[e];
     } else {
       for (int e = tid; e < nel; e += 256) sb[e] = src[e];
     }
     __syncthreads();
+    if (vec_ok) CS_FETCH(ch + gridDim.x)
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int pi = half * 32 + (tid >> 3);
@@ -218,6 +256,9 @@ __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__res
     __syncthreads();
   }
 }
+
+#undef CS_FETCH
+#undef CS_PUT
 
 __global__ void max_f64_kernel(const double *__restrict__ a, int64_t n, unsigned long long *__restrict__ mx) {
   // order-preserving encoding so atomicMax on uint64 is a max on doubles

@@ -51,7 +51,7 @@ def main():
         C = stack.shape[2]
         nb = H * W * (4 * C + 8)
         ms = timed(lambda: K.channel_sum(stack, mode=1))
-        print("channel_sum (log) 2048^2x95: %.3f ms  %.0f GB/s (%.1f %% of 8 TB/s)" % (ms, nb / ms / 1e6, nb / ms / 8e10))
+        print("channel_sum (log) 2048^2x95: %.3f ms  %.0f GB/s (%.1f %% of 8 TB/s)" % (ms, nb / ms / 1e6, nb / ms / 8e7))
         cal = torch.rand(C, device="cuda") + 0.5
         ms = timed(lambda: K.channel_sum(stack, cal=cal))
         print("channel_sum cal(C) 2048^2x95: %.3f ms  %.0f GB/s" % (ms, nb / ms / 1e6))
