@@ -81,11 +81,22 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
     const float *src = L.src[q] + (rs * W + (c0 - L.dc[q])) * (int64_t)cl;  // pixel c0's source (may be off-row)
     const int cmin = L.dc[q] > 0 ? L.dc[q] : 0, cmax = (int)W + (L.dc[q] < 0 ? L.dc[q] : 0);
     const int n = np * cl;
-    for (int i = tid; i < n; i += 256) {
-      const int p = i / cl, ch = i - p * cl;
-      const int64_t c = c0 + p;
-      const bool cov = row_ok && c >= cmin && c < cmax;
-      tile[p * C + off + ch] = cov ? src[i] : 0.0f;
+    // four loads in flight per thread per round (the run is at most 64 x 128 floats)
+    for (int i0 = tid; i0 < n; i0 += 1024) {
+      float v[4];
+      int pp[4], cc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u;
+        pp[u] = i / cl;
+        cc[u] = i - pp[u] * cl;
+        const int64_t c = c0 + pp[u];
+        const bool cov = i < n && row_ok && c >= cmin && c < cmax;
+        v[u] = cov ? src[i] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (i0 + 256 * u < n) tile[pp[u] * C + off + cc[u]] = v[u];
     }
   }
   __syncthreads();

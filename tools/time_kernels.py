@@ -52,6 +52,15 @@ def main():
         nb = H * W * (4 * C + 8)
         ms = timed(lambda: K.channel_sum(stack, mode=1))
         print("channel_sum (log) 2048^2x95: %.3f ms  %.0f GB/s (%.1f %% of 8 TB/s)" % (ms, nb / ms / 1e6, nb / ms / 8e7))
+        lasers, c0 = [], 0
+        for c1 in S.ECOLI_BOUNDS[1:]:
+            lasers.append(stack[:, :, c0:c1].contiguous())
+            c0 = c1
+        shifts = [(0, 0), (2, -1), (0, 3), (-1, 0), (1, 1)]
+        ms = timed(lambda: K.register_assemble(lasers, shifts, apply_mask=True))
+        nb3 = H * W * 8 * C
+        print("register_assemble 2048^2x95: %.3f ms  %.0f GB/s (%.1f %% of 8 TB/s)" % (ms, nb3 / ms / 1e6,
+                                                                                   nb3 / ms / 8e7))
         cal = torch.rand(C, device="cuda") + 0.5
         ms = timed(lambda: K.channel_sum(stack, cal=cal))
         print("channel_sum cal(C) 2048^2x95: %.3f ms  %.0f GB/s" % (ms, nb / ms / 1e6))
