@@ -124,12 +124,18 @@ def _hbm_kernels(dev):
         # bytes: label map read + the spectra of labelled pixels read (background is skipped)
         "label_sums": (lambda: K.label_sums(stack, seg, maxlab), H * W * 4 + fg * 4 * C),
     }
+    pmc = {}
+    try:   # HBM bytes per launch from the committed PMC passes (profiles/hbm_kernels_pmc.json)
+        pmc = json.load(open(os.path.join(REPO, "profiles", "hbm_kernels_pmc.json")))["kernels"]
+    except Exception:
+        pmc = {}
     out = {}
     for name, (fn, nbytes) in rows.items():
         ms = timed(fn)
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
-                     "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4)}
+                     "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4),
+                     "traffic": pmc.get(name, {}).get("hbm_bytes_per_launch")}
     return out
 
 
