@@ -825,16 +825,28 @@ int layout_id(const Bounds &bd, int C) {
 }
 
 // ---- per cell, f64, gated variants; one workgroup per cell ----
-__device__ double seg_dist(const double *x, const double *y, int lo, int hi) {
+// The library is read channel-major (refT[c * R + r], transposed once per call), so the 256
+// threads of a workgroup -- one library row each -- read consecutive addresses per channel:
+// coalesced, instead of 64 cache lines per load with row-major rows.  Same arithmetic order.
+__device__ double seg_dist(const double *x, const double *y, int64_t ys, int lo, int hi) {
   double d = 0, nx = 0, ny = 0;
   for (int i = lo; i < hi; ++i) {
-    d += x[i] * y[i];
+    const double yi = y[i * ys];
+    d += x[i] * yi;
     nx += x[i] * x[i];
-    ny += y[i] * y[i];
+    ny += yi * yi;
   }
   if (nx == 0.0 && ny == 0.0) return 0.0;
   if (nx == 0.0 || ny == 0.0) return 1.0;
   return 1.0 - d / sqrt(nx * ny);
+}
+
+__global__ void transpose_f64_kernel(const double *__restrict__ a, int32_t R, int32_t C, double *__restrict__ t) {
+  const int64_t n = (int64_t)R * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / C, c = e - r * C;
+    t[c * R + r] = a[e];
+  }
 }
 
 __global__ __launch_bounds__(256) void classify_cells_kernel(const double *__restrict__ X, int64_t N,
@@ -854,24 +866,24 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *__res
   double best = __builtin_inf();
   int bi = 0x7fffffff;
   for (int r = tid; r < R; r += 256) {
-    const double *y = ref + (int64_t)r * C;
+    const double *y = ref + r;  // channel-major: element c at y[c * R]
     double d;
     if (variant == 0) {
       double s = 0;
-      for (int k = 0; k < S; ++k) s += seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+      for (int k = 0; k < S; ++k) s += seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
       d = s / S;
     } else {
       double chk = 0;
       for (int k = 0; k < S; ++k) chk += fabs(fx[i * S + k] - fr[(int64_t)r * S + k]);
       if (chk < 0.01) {
         double s = 0;
-        for (int k = 0; k < S; ++k) s += fx[i * S + k] == 0 ? 0.0 : seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+        for (int k = 0; k < S; ++k) s += fx[i * S + k] == 0 ? 0.0 : seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
         d = variant == 1 ? s / S : 0.5 * s / S;
       } else if (variant == 2) {
         d = 1.0;
       } else {
         double s = 0;
-        for (int k = 0; k < S; ++k) s += seg_dist(xs, y, bd.b[k], bd.b[k + 1]);
+        for (int k = 0; k < S; ++k) s += seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
         d = s / S;
       }
     }
@@ -1069,9 +1081,14 @@ hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int
   HRF_REQUIRE(R >= 1 && C >= 1, "classify_cells: bad sizes");
   if (N == 0) return HRF_OK;
   HRF_REQUIRE(x && ref && arg && dmin, "classify_cells: null buffer");
-  classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, (hipStream_t)stream>>>(x, N, ref, R, C, bd, variant,
+  double *refT = nullptr;
+  HRF_HIP(hipMallocAsync((void **)&refT, sizeof(double) * (size_t)R * C, (hipStream_t)stream));
+  transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, (hipStream_t)stream>>>(ref, R, C, refT);
+  HRF_LAUNCHED();
+  classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, (hipStream_t)stream>>>(x, N, refT, R, C, bd, variant,
                                                                                        fx, fr, arg, dmin);
   HRF_LAUNCHED();
+  HRF_HIP(hipFreeAsync(refT, (hipStream_t)stream));
   return HRF_OK;
 }
 
