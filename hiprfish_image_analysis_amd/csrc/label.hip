@@ -127,13 +127,21 @@ __global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t
   }
 }
 
+// One thread per tile-border pixel that can have a neighbour in another tile: row 0 of the
+// tile (32) and columns 0 and 31 of rows 1..31 (62), 94 per tile -- a grid of 94/1024 of the
+// image instead of one thread per pixel that mostly exits at once.
+constexpr int CC_BORDER_PX = CC_T + 2 * (CC_T - 1);
 template <class V, int CONN>
 __global__ void cc_border_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t r = blockIdx.y;
-  if (c >= W) return;
-  const int lr = (int)(r & 31), lc = (int)(c & 31);
-  if (lr != 0 && lc != 0 && lc != 31) return;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tiles_x = (W + CC_T - 1) / CC_T;
+  const int64_t tile = t / CC_BORDER_PX;
+  if (tile >= tiles_x * ((H + CC_T - 1) / CC_T)) return;
+  const int k = (int)(t - tile * CC_BORDER_PX);
+  const int lr = k < CC_T ? 0 : 1 + ((k - CC_T) >> 1);
+  const int lc = k < CC_T ? k : (((k - CC_T) & 1) ? CC_T - 1 : 0);
+  const int64_t r = (tile / tiles_x) * CC_T + lr, c = (tile % tiles_x) * CC_T + lc;
+  if (r >= H || c >= W) return;
   const int64_t p = r * W + c;
   const int32_t v = val(p);
   if (!v) return;
@@ -429,7 +437,7 @@ __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t
 template <class V>
 hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s) {
   dim3 g((unsigned)hrf::cdiv(W, CC_T), (unsigned)hrf::cdiv(H, CC_T));
-  dim3 gb((unsigned)hrf::cdiv(W, 256), (unsigned)H);
+  const unsigned gb = (unsigned)hrf::cdiv(hrf::cdiv(W, CC_T) * hrf::cdiv(H, CC_T) * CC_BORDER_PX, 256);
   if (conn == 2) {
     cc_local_kernel<V, 2><<<g, 256, 0, s>>>(val, H, W, parent);
     cc_border_kernel<V, 2><<<gb, 256, 0, s>>>(val, H, W, parent);
