@@ -155,10 +155,12 @@ __global__ void cc_border_kernel(V val, int64_t H, int64_t W, int32_t *__restric
   }
 }
 
-__global__ void cc_compress_kernel(int32_t *__restrict__ parent, int64_t n) {
+// zero != nullptr: also clears a per-pixel size array for cc_sizes (saves its memset launch)
+__global__ void cc_compress_kernel(int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ zero) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
     const int32_t q = parent[p];
     if (q >= 0 && q != p) parent[p] = find_g(parent, q);
+    if (zero) zero[p] = 0;
   }
 }
 
@@ -435,7 +437,7 @@ __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t
 }
 
 template <class V>
-hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s) {
+hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s, int32_t *zero = nullptr) {
   dim3 g((unsigned)hrf::cdiv(W, CC_T), (unsigned)hrf::cdiv(H, CC_T));
   const unsigned gb = (unsigned)hrf::cdiv(hrf::cdiv(W, CC_T) * hrf::cdiv(H, CC_T) * CC_BORDER_PX, 256);
   if (conn == 2) {
@@ -445,7 +447,7 @@ hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStr
     cc_local_kernel<V, 1><<<g, 256, 0, s>>>(val, H, W, parent);
     cc_border_kernel<V, 1><<<gb, 256, 0, s>>>(val, H, W, parent);
   }
-  cc_compress_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(parent, H * W);
+  cc_compress_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(parent, H * W, zero);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -506,12 +508,31 @@ hrf_status hrf_cc_sizes(const int32_t *parent, int64_t n, int32_t *size, hrf_str
   return HRF_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// hrf_cc_roots + hrf_cc_sizes with the size array cleared by the compression pass
+hrf_status cc_roots_sizes(const uint8_t *mask, int dtype, int64_t H, int64_t W, int conn, int32_t *parent,
+                          int32_t *size, hipStream_t s) {
+  if (hrf_status st = check_hw(H, W, "cc_roots")) return st;
+  HRF_REQUIRE(conn == 1 || conn == 2, "cc_roots: connectivity must be 1 or 2");
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(mask && parent && size, "cc_roots: null buffer");
+  if (hrf_status st = run_cc(MaskV{mask, dtype == 2}, H, W, conn, parent, s, size)) return st;
+  cc_sizes_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(H * W, RUN_PX * 4), 4096), 256, 0, s>>>(parent, H * W,
+                                                                                                  size);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+}  // namespace
+
+extern "C" {
+
 hrf_status hrf_remove_small_objects_mask(const uint8_t *mask, int64_t H, int64_t W, int64_t min_size, int32_t conn,
                                          uint8_t *out, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
   const int64_t n = H * W;
-  if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, stream)) return st;
   if (n == 0) return HRF_OK;
-  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  if (hrf_status st = cc_roots_sizes(mask, 0, H, W, conn, parent_ws, size_ws, (hipStream_t)stream)) return st;
   cc_keep_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, min_size, 0, out);
   HRF_LAUNCHED();
   return HRF_OK;
@@ -520,9 +541,8 @@ hrf_status hrf_remove_small_objects_mask(const uint8_t *mask, int64_t H, int64_t
 hrf_status hrf_remove_small_holes(const uint8_t *mask, int64_t H, int64_t W, int64_t area_threshold, int32_t conn,
                                   uint8_t *out, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
   const int64_t n = H * W;
-  if (hrf_status st = hrf_cc_roots(mask, 2, H, W, conn, parent_ws, stream)) return st;
   if (n == 0) return HRF_OK;
-  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  if (hrf_status st = cc_roots_sizes(mask, 2, H, W, conn, parent_ws, size_ws, (hipStream_t)stream)) return st;
   cc_keep_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, area_threshold, 1,
                                                                         out);
   HRF_LAUNCHED();
@@ -532,9 +552,8 @@ hrf_status hrf_remove_small_holes(const uint8_t *mask, int64_t H, int64_t W, int
 hrf_status hrf_split_by_size(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int64_t thr, uint8_t *small_or,
                              uint8_t *large, int32_t *parent_ws, int32_t *size_ws, hrf_stream_t stream) {
   const int64_t n = H * W;
-  if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, stream)) return st;
   if (n == 0) return HRF_OK;
-  if (hrf_status st = hrf_cc_sizes(parent_ws, n, size_ws, stream)) return st;
+  if (hrf_status st = cc_roots_sizes(mask, 0, H, W, conn, parent_ws, size_ws, (hipStream_t)stream)) return st;
   split_by_size_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(parent_ws, size_ws, n, thr, small_or,
                                                                               large);
   HRF_LAUNCHED();
