@@ -129,7 +129,7 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
   if ((r = dalloc(&c->parent, n)) || (r = dalloc(&c->size, n)) || (r = dalloc(&c->blk, n / 1024 + 2)) ||
       (r = dalloc(&c->dint, 16)) || (r = dalloc(&c->ws_flag, 8)))
     return fail(r);
-  if ((r = dalloc((char **)&c->ws_state, 32 * n))) return fail(r);
+  if ((r = dalloc((char **)&c->ws_state, (size_t)hrf_watershed_workspace_bytes(H, W)))) return fail(r);
   if (hipHostMalloc((void **)&c->hpin, 16 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
     c->hpin = nullptr;
     ::hrf::set_error("seg_ctx: pinned host allocation failed");

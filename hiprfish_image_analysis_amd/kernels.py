@@ -466,19 +466,25 @@ def max_i32(a, sync=True):
 
 
 # ---- a12 ------------------------------------------------------------------------------------
-def watershed(image, markers, mask=None, negate=False, max_passes=100000):
-    """skimage.morphology.watershed(+/-image, markers, mask=mask), 4-connectivity"""
+def watershed(image, markers, mask=None, negate=False, max_passes=100000, ties: list | None = None):
+    """skimage.morphology.watershed(+/-image, markers, mask=mask), 4-connectivity, with the
+    heap's (value, age) order on ties.  `ties` (a list) receives [pixels that needed the exact
+    order, resolution rounds, equal-valued-marker decisions] (hrf_watershed_ex)."""
     import ctypes
     image = _dev(image, torch.float64, "image")
     mk = _i32(markers, "markers")
     H, W = image.shape
     m = _u8(mask, "mask") if mask is not None else None
     out = torch.empty((H, W), dtype=torch.int32, device=image.device)
-    ws = torch.empty(32 * H * W, dtype=torch.uint8, device=image.device)
+    nb = _lib.lib().hrf_watershed_workspace_bytes(H, W)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=image.device)
     fl = torch.empty(8, dtype=torch.int32, device=image.device)
     passes = ctypes.c_int32(0)
-    _lib.call("hrf_watershed", _ptr(image), int(negate), _ptr(mk), _ptr(m), H, W, _ptr(out), _ptr(ws), _ptr(fl),
-              max_passes, ctypes.addressof(passes), _stream())
+    st = (ctypes.c_int32 * 3)()
+    _lib.call("hrf_watershed_ex", _ptr(image), int(negate), _ptr(mk), _ptr(m), H, W, _ptr(out), _ptr(ws), _ptr(fl),
+              max_passes, ctypes.addressof(passes), ctypes.addressof(st), _stream())
+    if ties is not None:
+        ties[:] = list(st)
     return out
 
 

@@ -233,10 +233,20 @@ HRF_API hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hr
 
 /* ==== a12: watershed (watershed.hip) =====================================================
  * skimage.morphology.watershed(+/-image, markers, mask) (ecoli :113, multispecies :154),
- * 4-connectivity.  state_ws: 32*H*W bytes; flag_ws: >= 4 int32.  Synchronises after 8 passes, then per 4. */
+ * 4-connectivity, including the heap's (value, age) order on equal values.  state_ws:
+ * hrf_watershed_workspace_bytes(H, W) device bytes; flag_ws: >= 8 int32.  Synchronises after
+ * 8 relaxation passes, then per 4; HRF_EINVAL if not converged within max_passes.
+ * ties_host (nullable, 3 int32): pixels whose label needed the exact order, resolution
+ * rounds, and decisions between equal-valued markers (skimage: binary-heap layout; here
+ * raster order) -- see DESIGN.md "Watershed". */
+HRF_API int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W);
 HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
                                  int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
                                  int32_t max_passes, int32_t *passes_host, hrf_stream_t stream);
+HRF_API hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
+                                    int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
+                                    int32_t max_passes, int32_t *passes_host, int32_t *ties_host,
+                                    hrf_stream_t stream);
 
 /* ==== native segmentation drivers (segment.hip) ==========================================
  * One call runs a whole segmentation chain -- the same library calls, in the same order, as

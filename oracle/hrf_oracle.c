@@ -985,10 +985,36 @@ EXPORT void oracle_nl_means_skimage(const double *img, int64_t H, int64_t W, int
     free(I);
 }
 
-/* The same weights per pixel, in the summation order of libhrf's nl_means_kernel:
+/* The same weights per pixel, in the summation order AND arithmetic of libhrf's
+ * nl_means_kernel, so the two are bit-identical (tests/test_nlmeans_gpu.py) and the whole
+ * community chain can be compared without handing the GPU image to the oracle:
  * out[p] = (2 P[p] + sum_s w_s P[p+s]) / (2 + sum_s w_s) over the full (2d+1)^2 window
  * (s != 0) in raster order of s; patch distance = sum over 7 rows (top to bottom) of the
- * row's 7 squared differences (left to right); w = exp(-max(D,0)/h2s2) if <= 5 else 0. */
+ * row's 7 squared differences (left to right); skimage's cut max(D,0)/h2s2 <= 5 as the
+ * exact threshold D <= lim on D; w = e^{-max(D,0) * (1/h2s2)} by Cody-Waite reduction and
+ * the degree-13 Taylor polynomial (exp_neg_small below, the kernel's).  Agrees with the
+ * integral-image restatement above within 1e-12. */
+static double exp_neg_small(double x) {
+    const double k = rint(x * 1.4426950408889634);
+    double r = fma(-k, 6.93147180369123816490e-01, x);
+    r = fma(-k, 1.90821492927058770002e-10, r);
+    double p = 1.0 / 6227020800.0;
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
 EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, int dist, double h, double sigma,
                             double *out) {
     const int s = patch % 2 == 0 ? patch + 1 : patch;
@@ -996,6 +1022,14 @@ EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, 
     const int64_t pw = off + dist, wp = W + 2 * pw;
     double *P = reflect_pad(img, H, W, pw);
     const double h2 = h * h, s2 = (double)s * (double)s, h2s2 = 1.0 * h2 * s2, var = sigma * sigma;
+    /* the largest D whose quotient fl(D / h2s2) is still <= 5 */
+    double lim = 5.0 * h2s2;
+    while (lim / h2s2 > 5.0) lim = nextafter(lim, -1.0);
+    while (nextafter(lim, 2.0 * lim + 1.0) / h2s2 <= 5.0) lim = nextafter(lim, 2.0 * lim + 1.0);
+    const double inv = 1.0 / h2s2;
+    /* rows are independent (each pixel's sums run in a fixed order): OpenMP only shortens
+     * the wall time of full-size parity tests, the result does not depend on it */
+#pragma omp parallel for schedule(dynamic, 4)
     for (int64_t r = 0; r < H; ++r)
         for (int64_t c = 0; c < W; ++c) {
             const double *p = P + (r + pw) * wp + (c + pw);
@@ -1009,14 +1043,13 @@ EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, 
                         double hs = 0.0;
                         for (int dv = -off; dv <= off; ++dv) {
                             const double t = p[du * wp + dv] - q[du * wp + dv];
-                            const double sq = t * t - var;
+                            const double sq = var == 0.0 ? t * t : t * t - var;
                             hs = dv == -off ? sq : hs + sq;
                         }
                         D = du == -off ? hs : D + hs;
                     }
-                    const double d = (D > 0.0 ? D : 0.0) / h2s2;
-                    if (d <= 5.0) {
-                        const double w = exp(-d);
+                    if (D <= lim) {
+                        const double w = exp_neg_small(-(D > 0.0 ? D : 0.0) * inv);
                         ws += w;
                         acc += w * q[0];
                     }

@@ -19,8 +19,8 @@ _lib = None
 
 
 def build() -> str:
-    src = os.path.join(_HERE, "hrf_oracle.c")
-    if not os.path.exists(_LIB) or os.path.getmtime(src) > os.path.getmtime(_LIB):
+    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c")]
+    if not os.path.exists(_LIB) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(_LIB):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _LIB
 
@@ -247,6 +247,22 @@ def watershed(img, markers, mask=None):
         mp = _p(m)
     lib().oracle_watershed(_p(im), _p(mk), mp, I64(im.shape[0]), I64(im.shape[1]), _p(out))
     return out
+
+
+def watershed_ordered(img, markers, mask=None):
+    """ws_order.c: the tie-exact formulation libhrf's watershed implements (NOT a reference
+    restatement; checked against watershed() above).  -> (labels, stats) with stats =
+    [contested pixels, walk steps, heap-layout decisions, label rounds]"""
+    im = _c(img, np.float64)
+    mk = _c(markers, np.int32)
+    out = np.zeros(mk.shape, np.int32)
+    st = np.zeros(4, np.int64)
+    mp = None
+    if mask is not None:
+        m = _c(mask, np.uint8)
+        mp = _p(m)
+    lib().oracle_watershed_ordered(_p(im), _p(mk), mp, I64(im.shape[0]), I64(im.shape[1]), _p(out), _p(st))
+    return out, st
 
 
 # ---- a14/a15/a20 ---------------------------------------------------------------------

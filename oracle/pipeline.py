@@ -144,13 +144,14 @@ def _brighter_cluster(img, lab, cen):
 
 def segment_multispecies(stack, calibration=None, keep=None, nl=None):
     """multispecies :102-157 on the registered stack -> (segmentation, n, image_sum, final_bkg).
-    `nl` injects the NL-means image (a float step compared separately within tolerance) so the
-    discrete steps after it can be compared exactly."""
+    `nl` (optional) injects an NL-means image, e.g. the integral-image restatement's."""
     st = _calibrated(stack, calibration)                                          # :103-104
     s = np.sum(st, axis=2)                                                        # :105
     norm = s / np.max(s)                                                          # :106
     if nl is None:
-        nl = O.nl_means_skimage(norm, 7, 11, 0.02, 0.0)                           # :108
+        # skimage's fast 2-D NL-means in libhrf's arithmetic (bit-identical to the GPU; within
+        # 1e-12 of the integral-image restatement O.nl_means_skimage, tests/test_oracle_golden.py)
+        nl = O.nl_means(norm, 7, 11, 0.02, 0.0)                                   # :108
     final = O.enhance_2d(np.pad(nl, 5, mode='edge'))                              # :109-124
     l2, c2, _ = O.kmeans_1d(final, 2)                                             # :125
     rough = _brighter_cluster(final, l2, c2)                                      # :126-135

@@ -73,8 +73,8 @@ def test_multispecies_measure_and_classify_cli(tmp_path, orc):
     m2 = P.measure_multispecies(dreg, dcal, keep=keep)
     seg = np.load(sample + "_seg.npy")
     assert np.array_equal(seg, m2.segmentation.cpu().numpy())
-    # ... and the oracle restatement once the NL-means image is shared
-    oseg, olabs, oavg, oavgn = OP.measure_multispecies(reg, cal, nl=keep["nl"].cpu().numpy())
+    # ... and the oracle restatement of the whole chain
+    oseg, olabs, oavg, oavgn = OP.measure_multispecies(reg, cal)
     assert np.array_equal(seg, oseg) and len(olabs) >= 1
     csv = pd.read_csv(sample + "_avgint_norm.csv")
     assert list(csv.columns) == [str(i) for i in range(C)]

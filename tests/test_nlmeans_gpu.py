@@ -1,7 +1,7 @@
 """a4 non-local means (skimage.restoration.denoise_nl_means, multispecies measurement.py:108)
-on the device against the oracle restatement in the kernel's summation order (patch
-distances bit-identical; exp() may differ in the last ulp -> rtol 1e-13), and against the
-integral-image algorithm itself (rtol 1e-9).  skimage is not installed here: parity against
+on the device against the oracle restatement in the kernel's summation order and arithmetic
+(same exp polynomial: bit-identical), and against the integral-image algorithm itself (rtol
+1e-9).  skimage is not installed here: parity against
 skimage proper is unpinned."""
 import numpy as np
 import pytest
@@ -31,7 +31,7 @@ def test_nl_means_vs_oracle(K, orc, shape):
     img = smooth(shape, sum(shape))
     got = K.nl_means_2d(dev(img), h=0.02).cpu().numpy()
     ref = orc.nl_means(img, 7, 11, 0.02)
-    np.testing.assert_allclose(got, ref, rtol=1e-13, atol=0)
+    assert np.array_equal(got, ref)
 
 
 def test_nl_means_random_and_sigma(K, orc):
@@ -39,7 +39,7 @@ def test_nl_means_random_and_sigma(K, orc):
     img = rng.random((45, 77))
     for h, sigma in [(0.1, 0.0), (0.3, 0.05)]:
         got = K.nl_means_2d(dev(img), h=h, sigma=sigma).cpu().numpy()
-        np.testing.assert_allclose(got, orc.nl_means(img, 7, 11, h, sigma), rtol=1e-13, atol=0)
+        assert np.array_equal(got, orc.nl_means(img, 7, 11, h, sigma))
 
 
 def test_nl_means_vs_integral_image_algorithm(K, orc):
@@ -56,7 +56,7 @@ def test_nl_means_tile_sized(K, orc):
     s = (s / s.max()).cpu().numpy()
     got = K.nl_means_2d(dev(s), h=0.02).cpu().numpy()
     sub = orc.nl_means(s[200:260], 7, 11, 0.02)          # rows 200..259 with their own reflect
-    np.testing.assert_allclose(got[214:246], sub[14:46], rtol=1e-13, atol=0)
+    assert np.array_equal(got[214:246], sub[14:46])
 
 
 def test_nl_means_bad_parameters(K):

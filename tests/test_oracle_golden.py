@@ -143,3 +143,30 @@ def test_kmeans_partition_matches_sklearn(orc, golden, name):
     lab, cen, it = orc.kmeans_1d(x, k)
     assert it < 300
     assert _same_partition(lab, g["lab_" + name])
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_watershed_order_model_equals_heap(orc, block):
+    """a12: the order theorem libhrf's watershed implements (oracle/ws_order.c: keys (lambda, h),
+    candidate strings) gives the heap flood's label map (oracle_watershed, skimage's (value, age)
+    binary heap) on plateau-heavy integer images, whenever no decision comes down to
+    equal-valued markers of different labels (then skimage's choice is its heap's layout)."""
+    decided_by_layout = 0
+    for seed in range(block * 150, (block + 1) * 150):
+        rng = np.random.default_rng(seed)
+        H, W = 10 + seed % 37, 10 + (seed * 7) % 41
+        f = rng.integers(0, 2 + seed % 5, (H, W)).astype(np.float64)
+        mask = rng.random((H, W)) < 0.85 if seed % 4 else None
+        markers = np.zeros((H, W), np.int32)
+        idx = rng.choice(H * W, max(2, H * W // 60), replace=False)
+        markers.flat[idx] = rng.integers(1, 6, idx.size)
+        if seed % 2:
+            f = f + 1e-3 * markers       # no equal-valued markers of different labels
+        ref = orc.watershed(f, markers, mask)
+        got, st = orc.watershed_ordered(f, markers, mask)
+        if st[2] == 0:
+            assert np.array_equal(got, ref), seed
+        else:
+            assert seed % 2 == 0
+            decided_by_layout += 1
+    assert decided_by_layout < 150

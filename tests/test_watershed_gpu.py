@@ -1,0 +1,100 @@
+"""a12 watershed on inputs with exact ties: the device label map against the heap flood
+restated from skimage (oracle_watershed: (value, age) order, labels on push), on plateau-heavy
+integer images and on bioformats-like quantised E. coli / community tiles.
+
+skimage's binary heap orders equal-valued markers (all age 0) by its internal layout; when a
+decision comes down to that, libhrf takes the marker with the smaller raster index and reports
+the decision (ties[2]).  Tests whose markers cannot produce such a decision (distinct values
+per label) require ties[2] == 0 and the heap's map; tests with arbitrary markers require the
+heap's map whenever ties[2] == 0 and otherwise the ws_order.c model of the same rule."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from hiprfish_image_analysis_amd import kernels
+    return kernels
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def plateau_case(seed, H, W, nv, distinct, blob_markers):
+    rng = np.random.default_rng(seed)
+    f = rng.integers(0, nv, (H, W)).astype(np.float64)
+    if seed % 3 == 0:   # smoother plateaus: coarse blocks
+        f = np.kron(rng.integers(0, nv, (H // 4 + 1, W // 4 + 1)), np.ones((4, 4)))[:H, :W].astype(np.float64)
+    mask = rng.random((H, W)) < 0.9
+    markers = np.zeros((H, W), np.int32)
+    nl = max(2, H * W // 300)
+    if blob_markers:   # multi-pixel seeds, as label() of eroded regions gives
+        for l in range(1, nl + 1):
+            r, c = rng.integers(0, H), rng.integers(0, W)
+            markers[max(0, r - 1):r + 2, max(0, c - 1):c + 2] = l
+    else:
+        idx = rng.choice(H * W, nl, replace=False)
+        markers.flat[idx] = rng.integers(1, max(2, nl // 2), nl)
+    if distinct:   # per-label offset: equal-valued markers of different labels cannot occur
+        f = f + 1e-3 * markers
+    return f, markers, mask
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_watershed_plateaus_equal_heap(K, orc, seed):
+    H, W = [(37, 41), (64, 64), (130, 97), (200, 180)][seed % 4]
+    f, markers, mask = plateau_case(seed, H, W, 2 + seed % 4, True, seed % 2 == 0)
+    ref = orc.watershed(f, markers, mask)
+    ties = []
+    got = host(K.watershed(dev(f), dev(markers), dev(mask), ties=ties))
+    assert ties[2] == 0
+    assert np.array_equal(got, ref)
+    got_neg = host(K.watershed(dev(-f), dev(markers), dev(mask), negate=True))
+    assert np.array_equal(got_neg, ref)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_watershed_plateaus_any_markers(K, orc, seed):
+    H, W = [(50, 60), (128, 128), (97, 211)][seed % 3]
+    f, markers, mask = plateau_case(100 + seed, H, W, 2 + seed % 3, False, seed % 2 == 1)
+    ties = []
+    got = host(K.watershed(dev(f), dev(markers), dev(mask) if seed % 4 else None, ties=ties))
+    model, st = orc.watershed_ordered(f, markers, mask if seed % 4 else None)
+    assert np.array_equal(got, model)
+    if ties[2] == 0:
+        assert np.array_equal(got, orc.watershed(f, markers, mask if seed % 4 else None))
+
+
+def test_watershed_constant_image(K, orc):
+    """one plateau over the whole image: every meeting line is decided by FIFO order"""
+    H, W = 160, 150
+    f = np.zeros((H, W))
+    markers = np.zeros((H, W), np.int32)
+    rng = np.random.default_rng(5)
+    for l in range(1, 9):
+        r, c = rng.integers(0, H - 3), rng.integers(0, W - 3)
+        markers[r:r + 3, c:c + 3] = l
+    f = f + 1e-3 * markers            # distinct marker values per label
+    ties = []
+    got = host(K.watershed(dev(f), dev(markers), None, ties=ties))
+    assert ties[0] > 0 and ties[2] == 0
+    assert np.array_equal(got, orc.watershed(f, markers, None))
+
+
+def test_watershed_continuous_has_no_contest(K, orc):
+    rng = np.random.default_rng(3)
+    f = rng.random((300, 280))
+    markers = np.zeros(f.shape, np.int32)
+    markers.flat[rng.choice(f.size, 200, replace=False)] = np.arange(1, 201)
+    ties = []
+    got = host(K.watershed(dev(f), dev(markers), None, ties=ties))
+    assert ties == [0, 0, 0]
+    assert np.array_equal(got, orc.watershed(f, markers, None))
