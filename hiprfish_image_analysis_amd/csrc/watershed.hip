@@ -30,40 +30,51 @@
 // One departure from skimage remains, reported in ties_host[2]: when two competing strings
 // are equal down to markers of the same value, skimage's choice depends on where its binary
 // heap happens to hold the two age-0 items; here the marker with the smaller raster index wins.
+#include <cstdlib>
+
 #include "common.hpp"
+#include "ws_core.hpp"
 
 namespace {
 
+using namespace hrf_ws;
 constexpr int WT = 32, WL = WT + 2;
-constexpr int32_t HOP_INF = 0x7fffffff;
 
 struct WsState {
   double *lam;
   int32_t *hop;
   int32_t *lab;
+  int32_t *dst;  // basin distance (relaxation tie-break only, see ws_pass_kernel)
 };
 
 __global__ void ws_init_kernel(const double *__restrict__ f, int negate, const int32_t *__restrict__ markers,
                                const uint8_t *__restrict__ mask, int64_t n, double *__restrict__ lam,
-                               int32_t *__restrict__ hop, int32_t *__restrict__ lab, int32_t *__restrict__ ptr) {
+                               int32_t *__restrict__ hop, int32_t *__restrict__ lab, int32_t *__restrict__ dst,
+                               int32_t *__restrict__ ptr) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const bool in = !mask || mask[i];
     const int32_t m = in ? markers[i] : 0;
     lam[i] = m ? (negate ? -f[i] : f[i]) : __builtin_inf();
     hop[i] = m ? 0 : HOP_INF;
+    dst[i] = m ? 0 : HOP_INF;
     lab[i] = m;
     ptr[i] = -1;
   }
 }
 
-__device__ __forceinline__ bool better(double l1, int32_t h1, int32_t b1, double l2, int32_t h2, int32_t b2) {
+__device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_t b1, double l2, int32_t h2,
+                                       int32_t d2, int32_t b2) {
   if (l1 != l2) return l1 < l2;
   if (h1 != h2) return h1 < h2;
+  if (d1 != d2) return d1 < d2;
   return b1 < b2;
 }
 
-// One global pass.  RELABEL = false: relax (lambda, h, label) from the least-key labelled
-// neighbour (ties -> smaller label).  RELABEL = true: keys are final; a pixel with a resolved
+// One global pass.  RELABEL = false: relax (lambda, h, d, label) from the least labelled
+// neighbour (ties -> smaller label).  d, the distance into a basin from its slot, is not part
+// of the order the heap uses; it only makes the pointer relation strictly increasing inside a
+// basin (equal (lambda, h) there), without which simultaneous (Jacobi) updates of two basin
+// neighbours can swap stale labels forever.  RELABEL = true: keys are final; a pixel with a resolved
 // parent copies its label, any other takes the least non-zero label of its candidates (0 =
 // not yet reached, so labels flow out of the markers again after a reset).
 template <bool RELABEL>
@@ -78,6 +89,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   __shared__ double sl[WL * WL];
   __shared__ double sf[WL * WL];
   __shared__ int32_t sh[WL * WL];
+  __shared__ int32_t sd[WL * WL];
   __shared__ int32_t sb[WL * WL];
   __shared__ uint8_t sm[WL * WL];
   const int tid = threadIdx.x;
@@ -105,12 +117,14 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       const bool inm = !mask || mask[g];
       sl[idx] = in.lam[g];
       sh[idx] = in.hop[g];
+      sd[idx] = RELABEL ? 0 : in.dst[g];
       sb[idx] = in.lab[g];
       sf[idx] = negate ? -f[g] : f[g];
       sm[idx] = (uint8_t)((inm ? 1 : 0) | ((inm && markers[g]) ? 2 : 0));
     } else {
       sl[idx] = __builtin_inf();
       sh[idx] = HOP_INF;
+      sd[idx] = HOP_INF;
       sb[idx] = 0;
       sf[idx] = 0.0;
       sm[idx] = 0;
@@ -132,28 +146,30 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   bool any_change = false;
   for (int it = 0; it < 4 * WT * WT; ++it) {
     double nl[4];
-    int32_t nh[4], nb[4];
+    int32_t nh[4], nd[4], nb[4];
     bool ch = false;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = own[k];
       nl[k] = sl[i];
       nh[k] = sh[i];
+      nd[k] = sd[i];
       nb[k] = sb[i];
       if ((sm[i] & 3) != 1) continue;  // outside mask or a marker
       const int nbr[4] = {i - WL, i - 1, i + 1, i + WL};
       if (!RELABEL) {
         // first-popped neighbour = least (lambda, h) among labelled in-mask neighbours
         double bl = __builtin_inf();
-        int32_t bh = HOP_INF, bb = 0;
+        int32_t bh = HOP_INF, bd = HOP_INF, bb = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
           const int j = nbr[d];
           const int32_t bj = sb[j];
           if (!bj || !(sm[j] & 1)) continue;
-          if (better(sl[j], sh[j], bj, bl, bh, bb)) {
+          if (better(sl[j], sh[j], sd[j], bj, bl, bh, bd, bb)) {
             bl = sl[j];
             bh = sh[j];
+            bd = sd[j];
             bb = bj;
           }
         }
@@ -162,16 +178,19 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
           if (bl < fv) {  // entry of level fv
             nl[k] = fv;
             nh[k] = 0;
+            nd[k] = 0;
           } else if (bl == fv) {  // plateau pixel: next FIFO layer
             nl[k] = bl;
             nh[k] = bh + 1;
+            nd[k] = 0;
           } else {  // basin pixel: filled in the slot that reached it
             nl[k] = bl;
             nh[k] = bh;
+            nd[k] = bd + 1;
           }
           nb[k] = bb;
         }
-        ch |= (nb[k] != sb[i]) || (nl[k] != sl[i]) || (nh[k] != sh[i]);
+        ch |= (nb[k] != sb[i]) || (nl[k] != sl[i]) || (nh[k] != sh[i]) || (nd[k] != sd[i]);
       } else {
         int32_t lb = 0;
         if (par[k] >= 0) {
@@ -204,6 +223,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       if (!RELABEL) {
         sl[own[k]] = nl[k];
         sh[own[k]] = nh[k];
+        sd[own[k]] = nd[k];
       }
       sb[own[k]] = nb[k];
     }
@@ -220,6 +240,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       if (!RELABEL) {
         out.lam[g] = sl[i];
         out.hop[g] = sh[i];
+        out.dst[g] = sd[i];
       }
       out.lab[g] = sb[i];
     }
@@ -227,221 +248,6 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   if (__syncthreads_or(any_change) && tid == 0) {
     *changed = 1;
     cur_tile[blockIdx.y * gridDim.x + blockIdx.x] = 1;
-  }
-}
-
-// ---- exact resolution -----------------------------------------------------------------------
-struct WsGeom {
-  const double *f;
-  int negate;
-  const int32_t *mk;
-  const uint8_t *mask;
-  int64_t H, W;
-  const double *lam;
-  const int32_t *hop;
-};
-
-__device__ __forceinline__ bool g_in(const WsGeom &g, int64_t i) { return !g.mask || g.mask[i]; }
-__device__ __forceinline__ bool g_marker(const WsGeom &g, int64_t i) { return g_in(g, i) && g.mk[i] != 0; }
-__device__ __forceinline__ double g_f(const WsGeom &g, int64_t i) { return g.negate ? -g.f[i] : g.f[i]; }
-__device__ __forceinline__ bool g_basin(const WsGeom &g, int64_t i) { return !g_marker(g, i) && g_f(g, i) < g.lam[i]; }
-__device__ __forceinline__ bool kless(double l1, int32_t h1, double l2, int32_t h2) {
-  return l1 < l2 || (l1 == l2 && h1 < h2);
-}
-
-// candidates of x: in-mask reached neighbours with the least key
-__device__ int g_cands(const WsGeom &g, int64_t x, int32_t *out) {
-  const int64_t r = x / g.W, c = x - r * g.W;
-  int64_t nb[4];
-  int k = 0;
-  if (r > 0) nb[k++] = x - g.W;
-  if (c > 0) nb[k++] = x - 1;
-  if (c + 1 < g.W) nb[k++] = x + 1;
-  if (r + 1 < g.H) nb[k++] = x + g.W;
-  double bl = __builtin_inf();
-  int32_t bh = HOP_INF;
-  int m = 0;
-  for (int j = 0; j < k; ++j) {
-    const int64_t y = nb[j];
-    if (!g_in(g, y)) continue;
-    const double ly = g.lam[y];
-    if (ly == __builtin_inf()) continue;
-    const int32_t hy = g.hop[y];
-    if (kless(ly, hy, bl, bh)) {
-      bl = ly;
-      bh = hy;
-      m = 0;
-    }
-    if (ly == bl && hy == bh) out[m++] = (int32_t)y;
-  }
-  return m;
-}
-
-// Per-thread scratch: two member buffers (pixel, group), the basin slot list, a generation
-// hash set of (pixel, group) and per-group state.  Sized by the host; overflow -> retry larger.
-struct Walker {
-  int32_t *pa, *ga, *pb, *gb, *slots;
-  uint64_t *hkey;
-  uint32_t *hgen;
-  double *ml;
-  int32_t *mh, *mr;
-  uint8_t *alive;
-  int32_t cap, hcap, gcap;
-  uint32_t gen;
-  int32_t hcount;
-
-  __device__ void new_gen() {
-    ++gen;
-    hcount = 0;
-  }
-  // true if (p, grp) was not yet in this generation's set (then inserted); false if present
-  // or the table is full (*ovf set)
-  __device__ bool insert(int32_t p, int32_t grp, bool *ovf) {
-    const uint64_t key = ((uint64_t)(uint32_t)p << 32) | (uint32_t)grp;
-    if (2 * (hcount + 1) > hcap) {
-      *ovf = true;
-      return false;
-    }
-    uint64_t h = key * 0x9E3779B97F4A7C15ull;
-    uint32_t s = (uint32_t)(h >> 33) & (uint32_t)(hcap - 1);
-    for (;;) {
-      if (hgen[s] != gen) {
-        hgen[s] = gen;
-        hkey[s] = key;
-        ++hcount;
-        return true;
-      }
-      if (hkey[s] == key) return false;
-      s = (s + 1) & (uint32_t)(hcap - 1);
-    }
-  }
-};
-
-// index into cand[] of the candidate whose string is least (the one the heap pops first);
-// -1 on scratch overflow.  *layout += 1 when equal strings down to markers of different labels
-// are decided by raster index.
-__device__ int ws_walk(const WsGeom &g, const int32_t *cand, int k, Walker &w, int32_t *layout) {
-  if (k <= 0 || k > w.gcap || k > w.cap) return -1;
-  if (k == 1) return 0;
-  bool ovf = false;
-  int32_t *cp = w.pa, *cg = w.ga, *op = w.pb, *og = w.gb;
-  int32_t ncur = 0;
-  for (int j = 0; j < k; ++j) {
-    cp[ncur] = cand[j];
-    cg[ncur] = j;
-    ++ncur;
-    w.alive[j] = 1;
-  }
-  for (;;) {
-    // 1. basin members -> the non-basin pixels of equal key reachable through the basin
-    w.new_gen();
-    int32_t nout = 0;
-    for (int32_t i = 0; i < ncur; ++i) {
-      const int32_t x = cp[i], gr = cg[i];
-      if (!w.insert(x, gr, &ovf)) {
-        if (ovf) return -1;
-        continue;
-      }
-      if (g_basin(g, x)) {
-        int32_t cc[4];
-        const int m = g_cands(g, x, cc);
-        for (int t = 0; t < m; ++t) {
-          if (ncur >= w.cap) return -1;
-          cp[ncur] = cc[t];
-          cg[ncur] = gr;
-          ++ncur;
-        }
-      } else {
-        if (nout >= w.cap) return -1;
-        op[nout] = x;
-        og[nout] = gr;
-        ++nout;
-      }
-    }
-    if (nout == 0) return -1;  // cannot happen (every string ends at a marker)
-    // 2. least key per group; groups above the overall least drop out
-    for (int j = 0; j < k; ++j) {
-      w.ml[j] = __builtin_inf();
-      w.mh[j] = HOP_INF;
-      w.mr[j] = -1;
-    }
-    double bl = __builtin_inf();
-    int32_t bh = HOP_INF;
-    for (int32_t i = 0; i < nout; ++i) {
-      const int32_t x = op[i], gr = og[i];
-      const double lx = g.lam[x];
-      const int32_t hx = g.hop[x];
-      if (kless(lx, hx, w.ml[gr], w.mh[gr])) {
-        w.ml[gr] = lx;
-        w.mh[gr] = hx;
-      }
-      if (kless(lx, hx, bl, bh)) {
-        bl = lx;
-        bh = hx;
-      }
-    }
-    int nal = 0, last = -1;
-    for (int j = 0; j < k; ++j) {
-      if (!w.alive[j]) continue;
-      if (w.ml[j] != bl || w.mh[j] != bh) {
-        w.alive[j] = 0;
-        continue;
-      }
-      ++nal;
-      last = j;
-    }
-    if (nal == 1) return last;
-    // 3. members at the least key; markers among them end their string (BOTTOM . rank)
-    int32_t nkeep = 0;
-    bool anym = false;
-    for (int32_t i = 0; i < nout; ++i) {
-      const int32_t x = op[i], gr = og[i];
-      if (!w.alive[gr] || g.lam[x] != bl || g.hop[x] != bh) continue;
-      cp[nkeep] = x;
-      cg[nkeep] = gr;
-      ++nkeep;
-      if (g_marker(g, x)) {
-        anym = true;
-        if (w.mr[gr] < 0 || x < w.mr[gr]) w.mr[gr] = x;
-      }
-    }
-    if (anym) {
-      int win = -1, nm = 0;
-      int32_t l0 = 0;
-      bool multi = false;
-      for (int j = 0; j < k; ++j) {
-        if (!w.alive[j] || w.mr[j] < 0) continue;
-        ++nm;
-        if (nm == 1) l0 = g.mk[w.mr[j]];
-        else if (g.mk[w.mr[j]] != l0) multi = true;
-        if (win < 0 || w.mr[j] < w.mr[win]) win = j;
-      }
-      if (nm > 1 && multi) atomicAdd(layout, 1);
-      return win;
-    }
-    // 4. one symbol further: the union of the kept members' candidates, per group
-    w.new_gen();
-    int32_t nn = 0;
-    for (int32_t i = 0; i < nkeep; ++i) {
-      int32_t cc[4];
-      const int m = g_cands(g, cp[i], cc);
-      for (int t = 0; t < m; ++t) {
-        if (!w.insert(cc[t], cg[i], &ovf)) {
-          if (ovf) return -1;
-          continue;
-        }
-        if (nn >= w.cap) return -1;
-        op[nn] = cc[t];
-        og[nn] = cg[i];
-        ++nn;
-      }
-    }
-    int32_t *t0 = cp, *t1 = cg;
-    cp = op;
-    cg = og;
-    op = t0;
-    og = t1;
-    ncur = nn;
   }
 }
 
@@ -462,11 +268,11 @@ __global__ void ws_contest_kernel(WsGeom g, const int32_t *__restrict__ lab, con
 // candidate as parent; a basin pixel decides its whole basin component (every pixel of the
 // component points at the winning slot, so the component stays one label, no cycles).
 __global__ void ws_resolve_kernel(WsGeom g, const int32_t *__restrict__ list, int32_t count, int32_t *__restrict__ ptr,
-                                  char *__restrict__ scratch, int64_t stride, int32_t cap, int32_t hcap, int32_t gcap,
-                                  int32_t *__restrict__ retry, int32_t *__restrict__ nretry,
+                                  char *__restrict__ scratch, int64_t stride, int64_t nt, int32_t cap, int32_t hcap,
+                                  int32_t gcap, int32_t *__restrict__ retry, int32_t *__restrict__ nretry,
                                   int32_t *__restrict__ layout) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nt = (int64_t)gridDim.x * blockDim.x;
+  if (t >= nt) return;  // scratch exists for nt threads only
   char *base = scratch + t * stride;
   Walker w;
   w.pa = (int32_t *)base;
@@ -486,64 +292,14 @@ __global__ void ws_resolve_kernel(WsGeom g, const int32_t *__restrict__ list, in
   w.gen = 0;
   w.hcount = 0;
   for (int32_t i = 0; i < hcap; ++i) w.hgen[i] = 0;
+  int32_t lay = 0;
   for (int64_t li = t; li < count; li += nt) {
     const int32_t x = list[li];
     if (ptr[x] >= 0) continue;  // decided with its basin component by another thread
-    bool fail = false;
-    if (!g_basin(g, x)) {
-      int32_t cc[4];
-      const int m = g_cands(g, x, cc);
-      const int win = ws_walk(g, cc, m, w, layout);
-      if (win < 0) fail = true;
-      else ptr[x] = cc[win];
-    } else {
-      // component of equal-key basin pixels and its slots (equal-key non-basin neighbours)
-      bool ovf = false;
-      w.new_gen();
-      int32_t nq = 0, ns = 0;
-      w.insert(x, 0, &ovf);
-      w.pa[nq++] = x;
-      for (int32_t qi = 0; qi < nq && !fail; ++qi) {
-        int32_t cc[4];
-        const int m = g_cands(g, w.pa[qi], cc);
-        for (int j = 0; j < m; ++j) {
-          if (!w.insert(cc[j], 0, &ovf)) {
-            if (ovf) fail = true;
-            continue;
-          }
-          if (g_basin(g, cc[j])) {
-            if (nq >= cap) fail = true;
-            else w.pa[nq++] = cc[j];
-          } else {
-            if (ns >= cap) fail = true;
-            else w.slots[ns++] = cc[j];
-          }
-        }
-      }
-      int win = -1;
-      if (!fail) {
-        // ws_walk reuses pa/ga: move the component out of the way by re-deriving it afterwards
-        win = ws_walk(g, w.slots, ns, w, layout);
-        if (win < 0) fail = true;
-      }
-      if (!fail) {
-        const int32_t wp = w.slots[win];
-        w.new_gen();
-        nq = 0;
-        w.insert(x, 0, &ovf);
-        w.pa[nq++] = x;
-        for (int32_t qi = 0; qi < nq; ++qi) {
-          const int32_t b = w.pa[qi];
-          ptr[b] = wp;
-          int32_t cc[4];
-          const int m = g_cands(g, b, cc);
-          for (int j = 0; j < m; ++j)
-            if (g_basin(g, cc[j]) && w.insert(cc[j], 0, &ovf)) w.pa[nq++] = cc[j];
-        }
-      }
-    }
+    const bool fail = !ws_resolve_one(g, x, ptr, w, &lay);
     if (fail) retry[atomicAdd(nretry, 1)] = x;
   }
+  if (lay) atomicAdd(layout, lay);
 }
 
 // labels of every non-marker pixel back to 0 (both ping-pong buffers): relabel from markers
@@ -569,12 +325,12 @@ struct WsBuffers {
 WsBuffers carve(void *state_ws, int64_t n, int64_t ntiles) {
   char *ws = (char *)state_ws;
   WsBuffers B;
-  B.a = WsState{(double *)ws, (int32_t *)(ws + 8 * n), (int32_t *)(ws + 12 * n)};
-  B.b = WsState{(double *)(ws + 16 * n), (int32_t *)(ws + 24 * n), (int32_t *)(ws + 28 * n)};
-  B.ptr = (int32_t *)(ws + 32 * n);
-  B.list = (int32_t *)(ws + 36 * n);
-  B.retry = (int32_t *)(ws + 40 * n);
-  B.tf = (int32_t *)(ws + 44 * n);
+  B.a = WsState{(double *)ws, (int32_t *)(ws + 8 * n), (int32_t *)(ws + 12 * n), (int32_t *)(ws + 16 * n)};
+  B.b = WsState{(double *)(ws + 24 * n), (int32_t *)(ws + 32 * n), (int32_t *)(ws + 36 * n), (int32_t *)(ws + 40 * n)};
+  B.ptr = (int32_t *)(ws + 44 * n);
+  B.list = (int32_t *)(ws + 48 * n);
+  B.retry = (int32_t *)(ws + 52 * n);
+  B.tf = (int32_t *)(ws + 56 * n);
   (void)ntiles;
   return B;
 }
@@ -586,7 +342,7 @@ extern "C" {
 int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W) {
   if (H < 0 || W < 0) return -1;
   const int64_t ntiles = hrf::cdiv(W, WT) * hrf::cdiv(H, WT);
-  return 44 * H * W + 12 * ntiles + 256;
+  return 56 * H * W + 12 * ntiles + 256;
 }
 
 // flag_ws (>= 8 int32): [0] change flag of a batch's last pass, [1] the other passes',
@@ -606,12 +362,14 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   const int64_t ntiles = (int64_t)grid.x * grid.y;
   WsBuffers B = carve(state_ws, n, ntiles);
   WsState a = B.a, b = B.b;
-  ws_init_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(image, negate, markers, mask, n, a.lam, a.hop, a.lab, B.ptr);
+  ws_init_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(image, negate, markers, mask, n, a.lam, a.hop, a.lab, a.dst,
+                                                      B.ptr);
   HRF_LAUNCHED();
   int32_t *tf = B.tf;  // per-tile change flags, three rotating generations
   int32_t hflag[4] = {0, 0, 0, 0};  // host copies of flag_ws[0..3]
   HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 8, s));
   int passes = 0;
+  static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
 
   // Passes run in batches with one host read per batch (change flag + contest count): the
   // first batch of 8 covers the typical tile (~7 passes) with a single synchronisation, later
@@ -644,6 +402,9 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       HRF_LAUNCHED();
       HRF_HIP(hipMemcpyAsync(hflag, flag_ws, sizeof(int32_t) * 3, hipMemcpyDeviceToHost, s));
       HRF_HIP(hipStreamSynchronize(s));
+      if (dbg)
+        fprintf(stderr, "hrf_watershed: %s batch, passes %d, changed %d %d, contests %d\n",
+                relabel ? "relabel" : "relax", passes, hflag[0], hflag[1], hflag[2]);
       if (!hflag[0]) {
         *count_out = hflag[2];
         return HRF_OK;
@@ -684,13 +445,17 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
         scratch_bytes = nth * stride;
       }
       HRF_HIP(hipMemsetAsync(flag_ws + 3, 0, sizeof(int32_t), s));
-      ws_resolve_kernel<<<(unsigned)hrf::cdiv(nth, 64), 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, cap,
-                                                                     hcap, gcap, B.retry, flag_ws + 3, flag_ws + 4);
+      ws_resolve_kernel<<<(unsigned)hrf::cdiv(nth, 64), 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, nth,
+                                                                     cap, hcap, gcap, B.retry, flag_ws + 3,
+                                                                     flag_ws + 4);
       HRF_LAUNCHED();
       HRF_HIP(hipMemcpyAsync(hflag + 3, flag_ws + 3, sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HRF_HIP(hipStreamSynchronize(s));
+      if (dbg) fprintf(stderr, "hrf_watershed: round %d resolved %d (cap %d), retry %d\n", rounds, ntodo, cap, hflag[3]);
       if (!hflag[3]) break;
-      HRF_REQUIRE((int64_t)cap * 16 <= 4 * n + 64, "watershed: tie resolution exceeded its scratch (%d pixels)", cap);
+      // a group holds at most n pixels, and the queue each at most 4 times: beyond that an
+      // overflow means a corrupted state, not a large plateau
+      HRF_REQUIRE((int64_t)cap <= 16 * n + 65536, "watershed: tie resolution exceeded its scratch (%d entries)", cap);
       // retry list -> list (the retry buffer is rewritten by the next launch)
       HRF_HIP(hipMemcpyAsync(B.list, B.retry, sizeof(int32_t) * hflag[3], hipMemcpyDeviceToDevice, s));
       todo = B.list;
@@ -699,7 +464,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
     ws_reset_labels_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(markers, mask, n, a.lab, b.lab);
     HRF_LAUNCHED();
     if (hrf_status r = run(true, &ncontest)) return r;
-    HRF_REQUIRE(rounds < 100000, "watershed: tie resolution does not terminate");
+    HRF_REQUIRE(rounds < 4096, "watershed: tie resolution does not terminate");
   }
   if (ties_host) {
     ties_host[0] = total;

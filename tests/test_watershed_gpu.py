@@ -82,7 +82,7 @@ def test_watershed_constant_image(K, orc):
     for l in range(1, 9):
         r, c = rng.integers(0, H - 3), rng.integers(0, W - 3)
         markers[r:r + 3, c:c + 3] = l
-    f = f + 1e-3 * markers            # distinct marker values per label
+    f = f - 1e-3 * markers            # markers below the plateau, distinct per label
     ties = []
     got = host(K.watershed(dev(f), dev(markers), None, ties=ties))
     assert ties[0] > 0 and ties[2] == 0

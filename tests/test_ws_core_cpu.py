@@ -1,0 +1,64 @@
+"""a12: the device watershed's tie resolution (csrc/ws_core.hpp, compiled here for the host by
+tools/ws_emul.cpp, which replays hrf_watershed_ex's flow serially) against the heap flood
+restated from skimage (oracle_watershed) on plateau-heavy integer images -- the same code the
+GPU runs, checked without a GPU.  Skipped when hipcc is absent."""
+import ctypes
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+@pytest.fixture(scope="module")
+def emul(tmp_path_factory):
+    if not os.path.exists(HIPCC) and not shutil.which("hipcc"):
+        pytest.skip("hipcc not available")
+    out = str(tmp_path_factory.mktemp("wsemul") / "libws_emul.so")
+    subprocess.check_call([HIPCC, "-O2", "-fPIC", "-shared", "-o", out, os.path.join(REPO, "tools", "ws_emul.cpp")])
+    L = ctypes.CDLL(out)
+    V = ctypes.c_void_p
+    L.ws_emul.argtypes = [V, ctypes.c_int, V, V, ctypes.c_int64, ctypes.c_int64, V, V, V, V, V]
+    L.ws_emul.restype = ctypes.c_int
+
+    def run(f, markers, mask):
+        f = np.ascontiguousarray(f, np.float64)
+        mk = np.ascontiguousarray(markers, np.int32)
+        out = np.zeros(mk.shape, np.int32)
+        ties = np.zeros(3, np.int32)
+        mp = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        P = lambda a: a.ctypes.data_as(V)
+        r = L.ws_emul(P(f), 0, P(mk), None if mp is None else P(mp), f.shape[0], f.shape[1], P(out), P(ties),
+                      None, None, None)
+        assert r == 0
+        return out, ties
+    return run
+
+
+@pytest.mark.parametrize("block", range(3))
+def test_device_resolution_code_equals_heap(emul, orc, block):
+    layout_cases = 0
+    for seed in range(block * 100, (block + 1) * 100):
+        rng = np.random.default_rng(seed)
+        H, W = 12 + seed % 31, 12 + (seed * 5) % 37
+        f = rng.integers(0, 2 + seed % 4, (H, W)).astype(np.float64)
+        if seed % 3 == 0:
+            f = np.kron(rng.integers(0, 3, (H // 3 + 1, W // 3 + 1)), np.ones((3, 3)))[:H, :W].astype(np.float64)
+        mask = rng.random((H, W)) < 0.85 if seed % 5 else None
+        markers = np.zeros((H, W), np.int32)
+        idx = rng.choice(H * W, max(2, H * W // 50), replace=False)
+        markers.flat[idx] = rng.integers(1, 6, idx.size)
+        if seed % 2:
+            f = f + 1e-3 * markers
+        got, ties = emul(f, markers, mask)
+        model, _ = orc.watershed_ordered(f, markers, mask)
+        assert np.array_equal(got, model), seed
+        if ties[2] == 0:
+            assert np.array_equal(got, orc.watershed(f, markers, mask)), seed
+        else:
+            layout_cases += 1
+    assert layout_cases < 100
