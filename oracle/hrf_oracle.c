@@ -769,6 +769,31 @@ EXPORT void oracle_classify(const double *x, int64_t n, const double *ref, int R
     }
 }
 
+/* the same search keeping the runner-up distance too (d2[i] = second smallest over r != arg):
+ * lets tests require the exact argmin wherever best and runner-up are separated by more than
+ * the device's error bound.  Pixels are independent: OpenMP only shortens test wall time. */
+EXPORT void oracle_classify_top2(const double *x, int64_t n, const double *ref, int R, int C, const int32_t *bounds,
+                                 int nseg, int32_t *arg, double *d1, double *d2) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+        double best = INFINITY, second = INFINITY;
+        int32_t bi = 0;
+        for (int r = 0; r < R; ++r) {
+            double d = oracle_segcos(x + i * C, ref + (int64_t)r * C, bounds, nseg, 0, NULL, NULL);
+            if (d < best) {
+                second = best;
+                best = d;
+                bi = r;
+            } else if (d < second) {
+                second = d;
+            }
+        }
+        arg[i] = bi;
+        d1[i] = best;
+        d2[i] = second;
+    }
+}
+
 /* ------------------------------------------------------------------------------------
  * a8 1-D KMeans (sklearn KMeans(k, random_state=0).fit_predict(x.reshape(-1,1)), ecoli
  * :73,:85; multispecies :125,:141).  Restated as Lloyd iterations to a fixed point from

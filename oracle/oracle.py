@@ -302,6 +302,19 @@ def segcos(x, y, bounds, variant=0, fx=None, fy=None):
     return lib().oracle_segcos(_p(x), _p(y), _p(b), nseg, variant, fxp, fyp)
 
 
+def classify_top2(x, ref, bounds):
+    """ungated argmin (first minimum) with the best and runner-up distances"""
+    x = _c(x, np.float64)
+    ref = _c(ref, np.float64)
+    b = _c(bounds, np.int32)
+    n, C = x.shape
+    arg = np.zeros(n, np.int32)
+    d1 = np.zeros(n, np.float64)
+    d2 = np.zeros(n, np.float64)
+    lib().oracle_classify_top2(_p(x), I64(n), _p(ref), ref.shape[0], C, _p(b), len(b) - 1, _p(arg), _p(d1), _p(d2))
+    return arg, d1, d2
+
+
 def classify(x, ref, bounds, variant=0, fx=None, fr=None):
     x = _c(x, np.float64)
     ref = _c(ref, np.float64)

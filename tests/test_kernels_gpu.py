@@ -293,6 +293,23 @@ def test_counts_paint(K, orc):
 
 
 # ---- a19 classification ---------------------------------------------------------------
+# Per-pixel distances hold 1e-5 (abs/rel) of the f64 restatement, so two library rows whose
+# restated distances are more than MARGIN apart can never swap: wherever the oracle's best
+# beats its runner-up by more than MARGIN the device's argmin must be the oracle's, exactly;
+# where it does not, the device's row must be one of the rows within MARGIN of the best.
+MARGIN = 2e-5
+
+
+def check_pixel_argmin(orc, gi, gd, x64, ref64, bounds, min_separated=0.9):
+    ra, d1, d2 = orc.classify_top2(x64, ref64, bounds)
+    np.testing.assert_allclose(gd, d1, rtol=1e-5, atol=1e-5)
+    sep = (d2 - d1) > MARGIN
+    assert np.array_equal(gi[sep], ra[sep])
+    for i in np.nonzero(~sep)[0]:
+        assert orc.segcos(x64[i], ref64[gi[i]], bounds, 0) <= d1[i] + MARGIN
+    assert sep.mean() >= min_separated        # the exact check covers the bulk of the pixels
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63)), (5, (0, 32))])
 def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
@@ -310,24 +327,15 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
     st[7:20, bounds[0]:bounds[1]] = 0.0   # a zero segment
     refx = K.classify_prepare(dev(ref), bounds, mode=mode)
     idx, dist = K.classify_pixels(dev(st), refx, R, bounds)
-    ra, rd = orc.classify(st.astype(np.float64), ref.astype(np.float64), bounds, 0)
-    gi, gd = host(idx), host(dist)
-    np.testing.assert_allclose(gd, rd, rtol=1e-5, atol=1e-5)
-    # argmin must agree wherever the restatement's best is separated from the runner-up
-    x64 = st.astype(np.float64)
-    d_all = np.array([[orc.segcos(x64[i], ref[r].astype(np.float64), bounds, 0) for r in range(R)]
-                      for i in range(0, len(st), 37)])
-    srt = np.sort(d_all, axis=1)
-    sep = (srt[:, 1] - srt[:, 0]) > 2e-5
-    sub = np.arange(0, len(st), 37)
-    assert np.array_equal(gi[sub][sep], ra[sub][sep])
-    assert (gi == ra).mean() > 0.99
+    # every pixel of the tile (the background pixels are the near-ties)
+    check_pixel_argmin(orc, host(idx), host(dist), st.astype(np.float64), ref.astype(np.float64), bounds, 0.5)
 
 
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
 def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
     """mode 2 (indicator terms in the epilogue) vs mode 1 (indicator columns) on a 512x384
-    tile whose first rows carry zero segments; spot-checked against the restatement"""
+    tile whose first rows carry zero segments; the cell pixels checked exactly against the
+    restatement"""
     stack, truth, lay, ref = S.tile(512, 384, nbit=nbit, bounds=bounds, seed=21)
     R, C = ref.shape
     st = stack.clone()
@@ -339,13 +347,13 @@ def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
         refx = K.classify_prepare(dev(ref), bounds, mode=mode)
         out[mode] = [host(t).ravel() for t in K.classify_pixels(st, refx, R, bounds)]
     np.testing.assert_allclose(out[2][1], out[1][1], rtol=0, atol=2e-6)
-    assert (out[2][0] == out[1][0]).mean() > 0.999
-    sel = np.concatenate([np.arange(0, 9 * 384, 17), 100 * 384 + np.arange(0, 768, 13),
-                          np.random.default_rng(0).choice(512 * 384, 300, replace=False)])
+    rng = np.random.default_rng(0)
+    cells = np.nonzero(truth.ravel() > 0)[0]
+    sel = np.concatenate([np.arange(0, 9 * 384), 100 * 384 + np.arange(0, 768), rng.choice(cells, 4000, replace=False),
+                          rng.choice(512 * 384, 1000, replace=False)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
-    ri, rd = orc.classify(x, ref.astype(np.float64), bounds, 0)
-    np.testing.assert_allclose(out[2][1][sel], rd, rtol=1e-5, atol=1e-5)
-    assert (out[2][0][sel] == ri).mean() > 0.98
+    for mode in (1, 2):
+        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 0.5)
 
 
 def test_classify_pixels_mode2_negative_values(K, orc, S):
@@ -356,14 +364,13 @@ def test_classify_pixels_mode2_negative_values(K, orc, S):
     R, C = ref.shape
     st = stack.clone()
     st[0:4] -= 0.02                                 # some pixels (first 2 workgroups) go negative
-    sel = np.concatenate([np.arange(0, 4 * 128, 3), np.random.default_rng(1).choice(256 * 128, 200, replace=False)])
+    cells = np.nonzero(truth.ravel() > 0)[0]
+    sel = np.concatenate([np.arange(0, 4 * 128), np.random.default_rng(1).choice(cells, 1500, replace=False)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
     for lib in (ref, ref - 0.01):                   # then a library with negative entries
         refx = K.classify_prepare(dev(lib.astype(np.float32)), bounds, mode=2)
         gi, gd = [host(t).ravel()[sel] for t in K.classify_pixels(st, refx, R, bounds)]
-        ri, rd = orc.classify(x, lib.astype(np.float64), bounds, 0)
-        np.testing.assert_allclose(gd, rd, rtol=1e-5, atol=1e-5)
-        assert (gi == ri).mean() > 0.98
+        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 0.5)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
