@@ -1,55 +1,198 @@
-// kmeans.hip -- 1-D KMeans thresholding (a8).
+// kmeans.hip -- 1-D KMeans thresholding (a8): sklearn's KMeans, k-means++ and all.
 //
 // Reference: sklearn KMeans(n_clusters=k, random_state=0).fit_predict(x.reshape(-1,1))
-// (ecoli measurement.py:73,85; multispecies :125,141).  Restated (oracle/hrf_oracle.c
-// oracle_kmeans_1d) as Lloyd iterations from a deterministic init with EXACT centre updates:
-// each value is mapped to int64 fixed point q = rint(x * 2^s) once per pass and summed with
-// integer atomics, so the centres -- and therefore every label -- are independent of the
-// reduction order and identical to the CPU restatement bit for bit.
+// (ecoli measurement.py:73, :85; multispecies :125, :141) with the defaults of its era
+// (n_init=10).  Restated from sklearn 1.7.2 (KMeans.fit, _kmeans_plusplus,
+// _kmeans_single_lloyd, _relocate_empty_clusters_dense); the CPU restatement is
+// oracle/kmeans_sk.c, pinned to sklearn itself in tests/test_oracle_golden.py:
+//  * the random stream is numpy's RandomState(0) (MT19937, init_genrand) replayed on the host:
+//    per run the first centre (choice(n, p=1/n)) and 2 + int(log k) uniform draws per further
+//    centre;
+//  * k-means++ picks each further centre as the first sample whose running sum of
+//    closest-squared-distances reaches u * total; of a centre's trials the one leaving the
+//    least total wins;
+//  * Lloyd iterations stop on repeated labels (strict convergence) or a summed squared centre
+//    shift <= 1e-4 * var(x); empty clusters take the samples farthest from their centres;
+//    without strict convergence the labels are recomputed from the final centres;
+//  * of the n_init runs the one with the least inertia wins (strictly less, different
+//    partition in sklearn's one-sided sense).
+// Where sklearn's outcome hangs on its own floating-point summation order the restatement sums
+// exactly instead: squared distances as floor(d^2 * 2^S) in 128-bit integers, values as
+// rint(x * 2^s) in int64 (prefix sums over the value-sorted array, plus 128-bit prefix sums of
+// their squares), so every decision is independent of reduction order and equal to the CPU
+// restatement's bit for bit.
 //
-// Device-resident loop: ONE launch per Lloyd iteration.  Launch `it` first applies update
-// number `it` (every block derives the same centres from the previous launch's integer sums),
-// then streams the data once accumulating into a rotating sum buffer; it exits at once when
-// converged, so the host launches batches and polls rarely.
-//
-// Sorted path (hrf_kmeans_1d_sorted, the one the pipelines use): the valid values are sorted
-// once by value bucket (2^20 equal-width buckets, rocPRIM radix sort of 20-bit keys with the
-// values as payload) and their fixed-point values prefix-summed in that order.  With ascending, well separated centres the label
-// argmin_j (x - c_j)^2 (first minimum) is a non-decreasing step function of x, so one Lloyd
-// iteration reduces to locating the k - 1 label steps in the bucket-ordered array (a 4096-ary
-// search by one 1024-thread workgroup that narrows to whole buckets, then counts the few
-// values of the straddling bucket) and reading cluster sums and counts off the prefix array:
-// the same integer sums, hence the same centres, as the streaming pass -- with all iterations
-// in ONE launch and no per-iteration pass over the data.  A sort can serve several k on the
-// same input (E. coli :73 and :85 both cluster image_cn).  Whenever the step-function premise
-// cannot be guaranteed (a NaN among the values, centres not strictly ascending or closer than
-// 2^-40 of the data range) the call reruns the streaming path.
+// MI355X mapping.  The valid values are bucket sorted once (20-bit value buckets, rocPRIM
+// radix sort) and prefix-summed; a Lloyd step is then k - 1 label-step searches on the sorted
+// array (a 4096-ary search by one 1024-thread workgroup that narrows to whole buckets and
+// counts the straddling ones) -- no pass over the data per iteration.  The n_init runs proceed
+// in parallel: k-means++ needs two streaming passes per further centre for ALL runs at once
+// (block potentials, then the candidates' potentials), the candidate search itself touches one
+// 4096-sample block per trial; the Lloyd loops run one workgroup per run; a last kernel picks
+// the winner and a raster pass writes labels / the top-cluster mask.  No host synchronisation
+// is needed between the stages (the draws travel as kernel arguments).
 #include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include "common.hpp"
 #include "wave.hpp"
 
 namespace {
 
+typedef unsigned __int128 u128;
+
 constexpr int KMAX = 8;
+constexpr int NRUN = 10;                 // n_init (the reference era's default)
+constexpr int NTMAX = 4;                 // 2 + int(log 8)
+constexpr int PB = 4096;                 // samples per potential block
+constexpr int PT = 256;                  // threads per potential block (16 samples each)
+
+struct U128 {
+  unsigned long long lo, hi;
+};
+struct U128Plus {
+  __host__ __device__ U128 operator()(const U128 &a, const U128 &b) const {
+    U128 r;
+    r.lo = a.lo + b.lo;
+    r.hi = a.hi + b.hi + (r.lo < a.lo ? 1ull : 0ull);
+    return r;
+  }
+};
+__host__ __device__ inline u128 U(const U128 &a) { return ((u128)a.hi << 64) | a.lo; }
+__host__ __device__ inline U128 P(u128 v) { return U128{(unsigned long long)v, (unsigned long long)(v >> 64)}; }
+
+// correctly rounded (nearest even) u128 -> double, identical on host and device
+__host__ __device__ inline double u128_to_double(u128 v) {
+  const unsigned long long hi = (unsigned long long)(v >> 64);
+  if (!hi) return (double)(unsigned long long)v;
+  int z = 0;
+  while (!((hi << z) & 0x8000000000000000ull)) ++z;
+  const u128 t = v << z;                              // top bit at 127
+  const unsigned long long m64 = (unsigned long long)(t >> 64);
+  const bool sticky = (unsigned long long)t != 0;
+  unsigned long long mant = m64 >> 11;                // 53 bits
+  const unsigned long long rem = m64 & 0x7ffull;
+  if (rem > 0x400ull || (rem == 0x400ull && (sticky || (mant & 1ull)))) ++mant;
+  return ldexp((double)mant, 64 - z + 11);
+}
+
+// ceil(m * T / 2^53) for m < 2^53, T < 2^100 (exact)
+__host__ __device__ inline u128 thr_of(unsigned long long m, u128 T) {
+  const unsigned long long tl = (unsigned long long)T, th = (unsigned long long)(T >> 64);
+  const u128 a = (u128)m * tl;
+  const u128 b = (u128)m * th;
+  const u128 lo = a & ((((u128)1) << 53) - 1);
+  return (a >> 53) + (b << 11) + (lo != 0 ? 1 : 0);
+}
+
+__host__ __device__ inline unsigned long long qd(double x, double c, double scaleS) {
+  const double d = x - c;
+  return (unsigned long long)(d * d * scaleS);
+}
+
+// ---- host: numpy RandomState replay --------------------------------------------------------
+struct Mt19937 {
+  uint32_t mt[624];
+  int i = 624;
+  explicit Mt19937(uint32_t seed) {
+    mt[0] = seed;
+    for (int k = 1; k < 624; ++k) mt[k] = 1812433253u * (mt[k - 1] ^ (mt[k - 1] >> 30)) + (uint32_t)k;
+  }
+  uint32_t u32() {
+    if (i >= 624) {
+      for (int k = 0; k < 624; ++k) {
+        const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+        mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+      i = 0;
+    }
+    uint32_t y = mt[i++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  double random_sample() {  // numpy: (a >> 5, b >> 6) -> 53-bit double in [0, 1)
+    const uint32_t a = u32() >> 5, b = u32() >> 6;
+    return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+  }
+};
+
+// numpy RandomState.choice(nv, p = ones(nv) / nv): cdf = cumsum(p) / cdf[-1] (sequential),
+// index = searchsorted(cdf, u, side='right').  The cdf depends on nv only: cached.
+int64_t choice_uniform(int64_t nv, double u) {
+  static std::mutex mu;
+  static std::unordered_map<int64_t, std::vector<double>> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(nv);
+  if (it == cache.end()) {
+    if (cache.size() > 8) cache.clear();
+    std::vector<double> cdf((size_t)nv);
+    const double p = 1.0 / (double)nv;
+    double s = 0.0;
+    for (int64_t i = 0; i < nv; ++i) {
+      s += p;
+      cdf[(size_t)i] = s;
+    }
+    const double last = cdf[(size_t)nv - 1];
+    for (auto &v : cdf) v /= last;
+    it = cache.emplace(nv, std::move(cdf)).first;
+  }
+  const std::vector<double> &cdf = it->second;
+  return (int64_t)(std::upper_bound(cdf.begin(), cdf.end(), u) - cdf.begin());
+}
+
+struct Draws {  // kernel argument
+  long long first[NRUN];                 // rank of each run's first centre among the valid samples
+  unsigned long long m[NRUN][KMAX - 1][NTMAX];  // trial draws as integers (u = m / 2^53)
+  int nt, nrun;
+};
+
+Draws make_draws(int64_t nv, int k, int n_init, uint32_t seed) {
+  Draws d{};
+  Mt19937 rs(seed);
+  d.nt = 2 + (int)std::log((double)k);
+  d.nrun = n_init;
+  for (int r = 0; r < n_init; ++r) {
+    d.first[r] = (long long)choice_uniform(nv, rs.random_sample());
+    for (int c = 1; c < k; ++c)
+      for (int t = 0; t < d.nt; ++t) d.m[r][c - 1][t] = (unsigned long long)ldexp(rs.random_sample(), 53);
+  }
+  return d;
+}
+
+// ---- device state ----------------------------------------------------------------------------
+struct SkRun {
+  double cen[KMAX];    // final centres, sklearn order
+  double lcen[KMAX];   // centres that produced the final labels
+  double cand[NTMAX];  // candidates of the current k-means++ round
+  U128 T;              // current potential
+  double inertia;
+  long long cut[KMAX]; // final labels: samples with sorted rank <= p (value order)
+  int ids[KMAX];       // sorted rank -> sklearn id (final labels)
+  int iters, strict, reloc, ncen;
+};
 
 struct KmState {
-  double center[KMAX];         // final centres (read by the host and km_label_kernel)
-  double cen[2][KMAX];         // centres used by launch it live in cen[it & 1]
-  long long sum[3][KMAX];      // launch it accumulates into sum[it % 3]
-  unsigned long long cnt[3][KMAX];
-  unsigned long long lo_bits, hi_bits;  // order-preserving encodings of min / max
-  unsigned long long amax_bits;         // |x| max (non-negative doubles order as uint64)
-  unsigned long long nvalid;
-  unsigned long long nnan;              // NaN values among the valid ones (sorted path: fall back)
-  int scale;
-  int converged;
+  unsigned long long lo_bits, hi_bits, amax_bits, nvalid, nnan;
+  int s;          // value fixed point: q = rint(x * 2^s)
+  int S;          // potential fixed point: floor(d^2 * 2^S)
+  double tol;
+  int error;      // 1: NaN input (sklearn raises)
+  int best;       // winning run
+  int top;        // sklearn id of the top cluster (by the rule)
+  long long nle0; // samples <= 0 (rule 1)
+  double center[KMAX];
   int iters;
-  int k;
-  int fallback;                         // sorted path could not guarantee the step premise
+  SkRun run[NRUN];
 };
 
 __device__ __forceinline__ unsigned long long ord_enc(double x) {
@@ -78,13 +221,17 @@ __global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__
     for (int e = 0; e < 8; ++e) {
       if (!ok[e] || (valid && !valid[i + e * T])) continue;
       const double v = vv[e];
+      if (v != v) {
+        nn += 1;
+        nv += 1;
+        continue;
+      }
       const unsigned long long en = ord_enc(v);
       lo = en < lo ? en : lo;
       hi = en > hi ? en : hi;
       const unsigned long long a = (unsigned long long)__double_as_longlong(fabs(v));
       am = a > am ? a : am;
       nv += 1;
-      nn += v != v;
     }
   }
 #pragma unroll
@@ -122,204 +269,29 @@ __global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__
   }
 }
 
-__global__ void km_init_kernel(KmState *st, int k) {
-  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
+// value and potential scales (oracle_kmeans_scale / kmeans_sk.c)
+__global__ void km_scale_kernel(KmState *st) {
   const double amax = __longlong_as_double((long long)st->amax_bits);
   int e = 0;
   frexp(amax > 0 ? amax : 1.0, &e);
   const unsigned long long nv = st->nvalid;
   int ln = 0;
   while ((1ull << ln) < (nv > 1 ? nv : 1ull)) ++ln;
-  st->scale = 61 - ln - e;
-  for (int j = 0; j < KMAX; ++j) {
-    st->center[j] = j < k ? mn + ((double)j + 0.5) * (mx - mn) / (double)k : 0.0;
-    st->cen[0][j] = st->cen[1][j] = st->center[j];  // launch 0 reads cen[1]
-    st->sum[0][j] = 0;
-    st->cnt[0][j] = 0;
-  }
-  st->k = k;
-  st->converged = nv == 0;
-  st->iters = 0;
-  st->fallback = 0;
+  st->s = 61 - ln - e;
+  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
+  const double r = nv && !st->nnan ? mx - mn : 0.0, R2 = r * r;
+  int e2 = 0;
+  frexp(R2 > 0 ? R2 : 1.0, &e2);
+  st->S = 61 - e2;
+  st->error = st->nnan ? 1 : 0;
 }
 
-constexpr int KM_E = 8;  // elements in flight per thread
-
-template <int K>
-__device__ __forceinline__ int km_assign(double v, const double *c) {
-  int bj = 0;
-  double bd = (v - c[0]) * (v - c[0]);
-#pragma unroll
-  for (int j = 1; j < K; ++j) {
-    const double d = (v - c[j]) * (v - c[j]);
-    if (d < bd) {
-      bd = d;
-      bj = j;
-    }
-  }
-  return bj;
-}
-
-template <int K>
-__global__ __launch_bounds__(256) void km_step_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid,
-                                                     int64_t n, KmState *st, int it, int max_iter) {
-  if (st->converged) return;
-  const int s = st->scale;
-  double c[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) c[j] = st->cen[(it + 1) & 1][j];
-  if (it > 0) {
-    // update number `it` (the former km_update_kernel), identical in every block
-    const int pb = (it + 2) % 3;
-    int changed = 0;
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const unsigned long long cn = st->cnt[pb][j];
-      if (cn) {
-        const double cj = ldexp((double)st->sum[pb][j] / (double)cn, -s);
-        if (cj != c[j]) changed = 1;
-        c[j] = cj;
-      }
-    }
-    if (!changed || it >= max_iter) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        for (int j = 0; j < K; ++j) st->center[j] = c[j];
-        st->iters = it;
-        st->converged = 1;
-      }
-      return;
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x < K) {
-    st->cen[it & 1][threadIdx.x] = c[threadIdx.x];
-    st->sum[(it + 1) % 3][threadIdx.x] = 0;
-    st->cnt[(it + 1) % 3][threadIdx.x] = 0;
-  }
-  long long sum[K];
-  unsigned long long cnt[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    sum[j] = 0;
-    cnt[j] = 0;
-  }
-  // KM_E strided elements per thread per round, all loads issued before any is used: the pass
-  // is bound by memory-level parallelism, not arithmetic
-  const int64_t T = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += T * KM_E) {
-    double v[KM_E];
-    bool ok[KM_E];
-#pragma unroll
-    for (int e = 0; e < KM_E; ++e) {
-      const int64_t k = i + e * T;
-      ok[e] = k < n;
-      v[e] = ok[e] ? x[k] : 0.0;
-    }
-    if (valid) {
-#pragma unroll
-      for (int e = 0; e < KM_E; ++e) ok[e] = ok[e] && valid[i + e * T];
-    }
-#pragma unroll
-    for (int e = 0; e < KM_E; ++e) {
-      if (!ok[e]) continue;
-      const int bj = km_assign<K>(v[e], c);
-      const long long q = (long long)rint(ldexp(v[e], s));
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        sum[j] += bj == j ? q : 0;
-        cnt[j] += bj == j;
-      }
-    }
-  }
-  __shared__ long long ssum[4][K];
-  __shared__ unsigned long long scnt[4][K];
-  const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const long long a = hrf::wave_sum(sum[j]);
-    const unsigned long long b = hrf::wave_sum(cnt[j]);
-    if ((threadIdx.x & 63) == 0) {
-      ssum[w][j] = a;
-      scnt[w][j] = b;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < K) {
-    const int j = threadIdx.x;
-    const long long a = ssum[0][j] + ssum[1][j] + ssum[2][j] + ssum[3][j];
-    const unsigned long long b = scnt[0][j] + scnt[1][j] + scnt[2][j] + scnt[3][j];
-    if (b) {
-      atomicAdd((unsigned long long *)&st->sum[it % 3][j], (unsigned long long)a);
-      atomicAdd(&st->cnt[it % 3][j], b);
-    }
-  }
-}
-
-template <int K>
-__global__ void km_label_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
-                                const KmState *st, int32_t *__restrict__ labels, uint8_t *__restrict__ top) {
-  double c[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) c[j] = st->center[j];
-  int jt = 0;
-#pragma unroll
-  for (int j = 1; j < K; ++j)
-    if (c[j] > c[jt]) jt = j;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const bool ok = !valid || valid[i];
-    const int bj = ok ? km_assign<K>(x[i], c) : -1;
-    if (labels) labels[i] = bj;
-    if (top) top[i] = (uint8_t)(bj == jt);
-  }
-}
-
-template <int K>
-hrf_status km_run(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels, uint8_t *top,
-                  double *centers_host, int32_t *iters_host, KmState *st, hipStream_t s) {
-  const unsigned g = hrf::stream_grid(n);
-  const unsigned gr = std::min<unsigned>(g, 512);
-  KmState init{};
-  for (int j = 0; j < KMAX; ++j) init.center[j] = 0;
-  init.lo_bits = ~0ull;
-  init.hi_bits = 0;
-  init.amax_bits = 0;
-  init.nvalid = 0;
-  HRF_HIP(hipMemcpyAsync(st, &init, sizeof(KmState), hipMemcpyHostToDevice, s));
-  if (n > 0) km_minmax_kernel<<<gr, 256, 0, s>>>(x, valid, n, st);
-  km_init_kernel<<<1, 1, 0, s>>>(st, K);
-  HRF_LAUNCHED();
-  int done = 0;
-  int launched = 0;
-  int batch = 4;
-  int conv = 0;
-  while (!done) {
-    // launch `it` applies update `it`; update max_iter ends the fit, so at most max_iter + 1
-    for (int b = 0; b < batch && launched <= max_iter; ++b, ++launched)
-      km_step_kernel<K><<<gr, 256, 0, s>>>(x, valid, n, st, launched, max_iter);
-    HRF_LAUNCHED();
-    HRF_HIP(hipMemcpyAsync(&conv, &st->converged, sizeof(int), hipMemcpyDeviceToHost, s));
-    HRF_HIP(hipStreamSynchronize(s));
-    done = conv || launched > max_iter;
-    batch = batch < 16 ? batch * 2 : 16;
-  }
-  if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
-  HRF_LAUNCHED();
-  KmState fin;
-  HRF_HIP(hipMemcpyAsync(&fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
-  HRF_HIP(hipStreamSynchronize(s));
-  if (centers_host)
-    for (int j = 0; j < K; ++j) centers_host[j] = fin.center[j];
-  if (iters_host) *iters_host = fin.iters;
-  return HRF_OK;
-}
-
-
-// ---- sorted path: sort by value bucket ------------------------------------------------------
+// ---- sorted array ----------------------------------------------------------------------------
 // NB value buckets of equal width over [min, max]; bucket(x) is a non-decreasing function of
 // x, so every value of bucket b is below every value of bucket b' > b.  The valid values are
-// radix sorted by their 20-bit bucket index (rocPRIM pairs, 3 digit passes instead of 8 for
-// full 64-bit keys; invalid entries get key NB and land past them), in no particular order
-// inside a bucket -- only integer sums are read off the result, so that order never shows.
-// off[b] = first position of bucket b, then the fixed-point encodings are prefix-summed.
+// radix sorted by their 20-bit bucket index (invalid entries get key NB and land past them),
+// in no particular order inside a bucket -- only integer sums and counts are read off.
+// off[b] = first position of bucket b; q = rint(x 2^s), prefix sums of q and of q^2.
 constexpr int KM_NB = 1 << 20;
 constexpr int KM_NB_BITS = 21;  // keys 0..NB inclusive
 
@@ -328,7 +300,6 @@ __device__ __forceinline__ int km_bucket(double x, double mn, double inv) {
   return t >= 0.0 ? (t < (double)(KM_NB - 1) ? (int)t : KM_NB - 1) : 0;  // NaN -> 0
 }
 
-// bucket geometry from the min / max found by km_minmax_kernel
 __global__ void km_bucket_init_kernel(KmState *st, double *geo) {
   const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
   geo[0] = mn;
@@ -342,15 +313,17 @@ __global__ void km_bucket_key_kernel(const double *__restrict__ x, const uint8_t
     key[i] = (!valid || valid[i]) ? (uint32_t)km_bucket(x[i], mn, inv) : (uint32_t)KM_NB;
 }
 
-// off[b] = first sorted position whose key is >= b (b = 0..NB, a binary search each, so empty
-// stretches of buckets cost nothing extra); q = fixed-point values in sorted order
 __global__ void km_bucket_bounds_kernel(const uint32_t *__restrict__ key, const double *__restrict__ xs, int64_t n,
                                         const KmState *st, unsigned long long *__restrict__ off,
-                                        long long *__restrict__ q, long long *__restrict__ prefix0) {
-  const int s = st->scale;
+                                        long long *__restrict__ q, U128 *__restrict__ q2,
+                                        long long *__restrict__ prefix0, U128 *__restrict__ p20) {
+  const int s = st->s;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t0 == 0) *prefix0 = 0;
+  if (t0 == 0) {
+    *prefix0 = 0;
+    *p20 = U128{0, 0};
+  }
   for (int64_t b = t0; b <= KM_NB; b += T) {
     int64_t lo = 0, hi = n;
     while (lo < hi) {
@@ -360,38 +333,282 @@ __global__ void km_bucket_bounds_kernel(const uint32_t *__restrict__ key, const 
     }
     off[b] = (unsigned long long)lo;
   }
-  for (int64_t i = t0; i < n; i += T) q[i] = (long long)rint(ldexp(xs[i], s));
+  for (int64_t i = t0; i < n; i += T) {
+    const long long v = (long long)rint(ldexp(xs[i], s));
+    q[i] = v;
+    const unsigned long long a = (unsigned long long)(v < 0 ? -v : v);
+    q2[i] = P((u128)a * a);
+  }
 }
 
-constexpr int KS_T = 1024;           // threads of the iteration workgroup
+// tol = 1e-4 * var(x) from the exact sums (kmeans_sk.c)
+__global__ void km_tol_kernel(const long long *__restrict__ prefix, const U128 *__restrict__ p2, KmState *st) {
+  const long long nv = (long long)st->nvalid;
+  if (!nv) {
+    st->tol = 0;
+    return;
+  }
+  const double m1 = (double)prefix[nv] / (double)nv, m2 = u128_to_double(U(p2[nv])) / (double)nv;
+  st->tol = ldexp(m2 - m1 * m1, -2 * st->s) * 1e-4;
+}
+
+// ---- k-means++ -------------------------------------------------------------------------------
+// closest fixed-point squared distance of v to the run's first c centres
+__device__ __forceinline__ unsigned long long closest_q(double v, const double *cen, int c, double scaleS) {
+  unsigned long long b = qd(v, cen[0], scaleS);
+  for (int j = 1; j < c; ++j) {
+    const unsigned long long d = qd(v, cen[j], scaleS);
+    b = d < b ? d : b;
+  }
+  return b;
+}
+
+__device__ __forceinline__ U128 wave_sum128(U128 a) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    U128 b;
+    b.lo = __shfl_xor(a.lo, o, 64);
+    b.hi = __shfl_xor(a.hi, o, 64);
+    a = U128Plus()(a, b);
+  }
+  return a;
+}
+
+// block sum of per-thread u128 values (PT threads); result valid in thread 0
+__device__ __forceinline__ U128 block_sum128(U128 a, U128 *sh) {
+  a = wave_sum128(a);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = a;
+  __syncthreads();
+  U128 r{0, 0};
+  if (threadIdx.x == 0)
+    for (int q = 0; q < PT / 64; ++q) r = U128Plus()(r, sh[q]);
+  return r;
+}
+
+// the first centre of every run: first[r]-th valid sample in raster order (xr compacted)
+__global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, Draws d) {
+  const int r = threadIdx.x;
+  if (r >= d.nrun) return;
+  SkRun &R = st->run[r];
+  const long long nv = (long long)st->nvalid;
+  long long idx = d.first[r] < nv ? d.first[r] : nv - 1;
+  R.cen[0] = nv > 0 ? xr[idx] : 0.0;
+  R.ncen = 1;
+}
+
+// pass A (mode 0): per run, block sums of the closest potential -> part[r][blk]
+// pass C (mode 1): per run and trial, block sums of min(closest, d(candidate)) -> part[r*NTMAX+t][blk]
+template <int MODE>
+__global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict__ xr, const KmState *st, Draws d,
+                                                        U128 *__restrict__ part, int nblk) {
+  __shared__ U128 sh[PT / 64];
+  const int64_t nv = (int64_t)st->nvalid;
+  const double scaleS = ldexp(1.0, st->S);
+  const int64_t base = (int64_t)blockIdx.x * PB + threadIdx.x * (PB / PT);
+  double v[PB / PT];
+  int cnt = 0;
+#pragma unroll
+  for (int e = 0; e < PB / PT; ++e) {
+    const int64_t i = base + e;
+    v[e] = i < nv ? xr[i] : 0.0;
+    cnt += i < nv;
+  }
+  for (int r = 0; r < d.nrun; ++r) {
+    const SkRun &R = st->run[r];
+    const int c = R.ncen;
+    unsigned long long cl[PB / PT];
+#pragma unroll
+    for (int e = 0; e < PB / PT; ++e) cl[e] = e < cnt ? closest_q(v[e], R.cen, c, scaleS) : 0ull;
+    if (MODE == 0) {
+      u128 s = 0;
+#pragma unroll
+      for (int e = 0; e < PB / PT; ++e) s += cl[e];
+      const U128 tot = block_sum128(P(s), sh);
+      if (threadIdx.x == 0) part[(int64_t)r * nblk + blockIdx.x] = tot;
+    } else {
+      for (int t = 0; t < d.nt; ++t) {
+        const double cv = R.cand[t];
+        u128 s = 0;
+#pragma unroll
+        for (int e = 0; e < PB / PT; ++e) {
+          const unsigned long long dq = e < cnt ? qd(v[e], cv, scaleS) : 0ull;
+          s += dq < cl[e] ? dq : cl[e];
+        }
+        const U128 tot = block_sum128(P(s), sh);
+        if (threadIdx.x == 0) part[((int64_t)r * NTMAX + t) * nblk + blockIdx.x] = tot;
+      }
+    }
+  }
+}
+
+// per run (one workgroup each): total potential, then every trial's candidate = the first
+// sample whose running potential reaches thr = ceil(m T / 2^53)
+__global__ __launch_bounds__(PT) void km_pp_pick_kernel(const double *__restrict__ xr, KmState *st, Draws d,
+                                                        const U128 *__restrict__ part, int nblk, int c) {
+  __shared__ U128 pre[PT + 1];   // prefix over thread chunks of block partials
+  __shared__ U128 ts[PT];        // per-thread sums inside the crossing block
+  __shared__ U128 before_sh;
+  __shared__ int blk_sh, thr_t_sh;
+  __shared__ long long idx_sh;
+  __shared__ unsigned long long thr_lo, thr_hi;
+  const int r = blockIdx.x;
+  SkRun &R = st->run[r];
+  const int64_t nv = (int64_t)st->nvalid;
+  const double scaleS = ldexp(1.0, st->S);
+  const int tid = threadIdx.x;
+  const U128 *pr = part + (int64_t)r * nblk;
+  const int per = (nblk + PT - 1) / PT;
+  u128 loc = 0;
+  for (int b = tid * per; b < nblk && b < (tid + 1) * per; ++b) loc += U(pr[b]);
+  pre[tid + 1] = P(loc);
+  __syncthreads();
+  if (tid == 0) {
+    pre[0] = U128{0, 0};
+    for (int q = 1; q <= PT; ++q) pre[q] = U128Plus()(pre[q - 1], pre[q]);
+    R.T = pre[PT];
+  }
+  __syncthreads();
+  const u128 T = U(pre[PT]);
+  for (int t = 0; t < d.nt; ++t) {
+    if (tid == 0) {
+      const u128 thr = thr_of(d.m[r][c - 1][t], T);
+      thr_lo = (unsigned long long)thr;
+      thr_hi = (unsigned long long)(thr >> 64);
+      int b = -1;
+      u128 acc = 0;
+      for (int q = 0; q < PT && b < 0; ++q) {
+        if (U(pre[q + 1]) < thr) continue;
+        acc = U(pre[q]);
+        for (int bb = q * per; bb < nblk && bb < (q + 1) * per; ++bb) {
+          const u128 nx = acc + U(pr[bb]);
+          if (nx >= thr) {
+            b = bb;
+            break;
+          }
+          acc = nx;
+        }
+      }
+      blk_sh = b;
+      before_sh = P(acc);
+      idx_sh = -1;
+    }
+    __syncthreads();
+    const int b = blk_sh;
+    const u128 thr = ((u128)thr_hi << 64) | thr_lo;
+    unsigned long long cl[PB / PT];
+    const int64_t i0 = (int64_t)(b < 0 ? 0 : b) * PB + tid * (PB / PT);
+    u128 sthr = 0;
+#pragma unroll
+    for (int e = 0; e < PB / PT; ++e) {
+      const int64_t i = i0 + e;
+      cl[e] = (b >= 0 && i < nv) ? closest_q(xr[i], R.cen, c, scaleS) : 0ull;
+      sthr += cl[e];
+    }
+    ts[tid] = P(sthr);
+    __syncthreads();
+    if (tid == 0 && b >= 0) {
+      u128 acc = U(before_sh);
+      thr_t_sh = PT - 1;
+      for (int q = 0; q < PT; ++q) {
+        const u128 nx = acc + U(ts[q]);
+        if (nx >= thr) {
+          thr_t_sh = q;
+          break;
+        }
+        acc = nx;
+      }
+      before_sh = P(acc);
+    }
+    __syncthreads();
+    if (b >= 0 && tid == thr_t_sh) {
+      u128 acc = U(before_sh);
+      for (int e = 0; e < PB / PT; ++e) {
+        acc += cl[e];
+        if (acc >= thr && i0 + e < nv) {
+          idx_sh = i0 + e;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      // sklearn clips an out-of-range candidate to the last sample
+      const long long idx = idx_sh >= 0 ? idx_sh : nv - 1;
+      R.cand[t] = xr[idx];
+    }
+    __syncthreads();
+  }
+}
+
+// per run: totals of the trials' potentials, the least (first) wins
+__global__ void km_pp_choose_kernel(KmState *st, Draws d, const U128 *__restrict__ part, int nblk, int c) {
+  __shared__ U128 sh[PT / 64];
+  const int r = blockIdx.x;
+  SkRun &R = st->run[r];
+  __shared__ u128 tot[NTMAX];
+  for (int t = 0; t < d.nt; ++t) {
+    u128 s = 0;
+    for (int b = threadIdx.x; b < nblk; b += PT) s += U(part[((int64_t)r * NTMAX + t) * nblk + b]);
+    const U128 a = block_sum128(P(s), sh);
+    if (threadIdx.x == 0) tot[t] = U(a);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int bt = 0;
+    for (int t = 1; t < d.nt; ++t)
+      if (tot[t] < tot[bt]) bt = t;
+    R.cen[c] = R.cand[bt];
+    R.T = P(tot[bt]);
+    R.ncen = c + 1;
+  }
+}
+
+// ---- Lloyd on the sorted array ---------------------------------------------------------------
+constexpr int KS_T = 1024;           // threads of an iteration workgroup
 constexpr int KS_P = 4;              // probes per thread per round -> 4096-ary search
 static_assert(KS_T * KS_P == 4096, "index arithmetic below shifts by 12");
 
-// For label step j (labels <= j versus > j): the number of bucket-ordered values with label
-// <= j and the sum of their fixed-point encodings.  Invariant: the range [lo, hi) starts and
-// ends on bucket boundaries, every value before it has label <= j and every value after it
-// label > j (labels are non-decreasing in the value, buckets are ordered by value).  A round
-// probes 4096 evenly spaced values: the range shrinks to [start of the last bucket holding a
-// "<= j" probe, end of the first bucket holding a "> j" probe).  A range of <= 4096 values, or
-// one that a round could not halve, is counted exhaustively.
+// label of v: sklearn id of the first minimum of (v - c_j)^2 in sklearn order
+template <int K>
+__device__ __forceinline__ int sk_assign(double v, const double *c) {
+  int bj = 0;
+  double bd = (v - c[0]) * (v - c[0]);
+#pragma unroll
+  for (int j = 1; j < K; ++j) {
+    const double dd = (v - c[j]) * (v - c[j]);
+    if (dd < bd) {
+      bd = dd;
+      bj = j;
+    }
+  }
+  return bj;
+}
+
+// For sorted boundary j (sorted ranks <= j versus > j): the count of samples with rank <= j,
+// the sum of their q and of their q^2.  Invariant: the range [lo, hi) starts and ends on
+// bucket boundaries, every sample before it has rank <= j and every sample after it rank > j
+// (ranks are non-decreasing in the value, buckets ordered by value).  A round probes 4096
+// evenly spaced samples; the range shrinks to [start of the last bucket holding a "<= j"
+// probe, end of the first bucket holding a "> j" probe).  A range of <= 4096 samples, or one a
+// round could not halve, is counted exhaustively.
 template <int K>
 __device__ void km_bucket_step(const double *__restrict__ xs, const long long *__restrict__ q,
-                               const long long *__restrict__ prefix, const unsigned long long *__restrict__ off,
-                               int64_t nv, double mn, double inv, double range, const double *c, int j,
-                               int64_t *cnt_le, long long *sum_le) {
+                               const U128 *__restrict__ q2, const long long *__restrict__ prefix,
+                               const U128 *__restrict__ p2, const unsigned long long *__restrict__ off, int64_t nv,
+                               double mn, double inv, double range, const double *c, const int *pos,
+                               const double *cso, int j, int64_t *cnt_le, long long *sum_le, U128 *sq_le) {
   const int t = threadIdx.x;
   __shared__ int64_t lo_sh, hi_sh;
   __shared__ int bf_sh, bt_sh, exh_sh;
   __shared__ unsigned long long nf_sh;
   __shared__ long long sf_sh;
+  __shared__ U128 qf_sh[KS_T / 64];
   if (t == 0) {
-    // Direct bracket: the label step lies within delta of the midpoint m (the comparison's
-    // rounding moves it by ~2^-53 of the centre gap; delta is 2^-40 of the magnitudes), and
-    // km_bucket is monotone in the value, so every value in a bucket below bucket(m - delta)
-    // has label <= j and every value in a bucket above bucket(m + delta) label > j.  The
-    // range then starts on those bucket boundaries instead of [0, nv).
-    const double m = 0.5 * c[j] + 0.5 * c[j + 1];
-    const double delta = (fabs(c[j]) + fabs(c[j + 1]) + range) * 0x1p-40;
+    // direct bracket: the step lies within delta of the midpoint of the sorted centres j, j+1
+    const double m = 0.5 * cso[j] + 0.5 * cso[j + 1];
+    const double delta = (fabs(cso[j]) + fabs(cso[j + 1]) + range) * 0x1p-40;
     const int blo = km_bucket(m - delta, mn, inv), bhi = km_bucket(m + delta, mn, inv);
     const int64_t lo = (int64_t)off[blo], hi = (int64_t)off[bhi + 1];
     lo_sh = lo < 0 ? 0 : (lo > nv ? nv : lo);
@@ -403,7 +620,6 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
     const int64_t lo = lo_sh, hi = hi_sh;
     const int64_t len = hi - lo;
     if (exh_sh || len <= (int64_t)KS_T * KS_P) {
-      // count the range exhaustively: values with label <= j and the sum of their encodings
       if (t == 0) {
         nf_sh = 0;
         sf_sh = 0;
@@ -411,22 +627,30 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       __syncthreads();
       unsigned long long nf = 0;
       long long sf = 0;
-      const long long plo = t == 0 ? prefix[lo] : 0;  // issued before the scan's loads
+      u128 qf = 0;
       for (int64_t idx = lo + t; idx < hi; idx += KS_T)
-        if (km_assign<K>(xs[idx], c) <= j) {
+        if (pos[sk_assign<K>(xs[idx], c)] <= j) {
           nf += 1;
           sf += q[idx];
+          qf += U(q2[idx]);
         }
       nf = hrf::wave_sum(nf);
       sf = hrf::wave_sum(sf);
-      if ((t & 63) == 0 && nf) {
-        atomicAdd(&nf_sh, nf);
-        atomicAdd((unsigned long long *)&sf_sh, (unsigned long long)sf);
+      const U128 qw = wave_sum128(P(qf));
+      if ((t & 63) == 0) {
+        qf_sh[t >> 6] = qw;
+        if (nf) {
+          atomicAdd(&nf_sh, nf);
+          atomicAdd((unsigned long long *)&sf_sh, (unsigned long long)sf);
+        }
       }
       __syncthreads();
       if (t == 0) {
+        u128 qa = U(p2[lo]);
+        for (int w = 0; w < KS_T / 64; ++w) qa += U(qf_sh[w]);
         *cnt_le = lo + (int64_t)nf_sh;
-        *sum_le = plo + sf_sh;
+        *sum_le = prefix[lo] + sf_sh;
+        *sq_le = P(qa);
       }
       __syncthreads();
       return;
@@ -442,7 +666,7 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       const int64_t idx = lo + ((len * (t * KS_P + p)) >> 12);  // KS_T * KS_P = 4096; len < 2^51
       const double v = xs[idx];
       const int b = km_bucket(v, mn, inv);
-      if (km_assign<K>(v, c) <= j) bf = b > bf ? b : bf;
+      if (pos[sk_assign<K>(v, c)] <= j) bf = b > bf ? b : bf;
       else bt = b < bt ? b : bt;
     }
     if (bf >= 0) atomicMax(&bf_sh, bf);
@@ -460,96 +684,387 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
   }
 }
 
+// the assignment for the centres c (sklearn order): per sklearn id count, sum q, sum q^2;
+// the label signature (sorted ranks -> ids, cumulative counts)
 template <int K>
-__global__ __launch_bounds__(KS_T) void km_sorted_iter_kernel(const double *__restrict__ xs,
-                                                              const long long *__restrict__ q,
-                                                              const long long *__restrict__ prefix,
-                                                              const unsigned long long *__restrict__ off,
-                                                              const double *__restrict__ geo, KmState *st,
-                                                              int max_iter) {
-  __shared__ double c[KMAX];
-  __shared__ int64_t cle[KMAX];
-  __shared__ long long sle[KMAX];
-  __shared__ int stop;
+__device__ void km_assign_all(const double *xs, const long long *q, const U128 *q2, const long long *prefix,
+                              const U128 *p2, const unsigned long long *off, int64_t nv, double mn, double inv,
+                              double range, const double *c, int *ids, int *pos, double *cso, int64_t *cle,
+                              long long *sle, U128 *qle, long long *cnt, long long *sum, U128 *sq) {
   const int t = threadIdx.x;
-  const int64_t nv = (int64_t)st->nvalid;
-  const int s = st->scale;
-  const double mn = geo[0], inv = geo[1];
-  if (t < K) c[t] = st->center[t];
-  if (t == 0) stop = 0;
-  __syncthreads();
-  if (nv == 0) {
-    if (t == 0) st->iters = 0;
-    return;
+  if (t == 0) {
+    // sorted ranks by (value, sklearn id): among equal centres the first id takes the samples
+    for (int j = 0; j < K; ++j) ids[j] = j;
+    for (int a = 1; a < K; ++a)
+      for (int b = a; b > 0; --b) {
+        const int x = ids[b - 1], y = ids[b];
+        if (c[y] < c[x] || (c[y] == c[x] && y < x)) {
+          ids[b - 1] = y;
+          ids[b] = x;
+        } else
+          break;
+      }
+    for (int p = 0; p < K; ++p) {
+      pos[ids[p]] = p;
+      cso[p] = c[ids[p]];
+    }
   }
-  if (st->nnan) {
-    if (t == 0) st->fallback = 1;
+  __syncthreads();
+  for (int j = 0; j + 1 < K; ++j)
+    if (cso[j] != cso[j + 1])
+      km_bucket_step<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, pos, cso, j, &cle[j], &sle[j], &qle[j]);
+  __syncthreads();
+  if (t == 0) {
+    cle[K - 1] = nv;
+    sle[K - 1] = prefix[nv];
+    qle[K - 1] = p2[nv];
+    for (int j = K - 2; j >= 0; --j)
+      if (cso[j] == cso[j + 1]) {  // rank j+1 is never taken: the same cumulative state
+        cle[j] = cle[j + 1];
+        sle[j] = sle[j + 1];
+        qle[j] = qle[j + 1];
+      }
+    int64_t c0 = 0;
+    long long s0 = 0;
+    u128 q0 = 0;
+    for (int p = 0; p < K; ++p) {
+      cnt[ids[p]] = cle[p] - c0;
+      sum[ids[p]] = sle[p] - s0;
+      sq[ids[p]] = P(U(qle[p]) - q0);
+      c0 = cle[p];
+      s0 = sle[p];
+      q0 = U(qle[p]);
+    }
+  }
+  __syncthreads();
+}
+
+template <int K>
+__global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict__ xs, const long long *__restrict__ q,
+                                                        const U128 *__restrict__ q2,
+                                                        const long long *__restrict__ prefix,
+                                                        const U128 *__restrict__ p2,
+                                                        const unsigned long long *__restrict__ off,
+                                                        const double *__restrict__ geo, KmState *st, int max_iter) {
+  __shared__ double c[KMAX], cso[KMAX], oldc[KMAX];
+  __shared__ int ids[KMAX], pos[KMAX], oids[KMAX];
+  __shared__ int64_t cle[KMAX], ocle[KMAX];
+  __shared__ long long sle[KMAX], cnt[KMAX], sum[KMAX];
+  __shared__ U128 qle[KMAX], sq[KMAX];
+  __shared__ int stop, have_old, nempty;
+  __shared__ double rd[KS_T / 64][1];
+  __shared__ long long ri[KS_T / 64][1];
+  __shared__ long long far_sh[KMAX];
+  const int t = threadIdx.x;
+  const int r = blockIdx.x;
+  SkRun &R = st->run[r];
+  const int64_t nv = (int64_t)st->nvalid;
+  const int s = st->s;
+  const double mn = geo[0], inv = geo[1];
+  if (nv == 0 || st->error) {
+    if (t == 0) {
+      R.inertia = 0;
+      R.iters = 0;
+      for (int j = 0; j < K; ++j) R.cen[j] = R.lcen[j] = 0;
+    }
     return;
   }
   const double range = ord_dec(st->hi_bits) - ord_dec(st->lo_bits);
+  if (t < K) c[t] = R.cen[t];
+  if (t == 0) {
+    stop = 0;
+    have_old = 0;
+    R.reloc = 0;
+  }
+  __syncthreads();
   int it;
-  for (it = 1; it <= max_iter; ++it) {
+  for (it = 0; it < max_iter; ++it) {
+    km_assign_all<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
     if (t == 0) {
-      // premise of the step search: strictly ascending, well separated centres
-      for (int j = 0; j + 1 < K; ++j)
-        if (!(c[j + 1] - c[j] > range * 0x1p-40)) stop = 2;
+      nempty = 0;
+      for (int j = 0; j < K; ++j) nempty += cnt[j] == 0;
     }
     __syncthreads();
-    if (stop) break;
-    for (int j = 0; j + 1 < K; ++j) km_bucket_step<K>(xs, q, prefix, off, nv, mn, inv, range, c, j, &cle[j], &sle[j]);
-    if (t == 0) {
-      int changed = 0;
-      int64_t c0 = 0;
-      long long s0 = 0;
-      for (int j = 0; j < K; ++j) {
-        const int64_t c1 = j < K - 1 ? cle[j] : nv;
-        const long long s1 = j < K - 1 ? sle[j] : prefix[nv];
-        const int64_t cn = c1 - c0;
-        if (cn) {
-          const double cj = ldexp((double)(s1 - s0) / (double)cn, -s);
-          if (cj != c[j]) changed = 1;
-          c[j] = cj;
-        }
-        c0 = c1;
-        s0 = s1;
+    if (nempty) {
+      // the nempty samples farthest from their own centre (ties: lower value, then lower
+      // position) over all samples: per-thread ordered lists, then nempty block-wide rounds
+      const int m = nempty;
+      double bd[KMAX];
+      long long bi[KMAX];
+      for (int e = 0; e < KMAX; ++e) {
+        bd[e] = -1;
+        bi[e] = -1;
       }
-      if (!changed) stop = 1;
+      for (int64_t i = t; i < nv; i += KS_T) {
+        const double v = xs[i];
+        const double cc = c[sk_assign<K>(v, c)];
+        const double dd = (v - cc) * (v - cc);
+        for (int e = 0; e < m; ++e) {
+          // later samples of this thread have larger positions: on equal (d, value) the
+          // earlier one stays ahead
+          if (bi[e] < 0 || dd > bd[e] || (dd == bd[e] && v < xs[bi[e]])) {
+            for (int f = m - 1; f > e; --f) {
+              bd[f] = bd[f - 1];
+              bi[f] = bi[f - 1];
+            }
+            bd[e] = dd;
+            bi[e] = i;
+            break;
+          }
+        }
+      }
+      for (int e = 0; e < m; ++e) {
+        double d0 = bd[0];
+        long long i0 = bi[0];
+        for (int o = 32; o > 0; o >>= 1) {
+          const double d1 = __shfl_xor(d0, o, 64);
+          const long long i1 = __shfl_xor(i0, o, 64);
+          if (i1 >= 0 && (i0 < 0 || d1 > d0 || (d1 == d0 && (xs[i1] < xs[i0] || (xs[i1] == xs[i0] && i1 < i0))))) {
+            d0 = d1;
+            i0 = i1;
+          }
+        }
+        if ((t & 63) == 0) {
+          rd[t >> 6][0] = d0;
+          ri[t >> 6][0] = i0;
+        }
+        __syncthreads();
+        if (t == 0) {
+          double db = -1;
+          long long ib = -1;
+          for (int w = 0; w < KS_T / 64; ++w) {
+            const long long i1 = ri[w][0];
+            const double d1 = rd[w][0];
+            if (i1 >= 0 && (ib < 0 || d1 > db || (d1 == db && (xs[i1] < xs[ib] || (xs[i1] == xs[ib] && i1 < ib))))) {
+              db = d1;
+              ib = i1;
+            }
+          }
+          far_sh[e] = ib;
+        }
+        __syncthreads();
+        if (far_sh[e] >= 0 && bi[0] == far_sh[e]) {  // the owner drops its head
+          for (int f = 0; f + 1 < m; ++f) {
+            bd[f] = bd[f + 1];
+            bi[f] = bi[f + 1];
+          }
+          bd[m - 1] = -1;
+          bi[m - 1] = -1;
+        }
+        __syncthreads();
+      }
+      if (t == 0) {
+        // _relocate_empty_clusters_dense: the e-th empty cluster (ascending id) takes the e-th
+        // farthest sample; its old cluster loses it (its label stays)
+        int pk = 0;
+        for (int j = 0; j < K; ++j) {
+          if (cnt[j]) continue;
+          const long long fi = far_sh[pk++];
+          if (fi < 0) continue;
+          const int oj = sk_assign<K>(xs[fi], c);
+          sum[oj] -= q[fi];
+          cnt[oj] -= 1;
+          sum[j] = q[fi];
+          cnt[j] = 1;
+          R.reloc += 1;
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      double shift = 0;
+      double nc[KMAX];
+      for (int j = 0; j < K; ++j) {
+        nc[j] = cnt[j] ? ldexp((double)sum[j] / (double)cnt[j], -s) : c[j];
+        const double dd = nc[j] - c[j];
+        shift += dd * dd;
+      }
+      // labels equal to the previous iteration's: same cumulative counts and ids per
+      // non-empty sorted rank
+      bool same = have_old;
+      if (same) {
+        for (int p = 0; p < K && same; ++p) {
+          const int64_t a0 = p ? cle[p - 1] : 0, b0 = p ? ocle[p - 1] : 0;
+          if (cle[p] != ocle[p]) same = false;
+          else if (cle[p] - a0 > 0 && ids[p] != oids[p]) same = false;
+          (void)b0;
+        }
+      }
+      for (int j = 0; j < K; ++j) {
+        oldc[j] = c[j];
+        c[j] = nc[j];
+      }
+      if (same) stop = 2;
+      else if (shift <= st->tol) stop = 1;
+      for (int p = 0; p < K; ++p) {
+        ocle[p] = cle[p];
+        oids[p] = ids[p];
+      }
+      have_old = 1;
     }
     __syncthreads();
     if (stop) break;
   }
   if (t == 0) {
-    if (stop == 2) {
-      st->fallback = 1;
-    } else {
-      for (int j = 0; j < K; ++j) st->center[j] = c[j];
-      st->iters = it > max_iter ? max_iter : it;
-      st->converged = 1;
+    R.iters = it < max_iter ? it + 1 : max_iter;
+    R.strict = stop == 2;
+  }
+  __syncthreads();
+  // final labels: strict -> the last assignment (made with oldc); else an E-step with c
+  if (stop != 2) {
+    km_assign_all<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
+  }
+  if (t == 0) {
+    // inertia of the final labels (their own sums, before any relocation) and final centres
+    long long n_of[KMAX], s_of[KMAX];
+    u128 q_of[KMAX];
+    int64_t c0 = 0;
+    long long s0 = 0;
+    u128 q0 = 0;
+    for (int p = 0; p < K; ++p) {
+      n_of[ids[p]] = cle[p] - c0;
+      s_of[ids[p]] = sle[p] - s0;
+      q_of[ids[p]] = U(qle[p]) - q0;
+      c0 = cle[p];
+      s0 = sle[p];
+      q0 = U(qle[p]);
+    }
+    double I = 0;
+    for (int j = 0; j < K; ++j) {
+      if (!n_of[j]) continue;
+      const double cs = ldexp(c[j], s);
+      I += (u128_to_double(q_of[j]) - 2.0 * cs * (double)s_of[j]) + (double)n_of[j] * cs * cs;
+    }
+    R.inertia = ldexp(I, -2 * s);
+    for (int j = 0; j < K; ++j) {
+      R.cen[j] = c[j];
+      R.lcen[j] = stop == 2 ? oldc[j] : c[j];
+    }
+    for (int p = 0; p < K; ++p) {
+      R.cut[p] = cle[p];
+      R.ids[p] = ids[p];
     }
   }
 }
 
+// sklearn's _is_same_clustering(labels_a, labels_b): every cluster of a lies inside one cluster
+// of b, i.e. every cut of b (between non-empty sorted ranks) is a cut of a
+template <int K>
+__device__ bool same_clustering(const SkRun &a, const SkRun &b) {
+  for (int p = 0; p + 1 < K; ++p) {
+    const long long cb = b.cut[p];
+    if (cb == 0 || cb == b.cut[K - 1]) continue;
+    bool found = false;
+    for (int q = 0; q + 1 < K; ++q) found |= a.cut[q] == cb;
+    if (!found) return false;
+  }
+  return true;
+}
+
+// winner of the n_init runs; top cluster by `rule`: 0 the largest centre among non-empty
+// clusters; 1 (k = 2, multispecies :126-135) the cluster of larger mean positive value when
+// both hold a positive sample, else sklearn's cluster 0 (the reference's NaN comparison);
+// 2 (k = 2, ecoli :75-84) the larger cluster mean when both are non-empty, else cluster 0
+template <int K>
+__global__ void km_best_kernel(KmState *st, int nrun, int rule) {
+  if (threadIdx.x != 0) return;
+  int best = 0;
+  for (int r = 1; r < nrun; ++r)
+    if (st->run[r].inertia < st->run[best].inertia && !same_clustering<K>(st->run[r], st->run[best])) best = r;
+  st->best = best;
+  const SkRun &B = st->run[best];
+  for (int j = 0; j < K; ++j) st->center[j] = B.cen[j];
+  st->iters = B.iters;
+  long long n_of[KMAX];
+  long long c0 = 0;
+  for (int p = 0; p < K; ++p) {
+    n_of[B.ids[p]] = B.cut[p] - c0;
+    c0 = B.cut[p];
+  }
+  int top = -1;
+  for (int j = 0; j < K; ++j)
+    if (n_of[j] > 0 && (top < 0 || B.lcen[j] > B.lcen[top])) top = j;
+  if (top < 0) top = 0;
+  if (K == 2 && rule == 2 && (n_of[0] == 0 || n_of[1] == 0)) top = 0;
+  if (K == 2 && rule == 1) {
+    // lower interval = sorted rank 0; samples <= 0 fill it first
+    const int lo_id = B.ids[0], hi_id = B.ids[1];
+    const long long nl = n_of[lo_id], nh = n_of[hi_id], z = st->nle0;
+    const long long zl = z < nl ? z : nl, zh = z - zl;
+    const bool pos_lo = nl - zl > 0, pos_hi = nh - zh > 0;
+    top = (pos_lo && pos_hi) ? hi_id : 0;
+  }
+  st->top = top;
+}
+
+// samples <= 0 (rule 1), counted on the sorted array: whole buckets below, the straddling one
+__global__ void km_count_le0_kernel(const double *__restrict__ xs, const unsigned long long *__restrict__ off,
+                                    const double *__restrict__ geo, KmState *st) {
+  __shared__ unsigned long long acc;
+  const int64_t nv = (int64_t)st->nvalid;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
+  if (nv == 0) {
+    if (threadIdx.x == 0) st->nle0 = 0;
+    return;
+  }
+  const double mn = geo[0], inv = geo[1];
+  const int b0 = km_bucket(0.0, mn, inv);
+  const int64_t lo = mn > 0.0 ? 0 : (int64_t)off[b0], hi = mn > 0.0 ? 0 : (int64_t)off[b0 + 1];
+  unsigned long long c = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) c += xs[i] <= 0.0;
+  c = hrf::wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&acc, c);
+  __syncthreads();
+  if (threadIdx.x == 0) st->nle0 = mn > 0.0 ? 0 : lo + (long long)acc;
+}
+
+template <int K>
+__global__ void km_label_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
+                                const KmState *st, int32_t *__restrict__ labels, uint8_t *__restrict__ top) {
+  double c[K];
+  const SkRun &B = st->run[st->best];
+#pragma unroll
+  for (int j = 0; j < K; ++j) c[j] = B.lcen[j];
+  const int jt = st->top;
+  const bool err = st->error != 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool ok = (!valid || valid[i]) && !err;
+    const int bj = ok ? sk_assign<K>(x[i], c) : -1;
+    if (labels) labels[i] = bj;
+    if (top) top[i] = (uint8_t)(bj == jt);
+  }
+}
+
+// ---- workspace ---------------------------------------------------------------------------------
 struct SortWs {
   KmState *st;
   double *geo;
   uint32_t *key_in, *key;
   unsigned long long *off;
-  double *xs;
+  double *xs, *xr;
   long long *q, *prefix;
+  U128 *q2, *p2, *part;
+  unsigned long long *nsel;
   void *tmp;
   size_t tmp_bytes;
 };
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+int64_t nblocks(int64_t n) { return std::max<int64_t>(1, (n + PB - 1) / PB); }
+
 hrf_status sort_tmp_bytes(int64_t n, size_t *bytes) {
-  size_t a = 0, b = 0;
+  size_t a = 0, b = 0, c = 0, d = 0;
   const size_t m = (size_t)std::max<int64_t>(n, 1);
   HRF_HIP(rocprim::radix_sort_pairs(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr, (const double *)nullptr,
                                     (double *)nullptr, m, 0, KM_NB_BITS, (hipStream_t)0));
   HRF_HIP(rocprim::inclusive_scan(nullptr, b, (const unsigned long long *)nullptr, (unsigned long long *)nullptr, m,
                                   rocprim::plus<unsigned long long>(), (hipStream_t)0));
-  *bytes = std::max(a, b);
+  HRF_HIP(rocprim::inclusive_scan(nullptr, c, (const U128 *)nullptr, (U128 *)nullptr, m, U128Plus(), (hipStream_t)0));
+  HRF_HIP(rocprim::select(nullptr, d, (const double *)nullptr, (const uint8_t *)nullptr, (double *)nullptr,
+                          (unsigned long long *)nullptr, m, (hipStream_t)0));
+  *bytes = std::max(std::max(a, b), std::max(c, d));
   return HRF_OK;
 }
 
@@ -557,7 +1072,8 @@ int64_t sort_ws_bytes(int64_t n, size_t tmp_bytes) {
   const size_t m = (size_t)std::max<int64_t>(n, 1);
   return (int64_t)(align256(sizeof(KmState)) + 256 + 2 * align256(sizeof(uint32_t) * m) +
                    align256(sizeof(unsigned long long) * (KM_NB + 1)) + 2 * align256(sizeof(double) * m) +
-                   align256(sizeof(long long) * (m + 1)) + align256(tmp_bytes));
+                   2 * align256(sizeof(long long) * (m + 1)) + 2 * align256(sizeof(U128) * (m + 1)) +
+                   align256(sizeof(U128) * NRUN * NTMAX * nblocks(n)) + 256 + align256(tmp_bytes));
 }
 
 SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
@@ -576,20 +1092,30 @@ SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   w += align256(sizeof(unsigned long long) * (KM_NB + 1));
   ws.xs = (double *)w;
   w += align256(sizeof(double) * m);
-  ws.q = (long long *)w;
+  ws.xr = (double *)w;
   w += align256(sizeof(double) * m);
+  ws.q = (long long *)w;
+  w += align256(sizeof(long long) * (m + 1));
   ws.prefix = (long long *)w;
   w += align256(sizeof(long long) * (m + 1));
+  ws.q2 = (U128 *)w;
+  w += align256(sizeof(U128) * (m + 1));
+  ws.p2 = (U128 *)w;
+  w += align256(sizeof(U128) * (m + 1));
+  ws.part = (U128 *)w;
+  w += align256(sizeof(U128) * NRUN * NTMAX * nblocks(n));
+  ws.nsel = (unsigned long long *)w;
+  w += 256;
   ws.tmp = w;
   ws.tmp_bytes = tmp_bytes;
   return ws;
 }
 
-// Enqueue the sorted path (sort unless `reuse`, iterations, labels) and the read-back of its
-// final state into *fin (host); the caller synchronises before km_sorted_finish reads it.
+// Enqueue one KMeans(k) fit: sort (unless `reuse`), k-means++ for all runs, Lloyd, winner,
+// labels / top mask, and the read-back of the final state into *fin (host).
 template <int K>
-hrf_status km_sorted_launch(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
-                            uint8_t *top, const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
+hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int max_iter, int n_init, int rule,
+                        int32_t *labels, uint8_t *top, const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
   KmState *st = ws.st;
   const unsigned g = hrf::stream_grid(n);
   if (!reuse) {
@@ -597,107 +1123,90 @@ hrf_status km_sorted_launch(const double *x, const uint8_t *valid, int64_t n, in
     init.lo_bits = ~0ull;
     HRF_HIP(hipMemcpyAsync(st, &init, sizeof(KmState), hipMemcpyHostToDevice, s));
     if (n > 0) km_minmax_kernel<<<std::min<unsigned>(g, 512), 256, 0, s>>>(x, valid, n, st);
+    km_scale_kernel<<<1, 1, 0, s>>>(st);
     HRF_LAUNCHED();
+    if (n > 0) {
+      km_bucket_init_kernel<<<1, 1, 0, s>>>(st, ws.geo);
+      km_bucket_key_kernel<<<g, 256, 0, s>>>(x, valid, n, ws.geo, ws.key_in);
+      HRF_LAUNCHED();
+      size_t tb = ws.tmp_bytes;
+      HRF_HIP(rocprim::radix_sort_pairs(ws.tmp, tb, ws.key_in, ws.key, x, ws.xs, (size_t)n, 0, KM_NB_BITS, s));
+      km_bucket_bounds_kernel<<<hrf::stream_grid(std::max<int64_t>(n, KM_NB + 1)), 256, 0, s>>>(
+          ws.key, ws.xs, n, st, ws.off, ws.q, ws.q2, ws.prefix, ws.p2);
+      HRF_LAUNCHED();
+      // entries past the valid values (invalid ones, sorted last) are never read back
+      tb = ws.tmp_bytes;
+      HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, (const unsigned long long *)ws.q, (unsigned long long *)ws.prefix + 1,
+                                      (size_t)n, rocprim::plus<unsigned long long>(), s));
+      tb = ws.tmp_bytes;
+      HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, ws.q2, ws.p2 + 1, (size_t)n, U128Plus(), s));
+      if (valid) {  // the valid samples in raster order (sklearn's sample order)
+        tb = ws.tmp_bytes;
+        HRF_HIP(rocprim::select(ws.tmp, tb, x, valid, ws.xr, ws.nsel, (size_t)n, s));
+      }
+      km_tol_kernel<<<1, 1, 0, s>>>(ws.prefix, ws.p2, st);
+      km_count_le0_kernel<<<1, 1024, 0, s>>>(ws.xs, ws.off, ws.geo, st);
+      HRF_LAUNCHED();
+    }
   }
-  km_init_kernel<<<1, 1, 0, s>>>(st, K);
-  HRF_LAUNCHED();
-  if (!reuse && n > 0) {
-    km_bucket_init_kernel<<<1, 1, 0, s>>>(st, ws.geo);
-    km_bucket_key_kernel<<<g, 256, 0, s>>>(x, valid, n, ws.geo, ws.key_in);
-    HRF_LAUNCHED();
-    size_t tb = ws.tmp_bytes;
-    HRF_HIP(rocprim::radix_sort_pairs(ws.tmp, tb, ws.key_in, ws.key, x, ws.xs, (size_t)n, 0, KM_NB_BITS, s));
-    km_bucket_bounds_kernel<<<hrf::stream_grid(std::max<int64_t>(n, KM_NB + 1)), 256, 0, s>>>(ws.key, ws.xs, n, st, ws.off, ws.q, ws.prefix);
-    HRF_LAUNCHED();
-    tb = ws.tmp_bytes;
-    // entries past the valid values (invalid ones, sorted last) are never read back: the scan
-    // covers all n in unsigned (wrapping) arithmetic; prefixes up to nvalid are the exact sums
-    HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, (const unsigned long long *)ws.q, (unsigned long long *)ws.prefix + 1,
-                                    (size_t)n, rocprim::plus<unsigned long long>(), s));
-  }
-  km_sorted_iter_kernel<K><<<1, KS_T, 0, s>>>(ws.xs, ws.q, ws.prefix, ws.off, ws.geo, st, max_iter);
-  HRF_LAUNCHED();
-  if (n > 0) km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
-  HRF_LAUNCHED();
-  HRF_HIP(hipMemcpyAsync(fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
-  return HRF_OK;
-}
-
-// After the synchronisation: NaN input or merging centres send the call to the streaming
-// path, which recomputes everything (labels, top mask) in the workspace's state block.
-template <int K>
-hrf_status km_sorted_finish(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
-                            uint8_t *top, double *centers_host, int32_t *iters_host, const SortWs &ws,
-                            hipStream_t s, const KmState &fin) {
-  KmState *st = ws.st;
-  if (fin.fallback) {
-    // the streaming path recomputes everything from scratch in its own state block
-    if (hrf_status r = km_run<K>(x, valid, n, max_iter, labels, top, centers_host, iters_host, st, s)) return r;
+  if (n == 0) {
+    if (fin) HRF_HIP(hipMemcpyAsync(fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
     return HRF_OK;
   }
-  if (centers_host)
-    for (int j = 0; j < K; ++j) centers_host[j] = fin.center[j];
-  if (iters_host) *iters_host = fin.iters;
+  // the random stream does not depend on the data, only on the number of valid samples: the
+  // host needs it before the launches.  n itself when there is no mask; with a mask the count
+  // comes from the device (one synchronisation, masked calls only).
+  int64_t nv = n;
+  if (valid) {
+    unsigned long long h = 0;
+    HRF_HIP(hipMemcpyAsync(&h, &st->nvalid, sizeof(h), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+    nv = (int64_t)h;
+  }
+  const Draws d = make_draws(std::max<int64_t>(nv, 1), K, n_init, 0u);
+  const double *xr = valid ? ws.xr : x;
+  const int nblk = (int)nblocks(nv);
+  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d);
+  HRF_LAUNCHED();
+  for (int c = 1; c < K; ++c) {
+    km_pp_pass_kernel<0><<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk);
+    km_pp_pick_kernel<<<n_init, PT, 0, s>>>(xr, st, d, ws.part, nblk, c);
+    km_pp_pass_kernel<1><<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk);
+    km_pp_choose_kernel<<<n_init, PT, 0, s>>>(st, d, ws.part, nblk, c);
+    HRF_LAUNCHED();
+  }
+  km_lloyd_kernel<K><<<n_init, KS_T, 0, s>>>(ws.xs, ws.q, ws.q2, ws.prefix, ws.p2, ws.off, ws.geo, st, max_iter);
+  km_best_kernel<K><<<1, 64, 0, s>>>(st, n_init, rule);
+  km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
+  HRF_LAUNCHED();
+  if (fin) HRF_HIP(hipMemcpyAsync(fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
   return HRF_OK;
 }
 
-template <int K>
-hrf_status km_run_sorted(const double *x, const uint8_t *valid, int64_t n, int max_iter, int32_t *labels,
-                         uint8_t *top, double *centers_host, int32_t *iters_host, const SortWs &ws, int reuse,
-                         hipStream_t s) {
-  KmState fin;
-  if (hrf_status r = km_sorted_launch<K>(x, valid, n, max_iter, labels, top, ws, reuse, s, &fin)) return r;
-  HRF_HIP(hipStreamSynchronize(s));
-  return km_sorted_finish<K>(x, valid, n, max_iter, labels, top, centers_host, iters_host, ws, s, fin);
-}
-
-hrf_status km_launch_k(int k, const double *x, const uint8_t *valid, int64_t n, int max_iter, uint8_t *top,
-                       const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
+hrf_status km_launch_k(int k, const double *x, const uint8_t *valid, int64_t n, int max_iter, int n_init, int rule,
+                       int32_t *labels, uint8_t *top, const SortWs &ws, int reuse, hipStream_t s, KmState *fin) {
   switch (k) {
 #define HRF_KML(KK) \
-  case KK: return km_sorted_launch<KK>(x, valid, n, max_iter, nullptr, top, ws, reuse, s, fin);
+  case KK: return km_sk_launch<KK>(x, valid, n, max_iter, n_init, rule, labels, top, ws, reuse, s, fin);
     HRF_KML(1) HRF_KML(2) HRF_KML(3) HRF_KML(4) HRF_KML(5) HRF_KML(6) HRF_KML(7)
 #undef HRF_KML
-    default: return km_sorted_launch<8>(x, valid, n, max_iter, nullptr, top, ws, reuse, s, fin);
+    default: return km_sk_launch<8>(x, valid, n, max_iter, n_init, rule, labels, top, ws, reuse, s, fin);
   }
 }
 
-hrf_status km_finish_k(int k, const double *x, const uint8_t *valid, int64_t n, int max_iter, uint8_t *top,
-                       const SortWs &ws, hipStream_t s, const KmState &fin) {
-  switch (k) {
-#define HRF_KMF(KK) \
-  case KK: return km_sorted_finish<KK>(x, valid, n, max_iter, nullptr, top, nullptr, nullptr, ws, s, fin);
-    HRF_KMF(1) HRF_KMF(2) HRF_KMF(3) HRF_KMF(4) HRF_KMF(5) HRF_KMF(6) HRF_KMF(7)
-#undef HRF_KMF
-    default: return km_sorted_finish<8>(x, valid, n, max_iter, nullptr, top, nullptr, nullptr, ws, s, fin);
-  }
+hrf_status check_args(int32_t k, int64_t n, int32_t max_iter, int32_t n_init, int32_t rule, const void *work,
+                      const double *x) {
+  HRF_REQUIRE(k >= 1 && k <= KMAX, "kmeans_1d: k must be 1..8");
+  HRF_REQUIRE(n >= 0 && n < ((int64_t)1 << 40) && max_iter >= 1 && work, "kmeans_1d: bad arguments");
+  HRF_REQUIRE(n_init >= 1 && n_init <= NRUN, "kmeans_1d: n_init must be 1..10");
+  HRF_REQUIRE(rule >= 0 && rule <= 2, "kmeans_1d: top rule must be 0, 1 or 2");
+  HRF_REQUIRE(n == 0 || x, "kmeans_1d: null input");
+  return HRF_OK;
 }
 
 }  // namespace
 
 extern "C" {
-
-int64_t hrf_kmeans_state_bytes(void) { return (int64_t)sizeof(KmState); }
-
-hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
-                         int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host, void *state_ws,
-                         hrf_stream_t stream) {
-  HRF_REQUIRE(k >= 1 && k <= KMAX, "kmeans_1d: k must be 1..8");
-  HRF_REQUIRE(n >= 0 && max_iter >= 1 && state_ws, "kmeans_1d: bad arguments");
-  HRF_REQUIRE(n == 0 || x, "kmeans_1d: null input");
-  hipStream_t s = (hipStream_t)stream;
-  KmState *st = (KmState *)state_ws;
-  switch (k) {
-    case 1: return km_run<1>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 2: return km_run<2>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 3: return km_run<3>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 4: return km_run<4>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 5: return km_run<5>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 6: return km_run<6>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    case 7: return km_run<7>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-    default: return km_run<8>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, st, s);
-  }
-}
 
 int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n) {
   size_t tb = 0;
@@ -705,12 +1214,23 @@ int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n) {
   return sort_ws_bytes(n, tb);
 }
 
+hrf_status hrf_kmeans_draws(int64_t nv, int32_t k, int32_t n_init, int64_t *first_host, double *draws_host) {
+  HRF_REQUIRE(nv >= 1 && k >= 1 && k <= KMAX && n_init >= 1 && n_init <= NRUN, "kmeans_draws: bad arguments");
+  const Draws d = make_draws(nv, k, n_init, 0u);
+  int64_t o = 0;
+  for (int r = 0; r < n_init; ++r) {
+    first_host[r] = d.first[r];
+    for (int c = 1; c < k; ++c)
+      for (int t = 0; t < d.nt; ++t) draws_host[o++] = ldexp((double)d.m[r][c - 1][t], -53);
+  }
+  return HRF_OK;
+}
+
 hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
-                                int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host,
-                                void *work, int64_t work_bytes, int32_t reuse_sort, hrf_stream_t stream) {
-  HRF_REQUIRE(k >= 1 && k <= KMAX, "kmeans_1d: k must be 1..8");
-  HRF_REQUIRE(n >= 0 && max_iter >= 1 && work, "kmeans_1d: bad arguments");
-  HRF_REQUIRE(n == 0 || x, "kmeans_1d: null input");
+                                int32_t n_init, int32_t top_rule, int32_t *labels, uint8_t *top_mask,
+                                double *centers_host, int32_t *iters_host, void *work, int64_t work_bytes,
+                                int32_t reuse_sort, hrf_stream_t stream) {
+  if (hrf_status r = check_args(k, n, max_iter, n_init, top_rule, work, x)) return r;
   const int64_t need = hrf_kmeans_sorted_workspace_bytes(n);
   HRF_REQUIRE(need > 0, "kmeans_1d: workspace size query failed");
   if (work_bytes < need) {
@@ -721,21 +1241,23 @@ hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n
   if (hrf_status r = sort_tmp_bytes(n, &tb)) return r;
   const SortWs ws = carve(work, n, tb);
   hipStream_t s = (hipStream_t)stream;
-  switch (k) {
-#define HRF_KMS(KK) \
-  case KK: return km_run_sorted<KK>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, ws, reuse_sort, s);
-    HRF_KMS(1) HRF_KMS(2) HRF_KMS(3) HRF_KMS(4) HRF_KMS(5) HRF_KMS(6) HRF_KMS(7)
-#undef HRF_KMS
-    default: return km_run_sorted<8>(x, valid, n, max_iter, labels, top_mask, centers_host, iters_host, ws, reuse_sort, s);
-  }
+  static thread_local KmState *fin = nullptr;
+  if (!fin) HRF_HIP(hipHostMalloc((void **)&fin, sizeof(KmState), hipHostMallocDefault));
+  if (hrf_status r = km_launch_k(k, x, valid, n, max_iter, n_init, top_rule, labels, top_mask, ws, reuse_sort, s, fin))
+    return r;
+  HRF_HIP(hipStreamSynchronize(s));
+  HRF_REQUIRE(!fin->error, "kmeans_1d: input contains NaN (sklearn KMeans raises ValueError)");
+  if (centers_host)
+    for (int j = 0; j < k; ++j) centers_host[j] = fin->center[j];
+  if (iters_host) *iters_host = fin->iters;
+  return HRF_OK;
 }
 
 hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int64_t n, int32_t k1, int32_t k2,
-                                     int32_t max_iter, uint8_t *top1, uint8_t *top2, void *work, int64_t work_bytes,
-                                     hrf_stream_t stream) {
-  HRF_REQUIRE(k1 >= 1 && k1 <= KMAX && k2 >= 1 && k2 <= KMAX, "kmeans_1d_pair: k must be 1..8");
-  HRF_REQUIRE(n >= 0 && max_iter >= 1 && work, "kmeans_1d_pair: bad arguments");
-  HRF_REQUIRE(n == 0 || x, "kmeans_1d_pair: null input");
+                                     int32_t max_iter, int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1,
+                                     uint8_t *top2, void *work, int64_t work_bytes, hrf_stream_t stream) {
+  if (hrf_status r = check_args(k1, n, max_iter, n_init, rule1, work, x)) return r;
+  if (hrf_status r = check_args(k2, n, max_iter, n_init, rule2, work, x)) return r;
   const int64_t need = hrf_kmeans_sorted_workspace_bytes(n);
   HRF_REQUIRE(need > 0, "kmeans_1d_pair: workspace size query failed");
   if (work_bytes < need) {
@@ -746,18 +1268,14 @@ hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int6
   if (hrf_status r = sort_tmp_bytes(n, &tb)) return r;
   const SortWs ws = carve(work, n, tb);
   hipStream_t s = (hipStream_t)stream;
-  // both runs enqueued before the one synchronisation; the second reuses the sort.  A
-  // fallback of either (rare) then reruns that k on the streaming path, after both.
-  // pinned read-back slots (one pair per host thread, kept for the thread's lifetime), so the
-  // first state copy does not block the host before the second run is enqueued
+  // both fits enqueued (the second reuses the sort), one synchronisation for the NaN check
   static thread_local KmState *fin = nullptr;
-  if (!fin) HRF_HIP(hipHostMalloc((void **)&fin, 2 * sizeof(KmState), hipHostMallocDefault));
-  if (hrf_status r = km_launch_k(k1, x, valid, n, max_iter, top1, ws, 0, s, &fin[0])) return r;
-  if (hrf_status r = km_launch_k(k2, x, valid, n, max_iter, top2, ws, 1, s, &fin[1])) return r;
+  if (!fin) HRF_HIP(hipHostMalloc((void **)&fin, sizeof(KmState), hipHostMallocDefault));
+  if (hrf_status r = km_launch_k(k1, x, valid, n, max_iter, n_init, rule1, nullptr, top1, ws, 0, s, nullptr)) return r;
+  if (hrf_status r = km_launch_k(k2, x, valid, n, max_iter, n_init, rule2, nullptr, top2, ws, 1, s, fin)) return r;
   HRF_HIP(hipStreamSynchronize(s));
-  const KmState f1 = fin[0], f2 = fin[1];
-  if (hrf_status r = km_finish_k(k1, x, valid, n, max_iter, top1, ws, s, f1)) return r;
-  return km_finish_k(k2, x, valid, n, max_iter, top2, ws, s, f2);
+  HRF_REQUIRE(!fin->error, "kmeans_1d_pair: input contains NaN (sklearn KMeans raises ValueError)");
+  return HRF_OK;
 }
 
 }  // extern "C"

@@ -95,11 +95,10 @@ hrf_status label_conn2_deferred(hrf_seg_ctx *c, const uint8_t *mask, int32_t *la
   return HRF_OK;
 }
 
-// KMeans(k) top-cluster mask; `reuse` when the previous call sorted the same x
-hrf_status kmeans_top(hrf_seg_ctx *c, const double *x, int k, int reuse, uint8_t *top, hipStream_t s) {
-  double cen[8];
-  int32_t it = 0;
-  return hrf_kmeans_1d_sorted(x, nullptr, c->n, k, 300, nullptr, top, cen, &it, c->km, c->km_bytes, reuse, s);
+// KMeans(k) top-cluster mask (rule: see hrf.h); `reuse` when the previous call sorted the same x
+hrf_status kmeans_top(hrf_seg_ctx *c, const double *x, int k, int rule, int reuse, uint8_t *top, hipStream_t s) {
+  return hrf_kmeans_1d_sorted(x, nullptr, c->n, k, 300, 10, rule, nullptr, top, nullptr, nullptr, c->km, c->km_bytes,
+                              reuse, s);
 }
 
 }  // namespace
@@ -177,7 +176,7 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   uint8_t *rough = c->m[0], *interior = c->m[1], *a = c->m[2], *b = c->m[3], *d = c->m[4];
   int32_t *lab1 = c->l[0], *seeds = c->l[1], *ws = c->l[2], *lab3 = c->l[3];
   HRF_TRY(hrf_channel_sum(stack, n, C, nullptr, 1, 0, c->cn, s));               // :71-72
-  HRF_TRY(hrf_kmeans_1d_sorted_pair(c->cn, nullptr, c->n, 2, 3, 300, rough, interior, c->km, c->km_bytes,
+  HRF_TRY(hrf_kmeans_1d_sorted_pair(c->cn, nullptr, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes,
                                     s));                                        // :73-94
   HRF_TRY(hrf_remove_small_holes(interior, H, W, 64, 1, a, c->parent, c->size, s));   // :95
   HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
@@ -234,7 +233,7 @@ hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t 
   HRF_TRY(hrf_nl_means_2d(norm, H, W, 7, 11, 0.02, 0.0, nl, s));               // :108
   HRF_TRY(hrf_pad_edge_f64(nl, H, W, 5, c->pad, s));                            // :109
   HRF_TRY(hrf_enhance_2d(c->pad, H + 10, W + 10, W + 10, 11, 9, fin, s));      // :110-124
-  HRF_TRY(kmeans_top(c, fin, 2, 0, rough, s));                                  // :125-135
+  HRF_TRY(kmeans_top(c, fin, 2, 1, 0, rough, s));                               // :125-135
   HRF_TRY(hrf_binary_erosion(rough, H, W, 1, a, s));                            // :136
   HRF_TRY(hrf_binary_dilation(a, H, W, b, s));
   HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 1, a, c->parent, c->size, s));  // :137
@@ -242,7 +241,7 @@ hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t 
   HRF_TRY(hrf_fill_holes(rough, H, W, d, c->parent, c->size, s));              // :139
   HRF_TRY(hrf_and_u8(b, d, n, e, s));                                          // :140
   HRF_TRY(label_conn2_deferred(c, e, seeds, s));
-  HRF_TRY(kmeans_top(c, nl, 2, 0, bkg, s));                                     // :141-149
+  HRF_TRY(kmeans_top(c, nl, 2, 1, 0, bkg, s));                                  // :141-149
   const int32_t nseeds = c->hpin[0];  // read back by the KMeans synchronisation
   double *final_bkg = final_bkg_out ? final_bkg_out : c->cn;
   HRF_TRY(hrf_mask_mul_f64(fin, bkg, n, final_bkg, s));                         // :150

@@ -273,17 +273,13 @@ def nl_means_2d(img, patch_size=7, patch_distance=11, h=0.1, sigma=0.0):
 
 
 # ---- a8 -------------------------------------------------------------------------------------
-_KM_STATE = {}
 
 
-# "sorted" (one sort + step searches) or "stream" (one pass per Lloyd iteration); same results
-KMEANS_PATH = os.environ.get("HRF_KMEANS_PATH", "sorted")
-
-
-def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, path=None, share=None):
-    """1-D KMeans (sklearn KMeans(k, random_state=0) restated, see kmeans.hip)
-    -> labels int32 (or None), top-cluster mask u8, centres (list), iterations.
-    share: a dict passed to successive calls on the SAME x / valid so the sorted path sorts once."""
+def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, share=None, rule=0, n_init=10):
+    """sklearn KMeans(k, random_state=0, n_init=10).fit_predict on the values of x (kmeans.hip)
+    -> labels int32 (sklearn's cluster ids, or None), top-cluster mask u8 (by `rule`, see
+    include/hrf.h), centres (list, sklearn order), iterations.
+    share: a dict passed to successive calls on the SAME x / valid so the sort is done once."""
     import ctypes
     import numpy as np
     x = _dev(x, torch.float64, "x")
@@ -294,16 +290,6 @@ def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, path=None, share
     top = torch.empty(x.shape, dtype=torch.uint8, device=dev)
     cen = np.zeros(k, np.float64)
     it = ctypes.c_int32(0)
-    if (path or KMEANS_PATH) == "stream":
-        key = (dev, _stream())        # one workspace per stream: concurrent tiles must not share it
-        st = _KM_STATE.get(key)
-        if st is None:
-            nb = _lib.lib().hrf_kmeans_state_bytes()
-            st = torch.zeros(int(nb), dtype=torch.uint8, device=dev)
-            _KM_STATE[key] = st
-        _lib.call("hrf_kmeans_1d", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
-                  ctypes.addressof(it), _ptr(st), _stream())
-        return labels, top, cen.tolist(), it.value
     ident = (x.data_ptr(), n, v.data_ptr() if v is not None else 0)
     reuse = share is not None and share.get("ident") == ident
     if reuse:
@@ -315,12 +301,12 @@ def kmeans_1d(x, k, valid=None, max_iter=300, want_labels=True, path=None, share
         ws = torch.empty(nb, dtype=torch.uint8, device=dev)
         if share is not None:
             share.update(ident=ident, ws=ws, x=x, valid=v)   # keep the inputs alive with the sort
-    _lib.call("hrf_kmeans_1d_sorted", _ptr(x), _ptr(v), n, k, max_iter, _ptr(labels), _ptr(top), cen.ctypes.data,
-              ctypes.addressof(it), _ptr(ws), ws.numel(), int(reuse), _stream())
+    _lib.call("hrf_kmeans_1d_sorted", _ptr(x), _ptr(v), n, k, max_iter, n_init, rule, _ptr(labels), _ptr(top),
+              cen.ctypes.data, ctypes.addressof(it), _ptr(ws), ws.numel(), int(reuse), _stream())
     return labels, top, cen.tolist(), it.value
 
 
-def kmeans_1d_pair(x, k1, k2, valid=None, max_iter=300):
+def kmeans_1d_pair(x, k1, k2, valid=None, max_iter=300, rules=(2, 0), n_init=10):
     """top-cluster masks of KMeans(k1) and KMeans(k2) on the same x with one sort and one host
     synchronisation (ecoli measurement.py:73-94: k = 2 and k = 3 on image_cn)"""
     x = _dev(x, torch.float64, "x")
@@ -332,9 +318,19 @@ def kmeans_1d_pair(x, k1, k2, valid=None, max_iter=300):
     if nb <= 0:
         raise _lib.HrfError("hrf_kmeans_sorted_workspace_bytes failed")
     ws = torch.empty(nb, dtype=torch.uint8, device=x.device)
-    _lib.call("hrf_kmeans_1d_sorted_pair", _ptr(x), _ptr(v), n, k1, k2, max_iter, _ptr(top1), _ptr(top2), _ptr(ws),
-              ws.numel(), _stream())
+    _lib.call("hrf_kmeans_1d_sorted_pair", _ptr(x), _ptr(v), n, k1, k2, max_iter, n_init, rules[0], rules[1],
+              _ptr(top1), _ptr(top2), _ptr(ws), ws.numel(), _stream())
     return top1, top2
+
+
+def kmeans_draws(nv, k, n_init=10):
+    """the fit's random stream as libhrf replays it (host): first-centre ranks, trial draws"""
+    import numpy as np
+    nt = 2 + int(np.log(k))
+    first = np.zeros(n_init, np.int64)
+    draws = np.zeros(max(1, n_init * (k - 1) * nt), np.float64)
+    _lib.call("hrf_kmeans_draws", nv, k, n_init, first.ctypes.data, draws.ctypes.data)
+    return first, draws[:n_init * (k - 1) * nt]
 
 
 # ---- a9/a10/a13 -----------------------------------------------------------------------------

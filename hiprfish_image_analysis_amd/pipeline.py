@@ -50,8 +50,8 @@ def segment_ecoli(stack: torch.Tensor, keep: dict | None = None):
         return K.segment_ecoli_native(stack)
     image_cn = K.channel_sum(stack, mode=1)                              # :71-72 log(sum + 1e-2)
     share = {}                                                           # one sort for both fits
-    _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False, share=share)   # :73-84 brighter cluster
-    _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False, share=share)     # :85-94 brightest layer
+    _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False, share=share, rule=2)  # :73-84 brighter
+    _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False, share=share, rule=0)    # :85-94 brightest
     opened = K.binary_opening(K.remove_small_holes(interior, 64, 1))      # :95
     cell_sm = K.remove_small_objects(opened, 50, conn=1)                 # :96
     be = erosion_seeds(cell_sm)                                          # :97-110
@@ -116,19 +116,20 @@ def segment_multispecies(stack: torch.Tensor, calibration: torch.Tensor | None =
     -> (segmentation int32 relabelled 1..n, n, registered sum f64, final_bkg_filtered f64)
 
     The two KMeans(2) cluster choices (:125-135, :141-149) take the cluster whose positive
-    values have the larger mean; for a 1-D partition into intervals that is the cluster with
-    the larger centre (kernels.kmeans_1d's top mask)."""
+    values have the larger mean -- for a 1-D partition into intervals the upper one -- and
+    sklearn's cluster 0 when one of them holds no positive value (the reference compares a NaN
+    mean then): kernels.kmeans_1d rule 1."""
     if keep is None and NATIVE_SEG:
         return K.segment_multispecies_native(stack, calibration)
     s = K.channel_sum(stack, cal=calibration)                    # :104-105 sum(stack / cal)
     norm = K.div_scalar(s, K.max_f64(s))                         # :106
     nl = K.nl_means_2d(norm, 7, 11, 0.02, 0.0)                   # :108 (estimate_sigma :107 unused)
     final = K.enhance_2d(K.pad_edge(nl, 5))                      # :109-124
-    _, rough, _, _ = K.kmeans_1d(final, 2, want_labels=False)    # :125-135
+    _, rough, _, _ = K.kmeans_1d(final, 2, want_labels=False, rule=1)    # :125-135
     opened = K.remove_small_objects(K.binary_opening(rough), 10, conn=1)   # :136-137
     seeds_mask = K.and_mask(K.fill_holes(opened), K.fill_holes(rough))     # :138-140
     seeds, nseeds = K.label(seeds_mask, conn=2)                  # :140 measure.label (8-conn)
-    _, bkg, _, _ = K.kmeans_1d(nl, 2, want_labels=False)         # :141-149
+    _, bkg, _, _ = K.kmeans_1d(nl, 2, want_labels=False, rule=1)         # :141-149
     final_bkg = K.mask_mul(final, bkg)                           # :150
     seeds_bkg = K.mask_labels(seeds, bkg)                        # :152
     wmask = K.and_mask(rough, bkg)                               # :153

@@ -147,33 +147,34 @@ HRF_API hrf_status hrf_nl_means_2d(const double *img, int64_t H, int64_t W, int3
                                    double h, double sigma, double *out, hrf_stream_t stream);
 
 /* ==== a8: 1-D KMeans (kmeans.hip) ======================================================
- * sklearn KMeans(k, random_state=0).fit_predict(x.reshape(-1,1)) restated as exact-integer
- * Lloyd iterations from a deterministic init (see oracle_kmeans_1d).  valid (nullable)
- * excludes entries (label -1).  labels (nullable) int32; top_mask (nullable) = label of the
- * highest centre.  centers_host[k] / iters_host receive the result (synchronises).
- * state_ws: hrf_kmeans_state_bytes() device bytes. */
-HRF_API int64_t hrf_kmeans_state_bytes(void);
-HRF_API hrf_status hrf_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
-                                 int32_t *labels, uint8_t *top_mask, double *centers_host, int32_t *iters_host,
-                                 void *state_ws, hrf_stream_t stream);
-/* Same result (bit for bit: centres, labels, iteration count) from one radix sort of the
- * values plus a prefix sum of their fixed-point encodings; all Lloyd iterations run in one
- * launch as step searches on the sorted array.  work: hrf_kmeans_sorted_workspace_bytes(n)
- * device bytes.  reuse_sort != 0: `work` already holds the sort of this very x / valid from
- * a previous call (e.g. k = 2 then k = 3 on ecoli image_cn, :73 and :85).  Falls back to
- * the streaming path by itself when its premise fails (NaN input, coincident centres). */
+ * sklearn KMeans(n_clusters=k, random_state=0, n_init).fit_predict(x.reshape(-1, 1)) (ecoli
+ * measurement.py:73, :85; multispecies :125, :141; the reference era's n_init = 10), restated
+ * from sklearn 1.7.2 with its random stream (numpy RandomState(0)) replayed: k-means++ init,
+ * Lloyd with sklearn's stopping rule and empty-cluster relocation, best of n_init by inertia
+ * (see oracle/kmeans_sk.c).  Only entries with valid[i] (valid NULL: all) take part, in raster
+ * order.  labels (nullable) int32 = sklearn's cluster ids (-1 where not valid); top_mask
+ * (nullable) u8 = the cluster chosen by top_rule: 0 the largest centre; 1 (k = 2, multispecies
+ * :126-135/:142-149) the larger cluster when both hold a positive value, else cluster 0; 2
+ * (k = 2, ecoli :75-84) the larger cluster when both are non-empty, else cluster 0.
+ * centers_host[k] / iters_host (nullable) receive sklearn's cluster_centers_ / n_iter_.  NaN
+ * input -> HRF_EINVAL (sklearn raises).  work: hrf_kmeans_sorted_workspace_bytes(n) device
+ * bytes; reuse_sort != 0: `work` already holds the sort of this very x / valid from a
+ * previous call (e.g. k = 2 then k = 3 on ecoli image_cn).  Synchronises the stream once. */
 HRF_API int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n);
 HRF_API hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
-                                        int32_t *labels, uint8_t *top_mask, double *centers_host,
-                                        int32_t *iters_host, void *work, int64_t work_bytes, int32_t reuse_sort,
-                                        hrf_stream_t stream);
-/* Two KMeans runs (k1, then k2 reusing the sort) on the same x with ONE host
- * synchronisation: ecoli measurement.py:73-84 (k = 2, top cluster -> top1) and :85-94
- * (k = 3 -> top2).  Top masks equal two hrf_kmeans_1d_sorted calls'; each run falls back to
- * the streaming path by itself after the synchronisation. */
+                                        int32_t n_init, int32_t top_rule, int32_t *labels, uint8_t *top_mask,
+                                        double *centers_host, int32_t *iters_host, void *work, int64_t work_bytes,
+                                        int32_t reuse_sort, hrf_stream_t stream);
+/* Two fits (k1, then k2 reusing the sort) on the same x with ONE host synchronisation: ecoli
+ * measurement.py:73-84 (k = 2, rule 2 -> top1) and :85-94 (k = 3, rule 0 -> top2). */
 HRF_API hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int64_t n, int32_t k1, int32_t k2,
-                                             int32_t max_iter, uint8_t *top1, uint8_t *top2, void *work,
-                                             int64_t work_bytes, hrf_stream_t stream);
+                                             int32_t max_iter, int32_t n_init, int32_t rule1, int32_t rule2,
+                                             uint8_t *top1, uint8_t *top2, void *work, int64_t work_bytes,
+                                             hrf_stream_t stream);
+/* the random stream of the fit (host): per run the first centre's rank among the valid samples
+ * (numpy RandomState.choice(nv, p=1/nv)) and the k-means++ trial draws, for tests against
+ * numpy; draws_host holds n_init * (k - 1) * (2 + int(log k)) doubles */
+HRF_API hrf_status hrf_kmeans_draws(int64_t nv, int32_t k, int32_t n_init, int64_t *first_host, double *draws_host);
 
 /* ==== a9/a10/a13: components, morphology, label cleanup (label.hip) ====================
  * img dtype: 0 = uint8 mask, 1 = int32 label image (equal values connect), 2 = uint8 mask

@@ -795,15 +795,8 @@ EXPORT void oracle_classify_top2(const double *x, int64_t n, const double *ref, 
 }
 
 /* ------------------------------------------------------------------------------------
- * a8 1-D KMeans (sklearn KMeans(k, random_state=0).fit_predict(x.reshape(-1,1)), ecoli
- * :73,:85; multispecies :125,:141).  Restated as Lloyd iterations to a fixed point from
- * a deterministic init (centres at (j+0.5)/k of [min,max]); sklearn's random k-means++
- * init is not reproducible without its RNG stream (SURVEY.md §7 "KMeans init parity").
- * Assignment: argmin_j (x-c_j)^2, first minimum.  Centre update from exact int64
- * fixed-point sums: q = llrint(x * 2^s), s chosen so n*max|q| < 2^62; c = (sum/cnt)*2^-s.
- * Stops when no centre changes bitwise (max_iter 300).  Only entries with valid[i]
- * (or all when valid == NULL) take part; others get label -1.
- * Returns the iteration count.
+ * a8 1-D KMeans: the restatement of sklearn KMeans lives in kmeans_sk.c; this is the
+ * fixed-point scale it shares with libhrf: q = llrint(x * 2^s), s chosen so n * max|q| < 2^62.
  * ---------------------------------------------------------------------------------- */
 EXPORT int oracle_kmeans_scale(double amax, int64_t n) {
     int e = 0;
@@ -811,69 +804,6 @@ EXPORT int oracle_kmeans_scale(double amax, int64_t n) {
     int ln = 0;
     while (((int64_t)1 << ln) < (n > 1 ? n : 1)) ++ln;
     return 61 - ln - e;
-}
-
-EXPORT int oracle_kmeans_1d(const double *x, const uint8_t *valid, int64_t n, int k, int32_t *labels, double *centers) {
-    double mn = INFINITY, mx = -INFINITY, amax = 0;
-    int64_t nv = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        if (valid && !valid[i]) continue;
-        nv++;
-        mn = x[i] < mn ? x[i] : mn;
-        mx = x[i] > mx ? x[i] : mx;
-        double a = fabs(x[i]);
-        amax = a > amax ? a : amax;
-    }
-    int s = oracle_kmeans_scale(amax, nv);
-    for (int j = 0; j < k; ++j) centers[j] = mn + ((double)j + 0.5) * (mx - mn) / (double)k;
-    int it = 0;
-    int64_t *sum = (int64_t *)calloc(k, sizeof(int64_t)), *cnt = (int64_t *)calloc(k, sizeof(int64_t));
-    for (it = 1; it <= 300; ++it) {
-        memset(sum, 0, sizeof(int64_t) * k);
-        memset(cnt, 0, sizeof(int64_t) * k);
-        for (int64_t i = 0; i < n; ++i) {
-            if (valid && !valid[i]) continue;
-            int bj = 0;
-            double bd = (x[i] - centers[0]) * (x[i] - centers[0]);
-            for (int j = 1; j < k; ++j) {
-                double d = (x[i] - centers[j]) * (x[i] - centers[j]);
-                if (d < bd) {
-                    bd = d;
-                    bj = j;
-                }
-            }
-            sum[bj] += llrint(ldexp(x[i], s));
-            cnt[bj] += 1;
-        }
-        int changed = 0;
-        for (int j = 0; j < k; ++j) {
-            if (!cnt[j]) continue;
-            double c = ldexp((double)sum[j] / (double)cnt[j], -s);
-            if (c != centers[j]) changed = 1;
-            centers[j] = c;
-        }
-        if (!changed) break;
-    }
-    if (it > 300) it = 300;
-    for (int64_t i = 0; i < n; ++i) {
-        if (valid && !valid[i]) {
-            labels[i] = -1;
-            continue;
-        }
-        int bj = 0;
-        double bd = (x[i] - centers[0]) * (x[i] - centers[0]);
-        for (int j = 1; j < k; ++j) {
-            double d = (x[i] - centers[j]) * (x[i] - centers[j]);
-            if (d < bd) {
-                bd = d;
-                bj = j;
-            }
-        }
-        labels[i] = bj;
-    }
-    free(sum);
-    free(cnt);
-    return it;
 }
 
 /* ------------------------------------------------------------------------------------

@@ -19,7 +19,7 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c", "kmeans_sk.c")]
     if not os.path.exists(_LIB) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(_LIB):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _LIB
@@ -33,7 +33,6 @@ def lib():
         _lib.oracle_segcos.restype = ctypes.c_double
         _lib.oracle_label.restype = ctypes.c_int32
         _lib.oracle_relabel_sequential.restype = ctypes.c_int32
-        _lib.oracle_kmeans_1d.restype = ctypes.c_int
         _lib.oracle_kmeans_scale.restype = ctypes.c_int
         _lib.oracle_kmeans_scale.argtypes = [ctypes.c_double, ctypes.c_int64]
     return _lib
@@ -332,16 +331,39 @@ def classify(x, ref, bounds, variant=0, fx=None, fr=None):
 
 
 # ---- a8 ------------------------------------------------------------------------------
-def kmeans_1d(x, k, valid=None):
+def kmeans_draws(nv, k, n_init=10, seed=0):
+    """sklearn 1.7.2 KMeans(random_state=seed, n_init).fit's random stream on nv unit-weight
+    samples: per run the first centre (RandomState.choice(nv, p=1/nv)) and the k-means++
+    trial draws (RandomState.uniform(size=2 + int(log k)) per further centre), in call order"""
+    rs = np.random.RandomState(seed)
+    p = np.ones(nv) / np.ones(nv).sum()
+    nt = 2 + int(np.log(k))
+    first, draws = [], []
+    for _ in range(n_init):
+        first.append(int(rs.choice(nv, p=p)))
+        for _c in range(1, k):
+            draws.extend(rs.uniform(size=nt).tolist())
+    return np.array(first, np.int64), np.array(draws if draws else [0.0], np.float64)
+
+
+def kmeans_sk(x, k, valid=None, n_init=10, max_iter=300, seed=0):
+    """sklearn KMeans(k, random_state=0, n_init=10).fit_predict(x.reshape(-1,1)) restated
+    (kmeans_sk.c) -> labels (sklearn's cluster ids, -1 where not valid), centres, info
+    [winning run, its iterations, strict convergence, empty-cluster relocations]"""
     xv = _c(x, np.float64).ravel()
-    lab = np.zeros(xv.size, np.int32)
-    cen = np.zeros(k, np.float64)
     vp = None
+    nv = xv.size
     if valid is not None:
         va = _c(valid, np.uint8).ravel()
         vp = _p(va)
-    it = lib().oracle_kmeans_1d(_p(xv), vp, I64(xv.size), k, _p(lab), _p(cen))
-    return lab.reshape(np.shape(x)), cen, int(it)
+        nv = int(va.astype(bool).sum())
+    first, draws = kmeans_draws(max(nv, 1), k, n_init, seed)
+    lab = np.zeros(xv.size, np.int32)
+    cen = np.zeros(k, np.float64)
+    info = np.zeros(4, np.int64)
+    lib().oracle_kmeans_sk(_p(xv), vp, I64(xv.size), k, n_init, max_iter, _p(first), _p(draws), _p(lab), _p(cen),
+                           _p(info))
+    return lab.reshape(np.shape(x)), cen, info
 
 
 # ---- a21/a22/a23 ---------------------------------------------------------------------

@@ -38,10 +38,14 @@ def segment_ecoli(stack, keep=None, image_cn=None):
     """ecoli measurement.py:44-127 on the registered (H, W, C) stack"""
     if image_cn is None:
         image_cn = np.log(np.sum(stack.astype(np.float64), axis=2) + 1e-2)         # :71-72
-    l2, c2, _ = O.kmeans_1d(image_cn, 2)                                          # :73-84
-    rough_mask = l2 == int(np.argmax(c2))
-    l3, c3, _ = O.kmeans_1d(image_cn, 3)                                          # :85-94
-    interior = l3 == int(np.argmax(c3))
+    l2, _, _ = O.kmeans_sk(image_cn, 2)                                           # :73
+    i0, i1 = (image_cn[l2 == j].mean() if (l2 == j).any() else np.nan for j in (0, 1))
+    rough_mask = (l2 == 1) if i0 < i1 else (l2 == 0)                              # :74-84
+    l3, _, _ = O.kmeans_sk(image_cn, 3)                                           # :85
+    # :86-94 the layer of largest mean intensity (the reference raises IndexError on an empty
+    # layer; the largest mean among the non-empty layers here, as libhrf's rule 0)
+    means = [image_cn[l3 == j].mean() if (l3 == j).any() else -np.inf for j in range(3)]
+    interior = l3 == int(np.argmax(means))
     opened = O.opening(O.remove_small_holes(interior, 64, 1))                     # :95
     cell_sm = O.remove_small_objects_mask(opened, 50, 1)                          # :96
     be = erosion_seeds(cell_sm)                                                   # :97-110
@@ -128,17 +132,15 @@ def _calibrated(stack, calibration):
     return st / c
 
 
-def _brighter_cluster(img, lab, cen):
-    """multispecies :126-135 / :142-149: the cluster whose positive values have the larger mean
-    (i0 < i1 -> cluster 1).  When one cluster has no positive value the reference's choice
-    follows sklearn's arbitrary label order; the larger centre is taken then."""
+def _brighter_cluster(img, lab):
+    """multispecies :126-135 / :142-149 verbatim in effect: i_j = mean of the positive values of
+    cluster j (NaN when there is none); cluster 1 if i0 < i1, else cluster 0 (a NaN compares
+    False), with sklearn's own cluster ids from kmeans_sk"""
     i = []
     for j in (0, 1):
         v = img * (lab == j)
         v = v[v > 0]
         i.append(np.average(v) if v.size else np.nan)
-    if np.isnan(i[0]) or np.isnan(i[1]):
-        return lab == int(np.argmax(cen))
     return lab == 1 if i[0] < i[1] else lab == 0
 
 
@@ -153,12 +155,12 @@ def segment_multispecies(stack, calibration=None, keep=None, nl=None):
         # 1e-12 of the integral-image restatement O.nl_means_skimage, tests/test_oracle_golden.py)
         nl = O.nl_means(norm, 7, 11, 0.02, 0.0)                                   # :108
     final = O.enhance_2d(np.pad(nl, 5, mode='edge'))                              # :109-124
-    l2, c2, _ = O.kmeans_1d(final, 2)                                             # :125
-    rough = _brighter_cluster(final, l2, c2)                                      # :126-135
+    l2, _, _ = O.kmeans_sk(final, 2)                                              # :125
+    rough = _brighter_cluster(final, l2)                                          # :126-135
     opened = O.remove_small_objects_mask(O.opening(rough), 10, 1)                 # :136-137
     seeds, nseeds = O.label((O.fill_holes(opened) & O.fill_holes(rough)).astype(np.int32), 2)   # :138-140
-    lb, cb, _ = O.kmeans_1d(nl, 2)                                                # :141
-    bkg = _brighter_cluster(nl, lb, cb)                                           # :142-149
+    lb, _, _ = O.kmeans_sk(nl, 2)                                                 # :141
+    bkg = _brighter_cluster(nl, lb)                                               # :142-149
     final_bkg = final * bkg                                                       # :150
     seg = O.watershed(-final_bkg, seeds * bkg, rough & bkg)                       # :152-154
     seg = O.remove_small_objects_labels(seg, 60)                                  # :155

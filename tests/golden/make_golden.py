@@ -186,8 +186,44 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+def main_kmeans_images():
+    """sklearn KMeans(k, random_state=0, n_init=10) partitions of the images the reference
+    actually clusters: E. coli image_cn = log(sum + 1e-2) (ecoli :71-94, k = 2 and 3) and the
+    community final / NL-means images (multispecies :125, :141, k = 2), from synthetic 256^2
+    tiles (plain and 12-bit quantised) computed by the oracle pipeline."""
+    import torch
+    from sklearn.cluster import KMeans
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, REPO)
+    import pipeline as OP
+    from hiprfish_image_analysis_amd import synthetic as S
+    out = {}
+    for name, seed, q in [("ecoli_a", 201, None), ("ecoli_q", 202, 4095)]:
+        st = S.tile(256, 256, seed=seed, device="cpu")[0]
+        if q:
+            st = torch.round(st.double() * q) / q
+        x = np.log(np.sum(st.float().numpy().astype(np.float64), axis=2) + 1e-2)
+        out["x_" + name] = x
+        for k in (2, 3):
+            out["lab%d_%s" % (k, name)] = KMeans(n_clusters=k, random_state=0, n_init=10).fit_predict(
+                x.reshape(-1, 1)).astype(np.int8)
+    for name, seed in [("community", 203)]:
+        st = S.tile(256, 256, nbit=7, bounds=S.MULTI_BOUNDS, seed=seed, device="cpu")[0].numpy()
+        keep = {}
+        OP.segment_multispecies(st, keep=keep)
+        for im in ("final", "nl"):
+            x = keep[im]
+            out["x_%s_%s" % (name, im)] = x
+            out["lab2_%s_%s" % (name, im)] = KMeans(n_clusters=2, random_state=0, n_init=10).fit_predict(
+                x.reshape(-1, 1)).astype(np.int8)
+    np.savez_compressed(os.path.join(HERE, "kmeans_images.npz"), **out)
+    print("kmeans_images.npz written")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["v3"]:
         main_v3()
+    elif sys.argv[1:] == ["kmeans_images"]:
+        main_kmeans_images()
     else:
         main()

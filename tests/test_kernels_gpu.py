@@ -114,18 +114,42 @@ def test_label_cleanup(K, orc, S):
     assert n == rn and np.array_equal(host(got), ref)
 
 
-# ---- a8 KMeans ---------------------------------------------------------------------------
+# ---- a8 KMeans (sklearn restated, kmeans.hip) against the CPU restatement (kmeans_sk.c) ------
+def check_kmeans(K, orc, x, k, valid=None, rule=0):
+    lab, top, cen, it = K.kmeans_1d(dev(x), k, valid=dev(valid) if valid is not None else None, rule=rule)
+    rl, rc, info = orc.kmeans_sk(x, k, valid)
+    assert np.array_equal(host(lab), rl)         # sklearn's cluster ids
+    assert cen == rc.tolist()                    # bitwise equal centres
+    assert it == info[1]
+    return host(lab), host(top), rl, rc
+
+
 @pytest.mark.parametrize("name", ["bimodal", "logsum", "trimodal"])
 def test_kmeans_golden_and_oracle(K, orc, golden, name):
     g = golden("kmeans")
     x = g["x_" + name]
-    k = int(g["k_" + name])
-    lab, top, cen, it = K.kmeans_1d(dev(x), k)
-    rl, rc, rit = orc.kmeans_1d(x, k)
-    assert it == rit
-    assert cen == rc.tolist()  # bitwise equal centres
-    assert np.array_equal(host(lab), rl)
-    assert np.array_equal(host(top).astype(bool), rl == int(np.argmax(rc)))
+    for k in (int(g["k_" + name]), 3):
+        lab, top, rl, rc = check_kmeans(K, orc, x, k)
+        assert np.array_equal(lab, g["lab_" + name] if k == int(g["k_" + name]) else g["lab3_" + name])
+        assert np.array_equal(top.astype(bool), rl == int(np.argmax(rc)))
+
+
+@pytest.mark.parametrize("key", ["2_ecoli_a", "3_ecoli_a", "2_ecoli_q", "3_ecoli_q", "2_community_final",
+                                 "2_community_nl"])
+def test_kmeans_images_equal_sklearn(K, orc, golden, key):
+    g = golden("kmeans_images")
+    k = int(key[0])
+    name = key[2:]
+    lab, top, rl, rc = check_kmeans(K, orc, g["x_" + name].ravel(), k)
+    assert np.array_equal(lab, g["lab%d_%s" % (k, name)].ravel().astype(np.int32))
+
+
+def test_kmeans_random_stream(K, orc):
+    """libhrf's host replay of numpy's RandomState(0) equals numpy's"""
+    for nv, k in [(1000, 2), (1000, 3), (4194304, 3), (77, 8)]:
+        f1, d1 = K.kmeans_draws(nv, k)
+        f2, d2 = orc.kmeans_draws(nv, k)
+        assert np.array_equal(f1, f2) and np.array_equal(d1, d2[:len(d1)])
 
 
 def test_kmeans_valid_mask_and_large(K, orc):
@@ -133,70 +157,63 @@ def test_kmeans_valid_mask_and_large(K, orc):
     x = np.concatenate([rng.normal(0.2, 0.05, 300000), rng.normal(0.9, 0.1, 200000)])
     valid = rng.random(x.size) > 0.2
     for k in (2, 3):
-        lab, top, cen, it = K.kmeans_1d(dev(x), k, valid=dev(valid))
-        rl, rc, rit = orc.kmeans_1d(x, k, valid)
-        assert it == rit and cen == rc.tolist() and np.array_equal(host(lab), rl)
+        check_kmeans(K, orc, x, k, valid)
 
 
-@pytest.mark.parametrize("n,k", [(1, 1), (2, 2), (4097, 3), (1 << 20, 2), (3 * (1 << 20) + 17, 3), (200000, 5),
-                                 (100000, 8), (4096 * 4096 + 5, 3)])
-def test_kmeans_sorted_matches_streaming_and_oracle(K, orc, n, k):
-    """the sorted path (one sort + step searches) equals the streaming pass and the restatement"""
+@pytest.mark.parametrize("n,k", [(1, 1), (2, 2), (5, 3), (4097, 3), (1 << 20, 2), (200000, 5), (100000, 8),
+                                 (3 * (1 << 18) + 17, 3)])
+def test_kmeans_sizes_vs_oracle(K, orc, n, k):
     rng = np.random.default_rng(n + k)
     x = np.log(rng.gamma(2.0, 1.0, n) + 1e-2) if n > 10 else rng.random(n)
     x[rng.random(n) < 0.01] = x[0]          # repeated values
-    d = dev(x)
-    a = K.kmeans_1d(d, k, path="sorted")
-    b = K.kmeans_1d(d, k, path="stream")
-    assert a[3] == b[3] and a[2] == b[2] and torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
-    if n <= (1 << 20):
-        rl, rc, rit = orc.kmeans_1d(x, k)
-        assert a[3] == rit and a[2] == rc.tolist() and np.array_equal(host(a[0]), rl)
+    check_kmeans(K, orc, x, k)
 
 
-def test_kmeans_sorted_share_valid_and_fallbacks(K, orc):
+def test_kmeans_quantised_and_degenerate(K, orc):
     rng = np.random.default_rng(8)
-    x = np.concatenate([rng.normal(0.2, 0.05, 300000), rng.normal(0.9, 0.1, 200000), rng.normal(3, 0.2, 50000)])
-    valid = rng.random(x.size) > 0.2
-    share = {}
-    for k in (2, 3, 2):   # second and third calls reuse the sort
-        lab, top, cen, it = K.kmeans_1d(dev(x), k, valid=dev(valid), share=share)
-        rl, rc, rit = orc.kmeans_1d(x, k, valid)
-        assert it == rit and cen == rc.tolist() and np.array_equal(host(lab), rl)
-        assert np.array_equal(host(top).astype(bool), (rl == int(np.argmax(rc))) & valid)
-    # constant input (coincident centres) and NaN input take the streaming path inside
-    for y in (np.full(10000, 0.5), np.where(rng.random(20000) < 0.001, np.nan, rng.random(20000))):
-        for k in (2, 3):
-            a = K.kmeans_1d(dev(y), k, path="sorted")
-            b = K.kmeans_1d(dev(y), k, path="stream")
-            assert a[3] == b[3] and np.array_equal(np.array(a[2]), np.array(b[2]), equal_nan=True)
-            assert torch.equal(a[0], b[0])
+    # integer-valued data: many exact duplicates, exact midpoints avoided by the scale
+    x = np.log(rng.integers(0, 300, 200000) + 0.01)
+    for k in (2, 3):
+        check_kmeans(K, orc, x, k)
+    # constant input: sklearn leaves clusters empty and relocates
+    for k in (2, 3):
+        check_kmeans(K, orc, np.full(5000, 0.5), k)
+    # NaN: sklearn raises
+    y = rng.random(20000)
+    y[17] = np.nan
+    with pytest.raises(ValueError):
+        K.kmeans_1d(dev(y), 2)
     # empty
     lab, top, cen, it = K.kmeans_1d(dev(np.zeros(0)), 2)
-    assert lab.numel() == 0 and it == 0
+    assert lab.numel() == 0
 
 
-@pytest.mark.parametrize("case", ["mixture", "valid", "constant", "nan", "empty"])
-def test_kmeans_pair_equals_two_calls(K, case):
-    """hrf_kmeans_1d_sorted_pair (one sort, one synchronisation) gives the top masks of two
-    separate sorted calls, including the inputs that send a run to the streaming fallback"""
+def test_kmeans_share_and_pair(K, orc):
     rng = np.random.default_rng(11)
     x = np.concatenate([rng.normal(0.2, 0.05, 30000), rng.normal(0.9, 0.1, 20000), rng.normal(3, 0.2, 5000)])
-    valid = None
-    if case == "valid":
-        valid = dev(rng.random(x.size) > 0.2)
-    elif case == "constant":
-        x = np.full(10000, 0.5)
-    elif case == "nan":
-        x = np.where(rng.random(20000) < 0.001, np.nan, rng.random(20000))
-    elif case == "empty":
-        x = np.zeros(0)
     d = dev(x)
-    t1, t2 = K.kmeans_1d_pair(d, 2, 3, valid=valid)
     share = {}
-    a = K.kmeans_1d(d, 2, valid=valid, share=share, want_labels=False)
-    b = K.kmeans_1d(d, 3, valid=valid, share=share, want_labels=False)
+    a = K.kmeans_1d(d, 2, share=share, rule=2)
+    b = K.kmeans_1d(d, 3, share=share)          # reuses the sort
+    rl2, _, _ = orc.kmeans_sk(x, 2)
+    rl3, rc3, _ = orc.kmeans_sk(x, 3)
+    assert np.array_equal(host(a[0]), rl2) and np.array_equal(host(b[0]), rl3)
+    t1, t2 = K.kmeans_1d_pair(d, 2, 3)
     assert torch.equal(t1, a[1]) and torch.equal(t2, b[1])
+
+
+def test_kmeans_top_rules(K, orc):
+    """rule 1 (multispecies :126-135): the upper cluster when both hold a positive value, else
+    sklearn's cluster 0; rule 2 (ecoli :75-84): the upper cluster when both are non-empty"""
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.normal(0.2, 0.05, 3000), rng.normal(0.9, 0.1, 2000)])
+    lab, top, rl, rc = check_kmeans(K, orc, x, 2, rule=1)
+    assert np.array_equal(top.astype(bool), rl == int(np.argmax(rc)))
+    z = np.concatenate([-rng.random(3000), rng.normal(0.9, 0.1, 2000)])   # lower cluster: no positives
+    lab, top, rl, rc = check_kmeans(K, orc, z, 2, rule=1)
+    assert np.array_equal(top.astype(bool), rl == 0)
+    lab, top, rl, rc = check_kmeans(K, orc, z, 2, rule=2)
+    assert np.array_equal(top.astype(bool), rl == int(np.argmax(rc)))
 
 
 # ---- a12 watershed ----------------------------------------------------------------------
