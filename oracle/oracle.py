@@ -351,6 +351,8 @@ def kmeans_sk(x, k, valid=None, n_init=10, max_iter=300, seed=0):
     (kmeans_sk.c) -> labels (sklearn's cluster ids, -1 where not valid), centres, info
     [winning run, its iterations, strict convergence, empty-cluster relocations]"""
     xv = _c(x, np.float64).ravel()
+    if np.isnan(xv if valid is None else xv[_c(valid, np.uint8).ravel().astype(bool)]).any():
+        raise ValueError("Input contains NaN")          # sklearn's check_array
     vp = None
     nv = xv.size
     if valid is not None:
