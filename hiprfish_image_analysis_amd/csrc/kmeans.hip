@@ -353,14 +353,18 @@ __global__ void km_tol_kernel(const long long *__restrict__ prefix, const U128 *
 }
 
 // ---- k-means++ -------------------------------------------------------------------------------
-// closest fixed-point squared distance of v to the run's first c centres
-__device__ __forceinline__ unsigned long long closest_q(double v, const double *cen, int c, double scaleS) {
-  unsigned long long b = qd(v, cen[0], scaleS);
+// closest squared distance of v to the run's first c centres.  floor(. * 2^S) is monotone, so the
+// least fixed-point potential is the fixed point of the least square: one conversion per sample.
+__device__ __forceinline__ double closest_sq(double v, const double *cen, int c) {
+  double b = (v - cen[0]) * (v - cen[0]);
   for (int j = 1; j < c; ++j) {
-    const unsigned long long d = qd(v, cen[j], scaleS);
+    const double d = (v - cen[j]) * (v - cen[j]);
     b = d < b ? d : b;
   }
   return b;
+}
+__device__ __forceinline__ unsigned long long closest_q(double v, const double *cen, int c, double scaleS) {
+  return (unsigned long long)(closest_sq(v, cen, c) * scaleS);
 }
 
 __device__ __forceinline__ U128 wave_sum128(U128 a) {
@@ -387,9 +391,43 @@ __device__ __forceinline__ U128 block_sum128(U128 a, U128 *sh) {
   return r;
 }
 
-// the first centre of every run: first[r]-th valid sample in raster order (xr compacted)
-__global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, Draws d) {
+// block exclusive scan of per-thread u128 values (PT threads); *total = the block sum (all threads)
+__device__ __forceinline__ u128 block_excl_scan128(u128 v, U128 *sh, u128 *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  u128 inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long lo = __shfl_up((unsigned long long)inc, o, 64);
+    const unsigned long long hi = __shfl_up((unsigned long long)(inc >> 64), o, 64);
+    if (lane >= o) inc += ((u128)hi << 64) | lo;
+  }
+  __syncthreads();
+  if (lane == 63) sh[w] = P(inc);
+  __syncthreads();
+  u128 off = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < PT / 64; ++q) {
+    const u128 x = U(sh[q]);
+    off += q < w ? x : (u128)0;
+    tot += x;
+  }
+  *total = tot;
+  return off + inc - v;
+}
+
+// exact 128-bit atomic add (the carry out of the low word goes into the high word)
+__device__ __forceinline__ void atomic_add128(U128 *a, u128 v) {
+  const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+  const unsigned long long old = atomicAdd(&a->lo, lo);
+  const unsigned long long h = hi + (old + lo < old ? 1ull : 0ull);
+  if (h) atomicAdd(&a->hi, h);
+}
+
+// the first centre of every run: first[r]-th valid sample in raster order (xr compacted);
+// the trial corrections start at zero
+__global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, Draws d, U128 *__restrict__ corr) {
   const int r = threadIdx.x;
+  if (r < NRUN * NTMAX) corr[r] = U128{0, 0};
   if (r >= d.nrun) return;
   SkRun &R = st->run[r];
   const long long nv = (long long)st->nvalid;
@@ -398,132 +436,106 @@ __global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, D
   R.ncen = 1;
 }
 
-// pass A (mode 0): per run, block sums of the closest potential -> part[r][blk]
-// pass C (mode 1): per run and trial, block sums of min(closest, d(candidate)) -> part[r*NTMAX+t][blk]
-template <int MODE>
+// Every round (one further centre for all runs):
+//  pass  -- per run, block sums of the closest potential over the raster-ordered samples;
+//  pick  -- per run and trial, the total T and the candidate: the first raster sample whose
+//           running potential reaches thr = ceil(m T / 2^53); also the range of the value-sorted
+//           array that holds every sample the candidate is closer to than the run's centres;
+//  corr  -- per run and trial, the potential the candidate removes: sum over that range of
+//           closest - min(closest, candidate) (zero outside its cell);
+//  choose-- per run, the trial of least T - corr (the first on ties).
+// The candidate's cell is an interval of values (1-D): the range is bounded by whole buckets
+// around the midpoints to the neighbouring centres, widened by a margin far above the rounding
+// of the squares.  Work per round: one raster pass, one sweep of the cells.
 __global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict__ xr, const KmState *st, Draws d,
-                                                        U128 *__restrict__ part, int nblk) {
+                                                        U128 *__restrict__ part, int nblk, int c) {
   __shared__ U128 sh[PT / 64];
   const int64_t nv = (int64_t)st->nvalid;
   const double scaleS = ldexp(1.0, st->S);
-  const int64_t base = (int64_t)blockIdx.x * PB + threadIdx.x * (PB / PT);
+  const int64_t base = (int64_t)blockIdx.x * PB + threadIdx.x;
   double v[PB / PT];
   int cnt = 0;
 #pragma unroll
   for (int e = 0; e < PB / PT; ++e) {
-    const int64_t i = base + e;
+    const int64_t i = base + e * PT;
     v[e] = i < nv ? xr[i] : 0.0;
     cnt += i < nv;
   }
   for (int r = 0; r < d.nrun; ++r) {
     const SkRun &R = st->run[r];
-    const int c = R.ncen;
-    unsigned long long cl[PB / PT];
+    u128 s = 0;
 #pragma unroll
-    for (int e = 0; e < PB / PT; ++e) cl[e] = e < cnt ? closest_q(v[e], R.cen, c, scaleS) : 0ull;
-    if (MODE == 0) {
-      u128 s = 0;
-#pragma unroll
-      for (int e = 0; e < PB / PT; ++e) s += cl[e];
-      const U128 tot = block_sum128(P(s), sh);
-      if (threadIdx.x == 0) part[(int64_t)r * nblk + blockIdx.x] = tot;
-    } else {
-      for (int t = 0; t < d.nt; ++t) {
-        const double cv = R.cand[t];
-        u128 s = 0;
-#pragma unroll
-        for (int e = 0; e < PB / PT; ++e) {
-          const unsigned long long dq = e < cnt ? qd(v[e], cv, scaleS) : 0ull;
-          s += dq < cl[e] ? dq : cl[e];
-        }
-        const U128 tot = block_sum128(P(s), sh);
-        if (threadIdx.x == 0) part[((int64_t)r * NTMAX + t) * nblk + blockIdx.x] = tot;
-      }
-    }
+    for (int e = 0; e < PB / PT; ++e) s += e < cnt ? closest_q(v[e], R.cen, c, scaleS) : 0ull;
+    const U128 tot = block_sum128(P(s), sh);
+    if (threadIdx.x == 0) part[(int64_t)r * nblk + blockIdx.x] = tot;
   }
 }
 
-// per run (one workgroup each): total potential, then every trial's candidate = the first
-// sample whose running potential reaches thr = ceil(m T / 2^53)
-__global__ __launch_bounds__(PT) void km_pp_pick_kernel(const double *__restrict__ xr, KmState *st, Draws d,
-                                                        const U128 *__restrict__ part, int nblk, int c) {
-  __shared__ U128 pre[PT + 1];   // prefix over thread chunks of block partials
-  __shared__ U128 ts[PT];        // per-thread sums inside the crossing block
-  __shared__ U128 before_sh;
-  __shared__ int blk_sh, thr_t_sh;
+__global__ __launch_bounds__(PT) void km_pp_pick_kernel(const double *__restrict__ xr,
+                                                        const unsigned long long *__restrict__ off,
+                                                        const double *__restrict__ geo, KmState *st, Draws d,
+                                                        const U128 *__restrict__ part, int nblk, int c,
+                                                        long long *__restrict__ rng) {
+  __shared__ U128 sh[PT / 64];
+  __shared__ int first_sh;
   __shared__ long long idx_sh;
-  __shared__ unsigned long long thr_lo, thr_hi;
-  const int r = blockIdx.x;
+  __shared__ int blk_sh;
+  __shared__ U128 acc_sh;
+  const int r = blockIdx.x / d.nt, t = blockIdx.x % d.nt;
   SkRun &R = st->run[r];
   const int64_t nv = (int64_t)st->nvalid;
   const double scaleS = ldexp(1.0, st->S);
   const int tid = threadIdx.x;
   const U128 *pr = part + (int64_t)r * nblk;
   const int per = (nblk + PT - 1) / PT;
+  const int b0 = tid * per, b1 = b0 + per < nblk ? b0 + per : nblk;
   u128 loc = 0;
-  for (int b = tid * per; b < nblk && b < (tid + 1) * per; ++b) loc += U(pr[b]);
-  pre[tid + 1] = P(loc);
-  __syncthreads();
+  for (int b = b0; b < b1; ++b) loc += U(pr[b]);
+  u128 T;
+  const u128 before = block_excl_scan128(loc, sh, &T);
+  const u128 thr = thr_of(d.m[r][c - 1][t], T);
   if (tid == 0) {
-    pre[0] = U128{0, 0};
-    for (int q = 1; q <= PT; ++q) pre[q] = U128Plus()(pre[q - 1], pre[q]);
-    R.T = pre[PT];
+    first_sh = PT;
+    idx_sh = -1;
+    blk_sh = -1;
   }
   __syncthreads();
-  const u128 T = U(pre[PT]);
-  for (int t = 0; t < d.nt; ++t) {
-    if (tid == 0) {
-      const u128 thr = thr_of(d.m[r][c - 1][t], T);
-      thr_lo = (unsigned long long)thr;
-      thr_hi = (unsigned long long)(thr >> 64);
-      int b = -1;
-      u128 acc = 0;
-      for (int q = 0; q < PT && b < 0; ++q) {
-        if (U(pre[q + 1]) < thr) continue;
-        acc = U(pre[q]);
-        for (int bb = q * per; bb < nblk && bb < (q + 1) * per; ++bb) {
-          const u128 nx = acc + U(pr[bb]);
-          if (nx >= thr) {
-            b = bb;
-            break;
-          }
-          acc = nx;
-        }
+  // the block whose inclusive running sum first reaches thr: in the range of the first thread
+  // whose inclusive sum does
+  if (b0 < b1 && before + loc >= thr) atomicMin(&first_sh, tid);
+  __syncthreads();
+  if (tid == first_sh) {
+    u128 acc = before;
+    for (int b = b0; b < b1; ++b) {
+      const u128 nx = acc + U(pr[b]);
+      if (nx >= thr) {
+        blk_sh = b;
+        break;
       }
-      blk_sh = b;
-      before_sh = P(acc);
-      idx_sh = -1;
+      acc = nx;
     }
-    __syncthreads();
-    const int b = blk_sh;
-    const u128 thr = ((u128)thr_hi << 64) | thr_lo;
+    acc_sh = P(acc);
+  }
+  __syncthreads();
+  const int b = blk_sh;
+  if (b >= 0) {
+    const int64_t i0 = (int64_t)b * PB + tid * (PB / PT);
     unsigned long long cl[PB / PT];
-    const int64_t i0 = (int64_t)(b < 0 ? 0 : b) * PB + tid * (PB / PT);
     u128 sthr = 0;
 #pragma unroll
     for (int e = 0; e < PB / PT; ++e) {
       const int64_t i = i0 + e;
-      cl[e] = (b >= 0 && i < nv) ? closest_q(xr[i], R.cen, c, scaleS) : 0ull;
+      cl[e] = i < nv ? closest_q(xr[i], R.cen, c, scaleS) : 0ull;
       sthr += cl[e];
     }
-    ts[tid] = P(sthr);
+    u128 tb;
+    const u128 bt = block_excl_scan128(sthr, sh, &tb) + U(acc_sh);
+    if (tid == 0) first_sh = PT;
     __syncthreads();
-    if (tid == 0 && b >= 0) {
-      u128 acc = U(before_sh);
-      thr_t_sh = PT - 1;
-      for (int q = 0; q < PT; ++q) {
-        const u128 nx = acc + U(ts[q]);
-        if (nx >= thr) {
-          thr_t_sh = q;
-          break;
-        }
-        acc = nx;
-      }
-      before_sh = P(acc);
-    }
+    if (bt + sthr >= thr) atomicMin(&first_sh, tid);
     __syncthreads();
-    if (b >= 0 && tid == thr_t_sh) {
-      u128 acc = U(before_sh);
+    if (tid == first_sh) {
+      u128 acc = bt;
       for (int e = 0; e < PB / PT; ++e) {
         acc += cl[e];
         if (acc >= thr && i0 + e < nv) {
@@ -533,36 +545,102 @@ __global__ __launch_bounds__(PT) void km_pp_pick_kernel(const double *__restrict
       }
     }
     __syncthreads();
-    if (tid == 0) {
-      // sklearn clips an out-of-range candidate to the last sample
-      const long long idx = idx_sh >= 0 ? idx_sh : nv - 1;
-      R.cand[t] = xr[idx];
+  }
+  if (tid == 0) {
+    // sklearn clips an out-of-range candidate to the last sample
+    const long long idx = idx_sh >= 0 ? idx_sh : nv - 1;
+    const double cv = nv > 0 ? xr[idx] : 0.0;
+    R.cand[t] = cv;
+    if (t == 0) R.T = P(T);
+    // the sorted range holding the candidate's cell
+    bool eq = false, hl = false, hh = false;
+    double lo = 0, hi = 0;
+    for (int j = 0; j < c; ++j) {
+      const double cj = R.cen[j];
+      if (cj == cv) eq = true;
+      else if (cj < cv) {
+        if (!hl || cj > lo) lo = cj;
+        hl = true;
+      } else if (cj > cv) {
+        if (!hh || cj < hi) hi = cj;
+        hh = true;
+      }
     }
-    __syncthreads();
+    long long a = 0, e = nv;
+    if (eq || nv == 0) e = 0;
+    else {
+      const double mn = geo[0], inv = geo[1];
+      const double range = ord_dec(st->hi_bits) - ord_dec(st->lo_bits);
+      const double delta = (fabs(lo) + fabs(cv) + fabs(hi) + range) * 0x1p-40;
+      if (hl) a = (long long)off[km_bucket(0.5 * lo + 0.5 * cv - delta, mn, inv)];
+      if (hh) e = (long long)off[km_bucket(0.5 * cv + 0.5 * hi + delta, mn, inv) + 1];
+      if (e > nv) e = nv;
+      if (a > e) a = e;
+    }
+    rng[2 * (r * NTMAX + t)] = a;
+    rng[2 * (r * NTMAX + t) + 1] = e;
   }
 }
 
-// per run: totals of the trials' potentials, the least (first) wins
-__global__ void km_pp_choose_kernel(KmState *st, Draws d, const U128 *__restrict__ part, int nblk, int c) {
+__global__ __launch_bounds__(PT) void km_pp_corr_kernel(const double *__restrict__ xs, const KmState *st, Draws d,
+                                                        const long long *__restrict__ rng, U128 *__restrict__ corr,
+                                                        int c) {
+  __shared__ long long cs[NRUN * NTMAX + 1];
   __shared__ U128 sh[PT / 64];
-  const int r = blockIdx.x;
-  SkRun &R = st->run[r];
-  __shared__ u128 tot[NTMAX];
-  for (int t = 0; t < d.nt; ++t) {
-    u128 s = 0;
-    for (int b = threadIdx.x; b < nblk; b += PT) s += U(part[((int64_t)r * NTMAX + t) * nblk + b]);
-    const U128 a = block_sum128(P(s), sh);
-    if (threadIdx.x == 0) tot[t] = U(a);
-    __syncthreads();
-  }
+  const int np = d.nrun * d.nt;
   if (threadIdx.x == 0) {
-    int bt = 0;
-    for (int t = 1; t < d.nt; ++t)
-      if (tot[t] < tot[bt]) bt = t;
-    R.cen[c] = R.cand[bt];
-    R.T = P(tot[bt]);
-    R.ncen = c + 1;
+    long long s = 0;
+    for (int p = 0; p < np; ++p) {
+      const int q = (p / d.nt) * NTMAX + p % d.nt;
+      cs[p] = s;
+      s += (rng[2 * q + 1] - rng[2 * q] + PB - 1) / PB;
+    }
+    cs[np] = s;
   }
+  __syncthreads();
+  const double scaleS = ldexp(1.0, st->S);
+  for (long long g = blockIdx.x; g < cs[np]; g += gridDim.x) {
+    int p = 0;
+    while (cs[p + 1] <= g) ++p;
+    const int r = p / d.nt, t = p % d.nt, q = r * NTMAX + t;
+    const SkRun &R = st->run[r];
+    const double cv = R.cand[t];
+    const long long e = rng[2 * q + 1];
+    const long long i0 = rng[2 * q] + (g - cs[p]) * PB + threadIdx.x;
+    u128 s = 0;
+#pragma unroll 4
+    for (int k = 0; k < PB / PT; ++k) {
+      const long long i = i0 + (long long)k * PT;
+      if (i < e) {
+        const double v = xs[i];
+        const double dc = closest_sq(v, R.cen, c), dt = (v - cv) * (v - cv);
+        if (dt < dc) s += (unsigned long long)(dc * scaleS) - (unsigned long long)(dt * scaleS);
+      }
+    }
+    const U128 tot = block_sum128(P(s), sh);
+    if (threadIdx.x == 0 && (tot.lo | tot.hi)) atomic_add128(&corr[q], U(tot));
+  }
+}
+
+// per run: T - corr of every trial, the least (first) wins; the corrections are reset
+__global__ void km_pp_choose_kernel(KmState *st, Draws d, U128 *__restrict__ corr, int c) {
+  const int r = threadIdx.x;
+  if (r >= d.nrun) return;
+  SkRun &R = st->run[r];
+  const u128 T = U(R.T);
+  int bt = 0;
+  u128 best = 0;
+  for (int t = 0; t < d.nt; ++t) {
+    const u128 tt = T - U(corr[r * NTMAX + t]);
+    corr[r * NTMAX + t] = U128{0, 0};
+    if (t == 0 || tt < best) {
+      best = tt;
+      bt = t;
+    }
+  }
+  R.cen[c] = R.cand[bt];
+  R.T = P(best);
+  R.ncen = c + 1;
 }
 
 // ---- Lloyd on the sorted array ---------------------------------------------------------------
@@ -1044,7 +1122,8 @@ struct SortWs {
   unsigned long long *off;
   double *xs, *xr;
   long long *q, *prefix;
-  U128 *q2, *p2, *part;
+  U128 *q2, *p2, *part, *corr;
+  long long *rng;
   unsigned long long *nsel;
   void *tmp;
   size_t tmp_bytes;
@@ -1073,7 +1152,8 @@ int64_t sort_ws_bytes(int64_t n, size_t tmp_bytes) {
   return (int64_t)(align256(sizeof(KmState)) + 256 + 2 * align256(sizeof(uint32_t) * m) +
                    align256(sizeof(unsigned long long) * (KM_NB + 1)) + 2 * align256(sizeof(double) * m) +
                    2 * align256(sizeof(long long) * (m + 1)) + 2 * align256(sizeof(U128) * (m + 1)) +
-                   align256(sizeof(U128) * NRUN * NTMAX * nblocks(n)) + 256 + align256(tmp_bytes));
+                   align256(sizeof(U128) * NRUN * nblocks(n)) + align256(sizeof(U128) * NRUN * NTMAX) +
+                   align256(sizeof(long long) * 2 * NRUN * NTMAX) + 256 + align256(tmp_bytes));
 }
 
 SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
@@ -1103,7 +1183,11 @@ SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   ws.p2 = (U128 *)w;
   w += align256(sizeof(U128) * (m + 1));
   ws.part = (U128 *)w;
-  w += align256(sizeof(U128) * NRUN * NTMAX * nblocks(n));
+  w += align256(sizeof(U128) * NRUN * nblocks(n));
+  ws.corr = (U128 *)w;
+  w += align256(sizeof(U128) * NRUN * NTMAX);
+  ws.rng = (long long *)w;
+  w += align256(sizeof(long long) * 2 * NRUN * NTMAX);
   ws.nsel = (unsigned long long *)w;
   w += 256;
   ws.tmp = w;
@@ -1166,13 +1250,13 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   const Draws d = make_draws(std::max<int64_t>(nv, 1), K, n_init, 0u);
   const double *xr = valid ? ws.xr : x;
   const int nblk = (int)nblocks(nv);
-  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d);
+  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d, ws.corr);
   HRF_LAUNCHED();
   for (int c = 1; c < K; ++c) {
-    km_pp_pass_kernel<0><<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk);
-    km_pp_pick_kernel<<<n_init, PT, 0, s>>>(xr, st, d, ws.part, nblk, c);
-    km_pp_pass_kernel<1><<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk);
-    km_pp_choose_kernel<<<n_init, PT, 0, s>>>(st, d, ws.part, nblk, c);
+    km_pp_pass_kernel<<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk, c);
+    km_pp_pick_kernel<<<n_init * d.nt, PT, 0, s>>>(xr, ws.off, ws.geo, st, d, ws.part, nblk, c, ws.rng);
+    km_pp_corr_kernel<<<1024, PT, 0, s>>>(ws.xs, st, d, ws.rng, ws.corr, c);
+    km_pp_choose_kernel<<<1, 64, 0, s>>>(st, d, ws.corr, c);
     HRF_LAUNCHED();
   }
   km_lloyd_kernel<K><<<n_init, KS_T, 0, s>>>(ws.xs, ws.q, ws.q2, ws.prefix, ws.p2, ws.off, ws.geo, st, max_iter);
