@@ -22,23 +22,22 @@
 // their squares), so every decision is independent of reduction order and equal to the CPU
 // restatement's bit for bit.
 //
-// MI355X mapping.  The valid values are bucket sorted once (20-bit value buckets, rocPRIM
-// radix sort) and prefix-summed; a Lloyd step is then k - 1 label-step searches on the sorted
-// array (a 4096-ary search by one 1024-thread workgroup that narrows to whole buckets and
-// counts the straddling ones) -- no pass over the data per iteration.  The n_init runs proceed
-// in parallel: k-means++ needs two streaming passes per further centre for ALL runs at once
-// (block potentials, then the candidates' potentials), the candidate search itself touches one
-// 4096-sample block per trial; the Lloyd loops run one workgroup per run; a last kernel picks
-// the winner and a raster pass writes labels / the top-cluster mask.  No host synchronisation
-// is needed between the stages (the draws travel as kernel arguments).
+// MI355X mapping.  The valid values are bucket sorted once (2^20 value buckets, a two-digit
+// counting sort without global atomics) and per-bucket prefix sums of q and q^2 are taken; a
+// Lloyd step is then k - 1 label-step searches on the sorted array (one 1024-thread workgroup
+// narrows to whole buckets and counts the straddling ones) -- no pass over the data per
+// iteration.  The n_init runs proceed in parallel: a k-means++ round is one raster pass for the
+// block potentials of all runs, a parallel candidate pick per (run, trial), and one pass over the
+// sorted array for every trial's potential (a trial only changes the samples of its candidate's
+// value cell, a contiguous range of buckets); the Lloyd loops run one workgroup per run; a last
+// kernel picks the winner and a raster pass writes labels / the top-cluster mask.  No host
+// synchronisation is needed between the stages (the draws travel as kernel arguments).
 #include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
 
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
 
 #include "common.hpp"
@@ -190,6 +189,8 @@ struct KmState {
   int best;       // winning run
   int top;        // sklearn id of the top cluster (by the rule)
   long long nle0; // samples <= 0 (rule 1)
+  long long sumq; // sums of q and q^2 over the valid samples
+  U128 sumq2;
   double center[KMAX];
   int iters;
   SkRun run[NRUN];
@@ -286,87 +287,7 @@ __global__ void km_scale_kernel(KmState *st) {
   st->error = st->nnan ? 1 : 0;
 }
 
-// ---- sorted array ----------------------------------------------------------------------------
-// NB value buckets of equal width over [min, max]; bucket(x) is a non-decreasing function of
-// x, so every value of bucket b is below every value of bucket b' > b.  The valid values are
-// radix sorted by their 20-bit bucket index (invalid entries get key NB and land past them),
-// in no particular order inside a bucket -- only integer sums and counts are read off.
-// off[b] = first position of bucket b; q = rint(x 2^s), prefix sums of q and of q^2.
-constexpr int KM_NB = 1 << 20;
-constexpr int KM_NB_BITS = 21;  // keys 0..NB inclusive
-
-__device__ __forceinline__ int km_bucket(double x, double mn, double inv) {
-  const double t = (x - mn) * inv;
-  return t >= 0.0 ? (t < (double)(KM_NB - 1) ? (int)t : KM_NB - 1) : 0;  // NaN -> 0
-}
-
-__global__ void km_bucket_init_kernel(KmState *st, double *geo) {
-  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
-  geo[0] = mn;
-  geo[1] = mx > mn ? (double)KM_NB / (mx - mn) : 0.0;
-}
-
-__global__ void km_bucket_key_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
-                                     const double *__restrict__ geo, uint32_t *__restrict__ key) {
-  const double mn = geo[0], inv = geo[1];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    key[i] = (!valid || valid[i]) ? (uint32_t)km_bucket(x[i], mn, inv) : (uint32_t)KM_NB;
-}
-
-__global__ void km_bucket_bounds_kernel(const uint32_t *__restrict__ key, const double *__restrict__ xs, int64_t n,
-                                        const KmState *st, unsigned long long *__restrict__ off,
-                                        long long *__restrict__ q, U128 *__restrict__ q2,
-                                        long long *__restrict__ prefix0, U128 *__restrict__ p20) {
-  const int s = st->s;
-  const int64_t T = (int64_t)gridDim.x * blockDim.x;
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t0 == 0) {
-    *prefix0 = 0;
-    *p20 = U128{0, 0};
-  }
-  for (int64_t b = t0; b <= KM_NB; b += T) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if ((int64_t)key[mid] < b) lo = mid + 1;
-      else hi = mid;
-    }
-    off[b] = (unsigned long long)lo;
-  }
-  for (int64_t i = t0; i < n; i += T) {
-    const long long v = (long long)rint(ldexp(xs[i], s));
-    q[i] = v;
-    const unsigned long long a = (unsigned long long)(v < 0 ? -v : v);
-    q2[i] = P((u128)a * a);
-  }
-}
-
-// tol = 1e-4 * var(x) from the exact sums (kmeans_sk.c)
-__global__ void km_tol_kernel(const long long *__restrict__ prefix, const U128 *__restrict__ p2, KmState *st) {
-  const long long nv = (long long)st->nvalid;
-  if (!nv) {
-    st->tol = 0;
-    return;
-  }
-  const double m1 = (double)prefix[nv] / (double)nv, m2 = u128_to_double(U(p2[nv])) / (double)nv;
-  st->tol = ldexp(m2 - m1 * m1, -2 * st->s) * 1e-4;
-}
-
-// ---- k-means++ -------------------------------------------------------------------------------
-// closest squared distance of v to the run's first c centres.  floor(. * 2^S) is monotone, so the
-// least fixed-point potential is the fixed point of the least square: one conversion per sample.
-__device__ __forceinline__ double closest_sq(double v, const double *cen, int c) {
-  double b = (v - cen[0]) * (v - cen[0]);
-  for (int j = 1; j < c; ++j) {
-    const double d = (v - cen[j]) * (v - cen[j]);
-    b = d < b ? d : b;
-  }
-  return b;
-}
-__device__ __forceinline__ unsigned long long closest_q(double v, const double *cen, int c, double scaleS) {
-  return (unsigned long long)(closest_sq(v, cen, c) * scaleS);
-}
-
+// ---- exact 128-bit reductions -------------------------------------------------------------
 __device__ __forceinline__ U128 wave_sum128(U128 a) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -415,19 +336,377 @@ __device__ __forceinline__ u128 block_excl_scan128(u128 v, U128 *sh, u128 *total
   return off + inc - v;
 }
 
-// exact 128-bit atomic add (the carry out of the low word goes into the high word)
-__device__ __forceinline__ void atomic_add128(U128 *a, u128 v) {
-  const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
-  const unsigned long long old = atomicAdd(&a->lo, lo);
-  const unsigned long long h = hi + (old + lo < old ? 1ull : 0ull);
-  if (h) atomicAdd(&a->hi, h);
+
+// ---- bucket-sorted array ----------------------------------------------------------------------
+// NB value buckets of equal width over [min, max]; bucket(x) is a non-decreasing function of
+// x, so every value of bucket b is below every value of bucket b' > b.  The valid values are
+// counting sorted by bucket (xs, in no particular order inside a bucket -- only integer sums and
+// counts are read off): off[b] = first position of bucket b (off[NB] = nvalid).  For every
+// non-empty bucket b, bq[b] / bq2[b] = the sums of q = rint(x 2^s) and of q^2 over the samples
+// before it; the totals are in the state.
+//
+// The sort is a two-digit MSD counting sort without global atomics: the coarse digit (bucket >>
+// 10) per 4096-sample chunk of the raster input (LDS histogram, per-chunk counts written
+// digit-major, one scan -> every chunk's run of every digit), scattered into tmp; then the fine
+// digit per 4096-sample chunk of each coarse segment the same way into xs.  Ranks inside a chunk
+// come from LDS atomics (no order is needed inside a bucket).
+constexpr int KM_NB = 1 << 20;
+constexpr int KD = 1024;                  // digit values (2 x 10 bits)
+constexpr int KS_CH = 4096;               // samples per sort chunk (256 threads x 16)
+
+__device__ __forceinline__ int km_bucket(double x, double mn, double inv) {
+  const double t = (x - mn) * inv;
+  return t >= 0.0 ? (t < (double)(KM_NB - 1) ? (int)t : KM_NB - 1) : 0;  // NaN -> 0
 }
 
-// the first centre of every run: first[r]-th valid sample in raster order (xr compacted);
-// the trial corrections start at zero
-__global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, Draws d, U128 *__restrict__ corr) {
+__device__ __forceinline__ long long km_q(double x, int s) { return (long long)rint(ldexp(x, s)); }
+__device__ __forceinline__ u128 km_q2(long long v) {
+  const unsigned long long a = (unsigned long long)(v < 0 ? -v : v);
+  return (u128)a * a;
+}
+
+__global__ void km_bucket_init_kernel(KmState *st, double *geo) {
+  const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
+  geo[0] = mn;
+  geo[1] = mx > mn ? (double)KM_NB / (mx - mn) : 0.0;
+}
+
+__device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long *sh,
+                                                                  unsigned long long *total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned long long inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();
+  if (lane == 63) sh[w] = inc;
+  __syncthreads();
+  unsigned long long off = 0, tot = 0;
+  for (int q = 0; q < nw; ++q) {
+    off += q < w ? sh[q] : 0ull;
+    tot += sh[q];
+  }
+  *total = tot;
+  return off + inc - v;
+}
+
+// ---- exclusive scan of u32 counts (3 kernels: block sums, their scan, apply; in place) ----
+constexpr int KSC_B = 4096;  // entries per scan block (256 threads x 16)
+
+__global__ __launch_bounds__(256) void km_scan_sum_kernel(const unsigned *__restrict__ a, long long n,
+                                                          unsigned *__restrict__ bsum) {
+  const long long i0 = (long long)blockIdx.x * KSC_B;
+  unsigned long long s = 0;
+  for (int e = threadIdx.x; e < KSC_B; e += 256)
+    if (i0 + e < n) s += a[i0 + e];
+  s = hrf::wave_sum(s);
+  __shared__ unsigned long long sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (unsigned)(sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+__global__ __launch_bounds__(1024) void km_scan_blocks_kernel(unsigned *__restrict__ bsum, int nb) {
+  __shared__ unsigned long long sh[16];
+  unsigned long long carry = 0;
+  for (int b0 = 0; b0 < nb; b0 += 1024) {
+    const int i = b0 + threadIdx.x;
+    unsigned long long tot;
+    const unsigned long long e = block_excl_scan_u64(i < nb ? bsum[i] : 0u, sh, &tot);
+    if (i < nb) bsum[i] = (unsigned)(carry + e);
+    carry += tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void km_scan_apply_kernel(unsigned *__restrict__ a, long long n,
+                                                            const unsigned *__restrict__ bsum) {
+  __shared__ unsigned long long sh[4];
+  const long long i0 = (long long)blockIdx.x * KSC_B + threadIdx.x * 16;
+  unsigned v[16];
+  unsigned long long loc = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    v[e] = i0 + e < n ? a[i0 + e] : 0u;
+    loc += v[e];
+  }
+  unsigned long long tot;
+  unsigned long long acc = bsum[blockIdx.x] + block_excl_scan_u64(loc, sh, &tot);
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    if (i0 + e < n) {
+      a[i0 + e] = (unsigned)acc;
+      acc += v[e];
+    }
+}
+
+// ---- pass A: coarse digit over raster chunks ----
+// cntA[d * nchA + c] = samples of chunk c with coarse digit d
+__global__ __launch_bounds__(256) void km_hist_a_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid,
+                                                        int64_t n, const double *__restrict__ geo,
+                                                        unsigned *__restrict__ cntA, int nchA) {
+  __shared__ unsigned h[KD];
+  for (int i = threadIdx.x; i < KD; i += 256) h[i] = 0;
+  __syncthreads();
+  const double mn = geo[0], inv = geo[1];
+  const int64_t base = (int64_t)blockIdx.x * KS_CH + threadIdx.x;
+#pragma unroll 4
+  for (int e = 0; e < KS_CH / 256; ++e) {
+    const int64_t i = base + (int64_t)e * 256;
+    if (i < n && (!valid || valid[i])) atomicAdd(&h[km_bucket(x[i], mn, inv) >> 10], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KD; i += 256) cntA[(int64_t)i * nchA + blockIdx.x] = h[i];
+}
+
+__global__ __launch_bounds__(256) void km_scatter_a_kernel(const double *__restrict__ x,
+                                                           const uint8_t *__restrict__ valid, int64_t n,
+                                                           const double *__restrict__ geo,
+                                                           const unsigned *__restrict__ offA, int nchA,
+                                                           double *__restrict__ tmp) {
+  __shared__ unsigned h[KD];
+  for (int i = threadIdx.x; i < KD; i += 256) h[i] = offA[(int64_t)i * nchA + blockIdx.x];
+  __syncthreads();
+  const double mn = geo[0], inv = geo[1];
+  const int64_t base = (int64_t)blockIdx.x * KS_CH + threadIdx.x;
+#pragma unroll 4
+  for (int e = 0; e < KS_CH / 256; ++e) {
+    const int64_t i = base + (int64_t)e * 256;
+    if (i < n && (!valid || valid[i])) {
+      const double v = x[i];
+      tmp[atomicAdd(&h[km_bucket(v, mn, inv) >> 10], 1u)] = v;
+    }
+  }
+}
+
+// coarse segments: seg[d] = first position of digit d (seg[KD] = nvalid); their 4096-sample
+// chunks cB[d] (exclusive prefix, cB[KD] = number of chunks)
+__global__ __launch_bounds__(KD) void km_segments_kernel(const unsigned *__restrict__ offA, int nchA,
+                                                         const KmState *st, unsigned *__restrict__ seg,
+                                                         unsigned *__restrict__ cB) {
+  __shared__ unsigned long long sh[16];
+  const int d = threadIdx.x;
+  const unsigned nv = (unsigned)st->nvalid;
+  const unsigned s0 = offA[(int64_t)d * nchA];
+  const unsigned s1 = d + 1 < KD ? offA[(int64_t)(d + 1) * nchA] : nv;
+  seg[d] = s0;
+  if (d == 0) seg[KD] = nv;
+  unsigned long long tot;
+  const unsigned long long e = block_excl_scan_u64((s1 - s0 + KS_CH - 1) / KS_CH, sh, &tot);
+  cB[d] = (unsigned)e;
+  if (d == 0) cB[KD] = (unsigned)tot;
+}
+
+__device__ __forceinline__ int km_seg_of(const unsigned *cB, int j) {  // cB[d] <= j < cB[d + 1]
+  int lo = 0, hi = KD;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cB[mid] <= (unsigned)j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---- pass B: fine digit over the chunks of every coarse segment ----
+// cntB[f * L + j] = samples of chunk j with fine digit f (L = chunk bound + 1, the spare columns
+// zero)
+__global__ __launch_bounds__(256) void km_hist_b_kernel(const double *__restrict__ tmp, const double *__restrict__ geo,
+                                                        const unsigned *__restrict__ seg,
+                                                        const unsigned *__restrict__ cB, unsigned *__restrict__ cntB,
+                                                        int L) {
+  __shared__ unsigned h[KD];
+  for (int i = threadIdx.x; i < KD; i += 256) h[i] = 0;
+  __syncthreads();
+  const int j = blockIdx.x;
+  if (j < (int)cB[KD]) {
+    const int d = km_seg_of(cB, j);
+    const long long a = (long long)seg[d] + (long long)(j - (int)cB[d]) * KS_CH;
+    const long long b = a + KS_CH < (long long)seg[d + 1] ? a + KS_CH : (long long)seg[d + 1];
+    const double mn = geo[0], inv = geo[1];
+#pragma unroll 4
+    for (int e = 0; e < KS_CH / 256; ++e) {
+      const long long i = a + (long long)e * 256 + threadIdx.x;
+      if (i < b) atomicAdd(&h[km_bucket(tmp[i], mn, inv) & (KD - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KD; i += 256) {
+    cntB[(int64_t)i * L + j] = h[i];
+    if (j == L - 2) cntB[(int64_t)i * L + L - 1] = 0;
+  }
+}
+
+// bucket starts: off[d * KD + f] = seg[d] + samples of segment d with fine digit < f
+__global__ __launch_bounds__(KD) void km_bucket_off_kernel(const unsigned *__restrict__ S, int L,
+                                                           const unsigned *__restrict__ seg,
+                                                           const unsigned *__restrict__ cB,
+                                                           unsigned long long *__restrict__ off) {
+  __shared__ unsigned long long sh[16];
+  const int d = blockIdx.x, f = threadIdx.x;
+  const int j0 = (int)cB[d], j1 = (int)cB[d + 1];
+  const unsigned tot = S[(int64_t)f * L + j1] - S[(int64_t)f * L + j0];
+  unsigned long long t;
+  const unsigned long long e = block_excl_scan_u64(tot, sh, &t);
+  off[(int64_t)d * KD + f] = seg[d] + e;
+  if (d == KD - 1 && f == 0) off[KM_NB] = seg[KD];
+}
+
+__global__ __launch_bounds__(256) void km_scatter_b_kernel(const double *__restrict__ tmp,
+                                                           const double *__restrict__ geo,
+                                                           const unsigned *__restrict__ seg,
+                                                           const unsigned *__restrict__ cB,
+                                                           const unsigned *__restrict__ S, int L,
+                                                           const unsigned long long *__restrict__ off,
+                                                           double *__restrict__ xs) {
+  __shared__ unsigned h[KD];
+  const int j = blockIdx.x;
+  if (j >= (int)cB[KD]) return;
+  const int d = km_seg_of(cB, j), j0 = (int)cB[d];
+  for (int f = threadIdx.x; f < KD; f += 256)
+    h[f] = (unsigned)(off[(int64_t)d * KD + f] - seg[d]) + S[(int64_t)f * L + j] - S[(int64_t)f * L + j0];
+  __syncthreads();
+  const long long a = (long long)seg[d] + (long long)(j - j0) * KS_CH;
+  const long long b = a + KS_CH < (long long)seg[d + 1] ? a + KS_CH : (long long)seg[d + 1];
+  const double mn = geo[0], inv = geo[1];
+#pragma unroll 4
+  for (int e = 0; e < KS_CH / 256; ++e) {
+    const long long i = a + (long long)e * 256 + threadIdx.x;
+    if (i < b) {
+      const double v = tmp[i];
+      xs[(long long)seg[d] + atomicAdd(&h[km_bucket(v, mn, inv) & (KD - 1)], 1u)] = v;
+    }
+  }
+}
+
+// bucket prefix sums: per 4096-sample chunk of xs the sums of q and q^2, their scan, then per
+// non-empty bucket the sums before its first sample
+__global__ __launch_bounds__(PT) void km_chunk_sum_kernel(const double *__restrict__ xs, const KmState *st,
+                                                          long long *__restrict__ cq, U128 *__restrict__ cq2) {
+  __shared__ U128 sh[PT / 64];
+  __shared__ long long sa[PT / 64];
+  const int64_t nv = (int64_t)st->nvalid;
+  const int s = st->s;
+  const int64_t i0 = (int64_t)blockIdx.x * PB + threadIdx.x;
+  long long a = 0;
+  u128 b = 0;
+#pragma unroll
+  for (int e = 0; e < PB / PT; ++e) {
+    const int64_t i = i0 + (int64_t)e * PT;
+    if (i < nv) {
+      const long long q = km_q(xs[i], s);
+      a += q;
+      b += km_q2(q);
+    }
+  }
+  a = hrf::wave_sum(a);
+  if ((threadIdx.x & 63) == 0) sa[threadIdx.x >> 6] = a;
+  const U128 tb = block_sum128(P(b), sh);
+  if (threadIdx.x == 0) {
+    cq[blockIdx.x] = sa[0] + sa[1] + sa[2] + sa[3];
+    cq2[blockIdx.x] = tb;
+  }
+}
+
+__global__ __launch_bounds__(PT) void km_chunk_scan_kernel(long long *__restrict__ cq, U128 *__restrict__ cq2,
+                                                           int nch, KmState *st) {
+  __shared__ U128 sh[PT / 64];
+  __shared__ unsigned long long shq[PT / 64];
+  unsigned long long carry = 0;
+  u128 carry2 = 0;
+  for (int b0 = 0; b0 < nch; b0 += PT) {
+    const int i = b0 + threadIdx.x;
+    const unsigned long long a = i < nch ? (unsigned long long)cq[i] : 0ull;
+    const u128 b = i < nch ? U(cq2[i]) : (u128)0;
+    unsigned long long ta;
+    u128 tb;
+    const unsigned long long ea = block_excl_scan_u64(a, shq, &ta);  // two's complement: exact
+    const u128 eb = block_excl_scan128(b, sh, &tb);
+    if (i < nch) {
+      cq[i] = (long long)(carry + ea);
+      cq2[i] = P(carry2 + eb);
+    }
+    carry += ta;
+    carry2 += tb;
+  }
+  if (threadIdx.x == 0) {
+    st->sumq = (long long)carry;
+    st->sumq2 = P(carry2);
+  }
+}
+
+__global__ __launch_bounds__(PT) void km_bucket_prefix_kernel(const double *__restrict__ xs, const KmState *st,
+                                                              const double *__restrict__ geo,
+                                                              const long long *__restrict__ cq,
+                                                              const U128 *__restrict__ cq2, long long *__restrict__ bq,
+                                                              U128 *__restrict__ bq2) {
+  __shared__ U128 sh[PT / 64];
+  __shared__ unsigned long long shq[PT / 64];
+  const int64_t nv = (int64_t)st->nvalid;
+  const int s = st->s;
+  const double mn = geo[0], inv = geo[1];
+  const int64_t i0 = (int64_t)blockIdx.x * PB + threadIdx.x * (PB / PT);  // 16 consecutive samples
+  double v[PB / PT];
+  long long q[PB / PT];
+  unsigned long long a = 0;
+  u128 b = 0;
+#pragma unroll
+  for (int e = 0; e < PB / PT; ++e) {
+    const int64_t i = i0 + e;
+    v[e] = i < nv ? xs[i] : 0.0;
+    q[e] = i < nv ? km_q(v[e], s) : 0;
+    a += (unsigned long long)q[e];
+    b += km_q2(q[e]);
+  }
+  unsigned long long ta;
+  u128 tb;
+  unsigned long long ra = block_excl_scan_u64(a, shq, &ta) + (unsigned long long)cq[blockIdx.x];
+  u128 rb = block_excl_scan128(b, sh, &tb) + U(cq2[blockIdx.x]);
+  if (i0 >= nv) return;
+  int prev = i0 > 0 ? km_bucket(xs[i0 - 1], mn, inv) : -1;
+#pragma unroll
+  for (int e = 0; e < PB / PT; ++e) {
+    if (i0 + e >= nv) break;
+    const int kb = km_bucket(v[e], mn, inv);
+    if (kb != prev) {
+      bq[kb] = (long long)ra;
+      bq2[kb] = P(rb);
+    }
+    prev = kb;
+    ra += (unsigned long long)q[e];
+    rb += km_q2(q[e]);
+  }
+}
+
+// tol = 1e-4 * var(x) from the exact sums (kmeans_sk.c)
+__global__ void km_tol_kernel(KmState *st) {
+  const long long nv = (long long)st->nvalid;
+  if (!nv) {
+    st->tol = 0;
+    return;
+  }
+  const double m1 = (double)st->sumq / (double)nv, m2 = u128_to_double(U(st->sumq2)) / (double)nv;
+  st->tol = ldexp(m2 - m1 * m1, -2 * st->s) * 1e-4;
+}
+
+// ---- k-means++ -------------------------------------------------------------------------------
+// closest squared distance of v to the run's first c centres.  floor(. * 2^S) is monotone, so the
+// least fixed-point potential is the fixed point of the least square: one conversion per sample.
+__device__ __forceinline__ double closest_sq(double v, const double *cen, int c) {
+  double b = (v - cen[0]) * (v - cen[0]);
+  for (int j = 1; j < c; ++j) {
+    const double d = (v - cen[j]) * (v - cen[j]);
+    b = d < b ? d : b;
+  }
+  return b;
+}
+__device__ __forceinline__ unsigned long long closest_q(double v, const double *cen, int c, double scaleS) {
+  return (unsigned long long)(closest_sq(v, cen, c) * scaleS);
+}
+
+// the first centre of every run: first[r]-th valid sample in raster order (xr compacted)
+__global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, Draws d) {
   const int r = threadIdx.x;
-  if (r < NRUN * NTMAX) corr[r] = U128{0, 0};
   if (r >= d.nrun) return;
   SkRun &R = st->run[r];
   const long long nv = (long long)st->nvalid;
@@ -450,6 +729,8 @@ __global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, D
 __global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict__ xr, const KmState *st, Draws d,
                                                         U128 *__restrict__ part, int nblk, int c) {
   __shared__ U128 sh[PT / 64];
+  __shared__ double cen[NRUN][KMAX];
+  if (threadIdx.x < NRUN * KMAX) cen[threadIdx.x / KMAX][threadIdx.x % KMAX] = st->run[threadIdx.x / KMAX].cen[threadIdx.x % KMAX];
   const int64_t nv = (int64_t)st->nvalid;
   const double scaleS = ldexp(1.0, st->S);
   const int64_t base = (int64_t)blockIdx.x * PB + threadIdx.x;
@@ -461,11 +742,11 @@ __global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict
     v[e] = i < nv ? xr[i] : 0.0;
     cnt += i < nv;
   }
+  __syncthreads();
   for (int r = 0; r < d.nrun; ++r) {
-    const SkRun &R = st->run[r];
     u128 s = 0;
 #pragma unroll
-    for (int e = 0; e < PB / PT; ++e) s += e < cnt ? closest_q(v[e], R.cen, c, scaleS) : 0ull;
+    for (int e = 0; e < PB / PT; ++e) s += e < cnt ? closest_q(v[e], cen[r], c, scaleS) : 0ull;
     const U128 tot = block_sum128(P(s), sh);
     if (threadIdx.x == 0) part[(int64_t)r * nblk + blockIdx.x] = tot;
   }
@@ -582,65 +863,92 @@ __global__ __launch_bounds__(PT) void km_pp_pick_kernel(const double *__restrict
   }
 }
 
+// per sorted chunk (one pass over xs for all runs and trials): the chunk's part of every trial's
+// correction -> part2[(r * NTMAX + t) * nch + chunk] (zero where the cell misses the chunk)
 __global__ __launch_bounds__(PT) void km_pp_corr_kernel(const double *__restrict__ xs, const KmState *st, Draws d,
-                                                        const long long *__restrict__ rng, U128 *__restrict__ corr,
-                                                        int c) {
-  __shared__ long long cs[NRUN * NTMAX + 1];
-  __shared__ U128 sh[PT / 64];
-  const int np = d.nrun * d.nt;
-  if (threadIdx.x == 0) {
-    long long s = 0;
-    for (int p = 0; p < np; ++p) {
-      const int q = (p / d.nt) * NTMAX + p % d.nt;
-      cs[p] = s;
-      s += (rng[2 * q + 1] - rng[2 * q] + PB - 1) / PB;
-    }
-    cs[np] = s;
+                                                        const long long *__restrict__ rng, U128 *__restrict__ part2,
+                                                        int nch, int c) {
+  // per (run, trial) the chunk's sum: wave sums added into LDS (exact: carry into the high word)
+  __shared__ unsigned long long acc[NRUN * NTMAX][2];
+  __shared__ double cen[NRUN][KMAX], cand[NRUN * NTMAX];
+  __shared__ long long rg[NRUN * NTMAX][2];
+  for (int i = threadIdx.x; i < NRUN * NTMAX; i += PT) {
+    acc[i][0] = acc[i][1] = 0;
+    cand[i] = st->run[i / NTMAX].cand[i % NTMAX];
+    rg[i][0] = rng[2 * i];
+    rg[i][1] = rng[2 * i + 1];
   }
+  if (threadIdx.x < NRUN * KMAX) cen[threadIdx.x / KMAX][threadIdx.x % KMAX] = st->run[threadIdx.x / KMAX].cen[threadIdx.x % KMAX];
   __syncthreads();
+  const int64_t nv = (int64_t)st->nvalid;
+  const long long c0 = (long long)blockIdx.x * PB, c1 = c0 + PB < nv ? c0 + PB : nv;
   const double scaleS = ldexp(1.0, st->S);
-  for (long long g = blockIdx.x; g < cs[np]; g += gridDim.x) {
-    int p = 0;
-    while (cs[p + 1] <= g) ++p;
-    const int r = p / d.nt, t = p % d.nt, q = r * NTMAX + t;
-    const SkRun &R = st->run[r];
-    const double cv = R.cand[t];
-    const long long e = rng[2 * q + 1];
-    const long long i0 = rng[2 * q] + (g - cs[p]) * PB + threadIdx.x;
-    u128 s = 0;
-#pragma unroll 4
-    for (int k = 0; k < PB / PT; ++k) {
-      const long long i = i0 + (long long)k * PT;
-      if (i < e) {
-        const double v = xs[i];
-        const double dc = closest_sq(v, R.cen, c), dt = (v - cv) * (v - cv);
-        if (dt < dc) s += (unsigned long long)(dc * scaleS) - (unsigned long long)(dt * scaleS);
+  double v[PB / PT];
+#pragma unroll
+  for (int e = 0; e < PB / PT; ++e) {
+    const long long i = c0 + (long long)e * PT + threadIdx.x;
+    v[e] = i < c1 ? xs[i] : 0.0;
+  }
+  for (int r = 0; r < d.nrun; ++r) {
+    bool any = false;
+    for (int t = 0; t < d.nt; ++t) {
+      const int q = r * NTMAX + t;
+      any |= rg[q][0] < c1 && rg[q][1] > c0;
+    }
+    if (!any) continue;
+    double dc[PB / PT];
+#pragma unroll
+    for (int e = 0; e < PB / PT; ++e) dc[e] = closest_sq(v[e], cen[r], c);
+    for (int t = 0; t < d.nt; ++t) {
+      const int q = r * NTMAX + t;
+      const long long a = rg[q][0], b = rg[q][1];
+      if (!(a < c1 && b > c0)) continue;
+      const double cv = cand[q];
+      u128 s = 0;
+#pragma unroll
+      for (int e = 0; e < PB / PT; ++e) {
+        const long long i = c0 + (long long)e * PT + threadIdx.x;
+        const double dt = (v[e] - cv) * (v[e] - cv);
+        if (i >= a && i < b && i < c1 && dt < dc[e])
+          s += (unsigned long long)(dc[e] * scaleS) - (unsigned long long)(dt * scaleS);
+      }
+      const U128 w = wave_sum128(P(s));
+      if ((threadIdx.x & 63) == 0 && (w.lo | w.hi)) {
+        const unsigned long long old = atomicAdd(&acc[q][0], w.lo);
+        const unsigned long long h = w.hi + (old + w.lo < old ? 1ull : 0ull);
+        if (h) atomicAdd(&acc[q][1], h);
       }
     }
-    const U128 tot = block_sum128(P(s), sh);
-    if (threadIdx.x == 0 && (tot.lo | tot.hi)) atomic_add128(&corr[q], U(tot));
   }
+  __syncthreads();
+  for (int p = threadIdx.x; p < d.nrun * NTMAX; p += PT)
+    if (p % NTMAX < d.nt) part2[(int64_t)p * nch + blockIdx.x] = U128{acc[p][0], acc[p][1]};
 }
 
-// per run: T - corr of every trial, the least (first) wins; the corrections are reset
-__global__ void km_pp_choose_kernel(KmState *st, Draws d, U128 *__restrict__ corr, int c) {
-  const int r = threadIdx.x;
-  if (r >= d.nrun) return;
+// per run (one workgroup each): T - corr of every trial, the least (first) wins
+__global__ __launch_bounds__(PT) void km_pp_choose_kernel(KmState *st, Draws d, const U128 *__restrict__ part2,
+                                                          int nch, int c) {
+  __shared__ U128 sh[PT / 64];
+  const int r = blockIdx.x;
   SkRun &R = st->run[r];
   const u128 T = U(R.T);
   int bt = 0;
   u128 best = 0;
   for (int t = 0; t < d.nt; ++t) {
-    const u128 tt = T - U(corr[r * NTMAX + t]);
-    corr[r * NTMAX + t] = U128{0, 0};
+    const U128 *p = part2 + (int64_t)(r * NTMAX + t) * nch;
+    u128 s = 0;
+    for (int b = threadIdx.x; b < nch; b += PT) s += U(p[b]);
+    const u128 tt = T - U(block_sum128(P(s), sh));
     if (t == 0 || tt < best) {
       best = tt;
       bt = t;
     }
   }
-  R.cen[c] = R.cand[bt];
-  R.T = P(best);
-  R.ncen = c + 1;
+  if (threadIdx.x == 0) {
+    R.cen[c] = R.cand[bt];
+    R.T = P(best);
+    R.ncen = c + 1;
+  }
 }
 
 // ---- Lloyd on the sorted array ---------------------------------------------------------------
@@ -672,11 +980,11 @@ __device__ __forceinline__ int sk_assign(double v, const double *c) {
 // probe, end of the first bucket holding a "> j" probe).  A range of <= 4096 samples, or one a
 // round could not halve, is counted exhaustively.
 template <int K>
-__device__ void km_bucket_step(const double *__restrict__ xs, const long long *__restrict__ q,
-                               const U128 *__restrict__ q2, const long long *__restrict__ prefix,
-                               const U128 *__restrict__ p2, const unsigned long long *__restrict__ off, int64_t nv,
-                               double mn, double inv, double range, const double *c, const int *pos,
-                               const double *cso, int j, int64_t *cnt_le, long long *sum_le, U128 *sq_le) {
+__device__ void km_bucket_step(const double *__restrict__ xs, const long long *__restrict__ bq,
+                               const U128 *__restrict__ bq2, const unsigned long long *__restrict__ off,
+                               const KmState *st, int64_t nv, int s, double mn, double inv, double range,
+                               const double *c, const int *pos, const double *cso, int j, int64_t *cnt_le,
+                               long long *sum_le, U128 *sq_le) {
   const int t = threadIdx.x;
   __shared__ int64_t lo_sh, hi_sh;
   __shared__ int bf_sh, bt_sh, exh_sh;
@@ -706,12 +1014,15 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       unsigned long long nf = 0;
       long long sf = 0;
       u128 qf = 0;
-      for (int64_t idx = lo + t; idx < hi; idx += KS_T)
-        if (pos[sk_assign<K>(xs[idx], c)] <= j) {
+      for (int64_t idx = lo + t; idx < hi; idx += KS_T) {
+        const double v = xs[idx];
+        if (pos[sk_assign<K>(v, c)] <= j) {
+          const long long qi = km_q(v, s);
           nf += 1;
-          sf += q[idx];
-          qf += U(q2[idx]);
+          sf += qi;
+          qf += km_q2(qi);
         }
+      }
       nf = hrf::wave_sum(nf);
       sf = hrf::wave_sum(sf);
       const U128 qw = wave_sum128(P(qf));
@@ -724,10 +1035,17 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
       }
       __syncthreads();
       if (t == 0) {
-        u128 qa = U(p2[lo]);
+        // lo starts a bucket (or is nv): the sums before it
+        long long pa = st->sumq;
+        u128 qa = U(st->sumq2);
+        if (lo < nv) {
+          const int lb = km_bucket(xs[lo], mn, inv);
+          pa = bq[lb];
+          qa = U(bq2[lb]);
+        }
         for (int w = 0; w < KS_T / 64; ++w) qa += U(qf_sh[w]);
         *cnt_le = lo + (int64_t)nf_sh;
-        *sum_le = prefix[lo] + sf_sh;
+        *sum_le = pa + sf_sh;
         *sq_le = P(qa);
       }
       __syncthreads();
@@ -765,10 +1083,10 @@ __device__ void km_bucket_step(const double *__restrict__ xs, const long long *_
 // the assignment for the centres c (sklearn order): per sklearn id count, sum q, sum q^2;
 // the label signature (sorted ranks -> ids, cumulative counts)
 template <int K>
-__device__ void km_assign_all(const double *xs, const long long *q, const U128 *q2, const long long *prefix,
-                              const U128 *p2, const unsigned long long *off, int64_t nv, double mn, double inv,
-                              double range, const double *c, int *ids, int *pos, double *cso, int64_t *cle,
-                              long long *sle, U128 *qle, long long *cnt, long long *sum, U128 *sq) {
+__device__ void km_assign_all(const double *xs, const long long *bq, const U128 *bq2, const unsigned long long *off,
+                              const KmState *st, int64_t nv, int s, double mn, double inv, double range,
+                              const double *c, int *ids, int *pos, double *cso, int64_t *cle, long long *sle,
+                              U128 *qle, long long *cnt, long long *sum, U128 *sq) {
   const int t = threadIdx.x;
   if (t == 0) {
     // sorted ranks by (value, sklearn id): among equal centres the first id takes the samples
@@ -790,12 +1108,12 @@ __device__ void km_assign_all(const double *xs, const long long *q, const U128 *
   __syncthreads();
   for (int j = 0; j + 1 < K; ++j)
     if (cso[j] != cso[j + 1])
-      km_bucket_step<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, pos, cso, j, &cle[j], &sle[j], &qle[j]);
+      km_bucket_step<K>(xs, bq, bq2, off, st, nv, s, mn, inv, range, c, pos, cso, j, &cle[j], &sle[j], &qle[j]);
   __syncthreads();
   if (t == 0) {
     cle[K - 1] = nv;
-    sle[K - 1] = prefix[nv];
-    qle[K - 1] = p2[nv];
+    sle[K - 1] = st->sumq;
+    qle[K - 1] = st->sumq2;
     for (int j = K - 2; j >= 0; --j)
       if (cso[j] == cso[j + 1]) {  // rank j+1 is never taken: the same cumulative state
         cle[j] = cle[j + 1];
@@ -818,10 +1136,9 @@ __device__ void km_assign_all(const double *xs, const long long *q, const U128 *
 }
 
 template <int K>
-__global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict__ xs, const long long *__restrict__ q,
-                                                        const U128 *__restrict__ q2,
-                                                        const long long *__restrict__ prefix,
-                                                        const U128 *__restrict__ p2,
+__global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict__ xs,
+                                                        const long long *__restrict__ bq,
+                                                        const U128 *__restrict__ bq2,
                                                         const unsigned long long *__restrict__ off,
                                                         const double *__restrict__ geo, KmState *st, int max_iter) {
   __shared__ double c[KMAX], cso[KMAX], oldc[KMAX];
@@ -857,7 +1174,7 @@ __global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict
   __syncthreads();
   int it;
   for (it = 0; it < max_iter; ++it) {
-    km_assign_all<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
+    km_assign_all<K>(xs, bq, bq2, off, st, nv, s, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
     if (t == 0) {
       nempty = 0;
       for (int j = 0; j < K; ++j) nempty += cnt[j] == 0;
@@ -940,9 +1257,10 @@ __global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict
           const long long fi = far_sh[pk++];
           if (fi < 0) continue;
           const int oj = sk_assign<K>(xs[fi], c);
-          sum[oj] -= q[fi];
+          const long long qf = km_q(xs[fi], s);
+          sum[oj] -= qf;
           cnt[oj] -= 1;
-          sum[j] = q[fi];
+          sum[j] = qf;
           cnt[j] = 1;
           R.reloc += 1;
         }
@@ -990,7 +1308,7 @@ __global__ __launch_bounds__(KS_T) void km_lloyd_kernel(const double *__restrict
   __syncthreads();
   // final labels: strict -> the last assignment (made with oldc); else an E-step with c
   if (stop != 2) {
-    km_assign_all<K>(xs, q, q2, prefix, p2, off, nv, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
+    km_assign_all<K>(xs, bq, bq2, off, st, nv, s, mn, inv, range, c, ids, pos, cso, cle, sle, qle, cnt, sum, sq);
   }
   if (t == 0) {
     // inertia of the final labels (their own sums, before any relocation) and final centres
@@ -1118,11 +1436,11 @@ __global__ void km_label_kernel(const double *__restrict__ x, const uint8_t *__r
 struct SortWs {
   KmState *st;
   double *geo;
-  uint32_t *key_in, *key;
+  unsigned *cntA, *cntB, *seg, *cB, *sbsum;
   unsigned long long *off;
-  double *xs, *xr;
-  long long *q, *prefix;
-  U128 *q2, *p2, *part, *corr;
+  double *xs, *xr, *tmpx;
+  long long *bq, *cq;
+  U128 *bq2, *cq2, *part, *corr;
   long long *rng;
   unsigned long long *nsel;
   void *tmp;
@@ -1134,65 +1452,94 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 int64_t nblocks(int64_t n) { return std::max<int64_t>(1, (n + PB - 1) / PB); }
 
 hrf_status sort_tmp_bytes(int64_t n, size_t *bytes) {
-  size_t a = 0, b = 0, c = 0, d = 0;
+  size_t d = 0;
   const size_t m = (size_t)std::max<int64_t>(n, 1);
-  HRF_HIP(rocprim::radix_sort_pairs(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr, (const double *)nullptr,
-                                    (double *)nullptr, m, 0, KM_NB_BITS, (hipStream_t)0));
-  HRF_HIP(rocprim::inclusive_scan(nullptr, b, (const unsigned long long *)nullptr, (unsigned long long *)nullptr, m,
-                                  rocprim::plus<unsigned long long>(), (hipStream_t)0));
-  HRF_HIP(rocprim::inclusive_scan(nullptr, c, (const U128 *)nullptr, (U128 *)nullptr, m, U128Plus(), (hipStream_t)0));
   HRF_HIP(rocprim::select(nullptr, d, (const double *)nullptr, (const uint8_t *)nullptr, (double *)nullptr,
                           (unsigned long long *)nullptr, m, (hipStream_t)0));
-  *bytes = std::max(std::max(a, b), std::max(c, d));
+  *bytes = d;
   return HRF_OK;
 }
 
+// one table, carved in order by carve() (sizes kept in one place)
+int nch_b(int64_t n) { return (int)nblocks(n) + KD; }         // coarse-segment chunk bound
+int64_t scan_blocks(int64_t n) {
+  const int64_t a = (int64_t)KD * nblocks(n), b = (int64_t)KD * (nch_b(n) + 1);
+  return (std::max(a, b) + KSC_B - 1) / KSC_B;
+}
+
+// one table, carved in order by carve() (sizes kept in one place)
+template <class F>
+void ws_layout(int64_t n, size_t tmp_bytes, F &&f) {
+  const size_t m = (size_t)std::max<int64_t>(n, 1), nb = (size_t)nblocks(n);
+  f(align256(sizeof(KmState)));                          // st
+  f(256);                                                // geo
+  f(align256(sizeof(unsigned) * KD * nb));               // cntA
+  f(align256(sizeof(unsigned) * KD * (nch_b(n) + 1)));   // cntB
+  f(align256(sizeof(unsigned) * (KD + 1)));              // seg
+  f(align256(sizeof(unsigned) * (KD + 1)));              // cB
+  f(align256(sizeof(unsigned) * scan_blocks(n)));        // sbsum
+  f(align256(sizeof(unsigned long long) * (KM_NB + 1))); // off
+  f(align256(sizeof(double) * m));                       // xs
+  f(align256(sizeof(double) * m));                       // xr
+  f(align256(sizeof(double) * m));                       // tmpx
+  f(align256(sizeof(long long) * KM_NB));                // bq
+  f(align256(sizeof(long long) * nb));                   // cq
+  f(align256(sizeof(U128) * KM_NB));                     // bq2
+  f(align256(sizeof(U128) * nb));                        // cq2
+  f(align256(sizeof(U128) * NRUN * nb));                 // part
+  f(align256(sizeof(U128) * NRUN * NTMAX * nb));         // corr (per trial and sorted chunk)
+  f(align256(sizeof(long long) * 2 * NRUN * NTMAX));     // rng
+  f(256);                                                // nsel
+  f(align256(tmp_bytes));                                // tmp
+}
+
 int64_t sort_ws_bytes(int64_t n, size_t tmp_bytes) {
-  const size_t m = (size_t)std::max<int64_t>(n, 1);
-  return (int64_t)(align256(sizeof(KmState)) + 256 + 2 * align256(sizeof(uint32_t) * m) +
-                   align256(sizeof(unsigned long long) * (KM_NB + 1)) + 2 * align256(sizeof(double) * m) +
-                   2 * align256(sizeof(long long) * (m + 1)) + 2 * align256(sizeof(U128) * (m + 1)) +
-                   align256(sizeof(U128) * NRUN * nblocks(n)) + align256(sizeof(U128) * NRUN * NTMAX) +
-                   align256(sizeof(long long) * 2 * NRUN * NTMAX) + 256 + align256(tmp_bytes));
+  size_t tot = 0;
+  ws_layout(n, tmp_bytes, [&](size_t b) { tot += b; });
+  return (int64_t)tot;
 }
 
 SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   char *w = (char *)work;
-  const size_t m = (size_t)std::max<int64_t>(n, 1);
+  char *p[24];
+  int i = 0;
+  ws_layout(n, tmp_bytes, [&](size_t b) {
+    p[i++] = w;
+    w += b;
+  });
   SortWs ws{};
-  ws.st = (KmState *)w;
-  w += align256(sizeof(KmState));
-  ws.geo = (double *)w;
-  w += 256;
-  ws.key_in = (uint32_t *)w;
-  w += align256(sizeof(uint32_t) * m);
-  ws.key = (uint32_t *)w;
-  w += align256(sizeof(uint32_t) * m);
-  ws.off = (unsigned long long *)w;
-  w += align256(sizeof(unsigned long long) * (KM_NB + 1));
-  ws.xs = (double *)w;
-  w += align256(sizeof(double) * m);
-  ws.xr = (double *)w;
-  w += align256(sizeof(double) * m);
-  ws.q = (long long *)w;
-  w += align256(sizeof(long long) * (m + 1));
-  ws.prefix = (long long *)w;
-  w += align256(sizeof(long long) * (m + 1));
-  ws.q2 = (U128 *)w;
-  w += align256(sizeof(U128) * (m + 1));
-  ws.p2 = (U128 *)w;
-  w += align256(sizeof(U128) * (m + 1));
-  ws.part = (U128 *)w;
-  w += align256(sizeof(U128) * NRUN * nblocks(n));
-  ws.corr = (U128 *)w;
-  w += align256(sizeof(U128) * NRUN * NTMAX);
-  ws.rng = (long long *)w;
-  w += align256(sizeof(long long) * 2 * NRUN * NTMAX);
-  ws.nsel = (unsigned long long *)w;
-  w += 256;
-  ws.tmp = w;
+  int k = 0;
+  ws.st = (KmState *)p[k++];
+  ws.geo = (double *)p[k++];
+  ws.cntA = (unsigned *)p[k++];
+  ws.cntB = (unsigned *)p[k++];
+  ws.seg = (unsigned *)p[k++];
+  ws.cB = (unsigned *)p[k++];
+  ws.sbsum = (unsigned *)p[k++];
+  ws.off = (unsigned long long *)p[k++];
+  ws.xs = (double *)p[k++];
+  ws.xr = (double *)p[k++];
+  ws.tmpx = (double *)p[k++];
+  ws.bq = (long long *)p[k++];
+  ws.cq = (long long *)p[k++];
+  ws.bq2 = (U128 *)p[k++];
+  ws.cq2 = (U128 *)p[k++];
+  ws.part = (U128 *)p[k++];
+  ws.corr = (U128 *)p[k++];
+  ws.rng = (long long *)p[k++];
+  ws.nsel = (unsigned long long *)p[k++];
+  ws.tmp = p[k++];
   ws.tmp_bytes = tmp_bytes;
   return ws;
+}
+
+hrf_status scan_u32(unsigned *a, int64_t n, unsigned *bsum, hipStream_t s) {
+  const int nb = (int)((n + KSC_B - 1) / KSC_B);
+  km_scan_sum_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
+  km_scan_blocks_kernel<<<1, 1024, 0, s>>>(bsum, nb);
+  km_scan_apply_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
+  HRF_LAUNCHED();
+  return HRF_OK;
 }
 
 // Enqueue one KMeans(k) fit: sort (unless `reuse`), k-means++ for all runs, Lloyd, winner,
@@ -1210,25 +1557,26 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
     km_scale_kernel<<<1, 1, 0, s>>>(st);
     HRF_LAUNCHED();
     if (n > 0) {
+      const unsigned nch = (unsigned)nblocks(n);
       km_bucket_init_kernel<<<1, 1, 0, s>>>(st, ws.geo);
-      km_bucket_key_kernel<<<g, 256, 0, s>>>(x, valid, n, ws.geo, ws.key_in);
+      const int L = nch_b(n) + 1;
+      km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch);
+      if (hrf_status r = scan_u32(ws.cntA, (int64_t)KD * nch, ws.sbsum, s)) return r;
+      km_scatter_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, ws.tmpx);
+      km_segments_kernel<<<1, KD, 0, s>>>(ws.cntA, (int)nch, st, ws.seg, ws.cB);
+      km_hist_b_kernel<<<L - 1, 256, 0, s>>>(ws.tmpx, ws.geo, ws.seg, ws.cB, ws.cntB, L);
+      if (hrf_status r = scan_u32(ws.cntB, (int64_t)KD * L, ws.sbsum, s)) return r;
+      km_bucket_off_kernel<<<KD, KD, 0, s>>>(ws.cntB, L, ws.seg, ws.cB, ws.off);
+      km_scatter_b_kernel<<<L - 1, 256, 0, s>>>(ws.tmpx, ws.geo, ws.seg, ws.cB, ws.cntB, L, ws.off, ws.xs);
+      km_chunk_sum_kernel<<<nch, PT, 0, s>>>(ws.xs, st, ws.cq, ws.cq2);
+      km_chunk_scan_kernel<<<1, PT, 0, s>>>(ws.cq, ws.cq2, (int)nch, st);
+      km_bucket_prefix_kernel<<<nch, PT, 0, s>>>(ws.xs, st, ws.geo, ws.cq, ws.cq2, ws.bq, ws.bq2);
       HRF_LAUNCHED();
-      size_t tb = ws.tmp_bytes;
-      HRF_HIP(rocprim::radix_sort_pairs(ws.tmp, tb, ws.key_in, ws.key, x, ws.xs, (size_t)n, 0, KM_NB_BITS, s));
-      km_bucket_bounds_kernel<<<hrf::stream_grid(std::max<int64_t>(n, KM_NB + 1)), 256, 0, s>>>(
-          ws.key, ws.xs, n, st, ws.off, ws.q, ws.q2, ws.prefix, ws.p2);
-      HRF_LAUNCHED();
-      // entries past the valid values (invalid ones, sorted last) are never read back
-      tb = ws.tmp_bytes;
-      HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, (const unsigned long long *)ws.q, (unsigned long long *)ws.prefix + 1,
-                                      (size_t)n, rocprim::plus<unsigned long long>(), s));
-      tb = ws.tmp_bytes;
-      HRF_HIP(rocprim::inclusive_scan(ws.tmp, tb, ws.q2, ws.p2 + 1, (size_t)n, U128Plus(), s));
       if (valid) {  // the valid samples in raster order (sklearn's sample order)
-        tb = ws.tmp_bytes;
+        size_t tb = ws.tmp_bytes;
         HRF_HIP(rocprim::select(ws.tmp, tb, x, valid, ws.xr, ws.nsel, (size_t)n, s));
       }
-      km_tol_kernel<<<1, 1, 0, s>>>(ws.prefix, ws.p2, st);
+      km_tol_kernel<<<1, 1, 0, s>>>(st);
       km_count_le0_kernel<<<1, 1024, 0, s>>>(ws.xs, ws.off, ws.geo, st);
       HRF_LAUNCHED();
     }
@@ -1250,16 +1598,16 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   const Draws d = make_draws(std::max<int64_t>(nv, 1), K, n_init, 0u);
   const double *xr = valid ? ws.xr : x;
   const int nblk = (int)nblocks(nv);
-  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d, ws.corr);
+  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d);
   HRF_LAUNCHED();
   for (int c = 1; c < K; ++c) {
     km_pp_pass_kernel<<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk, c);
     km_pp_pick_kernel<<<n_init * d.nt, PT, 0, s>>>(xr, ws.off, ws.geo, st, d, ws.part, nblk, c, ws.rng);
-    km_pp_corr_kernel<<<1024, PT, 0, s>>>(ws.xs, st, d, ws.rng, ws.corr, c);
-    km_pp_choose_kernel<<<1, 64, 0, s>>>(st, d, ws.corr, c);
+    km_pp_corr_kernel<<<nblk, PT, 0, s>>>(ws.xs, st, d, ws.rng, ws.corr, nblk, c);
+    km_pp_choose_kernel<<<n_init, PT, 0, s>>>(st, d, ws.corr, nblk, c);
     HRF_LAUNCHED();
   }
-  km_lloyd_kernel<K><<<n_init, KS_T, 0, s>>>(ws.xs, ws.q, ws.q2, ws.prefix, ws.p2, ws.off, ws.geo, st, max_iter);
+  km_lloyd_kernel<K><<<n_init, KS_T, 0, s>>>(ws.xs, ws.bq, ws.bq2, ws.off, ws.geo, st, max_iter);
   km_best_kernel<K><<<1, 64, 0, s>>>(st, n_init, rule);
   km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
   HRF_LAUNCHED();
@@ -1281,7 +1629,7 @@ hrf_status km_launch_k(int k, const double *x, const uint8_t *valid, int64_t n, 
 hrf_status check_args(int32_t k, int64_t n, int32_t max_iter, int32_t n_init, int32_t rule, const void *work,
                       const double *x) {
   HRF_REQUIRE(k >= 1 && k <= KMAX, "kmeans_1d: k must be 1..8");
-  HRF_REQUIRE(n >= 0 && n < ((int64_t)1 << 40) && max_iter >= 1 && work, "kmeans_1d: bad arguments");
+  HRF_REQUIRE(n >= 0 && n < ((int64_t)1 << 32) - KS_CH && max_iter >= 1 && work, "kmeans_1d: bad arguments");
   HRF_REQUIRE(n_init >= 1 && n_init <= NRUN, "kmeans_1d: n_init must be 1..10");
   HRF_REQUIRE(rule >= 0 && rule <= 2, "kmeans_1d: top rule must be 0, 1 or 2");
   HRF_REQUIRE(n == 0 || x, "kmeans_1d: null input");
