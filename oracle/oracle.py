@@ -322,6 +322,8 @@ def classify(x, ref, bounds, variant=0, fx=None, fr=None):
     R = ref.shape[0]
     arg = np.zeros(n, np.int32)
     dmin = np.zeros(n, np.float64)
+    if variant and (fx is None or fr is None):
+        raise ValueError("classify: the gated variants need the presence flags fx and fr")
     fxa = _c(fx, np.float64) if fx is not None else None
     fra = _c(fr, np.float64) if fr is not None else None
     lib().oracle_classify(_p(x), I64(n), _p(ref), R, C, _p(b), len(b) - 1, variant,

@@ -75,8 +75,20 @@ def measure_ecoli(stack, calibration=None, keep=None, image_cn=None):
     return seg, labs.astype(np.int32), avgint, avgint_norm
 
 
-def classify_cells(avgint_norm, library, bounds, variant=0):
-    return O.classify(avgint_norm, library.astype(np.float64), bounds, variant)
+def segment_flags(x, bounds, thr=0.1):
+    """per-segment presence flags (segment max > thr): the stand-in for the per-laser check
+    SVCs that feed the gated metrics (a18; hiprfish_image_analysis_amd/pipeline.py:181)"""
+    x = np.asarray(x, np.float64)
+    return np.stack([x[:, bounds[k]:bounds[k + 1]].max(axis=1) > thr for k in range(len(bounds) - 1)],
+                    1).astype(np.float64)
+
+
+def classify_cells(avgint_norm, library, bounds, variant=0, flag_thr=0.1):
+    fx = fr = None
+    if variant:
+        fx = segment_flags(avgint_norm, bounds, flag_thr)
+        fr = segment_flags(library, bounds, flag_thr)
+    return O.classify(avgint_norm, library.astype(np.float64), bounds, variant, fx, fr)
 
 
 def process_tile(stack, library, bounds, calibration=None):
