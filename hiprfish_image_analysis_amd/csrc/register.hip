@@ -112,21 +112,26 @@ __global__ __launch_bounds__(256) void abs_argmax_final_kernel(const Best *__res
   }
 }
 
-}  // namespace
-
-extern "C" {
-
-int64_t hrf_register_workspace_bytes(int64_t H, int64_t W) {
-  const int64_t nc = H * (W / 2 + 1);
-  return 3 * nc * (int64_t)sizeof(hipfftDoubleComplex) + H * W * (int64_t)sizeof(double) +
-         AM_BLOCKS * (int64_t)sizeof(Best) + 64;
+// peak index -> (row, col) shift (midpoints = fix(n / 2)); |component| > clamp -> 0 (clamp >= 0;
+// ecoli measurement.py:47-57)
+__global__ void shift_of_peak_kernel(const int64_t *__restrict__ bidx, int64_t H, int64_t W, int32_t clamp,
+                                     int32_t *__restrict__ shift) {
+  const int64_t best = *bidx;
+  int64_t r = best / W, c = best % W;
+  if (r > H / 2) r -= H;
+  if (c > W / 2) c -= W;
+  if (clamp >= 0) {
+    r = (r > clamp || r < -clamp) ? 0 : r;
+    c = (c > clamp || c < -clamp) ? 0 : c;
+  }
+  shift[0] = (int32_t)r;
+  shift[1] = (int32_t)c;
 }
 
-hrf_status hrf_register_translation(const double *src, const double *target, int64_t H, int64_t W, void *work,
-                                    int32_t *shift_host, hrf_stream_t stream) {
-  HRF_REQUIRE(H >= 1 && W >= 1 && H <= (1 << 20) && W <= (1 << 20), "register_translation: bad image size");
-  HRF_REQUIRE(src && target && work && shift_host, "register_translation: null buffer");
-  hipStream_t s = (hipStream_t)stream;
+// the cross-correlation peak index into bidx (device); the FFT of src is taken unless
+// src_fft_ready (then work already holds it, from a previous call with the same src)
+hrf_status xcorr_peak(const double *src, const double *target, int64_t H, int64_t W, void *work, bool src_fft_ready,
+                      hipStream_t s, int64_t **bidx_out) {
   const int64_t nc = H * (W / 2 + 1);
   char *w = (char *)work;
   hipfftDoubleComplex *fa = (hipfftDoubleComplex *)w;
@@ -142,7 +147,7 @@ hrf_status hrf_register_translation(const double *src, const double *target, int
     HRF_FFT(hipfftSetStream(p.fwd, s));
     HRF_FFT(hipfftSetStream(p.inv, s));
     // hipFFT's real-to-complex transform does not modify its input
-    HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(src), fa));
+    if (!src_fft_ready) HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(src), fa));
     HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(target), fb));
     xcorr_product_kernel<<<hrf::stream_grid(nc), 256, 0, s>>>(fa, fb, nc, fp);
     HRF_LAUNCHED();
@@ -152,6 +157,40 @@ hrf_status hrf_register_translation(const double *src, const double *target, int
   abs_argmax_partial_kernel<<<nb, 256, 0, s>>>(cc, H * W, part);
   abs_argmax_final_kernel<<<1, 256, 0, s>>>(part, (int)nb, bidx);
   HRF_LAUNCHED();
+  *bidx_out = bidx;
+  return HRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t hrf_register_workspace_bytes(int64_t H, int64_t W) {
+  const int64_t nc = H * (W / 2 + 1);
+  return 3 * nc * (int64_t)sizeof(hipfftDoubleComplex) + H * W * (int64_t)sizeof(double) +
+         AM_BLOCKS * (int64_t)sizeof(Best) + 64;
+}
+
+hrf_status hrf_register_translation_dev(const double *src, const double *target, int64_t H, int64_t W, void *work,
+                                        int32_t clamp, int32_t *shift_dev, hrf_stream_t stream) {
+  HRF_REQUIRE(H >= 1 && W >= 1 && H <= (1 << 20) && W <= (1 << 20), "register_translation: bad image size");
+  HRF_REQUIRE(target && work && shift_dev, "register_translation: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *bidx = nullptr;
+  // src == nullptr: the FFT of the reference image is already in the workspace
+  if (hrf_status st = xcorr_peak(src, target, H, W, work, src == nullptr, s, &bidx)) return st;
+  shift_of_peak_kernel<<<1, 1, 0, s>>>(bidx, H, W, clamp, shift_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_register_translation(const double *src, const double *target, int64_t H, int64_t W, void *work,
+                                    int32_t *shift_host, hrf_stream_t stream) {
+  HRF_REQUIRE(H >= 1 && W >= 1 && H <= (1 << 20) && W <= (1 << 20), "register_translation: bad image size");
+  HRF_REQUIRE(src && target && work && shift_host, "register_translation: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  int64_t *bidx = nullptr;
+  if (hrf_status st = xcorr_peak(src, target, H, W, work, false, s, &bidx)) return st;
   int64_t best = 0;
   HRF_HIP(hipMemcpyAsync(&best, bidx, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));

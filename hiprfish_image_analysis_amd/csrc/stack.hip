@@ -21,7 +21,19 @@ struct Lasers {
   int32_t c0[LMAX + 1];  // channel offsets, c0[n] = C
   int32_t dr[LMAX], dc[LMAX];
   int32_t n;
+  const int32_t *dsh;  // non-null: the shifts are read from the device (dr, dc pairs)
 };
+
+// the shifts in force: from the device buffer when given (no host round trip), else the
+// kernel-argument copies
+__device__ __forceinline__ void load_shifts(const Lasers &L, int *sdr, int *sdc) {
+  if (threadIdx.x < LMAX) {
+    const int q = threadIdx.x;
+    sdr[q] = q < L.n ? (L.dsh ? L.dsh[2 * q] : L.dr[q]) : 0;
+    sdc[q] = q < L.n ? (L.dsh ? L.dsh[2 * q + 1] : L.dc[q]) : 0;
+  }
+  __syncthreads();
+}
 
 __device__ __forceinline__ bool covered(int64_t r, int64_t c, int64_t H, int64_t W, int dr, int dc) {
   // destination rows [max(0,dr), H + min(0,dr)), same for columns
@@ -29,6 +41,8 @@ __device__ __forceinline__ bool covered(int64_t r, int64_t c, int64_t H, int64_t
 }
 
 __global__ void assemble_kernel(Lasers L, int64_t H, int64_t W, int apply_mask, float *__restrict__ dst) {
+  __shared__ int sdr[LMAX], sdc[LMAX];
+  load_shifts(L, sdr, sdc);
   const int C = L.c0[L.n];
   const int64_t n = H * W * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
@@ -43,12 +57,12 @@ __global__ void assemble_kernel(Lasers L, int64_t H, int64_t W, int apply_mask, 
     if (apply_mask) {
 #pragma unroll
       for (int q = 0; q < LMAX; ++q)
-        if (q < L.n) ok = ok && covered(r, c, H, W, L.dr[q], L.dc[q]);
+        if (q < L.n) ok = ok && covered(r, c, H, W, sdr[q], sdc[q]);
     }
     float v = 0.0f;
-    if (ok && covered(r, c, H, W, L.dr[li], L.dc[li])) {
+    if (ok && covered(r, c, H, W, sdr[li], sdc[li])) {
       const int cl = L.c0[li + 1] - L.c0[li];
-      v = L.src[li][((r - L.dr[li]) * W + (c - L.dc[li])) * cl + (ch - L.c0[li])];
+      v = L.src[li][((r - sdr[li]) * W + (c - sdc[li])) * cl + (ch - L.c0[li])];
     }
     dst[e] = v;
   }
@@ -63,6 +77,8 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
                                                            float *__restrict__ dst, int vec_ok) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ uint8_t okp[AS_P];
+  __shared__ int sdr[LMAX], sdc[LMAX];
+  load_shifts(L, sdr, sdc);
   const int C = L.c0[L.n];
   const int tid = threadIdx.x;
   const int64_t r = blockIdx.y;
@@ -71,15 +87,16 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
   if (tid < AS_P) {
     bool ok = tid < np;
     if (apply_mask)
-      for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, L.dr[q], L.dc[q]);
+      for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, sdr[q], sdc[q]);
     okp[tid] = (uint8_t)ok;
   }
   for (int q = 0; q < L.n; ++q) {
     const int cl = L.c0[q + 1] - L.c0[q], off = L.c0[q];
-    const int64_t rs = r - L.dr[q];
-    const bool row_ok = r >= (L.dr[q] > 0 ? L.dr[q] : 0) && r < H + (L.dr[q] < 0 ? L.dr[q] : 0);
-    const float *src = L.src[q] + (rs * W + (c0 - L.dc[q])) * (int64_t)cl;  // pixel c0's source (may be off-row)
-    const int cmin = L.dc[q] > 0 ? L.dc[q] : 0, cmax = (int)W + (L.dc[q] < 0 ? L.dc[q] : 0);
+    const int dr = sdr[q], dc = sdc[q];
+    const int64_t rs = r - dr;
+    const bool row_ok = r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0);
+    const float *src = L.src[q] + (rs * W + (c0 - dc)) * (int64_t)cl;  // pixel c0's source (may be off-row)
+    const int cmin = dc > 0 ? dc : 0, cmax = (int)W + (dc < 0 ? dc : 0);
     const int n = np * cl;
     // four loads in flight per thread per round (the run is at most 64 x 128 floats)
     for (int i0 = tid; i0 < n; i0 += 1024) {
@@ -318,6 +335,20 @@ __global__ void pad_edge_kernel(const double *__restrict__ a, int64_t H, int64_t
   }
 }
 
+__global__ void pad_edge3_kernel(const double *__restrict__ a, int64_t X, int64_t Y, int64_t Z, int w,
+                                 double *__restrict__ o) {
+  const int64_t YP = Y + 2 * w, ZP = Z + 2 * w;
+  const int64_t n = (X + 2 * w) * YP * ZP;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t x = i / (YP * ZP), r = i - x * YP * ZP, y = r / ZP, z = r - y * ZP;
+    int64_t xx = x - w, yy = y - w, zz = z - w;
+    xx = xx < 0 ? 0 : (xx >= X ? X - 1 : xx);
+    yy = yy < 0 ? 0 : (yy >= Y ? Y - 1 : yy);
+    zz = zz < 0 ? 0 : (zz >= Z ? Z - 1 : zz);
+    o[i] = a[(xx * Y + yy) * Z + zz];
+  }
+}
+
 __global__ void mask_mul_kernel(const double *__restrict__ a, const uint8_t *__restrict__ m, int64_t n,
                                 double *__restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -360,19 +391,21 @@ __global__ void calibrate_kernel(const float *__restrict__ stack, int64_t npix, 
 
 extern "C" {
 
-hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *channels_host,
-                                 const int32_t *shifts_host, int32_t nlaser, int64_t H, int64_t W,
-                                 int32_t apply_mask, float *dst, hrf_stream_t stream) {
-  HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && shifts_host, "register_assemble: bad lasers");
+static hrf_status register_assemble(const float *const *src_host, const int32_t *channels_host,
+                                    const int32_t *shifts_host, const int32_t *shifts_dev, int32_t nlaser, int64_t H,
+                                    int64_t W, int32_t apply_mask, float *dst, hrf_stream_t stream) {
+  HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && (shifts_host || shifts_dev),
+              "register_assemble: bad lasers");
   Lasers L{};
   L.n = nlaser;
   L.c0[0] = 0;
+  L.dsh = shifts_dev;
   for (int i = 0; i < nlaser; ++i) {
     HRF_REQUIRE(channels_host[i] >= 1 && src_host[i], "register_assemble: laser %d empty", i);
     L.src[i] = src_host[i];
     L.c0[i + 1] = L.c0[i] + channels_host[i];
-    L.dr[i] = shifts_host[2 * i];
-    L.dc[i] = shifts_host[2 * i + 1];
+    L.dr[i] = shifts_host ? shifts_host[2 * i] : 0;
+    L.dc[i] = shifts_host ? shifts_host[2 * i + 1] : 0;
   }
   for (int i = nlaser + 1; i <= LMAX; ++i) L.c0[i] = L.c0[nlaser];
   const int64_t n = H * W * L.c0[nlaser];
@@ -389,6 +422,20 @@ hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *ch
   }
   HRF_LAUNCHED();
   return HRF_OK;
+}
+
+hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *channels_host,
+                                 const int32_t *shifts_host, int32_t nlaser, int64_t H, int64_t W,
+                                 int32_t apply_mask, float *dst, hrf_stream_t stream) {
+  HRF_REQUIRE(shifts_host, "register_assemble: null shifts");
+  return register_assemble(src_host, channels_host, shifts_host, nullptr, nlaser, H, W, apply_mask, dst, stream);
+}
+
+hrf_status hrf_register_assemble_dev(const float *const *src_host, const int32_t *channels_host,
+                                     const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                     int32_t apply_mask, float *dst, hrf_stream_t stream) {
+  HRF_REQUIRE(shifts_dev, "register_assemble: null device shifts");
+  return register_assemble(src_host, channels_host, nullptr, shifts_dev, nlaser, H, W, apply_mask, dst, stream);
 }
 
 hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,
@@ -489,6 +536,15 @@ hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32_t width
   HRF_REQUIRE(width >= 0 && H >= 1 && W >= 1 && a && out, "pad_edge: bad arguments");
   pad_edge_kernel<<<hrf::stream_grid((H + 2 * width) * (W + 2 * width)), 256, 0, (hipStream_t)stream>>>(a, H, W, width,
                                                                                                         out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_pad_edge3_f64(const double *a, int64_t X, int64_t Y, int64_t Z, int32_t width, double *out,
+                             hrf_stream_t stream) {
+  HRF_REQUIRE(width >= 0 && X >= 1 && Y >= 1 && Z >= 1 && a && out, "pad_edge3: bad arguments");
+  pad_edge3_kernel<<<hrf::stream_grid((X + 2 * width) * (Y + 2 * width) * (Z + 2 * width)), 256, 0,
+                     (hipStream_t)stream>>>(a, X, Y, Z, width, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -126,14 +126,23 @@ def _i32_host(seq):
 
 # ---- a1-a3 ----------------------------------------------------------------------------------
 def register_assemble(srcs, shifts, apply_mask=True):
-    """ecoli measurement.py:51-70: shift each (H,W,C_l) laser stack, concatenate on C."""
+    """ecoli measurement.py:51-70: shift each (H,W,C_l) laser stack, concatenate on C.
+    shifts: [(dr, dc), ...] on the host, or an (nlaser, 2) int32 device tensor (read by the
+    kernel: no synchronisation)."""
     import ctypes
     srcs = [_dev(s, torch.float32, "laser stack") for s in srcs]
     H, W = srcs[0].shape[:2]
     ch = _i32_host([s.shape[2] for s in srcs])
-    sh = _i32_host([v for d in shifts for v in (int(d[0]), int(d[1]))])
     ptrs = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
     out = torch.empty((H, W, int(ch.sum())), dtype=torch.float32, device=srcs[0].device)
+    if isinstance(shifts, torch.Tensor) and shifts.is_cuda:
+        sd = _dev(shifts, torch.int32, "shifts")
+        if sd.numel() != 2 * len(srcs):
+            raise ValueError("register_assemble: one (dr, dc) pair per laser expected")
+        _lib.call("hrf_register_assemble_dev", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd),
+                  len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _stream())
+        return out
+    sh = _i32_host([v for d in shifts for v in (int(d[0]), int(d[1]))])
     _lib.call("hrf_register_assemble", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, sh.ctypes.data,
               len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _stream())
     return out
@@ -209,6 +218,34 @@ def register_translation(src, target):
     sh = np.zeros(2, np.int32)
     _lib.call("hrf_register_translation", _ptr(src), _ptr(target), H, W, _ptr(work), sh.ctypes.data, _stream())
     return int(sh[0]), int(sh[1])
+
+
+def register_translations_dev(ref, targets, clamp=None):
+    """register_translation(ref, t) for every target, into an (1 + len(targets), 2) int32 device
+    tensor whose row 0 is (0, 0): the reference's transform is taken once, nothing synchronises.
+    clamp: |component| > clamp -> 0 (ecoli measurement.py:47-57), None keeps it."""
+    ref = _dev(ref, torch.float64, "src")
+    H, W = ref.shape
+    nb = int(_lib.lib().hrf_register_workspace_bytes(H, W))
+    work = torch.empty(nb, dtype=torch.uint8, device=ref.device)
+    out = torch.zeros((1 + len(targets), 2), dtype=torch.int32, device=ref.device)
+    cl = -1 if clamp is None else int(clamp)
+    for i, t in enumerate(targets):
+        t = _dev(t, torch.float64, "target")
+        if t.shape != ref.shape:
+            raise ValueError("register_translation: two equal-shape 2-D images expected")
+        _lib.call("hrf_register_translation_dev", _ptr(ref) if i == 0 else None, _ptr(t), H, W, _ptr(work), cl,
+                  _ptr(out[1 + i]), _stream())
+    return out
+
+
+def pad_edge_3d(a, width=5):
+    """skimage.util.pad(a, width, mode='edge') of an (X, Y, Z) f64 volume (biofilm :810)"""
+    a = _dev(a, torch.float64, "a")
+    X, Y, Z = a.shape
+    out = torch.empty((X + 2 * width, Y + 2 * width, Z + 2 * width), dtype=torch.float64, device=a.device)
+    _lib.call("hrf_pad_edge3_f64", _ptr(a), X, Y, Z, width, _ptr(out), _stream())
+    return out
 
 
 def max_f64(a):

@@ -91,13 +91,17 @@ def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, 
 # --------------------------------------------------------------------------------------------
 # Registration shift estimate
 # --------------------------------------------------------------------------------------------
-def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15):
+def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device: bool = False):
     """Integer shift of every laser stack against the first, skimage register_translation
     (upsample 1) on a per-laser projection:
     * reduce "max": np.max(image, axis=2), |shift| > clamp -> 0 (ecoli measurement.py:45-57);
     * reduce "sum": np.sum(image, axis=2), no clamp (multispecies measurement.py:82-84).
-    -> [(0, 0), (dr_1, dc_1), ...] ready for kernels.register_assemble."""
+    -> [(0, 0), (dr_1, dc_1), ...] ready for kernels.register_assemble; with `device` an
+    (nlaser, 2) int32 device tensor instead (no host synchronisation; register_assemble reads
+    it on the device)."""
     proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
+    if device:
+        return K.register_translations_dev(proj[0], proj[1:], clamp)
     shifts = [(0, 0)]
     for img in proj[1:]:
         r, c = K.register_translation(proj[0], img)
@@ -106,6 +110,27 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15):
             c = 0 if abs(c) > clamp else c
         shifts.append((r, c))
     return shifts
+
+
+def register_stack(lasers, reduce: str = "max", clamp: int | None = 15, apply_mask: bool = True):
+    """ecoli measurement.py:44-70 (-c T: plus load_calibration_images :33-38, applied to the
+    per-cell spectra by measure_ecoli): shift estimate on the per-laser projections, then the
+    registered, concatenated (H, W, C) stack -- one stream, no synchronisation."""
+    return K.register_assemble(lasers, estimate_shifts(lasers, reduce, clamp, device=True), apply_mask)
+
+
+# --------------------------------------------------------------------------------------------
+# Biofilm 3-D enhancement input (hiprfish_imaging_biofilm_analysis.py:808-817)
+# --------------------------------------------------------------------------------------------
+def enhance_volume(stack: torch.Tensor, v3: bool = False) -> torch.Tensor:
+    """biofilm :808-817 on the registered (X, Y, Z, C) volume: channel sum (numpy order),
+    / max, edge pad 5, line_profile_memory_efficient_v2 (v3 with `v3`) and the
+    average * (1 - quartile coefficient) post-chain -> image_final (X+10, Y+10, Z+10) f64"""
+    X, Y, Z, C = stack.shape
+    s = K.channel_sum(stack.reshape(X * Y, Z, C)).reshape(X, Y, Z)     # :808
+    s = K.div_scalar(s, K.max_f64(s))                                   # :809
+    pad = K.pad_edge_3d(s, 5)                                           # :810
+    return K.enhance_3d_v3(pad) if v3 else K.enhance_3d(pad)            # :811-817
 
 
 # --------------------------------------------------------------------------------------------

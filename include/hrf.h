@@ -97,6 +97,11 @@ HRF_API hrf_status hrf_enhance_3d_v3(const double *pad, int64_t xp, int64_t yp, 
 HRF_API hrf_status hrf_register_assemble(const float *const *src_host, const int32_t *channels_host,
                                          const int32_t *shifts_host, int32_t nlaser, int64_t H, int64_t W,
                                          int32_t apply_mask, float *dst, hrf_stream_t stream);
+/* the same with the shifts read from DEVICE memory (shifts_dev: nlaser (dr, dc) int32 pairs,
+ * e.g. written by hrf_register_translation_dev): no host round trip between estimate and apply */
+HRF_API hrf_status hrf_register_assemble_dev(const float *const *src_host, const int32_t *channels_host,
+                                             const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                             int32_t apply_mask, float *dst, hrf_stream_t stream);
 /* per-pixel sum over C in numpy pairwise order (== np.sum(stack, axis=2) in f64);
  * mode 0: sum, 1: log(sum + 1e-2) (ecoli :72), 2: log10(sum + 1) (biofilm :831);
  * mask (nullable) zeroes the sum; negate flips the sign (watershed input). */
@@ -126,6 +131,9 @@ HRF_API hrf_status hrf_div_scalar_f64(const double *a, int64_t n, const double *
 /* skimage.util.pad(img, width, mode='edge') (multispecies :109) */
 HRF_API hrf_status hrf_pad_edge_f64(const double *a, int64_t H, int64_t W, int32_t width, double *out,
                                     hrf_stream_t stream);
+/* skimage.util.pad(a, width, mode='edge') of an (X, Y, Z) volume (biofilm :810) */
+HRF_API hrf_status hrf_pad_edge3_f64(const double *a, int64_t X, int64_t Y, int64_t Z, int32_t width, double *out,
+                                     hrf_stream_t stream);
 HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out,
                                     hrf_stream_t stream);
 
@@ -137,6 +145,11 @@ HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_
 HRF_API int64_t hrf_register_workspace_bytes(int64_t H, int64_t W);
 HRF_API hrf_status hrf_register_translation(const double *src, const double *target, int64_t H, int64_t W,
                                             void *work, int32_t *shift_host, hrf_stream_t stream);
+/* the same, the (row, col) shift written to DEVICE memory (no synchronisation); clamp >= 0 zeroes
+ * a component whose magnitude exceeds it (ecoli :47-57), -1 keeps it.  src == NULL reuses the
+ * reference image's transform already in `work` from the previous call on that workspace. */
+HRF_API hrf_status hrf_register_translation_dev(const double *src, const double *target, int64_t H, int64_t W,
+                                                void *work, int32_t clamp, int32_t *shift_dev, hrf_stream_t stream);
 
 /* ==== a4: non-local means (nlmeans.hip) ==================================================
  * skimage.restoration.denoise_nl_means(img, patch_size, patch_distance, h, fast_mode=True,

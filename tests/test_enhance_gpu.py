@@ -116,3 +116,16 @@ def test_empty_and_too_small(K):
         K.enhance_2d(torch.zeros((9, 12), dtype=torch.float64, device="cuda"))
     with pytest.raises(ValueError):
         K.enhance_2d(torch.zeros((20, 20), dtype=torch.float32, device="cuda"))
+
+
+def test_enhance_volume_chain(K, orc):
+    """biofilm :808-817 from the (X, Y, Z, C) volume: channel sum / max / edge pad / fused
+    line-profile enhancement, against numpy's sum, max and pad plus the restated enhancement"""
+    from hiprfish_image_analysis_amd import pipeline as P
+    rng = np.random.default_rng(12)
+    vol = rng.random((14, 12, 9, 63)).astype(np.float32)
+    vol[:, :, :, :10] *= rng.random((14, 12, 9, 1)).astype(np.float32)
+    s = np.sum(vol.astype(np.float64), axis=3)       # the stack as f64 (bioformats hands over f64)
+    pad = np.pad(s / np.max(s), 5, mode="edge")
+    same(P.enhance_volume(dev(vol)).cpu().numpy(), orc.enhance_3d(pad))
+    same(P.enhance_volume(dev(vol), v3=True).cpu().numpy(), orc.enhance_3d_v3(pad))

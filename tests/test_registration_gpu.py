@@ -78,3 +78,39 @@ def test_estimate_shifts_pipeline(K, orc):
     # registered stack as the reference assembles it (no frame mask in multispecies :100-102)
     reg = K.register_assemble(dl, shifts, apply_mask=False).cpu().numpy()
     np.testing.assert_array_equal(reg, OP.register_stacks(lasers, shifts, False).astype(np.float32))
+
+
+def test_estimate_shifts_on_device_equals_host(K):
+    """estimate_shifts(device=True) + register_assemble on the device shifts (no host round
+    trip) == the host path: lasers cut from one smooth stack with known misregistrations"""
+    from hiprfish_image_analysis_amd import pipeline as P
+    rng = np.random.default_rng(9)
+    H, W = 160, 144
+    img = smooth_image(H, W, 40)                      # every channel a scaled copy: correlated projections
+    base = (img[:, :, None] * (0.5 + np.arange(20) / 40.0) + 0.01 * rng.random((H, W, 20))).astype(np.float32)
+    want_sh = [(0, 0), (3, -2), (0, 4), (-20, 1)]   # the last one beyond the clamp (15): -> (0, 1)
+    lasers = []
+    c0 = 0
+    for (dr, dc), cl in zip(want_sh, (6, 5, 5, 4)):
+        lasers.append(torch.from_numpy(np.ascontiguousarray(np.roll(base[:, :, c0:c0 + cl], (-dr, -dc), (0, 1)))).cuda())
+        c0 += cl
+    host = P.estimate_shifts(lasers)
+    dev = P.estimate_shifts(lasers, device=True)
+    assert dev.dtype == torch.int32 and dev.shape == (4, 2)
+    assert [tuple(r) for r in dev.cpu().tolist()] == host
+    assert host[1] == (3, -2) and host[2] == (0, 4) and host[3] == (0, 1)
+    for m in (True, False):
+        a = K.register_assemble(lasers, host, apply_mask=m)
+        b = K.register_assemble(lasers, dev, apply_mask=m)
+        assert torch.equal(a, b)
+    assert torch.equal(P.register_stack(lasers), K.register_assemble(lasers, host, apply_mask=True))
+    unclamped = P.estimate_shifts(lasers, clamp=None, device=True).cpu().tolist()
+    assert tuple(unclamped[3]) == (-20, 1) and [tuple(r) for r in unclamped] == P.estimate_shifts(lasers, clamp=None)
+
+
+def test_pad_edge_3d(K):
+    rng = np.random.default_rng(2)
+    a = rng.random((7, 5, 9))
+    for w in (0, 1, 5):
+        got = K.pad_edge_3d(torch.from_numpy(a).cuda(), w).cpu().numpy()
+        assert np.array_equal(got, np.pad(a, w, mode="edge"))
