@@ -1,18 +1,22 @@
 """bench.py -- HiPR-FISH segment+classify throughput on MI355X (BASELINE.json metric).
 
-A step = one pass of the hot path over one synthetic 2048x2048x95 tile per rank, inputs
-resident in HBM: E. coli measurement (log-sum -> KMeans -> morphology -> erosion seeds ->
-watershed -> cleanup -> shape filter -> per-cell mean spectra), per-cell segmented-cosine
-classification against the 1023-barcode library, per-pixel classification (split-fp16 MFMA
-GEMM + fused argmax), per-barcode counts and the identification map.  With N ranks every rank
-processes its own tiles (weak scaling) and the per-barcode counts are all-reduced over RCCL
-each step -- the path's only exchange (collect_measurement_results.py:92-98 across FOVs).
+A step = one pass of the hot path over one synthetic 2048x2048x95 E. coli tile per concurrent
+tile slot, inputs resident in HBM as the five per-laser acquisitions plus the flat-field image
+(the -c T configuration of ecoli measurement.py): registration (per-laser max projections,
+hipFFT cross-correlation, shifts applied on the device), E. coli measurement (log-sum -> KMeans
+-> morphology -> erosion seeds -> watershed -> cleanup -> shape filter -> flat-fielded per-cell
+mean spectra), per-cell segmented-cosine classification against the 1023-barcode library,
+per-pixel classification (split-fp16 MFMA GEMM + fused argmax), per-barcode counts and the
+identification map.  With N ranks every rank processes its own tiles (weak scaling); the
+per-barcode counts are summed on each rank and all-reduced over RCCL once, after the timed
+steps -- the path's only exchange (collect_measurement_results.py:92-98 across FOVs).
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-extras]
-At N=1 the line also carries "extras": the other GPU configurations of BASELINE.json measured
-the same way (cfg2: 2048x2048x63 synthetic-community tiles against the 127-barcode library;
-cfg4: the fused 3-D enhancement of a 1024x1024x64 volume).
-(for N > 1 launch with torch.distributed.run, one process per GPU)
+At N=1 the line also carries "extras": the other configurations of BASELINE.json measured the
+same way (cfg3 with the f32-MFMA classifier and without the per-pixel GEMM; cfg2 synthetic-
+community tiles against the 127-barcode library with the NL-means roofline; cfg4 the biofilm
+volume chain from a 1024x1024x64x63 stack with the enhance3d roofline; the streaming kernels
+against HBM).  (for N > 1 launch with torch.distributed.run, one process per GPU)
 """
 from __future__ import annotations
 
@@ -32,22 +36,70 @@ C = 95
 NBIT = 10
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (mode 0)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (modes 1, 2)
+F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
                2: "classify_pixels_lay_kernel<LayEcoli>"}
+# algorithmic work (DESIGN.md "Measurement"):
+NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixel, ~20 f64 ops each
+E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort
+
+
+def _cpu_info():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except AttributeError:
+        nproc = os.cpu_count()
+    return nproc, model
+
+
+def _cpu_worker(seed, hs, npx, barrier, q):
+    """one CPU process of the aggregate baseline: the oracle on its own hs x hs tile"""
+    os.environ["OMP_NUM_THREADS"] = "1"
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+    import pipeline as OP
+
+    from hiprfish_image_analysis_amd import synthetic as S
+    ref = S.reference_library(NBIT, S.ECOLI_BOUNDS)
+    lay = S.cell_layout(hs, hs, S.default_ncells(hs, hs), ref.shape[0], seed)
+    truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
+    st = S.render_stack(truth, lay, ref, seed=seed, device="cpu", profile=prof).numpy()
+    x = st.reshape(-1, C)[:npx].astype(np.float64)
+    barrier.wait()
+    t0 = time.perf_counter()
+    OP.process_tile(st, ref, S.ECOLI_BOUNDS)
+    t1 = time.perf_counter()
+    O.classify(x, ref.astype(np.float64), S.ECOLI_BOUNDS, 0)
+    t2 = time.perf_counter()
+    q.put(((t1 - t0) / (hs * hs), (t2 - t1) / npx))
 
 
 def _cpu_baseline(ref, bounds):
-    """Oracle restatement (oracle/pipeline.py, single-threaded C + numpy) on a bounded sample of
-    the same workload: segment+measure+per-cell classify of one whole 2048x2048x95 tile, and per-pixel
-    classification of 131072 of its pixels (~10 s of CPU); per-pixel costs summed into
-    Mpixel-spectra/s of the full step."""
+    """The oracle restatement (oracle/pipeline.py: C + numpy, OMP_NUM_THREADS=1 as the
+    Snakefiles run it) on the host cores, on bounded samples of the same workload:
+    (i) one process: segment + measure + per-cell classify of one whole 2048x2048x95 tile and
+    per-pixel classification of 131072 of its pixels (per-pixel costs summed into
+    Mpixel-spectra/s of the full step); (ii) one process per core (up to the box's 16-core
+    share), each on its own 1024x1024 tile plus 16384 per-pixel spectra, run together: the
+    aggregate throughput (snakemake -j $(nproc) style).  SURVEY.md §8(d)."""
+    import multiprocessing as mp
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     import pipeline as OP
 
     from hiprfish_image_analysis_amd import synthetic as S
     O.build()
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    nproc, model = _cpu_info()
     hs = 2048
     lay = S.cell_layout(hs, hs, S.default_ncells(hs, hs), ref.shape[0], seed=99)
     truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
@@ -60,10 +112,27 @@ def _cpu_baseline(ref, bounds):
     t0 = time.perf_counter()
     O.classify(x, ref.astype(np.float64), bounds, 0)
     t_pix = (time.perf_counter() - t0) / npx
-    return {"value": round(1e-6 / (t_seg + t_pix), 4), "unit": "Mpixel-spectra/s", "cores": 1, "kind": "port",
-            "sample": "oracle/pipeline.py process_tile on a 2048x2048x95 tile (%.1f s) + per-pixel classify of "
-                      "%d pixels vs 1023 refs (%.1f s), 1 thread; per-pixel costs summed" %
-                      (t_seg * hs * hs, npx, t_pix * npx)}
+    single = round(1e-6 / (t_seg + t_pix), 4)
+    del st, x
+    nw = max(1, min(nproc or 1, 16))
+    ctx = mp.get_context("spawn")          # fresh interpreters: no GPU state crosses
+    barrier, q = ctx.Barrier(nw), ctx.Queue()
+    procs = [ctx.Process(target=_cpu_worker, args=(1000 + i, 1024, 1 << 14, barrier, q)) for i in range(nw)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    agg = round(sum(1e-6 / (a + b) for a, b in res), 4)
+    return {"value": agg, "unit": "Mpixel-spectra/s", "cores": nw, "kind": "port",
+            "nproc": nproc, "cpu_model": model,
+            "single_process": {"value": single, "cores": 1,
+                               "sample": "oracle/pipeline.py process_tile on a 2048x2048x95 tile (%.1f s) + per-pixel "
+                                         "classify of %d pixels vs 1023 refs (%.1f s)" %
+                                         (t_seg * hs * hs, npx, t_pix * npx)},
+            "sample": "%d concurrent processes (OMP_NUM_THREADS=1), each oracle/pipeline.py process_tile on its own "
+                      "1024x1024x95 tile + per-pixel classify of 16384 pixels vs 1023 refs; aggregate = sum of the "
+                      "per-process rates (per-pixel costs summed into Mpixel-spectra/s of the full step)" % nw}
 
 
 def _timed_tiles(job, tiles, T, streams, pool, steps, warmup):
@@ -89,38 +158,35 @@ def _timed_tiles(job, tiles, T, streams, pool, steps, warmup):
     return time.perf_counter() - t0
 
 
+def _event_ms(fn, n=5):
+    """mean duration of fn() on the current stream (HIP events), after one untimed call"""
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n
+
+
 def _hbm_kernels(dev):
     """The streaming (HBM-bound) kernels of the path on one resident cfg3 tile, isolated:
     algorithmic bytes per launch / mean launch time (HIP events) against the 8 TB/s peak."""
-    import torch
-
     from hiprfish_image_analysis_amd import kernels as K
     from hiprfish_image_analysis_amd import pipeline as P
     from hiprfish_image_analysis_amd import synthetic as S
     stack, _, _, _ = S.tile(H, W, seed=20190301, device=dev)
     seg, maxlab = P.segment_ecoli(stack)
     fg = int(K.count_nonzero(seg))
-    lasers, c0 = [], 0
-    for c1 in S.ECOLI_BOUNDS[1:]:
-        lasers.append(stack[:, :, c0:c1].contiguous())
-        c0 = c1
-    shifts = [(0, 0), (2, -1), (0, 3), (-1, 0), (1, 1)]
-
-    def timed(fn, n=10):
-        fn()
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(n):
-            fn()
-        b.record()
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / n
+    lasers = S.laser_split(stack)
     rows = {
         # bytes: stack read + f64 image written
         "channel_sum": (lambda: K.channel_sum(stack, mode=1), H * W * (4 * C + 8)),
         # bytes: per-laser stacks read + assembled stack written
-        "register_assemble": (lambda: K.register_assemble(lasers, shifts, apply_mask=True), H * W * 8 * C),
+        "register_assemble": (lambda: K.register_assemble(lasers, S.LASER_SHIFTS, apply_mask=True), H * W * 8 * C),
         # bytes: label map read + the spectra of labelled pixels read (background is skipped)
         "label_sums": (lambda: K.label_sums(stack, seg, maxlab), H * W * 4 + fg * 4 * C),
     }
@@ -131,7 +197,7 @@ def _hbm_kernels(dev):
         pmc = {}
     out = {}
     for name, (fn, nbytes) in rows.items():
-        ms = timed(fn)
+        ms = _event_ms(fn, 10)
         gbs = nbytes / (ms * 1e-3) / 1e9
         out[name] = {"ms": round(ms, 4), "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
                      "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4),
@@ -139,61 +205,88 @@ def _hbm_kernels(dev):
     return out
 
 
-def _extras(dev, T, streams, pool):
-    """BASELINE.json configs 2 and 4 on this GPU (inputs resident, synthetic data)."""
+def _extras(dev, T, streams, pool, tiles, lib_main):
+    """BASELINE.json configs 3 (the other classifier settings), 2 and 4 on this GPU (inputs
+    resident, synthetic data)."""
     import torch
 
     from hiprfish_image_analysis_amd import kernels as K
     from hiprfish_image_analysis_amd import pipeline as P
     from hiprfish_image_analysis_amd import synthetic as S
     out = {}
+    steps = 20
+    # cfg3, MFMA distance-GEMM on (f32 MFMA, mode 0) and off (no per-pixel GEMM)
+    cfg3 = {}
+    for name, mode, pp in (("f32_mfma_mode0", 0, True), ("per_pixel_off", None, False)):
+        lib = lib_main
+        if mode is not None:
+            lib = P.Library(lib_main.spectra, lib_main.bounds, NBIT)
+            lib._refx = K.classify_prepare(lib.spectra.to(torch.float32), lib.bounds, mode=mode)
+        sec = _timed_tiles(lambda t, lib=lib, pp=pp: P.process_tile(P.register_stack(t[0]), lib, calibration=t[1],
+                                                                     per_pixel=pp),
+                           tiles, T, streams, pool, steps, 2)
+        cfg3[name] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
+                      "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
+                      "classifier_mode": mode if pp else None}
+    out["cfg3"] = cfg3
+    # cfg2: synthetic-community tiles
     b = S.MULTI_BOUNDS
     ref = S.reference_library(7, b)
     lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), b, 7)
     lib.refx()
-    tiles = [S.tile(H, W, nbit=7, bounds=b, seed=20190201 + t, device=dev)[0] for t in range(2 * T)]
-    steps = 10
-    sec = _timed_tiles(lambda st: P.process_tile(st, lib, measure=P.measure_multispecies, variant=2), tiles, T,
+    ctiles = [S.tile(H, W, nbit=7, bounds=b, seed=20190201 + t, device=dev)[0] for t in range(2 * T)]
+    sec = _timed_tiles(lambda st: P.process_tile(st, lib, measure=P.measure_multispecies, variant=2), ctiles, T,
                        streams, pool, steps, 2)
+    s = K.channel_sum(ctiles[0])
+    norm = K.div_scalar(s, K.max_f64(s))
+    ms_nl = _event_ms(lambda: K.nl_means_2d(norm, 7, 11, 0.02, 0.0), 5)
+    ach = NL_OPS_PER_PIXEL * H * W / (ms_nl * 1e-3) / 1e12
     out["cfg2"] = {"workload": "2048x2048x63 synthetic-community tiles, 127-barcode (7-bit) library: calibrated "
                                "sum, NL-means, 2-D enhancement, segmentation, per-cell means, per-cell (_7b_v2) "
-                               "and per-pixel classification, counts", "concurrent": T,
+                               "and per-pixel classification, counts", "concurrent": T, "steps": steps,
                    "value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
-                   "ms_per_tile": round(sec / (steps * T) * 1e3, 3)}
-    del tiles
-    X, Y, Z = 1024, 1024, 64
+                   "ms_per_tile": round(sec / (steps * T) * 1e3, 3),
+                   "roofline": {"kernel": "nl_means_kernel<false>", "bound": "valu-f64", "kernel_ms": round(ms_nl, 4),
+                                "algorithmic_ops_per_pixel": NL_OPS_PER_PIXEL, "achieved": round(ach, 3),
+                                "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s", "frac": round(ach / F64_VALU_PEAK_TOPS, 4)}}
+    del ctiles, s, norm
+    # cfg4: the biofilm volume chain from a 1024x1024x64x63 stack
+    X, Y, Z, CV = 1024, 1024, 64, 63
     g = torch.Generator(device=dev)
     g.manual_seed(4)
-    pad = torch.rand((X + 10, Y + 10, Z + 10), dtype=torch.float64, device=dev, generator=g)
-    K.enhance_3d(pad)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(3):
-        K.enhance_3d(pad)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / 3
+    vol = torch.rand((X, Y, Z, CV), dtype=torch.float32, device=dev, generator=g)
+    ms_chain = _event_ms(lambda: P.enhance_volume(vol), 3)
+    ssum = K.channel_sum(vol.reshape(X * Y, Z, CV)).reshape(X, Y, Z)
+    pad = K.pad_edge_3d(K.div_scalar(ssum, K.max_f64(ssum)), 5)
+    del vol, ssum
+    ms_e3 = _event_ms(lambda: K.enhance_3d(pad), 3)
     del pad
+    ach3 = E3_OPS_PER_VOXEL * X * Y * Z / (ms_e3 * 1e-3) / 1e12
+    out["cfg4"] = {"workload": "1024x1024x64x63 volume: channel sum, / max, edge pad 5, fused "
+                               "line_profile_memory_efficient_v2 + biofilm :812-817 post-chain (72 directions x 11 "
+                               "taps per voxel)", "value": round(X * Y * Z / ms_chain / 1e3, 3), "unit": "Mvoxel/s",
+                   "ms": round(ms_chain, 3),
+                   "roofline": {"kernel": "enhance3d_kernel<0>", "bound": "valu-f64", "kernel_ms": round(ms_e3, 3),
+                                "algorithmic_ops_per_voxel": E3_OPS_PER_VOXEL, "achieved": round(ach3, 3),
+                                "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s",
+                                "frac": round(ach3 / F64_VALU_PEAK_TOPS, 4)}}
     out["hbm_kernels"] = _hbm_kernels(dev)
-    out["cfg4"] = {"workload": "1024x1024x64 volume (edge-padded), fused line_profile_memory_efficient_v2 + "
-                               "biofilm :812-817 post-chain (72 directions x 11 taps per voxel)",
-                   "value": round(X * Y * Z / ms / 1e3, 3), "unit": "Mvoxel/s", "ms": round(ms, 3)}
     return out
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tiles", type=int, default=0, help="distinct resident tiles per rank (default 2*concurrent)")
     ap.add_argument("--concurrent", type=int, default=2, help="tiles processed concurrently per step per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-pixel", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the cfg2 / cfg4 measurements (N=1 only)")
+    ap.add_argument("--no-extras", action="store_true", help="skip the cfg2 / cfg3-variant / cfg4 measurements")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the per-pixel classification after the segmentation on one stream")
+    ap.add_argument("--dump-counts", default=None, help="rank 0 writes the all-reduced barcode counts (.npy)")
     args = ap.parse_args()
 
     import torch
@@ -205,10 +298,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("HRF_DIST_BACKEND", "nccl")     # gloo: the multi-rank test on one GPU
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local if (world > 1 and backend == "nccl") else 0)
     torch.cuda.set_device(dev)
 
     bounds = S.ECOLI_BOUNDS
@@ -218,11 +315,14 @@ def main():
     tiles = []
     if args.tiles <= 0:
         args.tiles = 2 * max(1, args.concurrent)
+    cal = S.flat_field(H, W, device=dev)
     for t in range(args.tiles):
         seed = 20190101 + rank * 1000 + t
         lay = S.cell_layout(H, W, S.default_ncells(H, W), lib.R, seed)
         truth, prof = S.render_truth(H, W, lay, with_profile=True)
-        tiles.append(S.render_stack(truth, lay, ref, seed=seed, device=dev, profile=prof))
+        stack = S.render_stack(truth, lay, ref, seed=seed, device=dev, profile=prof)
+        tiles.append((S.laser_split(stack), cal))          # the per-laser acquisitions + flat field
+        del stack
     torch.cuda.synchronize()
 
     per_pixel = not args.no_per_pixel
@@ -231,8 +331,7 @@ def main():
     T = max(1, args.concurrent)
     # HRF_PRIORITY=1 puts the segmentation chains on high-priority streams (their workgroups
     # dispatched ahead of the pending ones of the long classifier grid on its default-priority
-    # side stream): measured neutral on throughput (915.6 vs 912.9 Mpix/s, 5 interleaved runs
-    # each), so off by default -- it stretches the classifier's in-bench launch duration
+    # side stream): measured neutral on throughput, so off by default
     prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("HRF_PRIORITY", "0") == "1" else 0
     streams = [torch.cuda.Stream(device=dev, priority=prio) for _ in range(T)]
     pool = None
@@ -240,9 +339,10 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(T)
 
-    def tile_job(j, stack, timed):
+    def tile_job(j, tile, timed):
         with torch.cuda.stream(streams[j]):
-            return P.process_tile(stack, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
+            stack = P.register_stack(tile[0])                   # ecoli :45-70 (shifts stay on the device)
+            return P.process_tile(stack, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
                                   pixel_events=ev if timed else None)
 
     def worker(j, first, nsteps, timed):
@@ -268,8 +368,6 @@ def main():
         counts = outs[0][1]
         for _, a in outs[1:]:
             counts = counts + a
-        if world > 1:
-            P.allreduce_counts(counts)          # global per-barcode counts of the whole batch
         return outs[-1][0], counts
 
     run(0, args.warmup, False)
@@ -278,14 +376,23 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     res, counts = run(args.warmup, args.steps, True)
+    if world > 1:
+        if backend == "nccl":
+            P.allreduce_counts(counts)      # global per-barcode counts of the whole batch
+        else:
+            c = counts.cpu()
+            P.allreduce_counts(c)
+            counts = c.to(dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ncells = int(res.cell_idx.numel())
     total_cells = int(counts.sum().item())
+    if args.dump_counts and rank == 0:
+        np.save(args.dump_counts, counts.cpu().numpy())
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -296,29 +403,27 @@ def main():
         "value": round(value, 3), "unit": "Mpixel-spectra/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": "cfg3: 2048x2048x95 synthetic stack per rank per step, 1023-barcode library; "
-                               "E. coli segmentation + per-cell spectra + per-cell and per-pixel segmented-cosine "
-                               "classification + barcode counts" + (" (RCCL all-reduce of counts)" if world > 1 else ""),
+        "config": {"workload": "cfg3: 2048x2048x95 synthetic E. coli tiles (five per-laser acquisitions, "
+                               "misregistered, + flat field: the -c T configuration), 1023-barcode library; "
+                               "registration + segmentation + flat-fielded per-cell spectra + per-cell and per-pixel "
+                               "segmented-cosine classification + barcode counts" +
+                               (" (all-reduce of counts)" if world > 1 else ""),
                    "H": H, "W": W, "C": C, "R": lib.R, "per_pixel": per_pixel, "cells_last_tile": ncells,
-                   "cells_counted": total_cells,
+                   "cells_counted": total_cells, "registration": True, "calibration": True,
                    "parallelism": "tile-sharded x%d" % world, "tiles_per_step_per_gpu": T,
                    "global_batch": T * world,
                    "per_pixel_overlap": per_pixel and not args.no_overlap},
     }
+    if world > 1 and backend != "nccl":
+        out["config"]["dist_backend"] = backend
     if per_pixel and ev:
         from hiprfish_image_analysis_amd import kernels as K
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         # the same kernel alone on the GPU (after the timed region): with the overlap the
         # timed-region duration includes the compute units it shares with the segmentation
-        iso = []
-        for i in range(3):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            P.classify_pixels(tiles[i % len(tiles)], lib)
-            b.record()
-            iso.append((a, b))
-        torch.cuda.synchronize()
-        ms_iso = float(np.mean([a.elapsed_time(b) for a, b in iso]))
+        stack0 = P.register_stack(tiles[0][0])
+        ms_iso = _event_ms(lambda: P.classify_pixels(stack0, lib), 3)
+        del stack0
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
         ach = flops / (ms * 1e-3) / 1e12
         mode = K.refx_mode(lib.refx(), C, bounds)
@@ -347,7 +452,7 @@ def main():
                            "isolated_achieved": round(flops / (ms_iso * 1e-3) / 1e12, 2),
                            "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4)}
     if world == 1 and not args.no_extras:
-        out["extras"] = _extras(dev, T, streams, pool)
+        out["extras"] = _extras(dev, T, streams, pool, tiles, lib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_baseline(ref, bounds)
     if rank == 0:

@@ -127,3 +127,29 @@ def tile(H: int = 2048, W: int = 2048, nbit: int = 10, bounds=ECOLI_BOUNDS, seed
     truth, prof = render_truth(H, W, lay, with_profile=True)
     stack = render_stack(truth, lay, ref, seed=seed, device=device, profile=prof)
     return stack, truth, lay, ref
+
+
+# the misregistration applied to each laser's channels by laser_split (E. coli lasers
+# 405/488/514/561/633, ecoli measurement.py:45-70 estimates and undoes it)
+LASER_SHIFTS = ((0, 0), (2, -1), (0, 3), (-1, 0), (1, 1))
+
+
+def laser_split(stack, bounds=ECOLI_BOUNDS, shifts=LASER_SHIFTS):
+    """The per-laser (H, W, C_l) acquisitions of a registered stack, laser l displaced by
+    -shifts[l] (so registration recovers shifts[l]; the wrapped rows/columns fall outside the
+    coverage mask)."""
+    import torch
+    out = []
+    for k in range(len(bounds) - 1):
+        dr, dc = shifts[k]
+        out.append(torch.roll(stack[:, :, bounds[k]:bounds[k + 1]], shifts=(-dr, -dc), dims=(0, 1)).contiguous())
+    return out
+
+
+def flat_field(H: int, W: int, device="cuda"):
+    """A smooth flat-field calibration image (H, W) f32 in [0.7, 1.0] (the reference divides
+    channels 0..31 by its calibration image, ecoli measurement.py:33-38, :147-150)."""
+    import torch
+    y = torch.linspace(-1.0, 1.0, H, device=device)[:, None]
+    x = torch.linspace(-1.0, 1.0, W, device=device)[None, :]
+    return (1.0 - 0.3 * (0.6 * y * y + 0.4 * x * x)).to(torch.float32).contiguous()
