@@ -631,7 +631,9 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) pv0[reg] = pv1[reg] = -__builtin_inff();
   int pr = 0;  // first row of the pending block
-  const unsigned char *zrow = reinterpret_cast<const unsigned char *>(gref) + 4 * KP + (int64_t)(4 * h) * ROWB;
+  // ZS: the pending block's 16 row zero-segment masks (this lane's rows), packed 4 per word; read
+  // from the LDS chunk when the block's MFMAs are issued (the chunk may be gone by its epilogue)
+  uint32_t pz[4] = {0u, 0u, 0u, 0u};
   int bk0 = INT32_MIN, bk1 = INT32_MIN;        // KEYED: the pending block's keys
   int key0 = INT32_MIN, key1 = INT32_MIN;      // KEYED: best keys so far
   auto epi = [&](int lo, int hi) {
@@ -640,7 +642,7 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
       const int r = pr + (reg & 3) + 8 * (reg >> 2);
       float s0 = pv0[reg], s1 = pv1[reg];
       if (ZS) {
-        const uint32_t zr = zrow[(int64_t)r * ROWB];
+        const uint32_t zr = (pz[reg >> 2] >> (8 * (reg & 3))) & 0xffu;
         s0 += (float)__popc(zx0 & zr);
         s1 += (float)__popc(zx1 & zr);
       }
@@ -681,6 +683,13 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
 #pragma unroll
     for (int rb = 0; rb < RCH; rb += 32) {
       f32x16 acc0 = {0}, acc1 = {0};
+      uint32_t cz[4] = {0u, 0u, 0u, 0u};
+      if (ZS) {
+        const unsigned char *zl = reinterpret_cast<const unsigned char *>(buf) + (rb + 4 * h) * ROWB + 4 * KP;
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          cz[reg >> 2] |= (uint32_t)zl[((reg & 3) + 8 * (reg >> 2)) * ROWB] << (8 * (reg & 3));
+      }
       const char *row = buf + (rb + j) * ROWB + 16 * h;
 #pragma unroll
       for (int s = 0; s < KS16; ++s) {
@@ -696,6 +705,10 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
       }
       pv0 = acc0;
       pv1 = acc1;
+      if (ZS) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pz[q] = cz[q];
+      }
       pr = c * RCH + rb;
     }
   }

@@ -365,6 +365,50 @@ __global__ void channel_max_kernel(const float *__restrict__ stack, int64_t npix
   }
 }
 
+// 64-pixel chunks staged in LDS with 16-byte loads (a chunk is one contiguous 64 x C run), then
+// four lanes per pixel reduce a quarter of its channels each: coalesced, unlike a thread per
+// pixel walking its own channels.  Same NaN-propagating max.
+constexpr int CM_P = 64;
+__global__ __launch_bounds__(256) void channel_max_lds_kernel(const float *__restrict__ stack, int64_t npix, int C,
+                                                              double *__restrict__ out, int vec_ok) {
+  extern __shared__ __attribute__((aligned(16))) float sb[];
+  const int tid = threadIdx.x, pi = tid >> 2, q = tid & 3;
+  for (int64_t ch = blockIdx.x; ch * CM_P < npix; ch += gridDim.x) {
+    const int64_t p0 = ch * CM_P;
+    const int np = (int)min((int64_t)CM_P, npix - p0);
+    const int nel = np * C;
+    const float *src = stack + p0 * C;
+    int e0 = 0;
+    if (vec_ok) {
+      for (int v = tid; v < (nel >> 2); v += 256) reinterpret_cast<float4 *>(sb)[v] = reinterpret_cast<const float4 *>(src)[v];
+      e0 = (nel >> 2) << 2;
+    }
+    for (int e = e0 + tid; e < nel; e += 256) sb[e] = src[e];
+    __syncthreads();
+    float m = -__builtin_inff();
+    bool any = false;
+    if (pi < np) {
+      const float *a = sb + pi * C;
+      for (int c = q; c < C; c += 4) {
+        const float v = a[c];
+        m = (!any || v > m || v != v) ? v : m;
+        any = true;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o <= 2; o <<= 1) {
+      const float v = __shfl_xor(m, o, 64);
+      const bool va = __shfl_xor((int)any, o, 64) != 0;
+      if (va) {
+        m = (!any || v > m || v != v || m != m) ? (m != m ? m : v) : m;
+        any = true;
+      }
+    }
+    if (q == 0 && pi < np) out[p0 + pi] = (double)m;
+    __syncthreads();
+  }
+}
+
 __global__ void and_u8_kernel(const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, int64_t n,
                               uint8_t *__restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -479,7 +523,13 @@ hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *
   HRF_REQUIRE(C >= 1, "channel_max: C must be >= 1");
   if (npix == 0) return HRF_OK;
   HRF_REQUIRE(stack && out, "channel_max: null buffer");
-  channel_max_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, out);
+  if (C <= 256) {
+    const int vec_ok = ((uintptr_t)stack & 15) == 0 && (CM_P * C) % 4 == 0;
+    const unsigned g = (unsigned)std::min<int64_t>(hrf::cdiv(npix, CM_P), 4096);
+    channel_max_lds_kernel<<<g, 256, sizeof(float) * CM_P * C, (hipStream_t)stream>>>(stack, npix, C, out, vec_ok);
+  } else {
+    channel_max_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, out);
+  }
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -10,6 +10,9 @@ from hiprfish_image_analysis_amd import kernels as K, synthetic as S  # noqa: E4
 
 H = W = int(os.environ.get("HRF_PROF_HW", "2048"))
 st, truth, lay, ref = S.tile(H, W, seed=20190101)
+if os.environ.get("HRF_PROF_REG", "0") == "1":   # the registered stack (zero borders: all-zero pixels)
+    from hiprfish_image_analysis_amd import pipeline as P
+    st = P.register_stack(S.laser_split(st))
 b = S.ECOLI_BOUNDS
 R, C = ref.shape
 first = None
