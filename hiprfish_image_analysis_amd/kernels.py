@@ -761,3 +761,90 @@ def segment_multispecies_native(stack, cal=None):
     _lib.call("hrf_segment_multispecies", _seg_ctx(stack.device, H, W), _ptr(stack), C, calp, sp, sc, c0, c1,
               _ptr(seg), ctypes.addressof(n), _ptr(s), _ptr(fb), _stream())
     return seg, n.value, s, fb
+
+
+# ---- a17, a18, f2: classifier back-end ----------------------------------------------------
+def features_ecoli(avgint_norm):
+    """(n, 95) -> (n, 132): avgint_norm | np.diff(avgint_norm[:, 0:32]) | 6 zero flag columns
+    (ecoli image_classification.py:47-48)"""
+    x = _dev(avgint_norm, torch.float64, "avgint_norm")
+    out = torch.empty((x.shape[0], 132), dtype=torch.float64, device=x.device)
+    _lib.call("hrf_features_ecoli", _ptr(x), x.shape[0], _ptr(out), _stream())
+    return out
+
+
+def features_multi(avgint_norm):
+    """(n, 63) -> (n, 67): avgint_norm | 4 zero flag columns (classify_spectra.py:27-28)"""
+    x = _dev(avgint_norm, torch.float64, "avgint_norm")
+    out = torch.empty((x.shape[0], 67), dtype=torch.float64, device=x.device)
+    _lib.call("hrf_features_multi", _ptr(x), x.shape[0], _ptr(out), _stream())
+    return out
+
+
+def standard_scale(x, mean, scale):
+    """sklearn StandardScaler.transform on the columns of x (a column slice of a wider table
+    is read in place)"""
+    if x.stride(1) != 1:
+        raise ValueError("standard_scale: rows must be contiguous")
+    n, f = x.shape
+    out = torch.empty((n, f), dtype=torch.float64, device=x.device)
+    m = None if mean is None else _dev(mean, torch.float64, "mean")
+    s = None if scale is None else _dev(scale, torch.float64, "scale")
+    _lib.call("hrf_standard_scale", _ptr(x), n, f, x.stride(0), _ptr(m) if m is not None else None,
+              _ptr(s) if s is not None else None, _ptr(out), _stream())
+    return out
+
+
+def svc_predict(x, model, out_column=None, want_dec=False):
+    """sklearn SVC.predict with the arrays of `model` (backend.SvcModel).  x may be a column
+    slice of a wider f64 table (rows contiguous).  -> class index (int32, n); with out_column
+    (a column view of an f64 table) the class values are also written there; with want_dec the
+    one-vs-one decision values (n, pairs) too."""
+    if x.dtype != torch.float64 or not x.is_cuda or x.stride(1) != 1:
+        raise ValueError("svc_predict: an f64 device table with contiguous rows expected")
+    n, f = x.shape
+    if f != model.sv.shape[1]:
+        raise ValueError("svc_predict: %d features, the model has %d" % (f, model.sv.shape[1]))
+    pred = torch.empty(n, dtype=torch.int32, device=x.device)
+    nc = model.n_class
+    dec = torch.empty((n, nc * (nc - 1) // 2), dtype=torch.float64, device=x.device) if want_dec else None
+    vo, vs = (None, 0) if out_column is None else (out_column, out_column.stride(0))
+    _lib.call("hrf_svc_predict", _ptr(x), n, x.stride(0), f, _ptr(model.sv), model.sv.shape[0], _ptr(model.coef),
+              _ptr(model.intercept), _ptr(model.start), nc, model.kernel, float(model.gamma), float(model.coef0),
+              int(model.degree), _ptr(pred), _ptr(dec) if dec is not None else None,
+              _ptr(vo) if vo is not None else None, vs, _ptr(model.class_values), _stream())
+    return (pred, dec) if want_dec else pred
+
+
+KNN_METRICS = {"euclidean": 0, "channel_cosine_intensity_7b_v2": 1, "channel_cosine_intensity_violet_derivative_v2": 2}
+
+
+def knn(q, trainT, metric, k):
+    """exact k nearest training rows; trainT = the training table transposed (f, nt),
+    contiguous.  -> (idx int32 (nq, k), dist f64 (nq, k))"""
+    if q.dtype != torch.float64 or q.stride(1) != 1:
+        raise ValueError("knn: f64 queries with contiguous rows expected")
+    trainT = _dev(trainT, torch.float64, "trainT")
+    nq, f = q.shape
+    if trainT.shape[0] != f:
+        raise ValueError("knn: the training table has %d features, the queries %d" % (trainT.shape[0], f))
+    m = KNN_METRICS[metric] if isinstance(metric, str) else int(metric)
+    idx = torch.empty((nq, k), dtype=torch.int32, device=q.device)
+    dist = torch.empty((nq, k), dtype=torch.float64, device=q.device)
+    _lib.call("hrf_knn", _ptr(q), nq, q.stride(0), _ptr(trainT), trainT.shape[1], f, m, int(k), _ptr(idx), _ptr(dist),
+              _stream())
+    return idx, dist
+
+
+def umap_init_transform(idx, dist, embedding, n_neighbors, local_connectivity=0.0):
+    """umap-learn transform's initial embedding of the queries from their kNN (the mean knn
+    distance stays on the device)"""
+    idx = _i32(idx, "idx")
+    dist = _dev(dist, torch.float64, "dist")
+    emb = _dev(embedding, torch.float64, "embedding")
+    nq, k = idx.shape
+    mean = dist.mean().reshape(1) if dist.numel() else torch.zeros(1, dtype=torch.float64, device=dist.device)
+    out = torch.empty((nq, emb.shape[1]), dtype=torch.float64, device=dist.device)
+    _lib.call("hrf_umap_init_transform", _ptr(idx), _ptr(dist), nq, k, float(n_neighbors), float(local_connectivity),
+              _ptr(mean), _ptr(emb), emb.shape[1], _ptr(out), _stream())
+    return out

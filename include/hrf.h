@@ -335,6 +335,41 @@ HRF_API hrf_status hrf_classify_cells(const double *x, int64_t N, const double *
                                       const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
                                       const double *fr, int32_t *arg, double *dmin, hrf_stream_t stream);
 
+/* ==== a17, a18, f2: classifier back-end (backend.hip) ======================================
+ * ecoli image_classification.py:43-56, synthetic-community classify_spectra.py:27-35.  Models
+ * arrive as arrays (never pickles).  All f64. */
+/* E. coli features out (n x 132) = avgint_norm (n x 95) | np.diff(avgint_norm[:, 0:32]) | 0 x 6
+ * (the six check-SVC flag columns, filled by hrf_svc_predict) (:47-48) */
+HRF_API hrf_status hrf_features_ecoli(const double *avgint_norm, int64_t n, double *out, hrf_stream_t stream);
+/* community features out (n x 67) = avgint_norm (n x 63) | 0 x 4 (classify_spectra.py:27-28) */
+HRF_API hrf_status hrf_features_multi(const double *avgint_norm, int64_t n, double *out, hrf_stream_t stream);
+/* sklearn StandardScaler.transform: out (n x f) = (x - mean) / scale (either may be NULL) */
+HRF_API hrf_status hrf_standard_scale(const double *x, int64_t n, int32_t f, int64_t ldx, const double *mean,
+                                      const double *scale, double *out, hrf_stream_t stream);
+/* sklearn SVC.predict (libsvm one-vs-one voting; kernel 0 linear, 1 poly, 2 rbf, 3 sigmoid).
+ * sv (nsv x f); coef (n_class-1 x nsv) and intercept (n_class(n_class-1)/2) in libsvm's sign
+ * convention (pair (a, b) votes a when its sum > 0: sklearn's dual_coef_ / intercept_ for
+ * multi-class, both negated for two classes); start (n_class+1) first support vector per class.
+ * pred[i] = class index; dec (n x pairs) optional; val_out[i*val_stride] = class_values[pred]
+ * (or the index) when val_out is given -- e.g. a flag column of the feature table. */
+HRF_API hrf_status hrf_svc_predict(const double *x, int64_t n, int64_t ldx, int32_t f, const double *sv, int32_t nsv,
+                                   const double *coef, const double *intercept, const int32_t *start,
+                                   int32_t n_class, int32_t kernel, double gamma, double coef0, int32_t degree,
+                                   int32_t *pred, double *dec, double *val_out, int64_t val_stride,
+                                   const double *class_values, hrf_stream_t stream);
+/* exact k nearest training rows (trainT: f x nt, feature-major) under metric 0 euclidean, 1
+ * channel_cosine_intensity_7b_v2 (train_reference.py:993-1072), 2 the scalar of
+ * channel_cosine_intensity_violet_derivative_v2 (:569-731); ascending distance, ties to the
+ * lower row.  idx/dist (nq x k) */
+HRF_API hrf_status hrf_knn(const double *q, int64_t nq, int64_t ldq, const double *trainT, int64_t nt, int32_t f,
+                           int32_t metric, int32_t k, int32_t *idx_out, double *dist_out, hrf_stream_t stream);
+/* umap-learn transform's initial embedding from the kNN: smooth_knn_dist, membership strengths,
+ * l1 rows, init_transform.  mean_dist_dev: the mean of all knn distances (device scalar) */
+HRF_API hrf_status hrf_umap_init_transform(const int32_t *knn_idx, const double *knn_dist, int64_t nq, int32_t k,
+                                           double n_neighbors, double local_connectivity,
+                                           const double *mean_dist_dev, const double *embedding, int32_t d,
+                                           double *out, hrf_stream_t stream);
+
 /* ==== a22: label adjacency (rag.hip) ====================================================
  * skimage.future.graph.rag_boundary edge set (biofilm :1277-1278): edge[(maxlab+1)^2] u8,
  * edge[a*(maxlab+1)+b] = 1 for a < b. */

@@ -1,0 +1,234 @@
+/* oracle/backend.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product path): CPU
+ * restatement of the per-cell classifier back-end (a17, a18, f2), in the reference's operation
+ * order, f64.
+ *
+ *  oracle_svc_predict  sklearn SVC.predict / decision_function (ovo): libsvm svm_predict_values
+ *                      on dense vectors (sklearn's svm.cpp, _DENSE_REP): kernel values in
+ *                      feature order, per pair (a, b) the class-a support vectors with
+ *                      coef[b-1] then the class-b ones with coef[a], minus rho; vote a when > 0;
+ *                      first maximum.  Pinned to sklearn itself (tests/golden/backend.npz).
+ *  oracle_knn          brute-force k nearest rows under channel_cosine_intensity_7b_v2
+ *                      (train_reference.py:993-1072) / _violet_derivative_v2 (:569-731, the
+ *                      scalar (d + c1..c5)/6 it computes) / euclidean; ties to the lower row.
+ *                      The search pinned to sklearn NearestNeighbors(algorithm='brute').
+ *  oracle_umap_init    umap-learn (0.5) transform's initial embedding: smooth_knn_dist,
+ *                      compute_membership_strengths (bipartite), CSR l1 normalisation,
+ *                      init_transform.  umap-learn is absent here: parity unpinned.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static double svc_k(const double *x, const double *y, int f, int kernel, double gamma, double coef0, int degree) {
+  double s = 0.0;
+  if (kernel == 2) {
+    for (int i = 0; i < f; ++i) {
+      const double d = x[i] - y[i];
+      s += d * d;
+    }
+    return exp(-gamma * s);
+  }
+  for (int i = 0; i < f; ++i) s += x[i] * y[i];
+  if (kernel == 0) return s;
+  if (kernel == 1) {
+    double r = 1.0, t = gamma * s + coef0;
+    for (int d = degree; d > 0; d /= 2) {
+      if (d % 2 == 1) r *= t;
+      t = t * t;
+    }
+    return r;
+  }
+  return tanh(gamma * s + coef0);
+}
+
+void oracle_svc_predict(const double *x, int64_t n, int64_t ldx, int f, const double *sv, int nsv, const double *coef,
+                        const double *intercept, const int32_t *start, int n_class, int kernel, double gamma,
+                        double coef0, int degree, int32_t *pred, double *dec) {
+  double *kv = (double *)malloc(sizeof(double) * (size_t)nsv);
+  int *vote = (int *)malloc(sizeof(int) * (size_t)n_class);
+  const int npair = n_class * (n_class - 1) / 2;
+  for (int64_t i = 0; i < n; ++i) {
+    const double *xi = x + i * ldx;
+    for (int s = 0; s < nsv; ++s) kv[s] = svc_k(xi, sv + (int64_t)s * f, f, kernel, gamma, coef0, degree);
+    memset(vote, 0, sizeof(int) * (size_t)n_class);
+    int p = 0;
+    for (int a = 0; a < n_class; ++a)
+      for (int b = a + 1; b < n_class; ++b, ++p) {
+        const double *c1 = coef + (int64_t)(b - 1) * nsv, *c2 = coef + (int64_t)a * nsv;
+        double sum = 0.0;
+        for (int k = start[a]; k < start[a + 1]; ++k) sum += c1[k] * kv[k];
+        for (int k = start[b]; k < start[b + 1]; ++k) sum += c2[k] * kv[k];
+        sum += intercept[p];
+        if (dec) dec[i * npair + p] = sum;
+        ++vote[sum > 0 ? a : b];
+      }
+    int best = 0;
+    for (int c = 1; c < n_class; ++c)
+      if (vote[c] > vote[best]) best = c;
+    pred[i] = best;
+  }
+  free(kv);
+  free(vote);
+}
+
+static double seg_cos(const double *x, const double *y, int lo, int hi) {
+  double result = 0.0, nx = 0.0, ny = 0.0;
+  for (int i = lo; i < hi; ++i) {
+    result += x[i] * y[i];
+    nx += x[i] * x[i];
+    ny += y[i] * y[i];
+  }
+  if (nx == 0.0 && ny == 0.0) return 0.0;
+  if (nx == 0.0 || ny == 0.0) return 1.0;
+  return 1.0 - (result / sqrt(nx * ny));
+}
+
+double oracle_knn_metric(int metric, const double *x, const double *y, int f) {
+  if (metric == 0) {
+    double s = 0.0;
+    for (int i = 0; i < f; ++i) s += (x[i] - y[i]) * (x[i] - y[i]);
+    return sqrt(s);
+  }
+  if (metric == 1) {
+    double check = 0.0;
+    for (int i = 63; i < 67; ++i) check += fabs(x[i] - y[i]);
+    if (!(check < 0.01)) return 1.0;
+    static const int b[5] = {0, 23, 43, 57, 63};
+    double c[4];
+    for (int s = 0; s < 4; ++s) c[s] = x[63 + s] == 0 ? 0.0 : seg_cos(x, y, b[s], b[s + 1]);
+    return 0.5 * (c[0] + c[1] + c[2] + c[3]) / 4;
+  }
+  double check = 0.0;
+  for (int i = 126; i < 132; ++i) check += fabs(x[i] - y[i]);
+  static const int b[6] = {0, 32, 55, 75, 89, 95};
+  double c[5], d;
+  if (check < 0.01) {
+    d = 0.0;
+    for (int s = 0; s < 5; ++s) c[s] = x[126 + s] == 0 ? 0.0 : seg_cos(x, y, b[s], b[s + 1]);
+  } else {
+    d = 1.0;
+    for (int s = 0; s < 5; ++s) c[s] = seg_cos(x, y, b[s], b[s + 1]);
+  }
+  return (d + c[0] + c[1] + c[2] + c[3] + c[4]) / 6;
+}
+
+void oracle_knn(const double *q, int64_t nq, int64_t ldq, const double *train, int64_t nt, int f, int metric, int k,
+                int32_t *idx, double *dist) {
+  for (int64_t i = 0; i < nq; ++i) {
+    int n = 0;
+    double *bd = dist + i * k;
+    int32_t *bi = idx + i * k;
+    for (int64_t r = 0; r < nt; ++r) {
+      const double d = oracle_knn_metric(metric, q + i * ldq, train + r * f, f);
+      if (n == k && !(d < bd[k - 1])) continue;
+      int pos = n < k ? n : k - 1;
+      while (pos > 0 && d < bd[pos - 1]) {
+        bd[pos] = bd[pos - 1];
+        bi[pos] = bi[pos - 1];
+        --pos;
+      }
+      bd[pos] = d;
+      bi[pos] = (int32_t)r;
+      if (n < k) ++n;
+    }
+    for (int j = n; j < k; ++j) {
+      bi[j] = -1;
+      bd[j] = INFINITY;
+    }
+  }
+}
+
+void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k, double n_neighbors,
+                      double local_connectivity, const double *emb, int d, double *out) {
+  double mean_all = 0.0;
+  for (int64_t e = 0; e < nq * k; ++e) mean_all += dist[e];
+  mean_all /= (double)(nq * k);
+  const double target = log2(n_neighbors);
+  double *w = (double *)malloc(sizeof(double) * (size_t)k);
+  int *ord = (int *)malloc(sizeof(int) * (size_t)k);
+  for (int64_t i = 0; i < nq; ++i) {
+    const double *di = dist + i * k;
+    const int32_t *ii = idx + i * k;
+    double rho = 0.0;
+    int nnz = 0;
+    for (int j = 0; j < k; ++j) nnz += di[j] > 0.0;
+    if (nnz >= local_connectivity) {
+      const int index = (int)floor(local_connectivity);
+      const double interp = local_connectivity - index;
+      double nz[2] = {0, 0}, first = 0;
+      int seen = 0, got = 0;
+      for (int j = 0; j < k; ++j) {
+        if (!(di[j] > 0.0)) continue;
+        if (!got) {
+          first = di[j];
+          got = 1;
+        }
+        ++seen;
+        if (seen == index) nz[0] = di[j];
+        if (seen == index + 1) nz[1] = di[j];
+      }
+      if (index > 0) {
+        rho = nz[0];
+        if (interp > 1e-5) rho += interp * (nz[1] - nz[0]);
+      } else {
+        rho = interp * first;
+      }
+    } else if (nnz > 0) {
+      rho = -INFINITY;
+      for (int j = 0; j < k; ++j)
+        if (di[j] > 0.0 && di[j] > rho) rho = di[j];
+    }
+    double lo = 0.0, hi = INFINITY, mid = 1.0;
+    for (int it = 0; it < 64; ++it) {
+      double psum = 0.0;
+      for (int j = 1; j < k; ++j) {
+        const double dd = di[j] - rho;
+        psum += dd > 0 ? exp(-(dd / mid)) : 1.0;
+      }
+      if (fabs(psum - target) < 1e-5) break;
+      if (psum > target) {
+        hi = mid;
+        mid = (lo + hi) / 2.0;
+      } else {
+        lo = mid;
+        mid = isinf(hi) ? mid * 2 : (lo + hi) / 2.0;
+      }
+    }
+    double sigma = mid;
+    if (rho > 0.0) {
+      double m = 0.0;
+      for (int j = 0; j < k; ++j) m += di[j];
+      m /= k;
+      if (sigma < 1e-3 * m) sigma = 1e-3 * m;
+    } else if (sigma < 1e-3 * mean_all) {
+      sigma = 1e-3 * mean_all;
+    }
+    int n = 0;
+    for (int j = 0; j < k; ++j) {
+      if (ii[j] < 0) continue;
+      const double dd = di[j] - rho;
+      w[n] = (dd <= 0.0 || sigma == 0.0) ? 1.0 : exp(-(dd / sigma));
+      ord[n] = j;
+      ++n;
+    }
+    for (int a = 1; a < n; ++a)
+      for (int b = a; b > 0 && ii[ord[b]] < ii[ord[b - 1]]; --b) {
+        const int t = ord[b];
+        ord[b] = ord[b - 1];
+        ord[b - 1] = t;
+        const double tw = w[b];
+        w[b] = w[b - 1];
+        w[b - 1] = tw;
+      }
+    double s = 0.0;
+    for (int a = 0; a < n; ++a) s += fabs(w[a]);
+    for (int c = 0; c < d; ++c) out[i * d + c] = 0.0;
+    for (int a = 0; a < n; ++a) {
+      const double wn = s > 0 ? w[a] / s : w[a];
+      for (int c = 0; c < d; ++c) out[i * d + c] += wn * emb[(int64_t)ii[ord[a]] * d + c];
+    }
+  }
+  free(w);
+  free(ord);
+}

@@ -19,7 +19,7 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c", "kmeans_sk.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c", "kmeans_sk.c", "backend.c")]
     if not os.path.exists(_LIB) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(_LIB):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _LIB
@@ -35,6 +35,7 @@ def lib():
         _lib.oracle_relabel_sequential.restype = ctypes.c_int32
         _lib.oracle_kmeans_scale.restype = ctypes.c_int
         _lib.oracle_kmeans_scale.argtypes = [ctypes.c_double, ctypes.c_int64]
+        _lib.oracle_knn_metric.restype = ctypes.c_double
     return _lib
 
 
@@ -410,4 +411,51 @@ def shape_filter(lab, stats, lo=15.0, hi=35.0):
     out = np.zeros(l.shape, np.int32)
     lib().oracle_shape_filter(_p(l), I64(l.shape[0]), I64(l.shape[1]), _p(st), ctypes.c_int32(st.shape[0] - 1),
                               ctypes.c_double(lo), ctypes.c_double(hi), _p(out))
+    return out
+
+
+# ---- a17, a18, f2: classifier back-end (backend.c) -------------------------------------------
+def svc_predict(x, sv, coef, intercept, start, kernel, gamma=1.0, coef0=0.0, degree=3, want_dec=False):
+    """libsvm one-vs-one predict (coef / intercept in libsvm's sign convention) -> class index
+    (and the pair decision values)"""
+    x = _c(x, np.float64)
+    sv = _c(sv, np.float64)
+    coef = _c(coef, np.float64)
+    intercept = _c(intercept, np.float64)
+    start = _c(start, np.int32)
+    n, f = x.shape
+    nc = len(start) - 1
+    pred = np.zeros(n, np.int32)
+    dec = np.zeros((n, nc * (nc - 1) // 2), np.float64) if want_dec else None
+    lib().oracle_svc_predict(_p(x), I64(n), I64(f), f, _p(sv), sv.shape[0], _p(coef), _p(intercept), _p(start), nc,
+                             int(kernel), ctypes.c_double(gamma), ctypes.c_double(coef0), int(degree), _p(pred),
+                             _p(dec) if dec is not None else None)
+    return (pred, dec) if want_dec else pred
+
+
+def knn_metric(x, y, metric):
+    x = _c(x, np.float64)
+    y = _c(y, np.float64)
+    return lib().oracle_knn_metric(int(metric), _p(x), _p(y), x.shape[0])
+
+
+def knn(q, train, metric, k):
+    q = _c(q, np.float64)
+    train = _c(train, np.float64)
+    nq, f = q.shape
+    idx = np.zeros((nq, k), np.int32)
+    dist = np.zeros((nq, k), np.float64)
+    lib().oracle_knn(_p(q), I64(nq), I64(f), _p(train), I64(train.shape[0]), f, int(metric), int(k), _p(idx),
+                     _p(dist))
+    return idx, dist
+
+
+def umap_init(idx, dist, embedding, n_neighbors, local_connectivity=0.0):
+    idx = _c(idx, np.int32)
+    dist = _c(dist, np.float64)
+    emb = _c(embedding, np.float64)
+    nq, k = idx.shape
+    out = np.zeros((nq, emb.shape[1]), np.float64)
+    lib().oracle_umap_init(_p(idx), _p(dist), I64(nq), k, ctypes.c_double(n_neighbors),
+                           ctypes.c_double(local_connectivity), _p(emb), emb.shape[1], _p(out))
     return out

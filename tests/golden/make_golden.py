@@ -220,10 +220,99 @@ def main_kmeans_images():
     print("kmeans_images.npz written")
 
 
+def _seg_cos_py(x, y, lo, hi):
+    r = nx = ny = 0.0
+    for i in range(lo, hi):
+        r += x[i] * y[i]
+        nx += x[i] ** 2
+        ny += y[i] ** 2
+    if nx == 0.0 and ny == 0.0:
+        return 0.0
+    if nx == 0.0 or ny == 0.0:
+        return 1.0
+    return 1.0 - r / np.sqrt(nx * ny)
+
+
+def metric_7b_v2(x, y):
+    """channel_cosine_intensity_7b_v2 (train_reference.py:994-1072), restated for sklearn's
+    brute-force neighbour search"""
+    if np.sum(np.abs(x[63:67] - y[63:67])) < 0.01:
+        b = (0, 23, 43, 57, 63)
+        c = [0.0 if x[63 + s] == 0 else _seg_cos_py(x, y, b[s], b[s + 1]) for s in range(4)]
+        return 0.5 * (c[0] + c[1] + c[2] + c[3]) / 4
+    return 1.0
+
+
+def metric_violet_v2(x, y):
+    """the scalar (d + c1..c5) / 6 of channel_cosine_intensity_violet_derivative_v2 (:569-731)"""
+    b = (0, 32, 55, 75, 89, 95)
+    if np.sum(np.abs(x[126:132] - y[126:132])) < 0.01:
+        d = 0.0
+        c = [0.0 if x[126 + s] == 0 else _seg_cos_py(x, y, b[s], b[s + 1]) for s in range(5)]
+    else:
+        d = 1.0
+        c = [_seg_cos_py(x, y, b[s], b[s + 1]) for s in range(5)]
+    return (d + c[0] + c[1] + c[2] + c[3] + c[4]) / 6
+
+
+def main_backend():
+    """sklearn SVC (predict, ovo decision_function), StandardScaler and brute-force
+    NearestNeighbors on synthetic data: the a17/a18/f2 back-end fixtures (backend.npz)"""
+    from sklearn.neighbors import NearestNeighbors
+    from sklearn.preprocessing import StandardScaler
+    from sklearn.svm import SVC
+    rng = np.random.default_rng(7)
+    out = {}
+    cases = [("rbf5", dict(kernel="rbf", gamma=0.7, C=3.0), 5, 3), ("lin2", dict(kernel="linear", C=0.5), 2, 32),
+             ("poly3", dict(kernel="poly", degree=3, gamma=0.4, coef0=1.0, C=2.0), 3, 6),
+             ("sig2", dict(kernel="sigmoid", gamma=0.05, coef0=0.1, C=1.0), 2, 23),
+             ("rbf40", dict(kernel="rbf", gamma=2.0, C=10.0), 40, 2)]
+    for name, kw, ncls, f in cases:
+        centres = rng.normal(0, 1.5, (ncls, f))
+        y = rng.integers(0, ncls, 600)
+        x = centres[y] + rng.normal(0, 1.0, (600, f))
+        clf = SVC(decision_function_shape="ovo", **kw).fit(x, y)
+        xt = centres[rng.integers(0, ncls, 300)] + rng.normal(0, 1.2, (300, f))
+        out[name + "_sv"] = clf.support_vectors_
+        out[name + "_dual_coef"] = clf.dual_coef_
+        out[name + "_intercept"] = clf.intercept_
+        out[name + "_n_support"] = clf.n_support_.astype(np.int32)
+        out[name + "_classes"] = clf.classes_.astype(np.float64)
+        out[name + "_gamma"] = np.float64(clf._gamma)
+        out[name + "_coef0"] = np.float64(clf.coef0)
+        out[name + "_degree"] = np.int32(clf.degree)
+        out[name + "_kernel"] = np.int32({"linear": 0, "poly": 1, "rbf": 2, "sigmoid": 3}[kw["kernel"]])
+        out[name + "_x"] = xt
+        out[name + "_pred"] = clf.predict(xt).astype(np.float64)
+        out[name + "_dec"] = clf.decision_function(xt)
+    x = rng.normal(3, 2, (200, 63)) * rng.uniform(0.1, 4, 63)
+    sc = StandardScaler().fit(x)
+    out["scaler_x"] = x[:50] + 0.3
+    out["scaler_mean"] = sc.mean_
+    out["scaler_scale"] = sc.scale_
+    out["scaler_out"] = sc.transform(x[:50] + 0.3)
+    for name, f, flags, metric in (("knn7b", 67, (63, 67), metric_7b_v2), ("knnviolet", 132, (126, 132), metric_violet_v2)):
+        proto = rng.random((12, f))
+        tr = proto[rng.integers(0, 12, 400)] + 0.05 * rng.random((400, f))
+        qs = proto[rng.integers(0, 12, 40)] + 0.05 * rng.random((40, f))
+        for a in (tr, qs):   # flag columns 0/1, a few mismatching
+            a[:, flags[0]:flags[1]] = (rng.random((len(a), flags[1] - flags[0])) < 0.7).astype(np.float64)
+        nn = NearestNeighbors(n_neighbors=15, algorithm="brute", metric=metric).fit(tr)
+        d, i = nn.kneighbors(qs)
+        out[name + "_train"] = tr
+        out[name + "_q"] = qs
+        out[name + "_idx"] = i.astype(np.int32)
+        out[name + "_dist"] = d
+    np.savez_compressed(os.path.join(HERE, "backend.npz"), **out)
+    print("backend.npz written")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["v3"]:
         main_v3()
     elif sys.argv[1:] == ["kmeans_images"]:
         main_kmeans_images()
+    elif sys.argv[1:] == ["backend"]:
+        main_backend()
     else:
         main()

@@ -1,0 +1,185 @@
+"""The classifier back-end on the device (backend.hip through libhrf.so) against sklearn's
+outputs (backend.npz) and the oracle.  SVC predict, the scaler, the kNN search and the
+feature tables are exact-order f64 restatements: class decisions bit-exact, decision values
+and distances within 1e-12 (exp/tanh/sqrt of the device libm vs glibc).  UMAP initialisation
+against the oracle only (parity unpinned, umap-learn absent)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from hiprfish_image_analysis_amd import backend as B  # noqa: E402
+from hiprfish_image_analysis_amd import kernels as K  # noqa: E402
+
+SVC_CASES = ["rbf5", "lin2", "poly3", "sig2", "rbf40"]
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()
+
+
+def model(g, name):
+    return B.SvcModel.from_npz(g, name + "_")
+
+
+@pytest.mark.parametrize("name", SVC_CASES)
+def test_svc_predict(golden, orc, name):
+    g = golden("backend")
+    m = model(g, name)
+    x = g[name + "_x"]
+    pred, dec = K.svc_predict(dev(x), m, want_dec=True)
+    pred = pred.cpu().numpy()
+    assert np.array_equal(g[name + "_classes"][pred], g[name + "_pred"])
+    want = g[name + "_dec"]
+    if m.n_class == 2:
+        want = -want.reshape(-1, 1)
+    np.testing.assert_allclose(dec.cpu().numpy(), want, rtol=1e-12, atol=1e-12)
+    # and bit-equal class decisions with the oracle
+    opred = orc.svc_predict(x, m.sv.cpu().numpy(), m.coef.cpu().numpy(), m.intercept.cpu().numpy(),
+                            m.start.cpu().numpy(), m.kernel, m.gamma, m.coef0, m.degree)
+    assert np.array_equal(pred, opred)
+
+
+def test_svc_predict_into_column_of_wider_table(golden):
+    """the flag-column path: input a column slice, output written into another column"""
+    g = golden("backend")
+    m = model(g, "poly3")
+    x = g["poly3_x"]
+    table = torch.zeros((len(x), 12), dtype=torch.float64, device="cuda")
+    table[:, 2:8] = dev(x)
+    pred = m.predict(table[:, 2:8], out_column=table[:, 10])
+    t = table.cpu().numpy()
+    assert np.array_equal(t[:, 10], g["poly3_pred"])
+    assert np.array_equal(t[:, 2:8], x) and not t[:, [0, 1, 8, 9, 11]].any()
+    assert np.array_equal(g["poly3_classes"][pred.cpu().numpy()], g["poly3_pred"])
+
+
+def test_svc_empty_and_mismatch(golden):
+    g = golden("backend")
+    m = model(g, "rbf5")
+    assert K.svc_predict(torch.empty((0, 3), dtype=torch.float64, device="cuda"), m).numel() == 0
+    with pytest.raises(ValueError):
+        K.svc_predict(dev(np.zeros((4, 5))), m)
+
+
+def test_standard_scale(golden):
+    g = golden("backend")
+    wide = torch.zeros((50, 70), dtype=torch.float64, device="cuda")
+    wide[:, 3:66] = dev(g["scaler_x"])
+    out = K.standard_scale(wide[:, 3:66], dev(g["scaler_mean"]), dev(g["scaler_scale"]))
+    np.testing.assert_allclose(out.cpu().numpy(), g["scaler_out"], rtol=0, atol=1e-15)
+
+
+@pytest.mark.parametrize("name,metric", [("knn7b", "channel_cosine_intensity_7b_v2"),
+                                         ("knnviolet", "channel_cosine_intensity_violet_derivative_v2")])
+def test_knn_matches_sklearn(golden, orc, name, metric):
+    g = golden("backend")
+    trT = dev(g[name + "_train"].T)
+    idx, dist = K.knn(dev(g[name + "_q"]), trT, metric, 15)
+    dist = dist.cpu().numpy()
+    np.testing.assert_allclose(dist, g[name + "_dist"], rtol=0, atol=1e-13)
+    from test_backend_oracle import assert_same_neighbours
+    assert_same_neighbours(idx.cpu().numpy(), dist, g[name + "_idx"])
+    # the lower-row tie rule the oracle states, exactly
+    oi, _ = orc.knn(g[name + "_q"], g[name + "_train"], 1 if "7b" in name else 2, 15)
+    assert np.array_equal(idx.cpu().numpy(), oi)
+
+
+@pytest.mark.parametrize("metric", [0, 1, 2])
+@pytest.mark.parametrize("k", [1, 15, 64])
+def test_knn_random_vs_oracle(orc, metric, k):
+    rng = np.random.default_rng(100 + metric * 7 + k)
+    f = (20, 67, 132)[metric]
+    tr = rng.random((3000, f))
+    q = rng.random((700, f))
+    if metric:
+        fl = (63, 67) if metric == 1 else (126, 132)
+        tr[:, fl[0]:fl[1]] = (rng.random((3000, fl[1] - fl[0])) < 0.8)
+        q[:, fl[0]:fl[1]] = (rng.random((700, fl[1] - fl[0])) < 0.8)
+    idx, dist = K.knn(dev(q), dev(tr.T), metric, k)
+    oi, od = orc.knn(q, tr, metric, k)
+    np.testing.assert_allclose(dist.cpu().numpy(), od, rtol=0, atol=1e-13)
+    # ties (metric 1 returns exactly 1.0 for a flag mismatch) resolve to the lower row
+    assert np.array_equal(idx.cpu().numpy(), oi)
+
+
+def test_knn_fewer_train_rows_than_k(orc):
+    rng = np.random.default_rng(5)
+    tr, q = rng.random((5, 8)), rng.random((9, 8))
+    idx, dist = K.knn(dev(q), dev(tr.T), 0, 8)
+    oi, od = orc.knn(q, tr, 0, 8)
+    assert np.array_equal(idx.cpu().numpy(), oi)
+    assert np.array_equal(np.isinf(dist.cpu().numpy()), np.isinf(od))
+
+
+@pytest.mark.parametrize("lc", [0.0, 1.0, 1.5])
+def test_umap_init_vs_oracle(orc, golden, lc):
+    g = golden("backend")
+    idx, dist = orc.knn(g["knnviolet_q"], g["knnviolet_train"], 2, 15)
+    rng = np.random.default_rng(11)
+    emb = rng.normal(size=(len(g["knnviolet_train"]), 2))
+    out = K.umap_init_transform(torch.from_numpy(idx).cuda(), dev(dist), dev(emb), 15, lc)
+    want = orc.umap_init(idx, dist, emb, 15.0, lc)
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=1e-12, atol=1e-12)
+
+
+def _random_svc(rng, ncls, f, kernel="rbf"):
+    nsv = rng.integers(3, 8, ncls)
+    sv = rng.random((int(nsv.sum()), f))
+    dual = rng.normal(size=(ncls - 1, int(nsv.sum())))
+    inter = rng.normal(size=ncls * (ncls - 1) // 2) * 0.1
+    return B.SvcModel.from_arrays(sv, dual, inter, nsv, np.arange(ncls, dtype=np.float64), kernel, gamma=0.5)
+
+
+def test_features_and_classify_chain(orc):
+    """E. coli bundle: features (diff + check flags), kNN under the violet-derivative metric,
+    UMAP init, SVC on the embedding -- each stage against the oracle on the same inputs"""
+    rng = np.random.default_rng(21)
+    n = 500
+    avg = rng.random((n, 95))
+    avg /= avg.max(axis=1, keepdims=True)
+    checks = [_random_svc(rng, 2, hi - lo) for lo, hi in B.ECOLI_SEGMENTS]
+    feats = B.features_ecoli(dev(avg), checks).cpu().numpy()
+    want = np.zeros((n, 132))
+    want[:, :95] = avg
+    want[:, 95:126] = np.diff(avg[:, :32], axis=1)
+    for k, (lo, hi) in enumerate(B.ECOLI_SEGMENTS):
+        c = checks[k]
+        p = orc.svc_predict(want[:, lo:hi], c.sv.cpu().numpy(), c.coef.cpu().numpy(), c.intercept.cpu().numpy(),
+                            c.start.cpu().numpy(), c.kernel, c.gamma, c.coef0, c.degree)
+        want[:, 126 + k] = p
+    np.testing.assert_array_equal(feats, want)
+    assert 0 < want[:, 126:].mean() < 1     # both flag values occur
+
+    tr = np.vstack([want[:200] + 0.0, rng.random((300, 132))])
+    tr[200:, 126:] = (rng.random((300, 6)) < 0.5)
+    emb = rng.normal(size=(500, 2))
+    um = B.UmapModel(dev(tr.T), dev(emb), 15, 1.0, "channel_cosine_intensity_violet_derivative_v2")
+    svc = _random_svc(rng, 7, 2)
+    bundle = B.ClassifierModel(checks, um, svc)
+    cls, classes, f2 = bundle.classify(dev(avg))
+    oi, od = orc.knn(want, tr, 2, 15)
+    e = orc.umap_init(oi, od, emb, 15.0, 0.0)
+    op = orc.svc_predict(e, svc.sv.cpu().numpy(), svc.coef.cpu().numpy(), svc.intercept.cpu().numpy(),
+                         svc.start.cpu().numpy(), svc.kernel, svc.gamma, svc.coef0, svc.degree)
+    got = cls.cpu().numpy()
+    # the embedding matches to ~1e-15; a cell whose SVC decision sits within that of 0 could
+    # flip -- require agreement everywhere else
+    assert (got == op).mean() > 0.995
+
+
+def test_features_multi_with_scaler(orc):
+    rng = np.random.default_rng(22)
+    n = 300
+    avg = rng.random((n, 63))
+    mean, scale = rng.random(63), rng.uniform(0.5, 2, 63)
+    checks = [_random_svc(rng, 2, hi - lo, "linear") for lo, hi in B.MULTI_SEGMENTS]
+    feats = B.features_multi(dev(avg), dev(mean), dev(scale), checks).cpu().numpy()
+    sc = (avg - mean) / scale
+    assert np.array_equal(feats[:, :63], avg)
+    for k, (lo, hi) in enumerate(B.MULTI_SEGMENTS):
+        c = checks[k]
+        p = orc.svc_predict(sc[:, lo:hi], c.sv.cpu().numpy(), c.coef.cpu().numpy(), c.intercept.cpu().numpy(),
+                            c.start.cpu().numpy(), c.kernel, c.gamma, c.coef0, c.degree)
+        assert np.array_equal(feats[:, 63 + k], p.astype(np.float64))

@@ -1,0 +1,90 @@
+"""The classifier back-end's CPU restatement (oracle/backend.c) pinned to sklearn
+(tests/golden/backend.npz, written by make_golden.py backend) and to the reference's own
+metric functions (metrics.npz).  CPU only."""
+import numpy as np
+import pytest
+
+SVC_CASES = ["rbf5", "lin2", "poly3", "sig2", "rbf40"]
+
+
+def libsvm_arrays(g, name):
+    """sklearn public attributes -> libsvm convention (binary: sign flipped)"""
+    dual = g[name + "_dual_coef"]
+    inter = g[name + "_intercept"]
+    ns = g[name + "_n_support"]
+    if len(ns) == 2:
+        dual, inter = -dual, -inter
+    start = np.concatenate([[0], np.cumsum(ns)]).astype(np.int32)
+    return g[name + "_sv"], dual, inter, start
+
+
+@pytest.mark.parametrize("name", SVC_CASES)
+def test_svc_predict_matches_sklearn(orc, golden, name):
+    g = golden("backend")
+    sv, coef, inter, start = libsvm_arrays(g, name)
+    pred, dec = orc.svc_predict(g[name + "_x"], sv, coef, inter, start, int(g[name + "_kernel"]),
+                                float(g[name + "_gamma"]), float(g[name + "_coef0"]), int(g[name + "_degree"]),
+                                want_dec=True)
+    classes = g[name + "_classes"]
+    assert np.array_equal(classes[pred], g[name + "_pred"])
+    want = g[name + "_dec"]
+    if len(classes) == 2:
+        want = -want.reshape(-1, 1)      # sklearn reports the binary decision with the flipped sign
+    np.testing.assert_allclose(dec, want, rtol=1e-12, atol=1e-12)
+
+
+def test_knn_metrics_match_reference(orc, golden):
+    g = golden("metrics")
+    for key, met in (("7b", 1), ("vd", 2)):
+        x, y, d = (g["x67"], g["y67"], g["d7b"]) if key == "7b" else (g["x132"], g["y132"], g["dvd"])
+        got = np.array([orc.knn_metric(x[i], y[i], met) for i in range(len(x))])
+        if key == "vd":
+            # the reference function returns (d, c1..c5) pieces combined by the caller; the
+            # fixture holds what it returns -- reduce to the scalar the search uses
+            want = np.asarray(d, np.float64)
+            want = want if want.ndim == 1 else want.mean(axis=1)
+        else:
+            want = np.asarray(d, np.float64)
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-14)
+
+
+@pytest.mark.parametrize("name,metric", [("knn7b", 1), ("knnviolet", 2)])
+def test_knn_matches_sklearn_brute(orc, golden, name, metric):
+    g = golden("backend")
+    idx, dist = orc.knn(g[name + "_q"], g[name + "_train"], metric, 15)
+    np.testing.assert_allclose(dist, g[name + "_dist"], rtol=0, atol=1e-14)
+    assert_same_neighbours(idx, dist, g[name + "_idx"])
+
+
+def assert_same_neighbours(idx, dist, want_idx):
+    """equal neighbour sets below the k-th distance; rows tied AT the k-th distance (the 7b
+    metric's flat 1.0 for mismatched flags) are an unordered choice in sklearn
+    (argpartition) and in umap-learn alike -- there only the distances are compared"""
+    for i in range(len(idx)):
+        below = dist[i] < dist[i, -1]
+        assert set(idx[i][below]) == set(want_idx[i][below]), i
+    return True
+
+
+def test_umap_init_properties(orc, golden):
+    """parity unpinned (umap-learn absent): a convex combination of the neighbours' embedding,
+    weights decreasing with distance, the nearest neighbour weighted 1 before normalisation"""
+    g = golden("backend")
+    idx, dist = orc.knn(g["knn7b_q"], g["knn7b_train"], 1, 15)
+    rng = np.random.default_rng(3)
+    emb = rng.normal(size=(len(g["knn7b_train"]), 2))
+    out = orc.umap_init(idx, dist, emb, 15.0, 0.0)
+    for i in range(len(idx)):
+        pts = emb[idx[i]]
+        assert out[i].min() >= pts.min(0).min() - 1e-12
+        lo, hi = pts.min(0), pts.max(0)
+        assert np.all(out[i] >= lo - 1e-12) and np.all(out[i] <= hi + 1e-12)
+    # all neighbours at one distance -> the plain mean
+    same = np.full_like(dist, 0.3)
+    np.testing.assert_allclose(orc.umap_init(idx, same, emb, 15.0, 0.0), emb[idx].mean(axis=1), rtol=1e-12)
+
+
+def test_standard_scale_fixture(golden):
+    g = golden("backend")
+    np.testing.assert_allclose((g["scaler_x"] - g["scaler_mean"]) / g["scaler_scale"], g["scaler_out"], rtol=0,
+                               atol=1e-15)
