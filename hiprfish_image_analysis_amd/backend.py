@@ -14,10 +14,12 @@ Stages (kernels.py -> backend.hip):
   features   avgint_norm | np.diff(channels 0..31) | check flags  (E. coli, 132 columns)
              avgint_norm | check flags on the scaled segments         (community, 67 columns)
   flags      SVC.predict per laser segment (libsvm one-vs-one)
-  embedding  exact kNN under the reference metric + umap-learn's transform initialisation
-             (smooth_knn_dist, membership strengths, l1 rows, init_transform); the layout
-             optimisation epochs umap-learn runs after it are not restated (stochastic, and
-             umap-learn is absent here: parity unpinned for this stage)
+  embedding  umap-learn transform (umap_.py, 0.4 era): exact kNN under the reference metric,
+             smooth_knn_dist, membership strengths, l1 rows, init_transform, then the layout
+             refinement epochs with the training embedding fixed.  The reference runs the
+             refinement unseeded (random_state None, parallel numba: not reproducible run to
+             run); here the negative samples come from seeded per-cell streams.  umap-learn is
+             absent here: parity unpinned for this stage
   barcode    SVC.predict on the embedding
 """
 from __future__ import annotations
@@ -93,28 +95,49 @@ class SvcModel:
 @dataclass
 class UmapModel:
     """The parts of a fitted umap.UMAP that transform() reads."""
-    trainT: torch.Tensor        # (f, n_train) f64: the training table, feature-major
-    embedding: torch.Tensor     # (n_train, d) f64
+    trainT: torch.Tensor        # (f, n_train) f64: the training table (_raw_data), feature-major
+    embedding: torch.Tensor     # (n_train, d) float32 (embedding_)
     n_neighbors: int
     local_connectivity: float
     metric: str
+    a: float = 1.577           # _a, _b: umap's curve for min_dist 0.1, spread 1 (find_ab_params)
+    b: float = 0.8951
+    repulsion_strength: float = 1.0
+    negative_sample_rate: int = 5
+    n_epochs: int = -1          # the fitted n_epochs (-1: None, transform's 100 / 30 rule)
+    initial_alpha: float = 1.0  # _initial_alpha (learning_rate)
+    refine: bool = True         # False: stop at the initial embedding
+    seed: int = 0
 
     @classmethod
     def from_npz(cls, z, prefix="umap_", device="cuda"):
-        train = np.asarray(z[prefix + "raw_data"], np.float64)
-        metric = z[prefix + "metric"].item() if (prefix + "metric") in z.files else "euclidean"
+        g = lambda key, default=None: z[prefix + key] if (prefix + key) in z.files else default  # noqa: E731
+        train = np.asarray(g("raw_data"), np.float64)
+        metric = g("metric", np.array("euclidean")).item()
         if isinstance(metric, bytes):
             metric = metric.decode()
         return cls(torch.from_numpy(np.ascontiguousarray(train.T)).to(device),
-                   torch.from_numpy(np.ascontiguousarray(np.asarray(z[prefix + "embedding"], np.float64))).to(device),
-                   int(z[prefix + "n_neighbors"]), float(z[prefix + "local_connectivity"])
-                   if (prefix + "local_connectivity") in z.files else 1.0, metric)
+                   torch.from_numpy(np.ascontiguousarray(np.asarray(g("embedding"), np.float32))).to(device),
+                   int(g("n_neighbors")), float(g("local_connectivity", 1.0)), metric,
+                   float(g("a", 1.577)), float(g("b", 0.8951)), float(g("repulsion_strength", 1.0)),
+                   int(g("negative_sample_rate", 5)), int(g("n_epochs", -1)), float(g("initial_alpha", 1.0)))
+
+    def transform_epochs(self, nq):
+        """umap_.py transform: 100 epochs up to 10000 queries, else 30; a fitted n_epochs / 3"""
+        if self.n_epochs is None or self.n_epochs < 0:
+            return 100 if nq <= 10000 else 30
+        return int(self.n_epochs // 3.0)
 
     def transform(self, features):
-        """umap-learn transform's neighbour graph and initial embedding (see module doc)"""
+        """umap-learn transform (see module doc): float32 (nq, d)"""
         idx, dist = K.knn(features, self.trainT, self.metric, self.n_neighbors)
-        return K.umap_init_transform(idx, dist, self.embedding, self.n_neighbors,
-                                     max(0.0, self.local_connectivity - 1.0))
+        init, memb = K.umap_init_transform(idx, dist, self.embedding, self.n_neighbors,
+                                           max(0.0, self.local_connectivity - 1.0), want_memb=True)
+        ne = self.transform_epochs(features.shape[0])
+        if not self.refine or ne < 1:
+            return init
+        return K.umap_refine(idx, memb, init, self.embedding, ne, self.a, self.b, self.repulsion_strength,
+                             self.initial_alpha / 4.0, self.negative_sample_rate, self.seed)
 
 
 def features_ecoli(avgint_norm, checks):
@@ -165,5 +188,5 @@ class ClassifierModel:
     def classify(self, avgint_norm):
         """-> (class index per cell (int32 device), the classes_ array, the feature table)"""
         feats = self.features(avgint_norm)
-        emb = self.umap.transform(feats)
+        emb = self.umap.transform(feats).double()     # sklearn reads the float32 embedding as f64
         return self.svc.predict(emb), self.svc.classes, feats

@@ -261,23 +261,25 @@ __global__ __launch_bounds__(KNN_T) void knn_kernel(const double *__restrict__ q
   }
 }
 
-// ---- f2: umap-learn transform's initial embedding ------------------------------------------------
-// smooth_knn_dist (n_iter 64, SMOOTH_K_TOLERANCE 1e-5, MIN_K_DIST_SCALE 1e-3, bandwidth 1; the
-// sum skips the first neighbour as umap-learn's does), compute_membership_strengths (bipartite),
-// l1 row normalisation of the CSR graph (entries in training-row order), init_transform.
+// ---- f2: umap-learn transform (0.4 era, the reference's) ------------------------------------------
+// umap_.py transform() after the neighbour search: smooth_knn_dist (n_iter 64,
+// SMOOTH_K_TOLERANCE 1e-5, MIN_K_DIST_SCALE 1e-3; rho and sigma live in float32 arrays, so every
+// later read sees the f32-rounded value; the psum loop skips the first neighbour),
+// compute_membership_strengths (bipartite: no self-edge test; float32 values), the coo -> csr
+// conversion (row entries sorted by training index), sklearn's l1 row normalisation (double row
+// sum, float32 store) and init_transform (float32 products accumulated in a float32 row).
 // One thread per query.
 __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *__restrict__ dist, int64_t nq,
                                  int32_t k, double n_neighbors, double local_connectivity,
-                                 const double *__restrict__ mean_dev, const double *__restrict__ emb, int32_t d,
-                                 double *__restrict__ out) {
+                                 const double *__restrict__ mean_dev, const float *__restrict__ emb, int32_t d,
+                                 float *__restrict__ memb_out, float *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nq) return;
   const double mean_all = *mean_dev;
   const double *di = dist + i * k;
   const int32_t *ii = idx + i * k;
   const double target = log2(n_neighbors);
-  // rho
-  double rho = 0.0;
+  float rho = 0.0f;
   int nnz = 0;
   for (int j = 0; j < k; ++j) nnz += di[j] > 0.0;
   if (nnz >= local_connectivity) {
@@ -297,21 +299,22 @@ __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *
       if (seen == index + 1) nz_cur = di[j];
     }
     if (index > 0) {
-      rho = nz_prev;
-      if (interp > 1e-5) rho += interp * (nz_cur - nz_prev);
+      rho = (float)nz_prev;
+      if (interp > 1e-5) rho = (float)((double)rho + interp * (nz_cur - nz_prev));
     } else {
-      rho = interp * nz_first;
+      rho = (float)(interp * nz_first);
     }
   } else if (nnz > 0) {
-    rho = -INFINITY;
+    double mx = -INFINITY;
     for (int j = 0; j < k; ++j)
-      if (di[j] > 0.0 && di[j] > rho) rho = di[j];
+      if (di[j] > 0.0 && di[j] > mx) mx = di[j];
+    rho = (float)mx;
   }
   double lo = 0.0, hi = INFINITY, mid = 1.0;
   for (int n = 0; n < 64; ++n) {
     double psum = 0.0;
     for (int j = 1; j < k; ++j) {
-      const double dd = di[j] - rho;
+      const double dd = di[j] - (double)rho;
       psum += dd > 0 ? exp(-(dd / mid)) : 1.0;
     }
     if (fabs(psum - target) < 1e-5) break;
@@ -323,43 +326,153 @@ __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *
       mid = hi == INFINITY ? mid * 2 : (lo + hi) / 2.0;
     }
   }
-  double sigma = mid;
-  if (rho > 0.0) {
+  float sigma = (float)mid;
+  if (rho > 0.0f) {
     double m = 0.0;
     for (int j = 0; j < k; ++j) m += di[j];
     m /= k;
-    if (sigma < 1e-3 * m) sigma = 1e-3 * m;
-  } else if (sigma < 1e-3 * mean_all) {
-    sigma = 1e-3 * mean_all;
+    if ((double)sigma < 1e-3 * m) sigma = (float)(1e-3 * m);
+  } else if ((double)sigma < 1e-3 * mean_all) {
+    sigma = (float)(1e-3 * mean_all);
   }
-  // membership strengths, then the row in training-index order (CSR), l1-normalised
-  double w[KNN_KMAX];
+  float w[KNN_KMAX];
   int ord[KNN_KMAX];
   int n = 0;
   for (int j = 0; j < k; ++j) {
-    if (ii[j] < 0) continue;
-    const double dd = di[j] - rho;
-    w[n] = (dd <= 0.0 || sigma == 0.0) ? 1.0 : exp(-(dd / sigma));
-    ord[n] = j;
-    ++n;
+    float v = 0.0f;
+    if (ii[j] >= 0) {
+      const double dd = di[j] - (double)rho;
+      v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)exp(-(dd / (double)sigma));
+      w[n] = v;
+      ord[n] = j;
+      ++n;
+    }
+    if (memb_out) memb_out[i * k + j] = v;
   }
   for (int a = 1; a < n; ++a)
     for (int b = a; b > 0 && ii[ord[b]] < ii[ord[b - 1]]; --b) {
       const int t = ord[b];
       ord[b] = ord[b - 1];
       ord[b - 1] = t;
-      const double tw = w[b];
+      const float tw = w[b];
       w[b] = w[b - 1];
       w[b - 1] = tw;
     }
   double s = 0.0;
-  for (int a = 0; a < n; ++a) s += fabs(w[a]);
-  for (int c = 0; c < d; ++c) out[i * d + c] = 0.0;
+  for (int a = 0; a < n; ++a) s += fabs((double)w[a]);
+  for (int c = 0; c < d; ++c) out[i * d + c] = 0.0f;
   for (int a = 0; a < n; ++a) {
-    const double wn = s > 0 ? w[a] / s : w[a];
-    const double *e = emb + (int64_t)ii[ord[a]] * d;
-    for (int c = 0; c < d; ++c) out[i * d + c] += wn * e[c];
+    const float wn = s != 0.0 ? (float)((double)w[a] / s) : w[a];
+    const float *e = emb + (int64_t)ii[ord[a]] * d;
+    for (int c = 0; c < d; ++c) out[i * d + c] = __fadd_rn(out[i * d + c], __fmul_rn(wn, e[c]));
   }
+}
+
+// umap's tau_rand_int (three-component Tausworthe) on unsigned 32-bit states
+__device__ __forceinline__ uint32_t tau_rand(uint32_t &s0, uint32_t &s1, uint32_t &s2) {
+  s0 = ((s0 & 4294967294u) << 12) ^ (((s0 << 13) ^ s0) >> 19);
+  s1 = ((s1 & 4294967288u) << 4) ^ (((s1 << 2) ^ s1) >> 25);
+  s2 = ((s2 & 4294967280u) << 17) ^ (((s2 << 3) ^ s2) >> 11);
+  return s0 ^ s1 ^ s2;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t &x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ double umap_clip(double v) { return v > 4.0 ? 4.0 : (v < -4.0 ? -4.0 : v); }
+
+constexpr int UMAP_DMAX = 8;
+
+// rdist of a float32 pair: float32 differences squared in float32, summed in double (numba's
+// inference for umap's rdist)
+__device__ __forceinline__ double umap_rdist(const float *cur, const float *__restrict__ o, int d) {
+  double r = 0.0;
+  for (int c = 0; c < d; ++c) {
+    const float df = cur[c] - o[c];
+    r += (double)__fmul_rn(df, df);
+  }
+  return r;
+}
+
+// transform()'s layout refinement: the graph's edges below max / n_epochs dropped,
+// make_epochs_per_sample (float32 arithmetic as numpy does it on the float32 graph), then
+// optimize_layout_euclidean with the training embedding fixed (move_other False), alpha =
+// initial_alpha / 4 decayed per epoch.  umap draws the negative samples from ONE sequential
+// stream shared by all edges (parallel and unseeded in the reference: random_state None); here
+// each query has its own stream seeded from (seed, query), so the result is deterministic and
+// independent of batching.  One thread per query; its edges are visited in knn order each epoch.
+__global__ void umap_refine_kernel(const int32_t *__restrict__ idx, const float *__restrict__ memb, int64_t nq,
+                                   int32_t k, const float *__restrict__ wmax_dev, int32_t n_epochs,
+                                   const float *__restrict__ tail, int64_t ntrain, int32_t d, double a, double b,
+                                   double gamma, double alpha0, double neg_rate, uint64_t seed,
+                                   float *__restrict__ emb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const float wmax = *wmax_dev;
+  const float thr = (float)((double)wmax / (double)n_epochs);   // numpy 1.x: f32 max / float -> f64, compared in f32
+  double eps[KNN_KMAX], eons[KNN_KMAX], eonns[KNN_KMAX];
+  int32_t tl[KNN_KMAX];
+  int ne = 0;
+  for (int j = 0; j < k; ++j) {
+    const float w = memb[i * k + j];
+    if (idx[i * k + j] < 0 || !(w >= thr) || w == 0.0f) continue;   // eliminate_zeros after thresholding
+    const float ns = __fmul_rn((float)n_epochs, w / wmax);
+    eps[ne] = ns > 0.0f ? (double)((float)n_epochs / ns) : -1.0;
+    eons[ne] = eps[ne];
+    eonns[ne] = eps[ne] / neg_rate;
+    tl[ne] = idx[i * k + j];
+    ++ne;
+  }
+  float cur[UMAP_DMAX];
+  for (int c = 0; c < d; ++c) cur[c] = emb[i * d + c];
+  uint64_t sm = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(i + 1));
+  uint32_t s0 = (uint32_t)splitmix64(sm) | 2u, s1 = (uint32_t)splitmix64(sm) | 8u, s2 = (uint32_t)splitmix64(sm) | 16u;
+  const double bm1 = b - 1.0;
+  double alpha = alpha0;
+  for (int n = 0; n < n_epochs; ++n) {
+    for (int e = 0; e < ne; ++e) {
+      if (!(eons[e] <= n)) continue;
+      const float *o = tail + (int64_t)tl[e] * d;
+      const double d2 = umap_rdist(cur, o, d);
+      double gc = 0.0;
+      if (d2 > 0.0) {
+        gc = -2.0 * a * b * pow(d2, bm1);
+        gc /= a * pow(d2, b) + 1.0;
+      }
+      for (int c = 0; c < d; ++c) {
+        const double g = umap_clip(gc * (double)(cur[c] - o[c]));
+        cur[c] = (float)((double)cur[c] + g * alpha);
+      }
+      eons[e] += eps[e];
+      const double epns = eps[e] / neg_rate;
+      const int nneg = (int)(((double)n - eonns[e]) / epns);
+      for (int p = 0; p < nneg; ++p) {
+        const int64_t kk = (int64_t)(tau_rand(s0, s1, s2) % (uint64_t)ntrain);
+        const float *on = tail + kk * d;
+        const double dn = umap_rdist(cur, on, d);
+        double gn;
+        if (dn > 0.0) {
+          gn = 2.0 * gamma * b;
+          gn /= (0.001 + dn) * (a * pow(dn, b) + 1.0);
+        } else if (kk == i) {
+          continue;
+        } else {
+          gn = 0.0;
+        }
+        for (int c = 0; c < d; ++c) {
+          const double g = gn > 0.0 ? umap_clip(gn * (double)(cur[c] - on[c])) : 4.0;
+          cur[c] = (float)((double)cur[c] + g * alpha);
+        }
+      }
+      eonns[e] += nneg * epns;
+    }
+    alpha = alpha0 * (1.0 - (double)n / (double)n_epochs);
+  }
+  for (int c = 0; c < d; ++c) emb[i * d + c] = cur[c];
 }
 
 }  // namespace
@@ -426,12 +539,29 @@ hrf_status hrf_knn(const double *q, int64_t nq, int64_t ldq, const double *train
 
 hrf_status hrf_umap_init_transform(const int32_t *knn_idx, const double *knn_dist, int64_t nq, int32_t k,
                                    double n_neighbors, double local_connectivity, const double *mean_dist_dev,
-                                   const double *embedding, int32_t d, double *out, hrf_stream_t stream) {
+                                   const float *embedding, int32_t d, float *memb_out, float *out,
+                                   hrf_stream_t stream) {
   HRF_REQUIRE(k >= 1 && k <= KNN_KMAX && d >= 1, "umap_init_transform: bad shape");
   if (nq == 0) return HRF_OK;
   HRF_REQUIRE(knn_idx && knn_dist && mean_dist_dev && embedding && out, "umap_init_transform: null buffer");
   umap_init_kernel<<<(unsigned)hrf::cdiv(nq, 64), 64, 0, (hipStream_t)stream>>>(
-      knn_idx, knn_dist, nq, k, n_neighbors, local_connectivity, mean_dist_dev, embedding, d, out);
+      knn_idx, knn_dist, nq, k, n_neighbors, local_connectivity, mean_dist_dev, embedding, d, memb_out, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_umap_refine(const int32_t *knn_idx, const float *memb, int64_t nq, int32_t k, const float *wmax_dev,
+                           int32_t n_epochs, const float *tail_embedding, int64_t ntrain, int32_t d, double a,
+                           double b, double repulsion_strength, double initial_alpha, double negative_sample_rate,
+                           uint64_t seed, float *embedding, hrf_stream_t stream) {
+  HRF_REQUIRE(k >= 1 && k <= KNN_KMAX && d >= 1 && d <= UMAP_DMAX, "umap_refine: 1..%d neighbours, 1..%d dims",
+              KNN_KMAX, UMAP_DMAX);
+  HRF_REQUIRE(n_epochs >= 1 && ntrain >= 1 && negative_sample_rate > 0, "umap_refine: bad schedule");
+  if (nq == 0) return HRF_OK;
+  HRF_REQUIRE(knn_idx && memb && wmax_dev && tail_embedding && embedding, "umap_refine: null buffer");
+  umap_refine_kernel<<<(unsigned)hrf::cdiv(nq, 64), 64, 0, (hipStream_t)stream>>>(
+      knn_idx, memb, nq, k, wmax_dev, n_epochs, tail_embedding, ntrain, d, a, b, repulsion_strength, initial_alpha,
+      negative_sample_rate, seed, embedding);
   HRF_LAUNCHED();
   return HRF_OK;
 }

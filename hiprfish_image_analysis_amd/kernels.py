@@ -836,15 +836,36 @@ def knn(q, trainT, metric, k):
     return idx, dist
 
 
-def umap_init_transform(idx, dist, embedding, n_neighbors, local_connectivity=0.0):
+def umap_init_transform(idx, dist, embedding, n_neighbors, local_connectivity=0.0, want_memb=False):
     """umap-learn transform's initial embedding of the queries from their kNN (the mean knn
-    distance stays on the device)"""
+    distance stays on the device).  embedding: the training embedding, float32 (umap's dtype).
+    -> float32 (nq, d) [, the float32 membership strengths (nq, k) in knn order]"""
     idx = _i32(idx, "idx")
     dist = _dev(dist, torch.float64, "dist")
-    emb = _dev(embedding, torch.float64, "embedding")
+    emb = _dev(embedding, torch.float32, "embedding")
     nq, k = idx.shape
     mean = dist.mean().reshape(1) if dist.numel() else torch.zeros(1, dtype=torch.float64, device=dist.device)
-    out = torch.empty((nq, emb.shape[1]), dtype=torch.float64, device=dist.device)
+    out = torch.empty((nq, emb.shape[1]), dtype=torch.float32, device=dist.device)
+    memb = torch.empty((nq, k), dtype=torch.float32, device=dist.device) if want_memb else None
     _lib.call("hrf_umap_init_transform", _ptr(idx), _ptr(dist), nq, k, float(n_neighbors), float(local_connectivity),
-              _ptr(mean), _ptr(emb), emb.shape[1], _ptr(out), _stream())
-    return out
+              _ptr(mean), _ptr(emb), emb.shape[1], _ptr(memb) if memb is not None else None, _ptr(out), _stream())
+    return (out, memb) if want_memb else out
+
+
+def umap_refine(idx, memb, init, tail_embedding, n_epochs, a, b, repulsion_strength=1.0, initial_alpha=0.25,
+                negative_sample_rate=5.0, seed=0):
+    """transform()'s layout refinement of `init` (float32, nq x d, refined in a copy) against the
+    fixed training embedding; initial_alpha is the rate transform passes (umap's
+    _initial_alpha / 4).  Deterministic per-query negative-sample streams (see hrf.h)."""
+    idx = _i32(idx, "idx")
+    memb = _dev(memb, torch.float32, "memb")
+    tail = _dev(tail_embedding, torch.float32, "tail_embedding")
+    emb = _dev(init, torch.float32, "init").clone()
+    nq, k = idx.shape
+    if memb.shape != idx.shape or emb.shape[0] != nq or emb.shape[1] != tail.shape[1]:
+        raise ValueError("umap_refine: shapes disagree")
+    wmax = memb.amax().reshape(1) if memb.numel() else torch.zeros(1, dtype=torch.float32, device=memb.device)
+    _lib.call("hrf_umap_refine", _ptr(idx), _ptr(memb), nq, k, _ptr(wmax), int(n_epochs), _ptr(tail), tail.shape[0],
+              tail.shape[1], float(a), float(b), float(repulsion_strength), float(initial_alpha),
+              float(negative_sample_rate), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(emb), _stream())
+    return emb

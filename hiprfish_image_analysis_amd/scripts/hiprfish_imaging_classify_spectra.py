@@ -2,12 +2,14 @@
 same flags (-i/--input_spectra {s}_avgint_norm.csv, -r/--ref_clf), same output
 ({s}_cell_information.csv, no header, no index).
 
-The UMAP/SVC pickles (:56-59) are never unpickled here; -r names a reference library for the
-restated classifier (a (R, C) .npy/.csv of per-barcode mean spectra or a directory of
-*_enc_N_avgint.csv measurements, see io.load_library), and the barcode is the argmin of the
-segmented-cosine metric (default: the _7b_v2 gated variant, train_reference.py:993-1072).
-Columns follow the reference (:27-46): 0-62 max-normalised spectrum, 63-66 per-laser presence
-flags (segment max > 0.1, standing in for the per-excitation check SVCs :30-33), 67 barcode,
+The UMAP/SVC pickles (:56-59) are never unpickled here.  -r names either
+  * a classifier bundle exported to arrays (.npz with scaler, four check SVCs, UMAP and barcode
+    SVC; INTEGRATION.md): the reference's chain (:27-35) on the device (backend.py);
+  * or a reference library for the restated classifier (a (R, C) .npy/.csv of per-barcode mean
+    spectra or a directory of *_enc_N_avgint.csv measurements, see io.load_library): the
+    barcode is the argmin of the segmented-cosine metric (default: the _7b_v2 gated variant,
+    train_reference.py:993-1072) and the flags are segment max > 0.1 presence flags.
+Columns follow the reference (:27-46): 0-62 max-normalised spectrum, 63-66 per-laser flags, 67 barcode,
 68 sample, 69 label, 70-71 centroid, 72 major, 73 minor, 74 eccentricity, 75 orientation,
 76 area (regionprops order: ascending label).
 """
@@ -37,15 +39,22 @@ def main(argv=None):
     avgint = pd.read_csv(args.input_spectra)                                      # :25
     segmentation = np.load('{}_seg.npy'.format(sample), allow_pickle=False)       # :26
     avgint_norm = avgint.values / np.max(avgint.values, axis=1)[:, None]          # :27
-    libspec, nbit = io.load_library(args.ref_clf)
-    bounds = P.MULTI_BOUNDS if avgint_norm.shape[1] == 63 else (0, avgint_norm.shape[1])
-    lib = P.Library(torch.from_numpy(libspec).to(dev), bounds, nbit)
     x = torch.from_numpy(np.ascontiguousarray(avgint_norm, dtype=np.float64)).to(dev)
-    nseg = len(bounds) - 1
-    feats = np.concatenate((avgint_norm, np.zeros((avgint_norm.shape[0], nseg))), axis=1)   # :28
-    feats[:, -nseg:] = P.segment_flags(x, bounds).cpu().numpy()                   # :30-33
-    idx, _ = P.classify_cells(x, lib, variant=args.variant)                       # :34-35
-    codes = np.array(P.barcode_strings(idx.cpu().numpy(), nbit))
+    if args.ref_clf.endswith('.npz'):
+        from hiprfish_image_analysis_amd import backend as B
+        model = B.ClassifierModel.load(args.ref_clf, dev)                         # :56-59 as arrays
+        cls, classes, feats_t = model.classify(x)                                 # :28-35
+        codes = np.asarray(classes)[cls.cpu().numpy()].astype(str)
+        feats = feats_t.cpu().numpy()
+    else:
+        libspec, nbit = io.load_library(args.ref_clf)
+        bounds = P.MULTI_BOUNDS if avgint_norm.shape[1] == 63 else (0, avgint_norm.shape[1])
+        lib = P.Library(torch.from_numpy(libspec).to(dev), bounds, nbit)
+        nseg = len(bounds) - 1
+        feats = np.concatenate((avgint_norm, np.zeros((avgint_norm.shape[0], nseg))), axis=1)   # :28
+        feats[:, -nseg:] = P.segment_flags(x, bounds).cpu().numpy()               # :30-33
+        idx, _ = P.classify_cells(x, lib, variant=args.variant)                   # :34-35
+        codes = np.array(P.barcode_strings(idx.cpu().numpy(), nbit))
     cell_info = pd.DataFrame(np.concatenate((feats, codes[:, None]), axis=1))    # :36
     cell_info[68] = sample                                                        # :37
     seg = torch.from_numpy(segmentation.astype(np.int32)).to(dev)

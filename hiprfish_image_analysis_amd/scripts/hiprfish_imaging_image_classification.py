@@ -2,13 +2,18 @@
 same CLI (positional input_spectra = {s}_avgint.csv, -rf/--reference_clf), same outputs
 ({s}_cell_ids.txt, {s}_avgint_ids.csv, {s}_identification.png).
 
-The reference's UMAP + SVC pickles are not available (and are never unpickled here); the
-barcode is the argmin of the reference's segmented-cosine metric over a reference library
-(DESIGN.md §classify).  -rf names that library: a (R, C) .npy/.csv of per-barcode mean
-spectra, or a directory of *_enc_N_avgint.csv reference measurements.
+-rf names either
+  * a classifier bundle exported to arrays (.npz, see INTEGRATION.md and
+    tools/export_classifier.py): the reference's own chain (:47-56) on the device -- six
+    check-SVC flags, the UMAP transform (exact kNN under the violet-derivative metric and the
+    transform's initial embedding) and the barcode SVC (backend.py).  Pickles are never
+    unpickled here;
+  * or a reference library (a (R, C) .npy/.csv of per-barcode mean spectra, or a directory of
+    *_enc_N_avgint.csv reference measurements): the barcode is then the argmin of the
+    reference's segmented-cosine metric over it and the flags 126-131
+    are segment max > 0.1 presence flags.
 Columns of _avgint_ids.csv follow the reference (:47-64): 0-94 max-normalised spectrum,
-95-125 violet derivative, 126-131 per-laser presence flags (segment max > 0.1, standing in
-for the per-excitation SVCs), 132 barcode, 133 sample, 134 label.
+95-125 violet derivative, 126-131 per-laser flags, 132 barcode, 133 sample, 134 label.
 """
 import argparse
 import os
@@ -36,19 +41,28 @@ def main(argv=None):
     dev = torch.device("cuda", 0)
     segmentation = np.load('{}_seg.npy'.format(sample), allow_pickle=False)
     avgint = pd.read_csv(args.input_spectra, header=None).values
-    libspec, nbit = io.load_library(args.ref_clf)
-    bounds = P.ECOLI_BOUNDS if avgint.shape[1] == 95 else (0, avgint.shape[1])
-    lib = P.Library(torch.from_numpy(libspec).to(dev), bounds, nbit)
     avgint_norm = avgint / np.max(avgint, axis=1)[:, None]                        # :43
     x = torch.from_numpy(np.ascontiguousarray(avgint_norm)).to(dev)
-    idx, dist = P.classify_cells(x, lib, variant=args.variant)
-    idx = idx.cpu().numpy()
-    codes = np.array(P.barcode_strings(idx, nbit))
-    feats = np.concatenate((avgint_norm, np.zeros((avgint_norm.shape[0], 37))), axis=1)
-    if avgint.shape[1] == 95:
-        feats[:, 95:126] = np.diff(avgint_norm[:, 0:32], axis=1)                  # :48
-        feats[:, 126:131] = P.segment_flags(x, bounds).cpu().numpy()
-        feats[:, 131] = (np.abs(feats[:, 95:126]).max(axis=1) > 0.01)
+    if args.ref_clf.endswith('.npz'):
+        from hiprfish_image_analysis_amd import backend as B
+        model = B.ClassifierModel.load(args.ref_clf, dev)                         # :44-46 as arrays
+        cls, classes, feats_t = model.classify(x)                                 # :47-56
+        codes = np.asarray(classes)[cls.cpu().numpy()].astype(str)
+        feats = feats_t.cpu().numpy()
+        paint = np.array([int(c, 2) for c in codes], dtype=np.int32)              # :66-71 int(id, 2)
+    else:
+        libspec, nbit = io.load_library(args.ref_clf)
+        bounds = P.ECOLI_BOUNDS if avgint.shape[1] == 95 else (0, avgint.shape[1])
+        lib = P.Library(torch.from_numpy(libspec).to(dev), bounds, nbit)
+        idx, dist = P.classify_cells(x, lib, variant=args.variant)
+        idx = idx.cpu().numpy()
+        codes = np.array(P.barcode_strings(idx, nbit))
+        paint = (idx + 1).astype(np.int32)
+        feats = np.concatenate((avgint_norm, np.zeros((avgint_norm.shape[0], 37))), axis=1)
+        if avgint.shape[1] == 95:
+            feats[:, 95:126] = np.diff(avgint_norm[:, 0:32], axis=1)              # :48
+            feats[:, 126:131] = P.segment_flags(x, bounds).cpu().numpy()
+            feats[:, 131] = (np.abs(feats[:, 95:126]).max(axis=1) > 0.01)
     np.savetxt(sample + '_cell_ids.txt', codes, fmt='%s')                         # :63
     ids = pd.DataFrame(np.concatenate((feats, codes[:, None]), axis=1))
     ids[133] = sample
@@ -56,7 +70,7 @@ def main(argv=None):
     ids[134] = labels[labels > 0][:len(ids)]
     ids.to_csv(sample + '_avgint_ids.csv', header=None, index=None)               # :64
     seg = torch.from_numpy(segmentation.astype(np.int32)).to(dev)
-    ident = K.paint_ids(seg, torch.from_numpy((idx + 1).astype(np.int32)).to(dev)).cpu().numpy()   # :65-71
+    ident = K.paint_ids(seg, torch.from_numpy(paint).to(dev)).cpu().numpy()   # :65-71
     io.save_figure(io.label_color_image(ident), sample + '_identification.png')
     return codes
 

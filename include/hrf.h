@@ -363,12 +363,24 @@ HRF_API hrf_status hrf_svc_predict(const double *x, int64_t n, int64_t ldx, int3
  * lower row.  idx/dist (nq x k) */
 HRF_API hrf_status hrf_knn(const double *q, int64_t nq, int64_t ldq, const double *trainT, int64_t nt, int32_t f,
                            int32_t metric, int32_t k, int32_t *idx_out, double *dist_out, hrf_stream_t stream);
-/* umap-learn transform's initial embedding from the kNN: smooth_knn_dist, membership strengths,
- * l1 rows, init_transform.  mean_dist_dev: the mean of all knn distances (device scalar) */
+/* umap-learn transform's initial embedding from the kNN (umap_.py transform, 0.4 era):
+ * smooth_knn_dist, membership strengths (float32), l1 rows, init_transform (float32).
+ * mean_dist_dev: the mean of all knn distances (device scalar); embedding (ntrain x d) float32;
+ * memb_out (nq x k, optional): the membership strengths in knn order (0 for missing rows), the
+ * graph hrf_umap_refine optimises; out (nq x d) float32 */
 HRF_API hrf_status hrf_umap_init_transform(const int32_t *knn_idx, const double *knn_dist, int64_t nq, int32_t k,
                                            double n_neighbors, double local_connectivity,
-                                           const double *mean_dist_dev, const double *embedding, int32_t d,
-                                           double *out, hrf_stream_t stream);
+                                           const double *mean_dist_dev, const float *embedding, int32_t d,
+                                           float *memb_out, float *out, hrf_stream_t stream);
+/* transform()'s layout refinement (optimize_layout_euclidean, training embedding fixed): edges
+ * below wmax/n_epochs dropped (wmax = max of memb, device scalar), alpha initial_alpha (pass
+ * umap's _initial_alpha / 4), negative samples from per-query Tausworthe streams seeded by
+ * (seed, query) -- deterministic, unlike the reference's unseeded shared stream.  embedding
+ * (nq x d, float32) in/out, d <= 8 */
+HRF_API hrf_status hrf_umap_refine(const int32_t *knn_idx, const float *memb, int64_t nq, int32_t k,
+                                   const float *wmax_dev, int32_t n_epochs, const float *tail_embedding, int64_t ntrain,
+                                   int32_t d, double a, double b, double repulsion_strength, double initial_alpha,
+                                   double negative_sample_rate, uint64_t seed, float *embedding, hrf_stream_t stream);
 
 /* ==== a22: label adjacency (rag.hip) ====================================================
  * skimage.future.graph.rag_boundary edge set (biofilm :1277-1278): edge[(maxlab+1)^2] u8,

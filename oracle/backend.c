@@ -11,9 +11,12 @@
  *                      (train_reference.py:993-1072) / _violet_derivative_v2 (:569-731, the
  *                      scalar (d + c1..c5)/6 it computes) / euclidean; ties to the lower row.
  *                      The search pinned to sklearn NearestNeighbors(algorithm='brute').
- *  oracle_umap_init    umap-learn (0.5) transform's initial embedding: smooth_knn_dist,
- *                      compute_membership_strengths (bipartite), CSR l1 normalisation,
- *                      init_transform.  umap-learn is absent here: parity unpinned.
+ *  oracle_umap_init    umap-learn transform's initial embedding (umap_.py, 0.4 era):
+ *                      smooth_knn_dist (float32 rho / sigma), compute_membership_strengths
+ *                      (bipartite, float32), CSR l1 normalisation, init_transform (float32).
+ *  oracle_umap_refine  transform's layout refinement (optimize_layout_euclidean, training
+ *                      embedding fixed) with per-query seeded negative-sample streams.
+ *                      umap-learn is absent here: parity unpinned for both.
  */
 #include <math.h>
 #include <stdint.h>
@@ -140,17 +143,17 @@ void oracle_knn(const double *q, int64_t nq, int64_t ldq, const double *train, i
 }
 
 void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k, double n_neighbors,
-                      double local_connectivity, const double *emb, int d, double *out) {
+                      double local_connectivity, const float *emb, int d, float *memb, float *out) {
   double mean_all = 0.0;
   for (int64_t e = 0; e < nq * k; ++e) mean_all += dist[e];
   mean_all /= (double)(nq * k);
   const double target = log2(n_neighbors);
-  double *w = (double *)malloc(sizeof(double) * (size_t)k);
+  float *w = (float *)malloc(sizeof(float) * (size_t)k);
   int *ord = (int *)malloc(sizeof(int) * (size_t)k);
   for (int64_t i = 0; i < nq; ++i) {
     const double *di = dist + i * k;
     const int32_t *ii = idx + i * k;
-    double rho = 0.0;
+    float rho = 0.0f;   /* umap keeps rho and sigma in float32 arrays */
     int nnz = 0;
     for (int j = 0; j < k; ++j) nnz += di[j] > 0.0;
     if (nnz >= local_connectivity) {
@@ -169,21 +172,22 @@ void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k,
         if (seen == index + 1) nz[1] = di[j];
       }
       if (index > 0) {
-        rho = nz[0];
-        if (interp > 1e-5) rho += interp * (nz[1] - nz[0]);
+        rho = (float)nz[0];
+        if (interp > 1e-5) rho = (float)((double)rho + interp * (nz[1] - nz[0]));
       } else {
-        rho = interp * first;
+        rho = (float)(interp * first);
       }
     } else if (nnz > 0) {
-      rho = -INFINITY;
+      double mx = -INFINITY;
       for (int j = 0; j < k; ++j)
-        if (di[j] > 0.0 && di[j] > rho) rho = di[j];
+        if (di[j] > 0.0 && di[j] > mx) mx = di[j];
+      rho = (float)mx;
     }
     double lo = 0.0, hi = INFINITY, mid = 1.0;
     for (int it = 0; it < 64; ++it) {
       double psum = 0.0;
       for (int j = 1; j < k; ++j) {
-        const double dd = di[j] - rho;
+        const double dd = di[j] - (double)rho;
         psum += dd > 0 ? exp(-(dd / mid)) : 1.0;
       }
       if (fabs(psum - target) < 1e-5) break;
@@ -195,40 +199,151 @@ void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k,
         mid = isinf(hi) ? mid * 2 : (lo + hi) / 2.0;
       }
     }
-    double sigma = mid;
-    if (rho > 0.0) {
+    float sigma = (float)mid;
+    if (rho > 0.0f) {
       double m = 0.0;
       for (int j = 0; j < k; ++j) m += di[j];
       m /= k;
-      if (sigma < 1e-3 * m) sigma = 1e-3 * m;
-    } else if (sigma < 1e-3 * mean_all) {
-      sigma = 1e-3 * mean_all;
+      if ((double)sigma < 1e-3 * m) sigma = (float)(1e-3 * m);
+    } else if ((double)sigma < 1e-3 * mean_all) {
+      sigma = (float)(1e-3 * mean_all);
     }
     int n = 0;
     for (int j = 0; j < k; ++j) {
-      if (ii[j] < 0) continue;
-      const double dd = di[j] - rho;
-      w[n] = (dd <= 0.0 || sigma == 0.0) ? 1.0 : exp(-(dd / sigma));
-      ord[n] = j;
-      ++n;
+      float v = 0.0f;
+      if (ii[j] >= 0) {
+        const double dd = di[j] - (double)rho;
+        v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)exp(-(dd / (double)sigma));
+        w[n] = v;
+        ord[n] = j;
+        ++n;
+      }
+      if (memb) memb[i * k + j] = v;
     }
     for (int a = 1; a < n; ++a)
       for (int b = a; b > 0 && ii[ord[b]] < ii[ord[b - 1]]; --b) {
         const int t = ord[b];
         ord[b] = ord[b - 1];
         ord[b - 1] = t;
-        const double tw = w[b];
+        const float tw = w[b];
         w[b] = w[b - 1];
         w[b - 1] = tw;
       }
-    double s = 0.0;
-    for (int a = 0; a < n; ++a) s += fabs(w[a]);
-    for (int c = 0; c < d; ++c) out[i * d + c] = 0.0;
+    double s = 0.0;   /* sklearn normalize(norm='l1'): double row sum, float32 store */
+    for (int a = 0; a < n; ++a) s += fabs((double)w[a]);
+    for (int c = 0; c < d; ++c) out[i * d + c] = 0.0f;
     for (int a = 0; a < n; ++a) {
-      const double wn = s > 0 ? w[a] / s : w[a];
-      for (int c = 0; c < d; ++c) out[i * d + c] += wn * emb[(int64_t)ii[ord[a]] * d + c];
+      const float wn = s != 0.0 ? (float)((double)w[a] / s) : w[a];
+      for (int c = 0; c < d; ++c) {
+        const volatile float prod = wn * emb[(int64_t)ii[ord[a]] * d + c];
+        out[i * d + c] = out[i * d + c] + prod;
+      }
     }
   }
   free(w);
   free(ord);
+}
+
+/* umap's tau_rand_int on unsigned 32-bit states; per-query streams seeded by splitmix64 of
+ * (seed, query) -- the device's stream (backend.hip umap_refine_kernel) */
+static uint32_t tau_rand(uint32_t *s) {
+  s[0] = ((s[0] & 4294967294u) << 12) ^ (((s[0] << 13) ^ s[0]) >> 19);
+  s[1] = ((s[1] & 4294967288u) << 4) ^ (((s[1] << 2) ^ s[1]) >> 25);
+  s[2] = ((s[2] & 4294967280u) << 17) ^ (((s[2] << 3) ^ s[2]) >> 11);
+  return s[0] ^ s[1] ^ s[2];
+}
+
+static uint64_t splitmix64(uint64_t *x) {
+  uint64_t z = (*x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static double uclip(double v) { return v > 4.0 ? 4.0 : (v < -4.0 ? -4.0 : v); }
+
+static double urdist(const float *x, const float *y, int d) {
+  double r = 0.0;
+  for (int c = 0; c < d; ++c) {
+    const float df = x[c] - y[c];
+    const volatile float sq = df * df;
+    r += (double)sq;
+  }
+  return r;
+}
+
+/* umap_.py transform() after init (0.4): threshold the graph at max / n_epochs,
+ * make_epochs_per_sample, optimize_layout_euclidean with the training embedding fixed */
+void oracle_umap_refine(const int32_t *idx, const float *memb, int64_t nq, int k, int n_epochs, const float *tail,
+                        int64_t ntrain, int d, double a, double b, double gamma, double alpha0, double neg_rate,
+                        uint64_t seed, float *emb) {
+  float wmax = 0.0f;
+  for (int64_t e = 0; e < nq * k; ++e)
+    if (memb[e] > wmax) wmax = memb[e];
+  const float thr = (float)((double)wmax / (double)n_epochs);
+  double *eps = (double *)malloc(sizeof(double) * (size_t)k * 3);
+  double *eons = eps + k, *eonns = eps + 2 * k;
+  int32_t *tl = (int32_t *)malloc(sizeof(int32_t) * (size_t)k);
+  for (int64_t i = 0; i < nq; ++i) {
+    int ne = 0;
+    for (int j = 0; j < k; ++j) {
+      const float w = memb[i * k + j];
+      if (idx[i * k + j] < 0 || !(w >= thr) || w == 0.0f) continue;
+      const float ratio = w / wmax;
+      const float ns = (float)n_epochs * ratio;
+      eps[ne] = ns > 0.0f ? (double)((float)n_epochs / ns) : -1.0;
+      eons[ne] = eps[ne];
+      eonns[ne] = eps[ne] / neg_rate;
+      tl[ne] = idx[i * k + j];
+      ++ne;
+    }
+    float *cur = emb + i * d;
+    uint64_t sm = seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(i + 1));
+    uint32_t st[3];
+    st[0] = (uint32_t)splitmix64(&sm) | 2u;
+    st[1] = (uint32_t)splitmix64(&sm) | 8u;
+    st[2] = (uint32_t)splitmix64(&sm) | 16u;
+    double alpha = alpha0;
+    for (int n = 0; n < n_epochs; ++n) {
+      for (int e = 0; e < ne; ++e) {
+        if (!(eons[e] <= n)) continue;
+        const float *o = tail + (int64_t)tl[e] * d;
+        const double d2 = urdist(cur, o, d);
+        double gc = 0.0;
+        if (d2 > 0.0) {
+          gc = -2.0 * a * b * pow(d2, b - 1.0);
+          gc /= a * pow(d2, b) + 1.0;
+        }
+        for (int c = 0; c < d; ++c) {
+          const double g = uclip(gc * (double)(cur[c] - o[c]));
+          cur[c] = (float)((double)cur[c] + g * alpha);
+        }
+        eons[e] += eps[e];
+        const double epns = eps[e] / neg_rate;
+        const int nneg = (int)(((double)n - eonns[e]) / epns);
+        for (int p = 0; p < nneg; ++p) {
+          const int64_t kk = (int64_t)(tau_rand(st) % (uint64_t)ntrain);
+          const float *on = tail + kk * d;
+          const double dn = urdist(cur, on, d);
+          double gn;
+          if (dn > 0.0) {
+            gn = 2.0 * gamma * b;
+            gn /= (0.001 + dn) * (a * pow(dn, b) + 1.0);
+          } else if (kk == i) {
+            continue;
+          } else {
+            gn = 0.0;
+          }
+          for (int c = 0; c < d; ++c) {
+            const double g = gn > 0.0 ? uclip(gn * (double)(cur[c] - on[c])) : 4.0;
+            cur[c] = (float)((double)cur[c] + g * alpha);
+          }
+        }
+        eonns[e] += nneg * epns;
+      }
+      alpha = alpha0 * (1.0 - (double)n / (double)n_epochs);
+    }
+  }
+  free(eps);
+  free(tl);
 }

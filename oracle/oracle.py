@@ -450,12 +450,25 @@ def knn(q, train, metric, k):
     return idx, dist
 
 
-def umap_init(idx, dist, embedding, n_neighbors, local_connectivity=0.0):
+def umap_init(idx, dist, embedding, n_neighbors, local_connectivity=0.0, want_memb=False):
     idx = _c(idx, np.int32)
     dist = _c(dist, np.float64)
-    emb = _c(embedding, np.float64)
+    emb = _c(embedding, np.float32)
     nq, k = idx.shape
-    out = np.zeros((nq, emb.shape[1]), np.float64)
+    out = np.zeros((nq, emb.shape[1]), np.float32)
+    memb = np.zeros((nq, k), np.float32)
     lib().oracle_umap_init(_p(idx), _p(dist), I64(nq), k, ctypes.c_double(n_neighbors),
-                           ctypes.c_double(local_connectivity), _p(emb), emb.shape[1], _p(out))
-    return out
+                           ctypes.c_double(local_connectivity), _p(emb), emb.shape[1], _p(memb), _p(out))
+    return (out, memb) if want_memb else out
+
+
+def umap_refine(idx, memb, init, tail, n_epochs, a, b, gamma=1.0, alpha=0.25, neg_rate=5.0, seed=0):
+    idx = _c(idx, np.int32)
+    memb = _c(memb, np.float32)
+    tail = _c(tail, np.float32)
+    emb = np.array(init, dtype=np.float32, order="C", copy=True)
+    nq, k = idx.shape
+    lib().oracle_umap_refine(_p(idx), _p(memb), I64(nq), k, int(n_epochs), _p(tail), I64(tail.shape[0]),
+                             tail.shape[1], ctypes.c_double(a), ctypes.c_double(b), ctypes.c_double(gamma),
+                             ctypes.c_double(alpha), ctypes.c_double(neg_rate), ctypes.c_uint64(seed), _p(emb))
+    return emb

@@ -118,10 +118,31 @@ def test_umap_init_vs_oracle(orc, golden, lc):
     g = golden("backend")
     idx, dist = orc.knn(g["knnviolet_q"], g["knnviolet_train"], 2, 15)
     rng = np.random.default_rng(11)
-    emb = rng.normal(size=(len(g["knnviolet_train"]), 2))
-    out = K.umap_init_transform(torch.from_numpy(idx).cuda(), dev(dist), dev(emb), 15, lc)
-    want = orc.umap_init(idx, dist, emb, 15.0, lc)
-    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=1e-12, atol=1e-12)
+    emb = rng.normal(size=(len(g["knnviolet_train"]), 2)).astype(np.float32)
+    out, memb = K.umap_init_transform(torch.from_numpy(idx).cuda(), dev(dist), torch.from_numpy(emb).cuda(), 15, lc,
+                                      want_memb=True)
+    want, wmemb = orc.umap_init(idx, dist, emb, 15.0, lc, want_memb=True)
+    # float32 memberships: the device exp and glibc's may round one ulp apart
+    np.testing.assert_allclose(memb.cpu().numpy(), wmemb, rtol=2e-7, atol=0)
+    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=1e-5, atol=1e-6)
+    assert (memb.cpu().numpy() == wmemb).mean() > 0.95
+
+
+def test_umap_refine_vs_oracle(orc, golden):
+    """the layout refinement on the same float32 inputs: same per-cell streams, same schedule;
+    float32 state with f64 gradients (pow of the device libm vs glibc may differ by an ulp, which
+    the float32 store nearly always absorbs)"""
+    g = golden("backend")
+    idx, dist = orc.knn(g["knn7b_q"], g["knn7b_train"], 1, 15)
+    rng = np.random.default_rng(12)
+    emb = (rng.normal(size=(len(g["knn7b_train"]), 2)) * 4).astype(np.float32)
+    init, memb = orc.umap_init(idx, dist, emb, 15.0, 0.0, want_memb=True)
+    for ne, seed in ((100, 0), (30, 77)):
+        want = orc.umap_refine(idx, memb, init, emb, ne, 1.577, 0.8951, 1.0, 0.25, 5.0, seed=seed)
+        got = K.umap_refine(torch.from_numpy(idx).cuda(), torch.from_numpy(memb).cuda(), torch.from_numpy(init).cuda(),
+                            torch.from_numpy(emb).cuda(), ne, 1.577, 0.8951, 1.0, 0.25, 5.0, seed=seed).cpu().numpy()
+        assert (got == want).all(axis=1).mean() > 0.9
+        np.testing.assert_allclose(got, want, rtol=0, atol=1e-3)
 
 
 def _random_svc(rng, ncls, f, kernel="rbf"):
@@ -154,13 +175,14 @@ def test_features_and_classify_chain(orc):
 
     tr = np.vstack([want[:200] + 0.0, rng.random((300, 132))])
     tr[200:, 126:] = (rng.random((300, 6)) < 0.5)
-    emb = rng.normal(size=(500, 2))
-    um = B.UmapModel(dev(tr.T), dev(emb), 15, 1.0, "channel_cosine_intensity_violet_derivative_v2")
+    emb = rng.normal(size=(500, 2)).astype(np.float32)
+    um = B.UmapModel(dev(tr.T), torch.from_numpy(emb).cuda(), 15, 1.0, "channel_cosine_intensity_violet_derivative_v2")
     svc = _random_svc(rng, 7, 2)
     bundle = B.ClassifierModel(checks, um, svc)
     cls, classes, f2 = bundle.classify(dev(avg))
     oi, od = orc.knn(want, tr, 2, 15)
-    e = orc.umap_init(oi, od, emb, 15.0, 0.0)
+    e, memb = orc.umap_init(oi, od, emb, 15.0, 0.0, want_memb=True)
+    e = orc.umap_refine(oi, memb, e, emb, 100, um.a, um.b, 1.0, 0.25, 5.0, seed=0).astype(np.float64)
     op = orc.svc_predict(e, svc.sv.cpu().numpy(), svc.coef.cpu().numpy(), svc.intercept.cpu().numpy(),
                          svc.start.cpu().numpy(), svc.kernel, svc.gamma, svc.coef0, svc.degree)
     got = cls.cpu().numpy()

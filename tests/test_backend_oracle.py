@@ -72,16 +72,48 @@ def test_umap_init_properties(orc, golden):
     g = golden("backend")
     idx, dist = orc.knn(g["knn7b_q"], g["knn7b_train"], 1, 15)
     rng = np.random.default_rng(3)
-    emb = rng.normal(size=(len(g["knn7b_train"]), 2))
-    out = orc.umap_init(idx, dist, emb, 15.0, 0.0)
+    emb = rng.normal(size=(len(g["knn7b_train"]), 2)).astype(np.float32)
+    out, memb = orc.umap_init(idx, dist, emb, 15.0, 0.0, want_memb=True)
+    assert out.dtype == np.float32 and memb.dtype == np.float32
     for i in range(len(idx)):
         pts = emb[idx[i]]
-        assert out[i].min() >= pts.min(0).min() - 1e-12
         lo, hi = pts.min(0), pts.max(0)
-        assert np.all(out[i] >= lo - 1e-12) and np.all(out[i] <= hi + 1e-12)
+        assert np.all(out[i] >= lo - 1e-5) and np.all(out[i] <= hi + 1e-5)
+        # membership decreases with distance (knn order is ascending)
+        assert np.all(np.diff(memb[i]) <= 0)
+    # smooth_knn_dist's target: the memberships after the first sum to log2(k) (within tolerance
+    # of the bisection) where no neighbour sits at rho
+    s = memb[:, 1:].sum(axis=1)
+    assert np.median(np.abs(s - np.log2(15))) < 1e-3
     # all neighbours at one distance -> the plain mean
     same = np.full_like(dist, 0.3)
-    np.testing.assert_allclose(orc.umap_init(idx, same, emb, 15.0, 0.0), emb[idx].mean(axis=1), rtol=1e-12)
+    np.testing.assert_allclose(orc.umap_init(idx, same, emb, 15.0, 0.0), emb[idx].mean(axis=1), rtol=1e-5,
+                               atol=1e-6)
+
+
+def test_umap_refine_properties(orc, golden):
+    """the refinement is deterministic per seed, moves queries toward their neighbours, and a
+    query whose neighbours all sit on one point converges onto it (parity unpinned)"""
+    g = golden("backend")
+    idx, dist = orc.knn(g["knn7b_q"], g["knn7b_train"], 1, 15)
+    rng = np.random.default_rng(4)
+    emb = (rng.normal(size=(len(g["knn7b_train"]), 2)) * 5).astype(np.float32)
+    init, memb = orc.umap_init(idx, dist, emb, 15.0, 0.0, want_memb=True)
+    a, b = 1.577, 0.8951
+    r1 = orc.umap_refine(idx, memb, init, emb, 100, a, b, 1.0, 0.25, 5.0, seed=1)
+    r1b = orc.umap_refine(idx, memb, init, emb, 100, a, b, 1.0, 0.25, 5.0, seed=1)
+    r2 = orc.umap_refine(idx, memb, init, emb, 100, a, b, 1.0, 0.25, 5.0, seed=2)
+    assert np.array_equal(r1, r1b) and not np.array_equal(r1, r2)
+    assert np.all(np.isfinite(r1))
+    # closer to the nearest neighbour's embedding than a random training point on average
+    d_nn = np.linalg.norm(r1 - emb[idx[:, 0]], axis=1)
+    d_rand = np.linalg.norm(r1 - emb[rng.integers(0, len(emb), len(r1))], axis=1)
+    assert np.median(d_nn) < np.median(d_rand)
+    # one cluster: every neighbour at the same embedding point
+    emb1 = emb.copy()
+    emb1[idx[0]] = np.float32([3.0, -2.0])
+    one = orc.umap_refine(idx[:1], memb[:1], init[:1], emb1, 100, a, b, 1.0, 0.25, 5.0, seed=3)
+    assert np.linalg.norm(one[0] - np.float32([3.0, -2.0])) < 0.5
 
 
 def test_standard_scale_fixture(golden):

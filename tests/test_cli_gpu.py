@@ -185,3 +185,82 @@ def test_ecoli_image_classification_cli(tmp_path, orc):
                                rtol=1e-15, atol=1e-15)
     seg = np.load(sample + "_seg.npy")
     assert list(ids[134].astype(int)) == sorted(set(np.unique(seg)) - {0})
+
+
+def _bundle(tmp_path, lib95, rng):
+    """A classifier bundle of the reference's shape fitted here with sklearn (synthetic training
+    spectra from 12 library barcodes; a stand-in UMAP whose embedding puts each barcode in its
+    own cluster), exported with tools/export_classifier.py"""
+    from types import SimpleNamespace
+
+    from sklearn.svm import SVC
+    sys.path.insert(0, ROOT)
+    from tools.export_classifier import export_bundle
+    from hiprfish_image_analysis_amd import backend as B
+    rows = rng.choice(len(lib95), 12, replace=False)
+    y = np.repeat(rows, 25)
+    x = lib95[y] * rng.uniform(0.8, 1.2, (len(y), 1)) + rng.normal(0, 0.02, (len(y), 95))
+    x = np.clip(x, 1e-3, None)
+    x /= x.max(axis=1, keepdims=True)
+    feats = np.zeros((len(x), 132))
+    feats[:, :95] = x
+    feats[:, 95:126] = np.diff(x[:, :32], axis=1)
+    checks = []
+    for k, (lo, hi) in enumerate(B.ECOLI_SEGMENTS):
+        seg = np.abs(feats[:, lo:hi]).max(axis=1)
+        lab = (seg > np.median(seg)).astype(np.float64)
+        checks.append(SVC(kernel="rbf", gamma=2.0, C=5.0).fit(feats[:, lo:hi], lab))
+        feats[:, 126 + k] = checks[-1].predict(feats[:, lo:hi])
+    centres = rng.normal(0, 6, (12, 2))
+    emb = (centres[np.repeat(np.arange(12), 25)] + rng.normal(0, 0.5, (len(y), 2))).astype(np.float32)
+    codes = np.array([format(r + 1, "010b") for r in y])
+    clf_umap = SVC(kernel="rbf", gamma=0.5, C=10.0).fit(emb.astype(np.float64), codes)
+    um = SimpleNamespace(_raw_data=feats, embedding_=emb, n_neighbors=15, local_connectivity=1.0,
+                         metric=SimpleNamespace(__name__="channel_cosine_intensity_violet_derivative_v2"),
+                         _a=1.577, _b=0.8951, repulsion_strength=1.0, negative_sample_rate=5, n_epochs=None,
+                         _initial_alpha=1.0)
+    path = str(tmp_path / "bundle.npz")
+    export_bundle(path, um, clf_umap, checks)
+    return path, checks, feats, emb, clf_umap
+
+
+def test_ecoli_image_classification_cli_with_bundle(tmp_path, orc):
+    """image_classification.py with an exported classifier bundle: the reference's chain
+    (:47-56) -- check-SVC flags, UMAP transform, barcode SVC -- on the device, against the
+    oracle restatement of every stage on the same spectra"""
+    import pandas as pd
+    import hiprfish_imaging_image_classification as ccli
+    import hiprfish_imaging_spectral_image_measurement as mcli
+
+    from hiprfish_image_analysis_amd import synthetic as S
+    stack, _, _, ref = S.tile(256, 256, seed=34)
+    lasers = split_lasers(stack.cpu().numpy(), S.ECOLI_BOUNDS, [(0, 0)] * 5)
+    files = []
+    for i, l in enumerate(lasers):
+        np.save(tmp_path / ("b_%d.npy" % (i + 1)), l)
+        files.append(str(tmp_path / ("b_%d.czi" % (i + 1))))
+    mcli.main(['-i'] + files + ['-c', 'F'])
+    sample = str(tmp_path / "b")
+    lib95 = ref.astype(np.float64) / ref.astype(np.float64).max(axis=1, keepdims=True)
+    path, checks, tfeats, temb, clf_umap = _bundle(tmp_path, lib95, np.random.default_rng(9))
+    codes = ccli.main([sample + "_avgint.csv", "-rf", path])
+
+    avg = np.loadtxt(sample + "_avgint.csv", delimiter=",", ndmin=2)
+    x = avg / avg.max(axis=1)[:, None]
+    f = np.zeros((len(x), 132))
+    f[:, :95] = x
+    f[:, 95:126] = np.diff(x[:, :32], axis=1)
+    from hiprfish_image_analysis_amd import backend as B
+    for k, (lo, hi) in enumerate(B.ECOLI_SEGMENTS):
+        c = checks[k]
+        f[:, 126 + k] = c.predict(f[:, lo:hi])                # sklearn itself for the flags
+    oi, od = orc.knn(f, tfeats, 2, 15)
+    e, memb = orc.umap_init(oi, od, temb, 15.0, 0.0, want_memb=True)
+    e = orc.umap_refine(oi, memb, e, temb, 100, 1.577, 0.8951, 1.0, 0.25, 5.0, seed=0)
+    want = clf_umap.predict(e.astype(np.float64))             # and for the barcode
+    assert list(codes) == list(want)
+    ids = pd.read_csv(sample + "_avgint_ids.csv", header=None, dtype=str)
+    assert ids.shape == (len(want), 135)
+    np.testing.assert_array_equal(ids.iloc[:, 126:132].values.astype(np.float64), f[:, 126:132])
+    assert list(ids[132]) == list(want)
+    assert len(set(want)) > 1
