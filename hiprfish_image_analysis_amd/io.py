@@ -13,12 +13,18 @@ import numpy as np
 
 
 def load_laser_stack(path: str) -> np.ndarray:
+    """One laser's (H, W, C) float32 acquisition, as bioformats.load_image returns it (ecoli
+    measurement.py:145): a .czi is read by czi.load_image; otherwise (or when only the array is
+    at hand) {stem}.npy holds the (H, W, C) float array."""
     stem, ext = os.path.splitext(path)
-    cand = path if ext == ".npy" else stem + ".npy"
-    if not os.path.exists(cand):
-        raise FileNotFoundError("%s: CZI decoding is not part of this build; provide %s (H, W, C) float array"
-                                % (path, cand))
-    a = np.load(cand, allow_pickle=False)
+    if ext.lower() == ".czi" and os.path.exists(path):
+        from . import czi
+        a = czi.load_image(path)
+    else:
+        cand = path if ext == ".npy" else stem + ".npy"
+        if not os.path.exists(cand):
+            raise FileNotFoundError("%s: neither the CZI file nor %s exists" % (path, cand))
+        a = np.load(cand, allow_pickle=False)
     if a.ndim == 2:
         a = a[:, :, None]
     return np.ascontiguousarray(a, dtype=np.float32)
