@@ -49,6 +49,8 @@ class SvcModel:
     gamma: float
     coef0: float
     degree: int
+    probA: torch.Tensor | None = None   # (pairs,) f64: probA_ / probB_ (probability=True)
+    probB: torch.Tensor | None = None
 
     @property
     def n_class(self):
@@ -56,7 +58,7 @@ class SvcModel:
 
     @classmethod
     def from_arrays(cls, support_vectors, dual_coef, intercept, n_support, classes, kernel="rbf", gamma=1.0,
-                    coef0=0.0, degree=3, device="cuda"):
+                    coef0=0.0, degree=3, device="cuda", probA=None, probB=None):
         """sklearn's public attributes (support_vectors_, dual_coef_, intercept_, n_support_,
         classes_, kernel, _gamma, coef0, degree).  sklearn flips the sign of dual_coef_ and
         intercept_ for two classes; libsvm's own signs are restored here."""
@@ -73,8 +75,10 @@ class SvcModel:
             cv = np.arange(len(classes), dtype=np.float64)
         k = KERNELS[kernel] if isinstance(kernel, str) else int(kernel)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        pa = None if probA is None else t(np.asarray(probA, np.float64).ravel())
+        pb = None if probB is None else t(np.asarray(probB, np.float64).ravel())
         return cls(t(np.asarray(support_vectors, np.float64)), t(dual), t(inter), t(start), t(cv), classes, k,
-                   float(gamma), float(coef0), int(degree))
+                   float(gamma), float(coef0), int(degree), pa, pb)
 
     @classmethod
     def from_npz(cls, z, prefix, device="cuda"):
@@ -86,10 +90,13 @@ class SvcModel:
         sv = g("support_vectors")
         return cls.from_arrays(g("sv") if sv is None else sv, g("dual_coef"), g("intercept"), g("n_support"), g("classes"),
                                kernel if isinstance(kernel, str) else int(kernel), float(g("gamma", 1.0)),
-                               float(g("coef0", 0.0)), int(g("degree", 3)), device)
+                               float(g("coef0", 0.0)), int(g("degree", 3)), device, g("probA"), g("probB"))
 
     def predict(self, x, out_column=None):
         return K.svc_predict(x, self, out_column)
+
+    def predict_proba(self, x):
+        return K.svc_predict_proba(x, self)
 
 
 @dataclass

@@ -141,6 +141,114 @@ __global__ __launch_bounds__(SVC_T) void svc_predict_kernel(const double *__rest
   }
 }
 
+// ---- f2: SVC.predict_proba (libsvm svm_predict_probability) ---------------------------------------
+// biofilm_analysis.py:1229 clf_umap.predict_proba: pairwise Platt sigmoids of the one-vs-one
+// decision values (sigmoid_predict, clamped to [1e-7, 1 - 1e-7]) coupled by libsvm's
+// multiclass_probability (Wu, Lin & Weng's second method: fixed-point iteration on Q p with
+// the in-loop renormalisation, max(100, k) iterations, stop at max |Qp_t - pQp| < 0.005 / k).
+// One wavefront per cell: the support-vector kernel values and the k x k pairwise matrix r in
+// LDS; p and Qp live in registers, two classes per lane (k <= 128), and the sequential sweep
+// over t broadcasts Qp[t] / Q[t][t] from the owning lane, so the sweep needs no barrier.  Every
+// sum runs in libsvm's order.
+constexpr int PROB_T = 64;
+constexpr int PROB_KMAX = 128;
+constexpr int PROB_SLOTS = PROB_KMAX / PROB_T;
+
+__device__ __forceinline__ double platt(double dec, double A, double B) {
+  const double fApB = dec * A + B;
+  return fApB >= 0 ? exp(-fApB) / (1.0 + exp(-fApB)) : 1.0 / (1 + exp(fApB));
+}
+
+__global__ __launch_bounds__(PROB_T) void svc_proba_kernel(const double *__restrict__ x, int64_t ldx, SvcModel m,
+                                                           const double *__restrict__ probA,
+                                                           const double *__restrict__ probB,
+                                                           double *__restrict__ prob) {
+  extern __shared__ double sh[];
+  const int k = m.n_class;
+  double *kv = sh;
+  double *r = kv + m.nsv;          // r[i * k + j]
+  double *pl = r + k * k;          // p broadcast copy for the Qp products
+  const int lane = threadIdx.x;
+  const int64_t i = blockIdx.x;
+  const double *xi = x + i * ldx;
+  for (int s = lane; s < m.nsv; s += PROB_T) kv[s] = svc_kernel(xi, m.sv + (int64_t)s * m.f, m);
+  __syncthreads();
+  const int npair = k * (k - 1) / 2;
+  for (int q = lane; q < npair; q += PROB_T) {
+    auto P = [&](int64_t a) { return a * k - a * (a + 1) / 2; };
+    const double nn = 2.0 * k - 1.0;
+    int a = (int)floor((nn - sqrt(nn * nn - 8.0 * (double)q)) / 2.0);
+    if (a < 0) a = 0;
+    while (a > 0 && P(a) > q) --a;
+    while (a + 1 < k && P(a + 1) <= q) ++a;
+    const int b = a + 1 + (int)(q - P(a));
+    const double *c1 = m.coef + (int64_t)(b - 1) * m.nsv, *c2 = m.coef + (int64_t)a * m.nsv;
+    double sum = 0.0;
+    for (int t = m.start[a]; t < m.start[a + 1]; ++t) sum += c1[t] * kv[t];
+    for (int t = m.start[b]; t < m.start[b + 1]; ++t) sum += c2[t] * kv[t];
+    sum += m.intercept[q];
+    const double rr = fmin(fmax(platt(sum, probA[q], probB[q]), 1e-7), 1 - 1e-7);
+    r[a * k + b] = rr;
+    r[b * k + a] = 1 - rr;
+  }
+  __syncthreads();
+  double *out = prob + i * k;   // two classes are coupled too (sklearn's libsvm has no k == 2 shortcut)
+  double p[PROB_SLOTS], Qp[PROB_SLOTS], Qtt[PROB_SLOTS];
+#pragma unroll
+  for (int s = 0; s < PROB_SLOTS; ++s) {
+    const int t = lane + s * PROB_T;
+    p[s] = 1.0 / k;
+    double q = 0.0;
+    if (t < k) {
+      for (int j = 0; j < t; ++j) q += r[j * k + t] * r[j * k + t];
+      for (int j = t + 1; j < k; ++j) q += r[j * k + t] * r[j * k + t];
+    }
+    Qtt[s] = q;
+    Qp[s] = 0.0;
+  }
+  const int max_iter = k > 100 ? k : 100;
+  const double eps = 0.005 / k;
+  for (int iter = 0; iter < max_iter; ++iter) {
+#pragma unroll
+    for (int s = 0; s < PROB_SLOTS; ++s)
+      if (lane + s * PROB_T < k) pl[lane + s * PROB_T] = p[s];
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < PROB_SLOTS; ++s) {
+      const int t = lane + s * PROB_T;
+      double acc = 0.0;
+      if (t < k)
+        for (int j = 0; j < k; ++j) acc += (j == t ? Qtt[s] : -r[j * k + t] * r[t * k + j]) * pl[j];
+      Qp[s] = acc;
+    }
+    __syncthreads();
+    double pQp = 0.0, maxe = 0.0;
+    for (int t = 0; t < k; ++t) pQp += pl[t] * __shfl(Qp[t / PROB_T], t % PROB_T, PROB_T);
+    for (int t = 0; t < k; ++t) {
+      const double e = fabs(__shfl(Qp[t / PROB_T], t % PROB_T, PROB_T) - pQp);
+      if (e > maxe) maxe = e;
+    }
+    if (maxe < eps) break;
+    for (int t = 0; t < k; ++t) {
+      const double qpt = __shfl(Qp[t / PROB_T], t % PROB_T, PROB_T);
+      const double qtt = __shfl(Qtt[t / PROB_T], t % PROB_T, PROB_T);
+      const double diff = (-qpt + pQp) / qtt;
+      pQp = (pQp + diff * (diff * qtt + 2 * qpt)) / (1 + diff) / (1 + diff);
+#pragma unroll
+      for (int s = 0; s < PROB_SLOTS; ++s) {
+        const int j = lane + s * PROB_T;
+        if (j >= k) continue;
+        const double qtj = j == t ? qtt : -r[j * k + t] * r[t * k + j];
+        Qp[s] = (Qp[s] + diff * qtj) / (1 + diff);
+        p[s] = (j == t ? p[s] + diff : p[s]) / (1 + diff);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < PROB_SLOTS; ++s)
+    if (lane + s * PROB_T < k) out[lane + s * PROB_T] = p[s];
+}
+
 // ---- f2: kNN under the reference metrics ---------------------------------------------------------
 // metric 0: euclidean; 1: channel_cosine_intensity_7b_v2 (67 columns); 2: the scalar of
 // channel_cosine_intensity_violet_derivative_v2 (132 columns: (d + c1 + ... + c5) / 6 -- the
@@ -519,6 +627,24 @@ hrf_status hrf_svc_predict(const double *x, int64_t n, int64_t ldx, int32_t f, c
   hipFuncSetAttribute((const void *)svc_predict_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   svc_predict_kernel<<<(unsigned)n, SVC_T, shm, (hipStream_t)stream>>>(x, ldx, m, pred, dec, val_out, val_stride,
                                                                        class_values);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_svc_predict_proba(const double *x, int64_t n, int64_t ldx, int32_t f, const double *sv, int32_t nsv,
+                                 const double *coef, const double *intercept, const int32_t *start, int32_t n_class,
+                                 int32_t kernel, double gamma, double coef0, int32_t degree, const double *probA,
+                                 const double *probB, double *prob, hrf_stream_t stream) {
+  HRF_REQUIRE(f >= 1 && ldx >= f && nsv >= 1 && n_class >= 2 && n_class <= PROB_KMAX && kernel >= 0 && kernel <= 3,
+              "svc_predict_proba: bad model shape (2..%d classes)", PROB_KMAX);
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(x && sv && coef && intercept && start && probA && probB && prob, "svc_predict_proba: null buffer");
+  const size_t shm = sizeof(double) * ((size_t)nsv + (size_t)n_class * n_class + n_class);
+  HRF_REQUIRE(shm <= 160 * 1024, "svc_predict_proba: %d support vectors and %d classes exceed the LDS budget", nsv,
+              n_class);
+  SvcModel m{sv, coef, intercept, start, nsv, f, n_class, kernel, degree, gamma, coef0};
+  hipFuncSetAttribute((const void *)svc_proba_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  svc_proba_kernel<<<(unsigned)n, PROB_T, shm, (hipStream_t)stream>>>(x, ldx, m, probA, probB, prob);
   HRF_LAUNCHED();
   return HRF_OK;
 }

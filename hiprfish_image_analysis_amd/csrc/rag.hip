@@ -47,6 +47,50 @@ __global__ void rag_count_kernel(const uint8_t *__restrict__ edge, int64_t L, co
   }
 }
 
+// raw and "cell"-filtered counts in one pass (biofilm :1290-1291: the filtered matrix counts an
+// edge only when both endpoint rows are typed 'cell')
+__global__ void rag_count2_kernel(const uint8_t *__restrict__ edge, int64_t L, const int32_t *__restrict__ bc,
+                                  const uint8_t *__restrict__ keep, int32_t R, unsigned long long *__restrict__ adj,
+                                  unsigned long long *__restrict__ adjf) {
+  const int64_t n = L * L;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    if (!edge[e]) continue;
+    const int64_t a = e / L, b = e - a * L;
+    if (a < 1 || b <= a) continue;
+    const int32_t ba = bc[a], bb = bc[b];
+    if (ba < 0 || ba >= R || bb < 0 || bb >= R) continue;
+    atomicAdd(&adj[(int64_t)ba * R + bb], 1ull);
+    atomicAdd(&adj[(int64_t)bb * R + ba], 1ull);
+    if (keep[a] && keep[b]) {
+      atomicAdd(&adjf[(int64_t)ba * R + bb], 1ull);
+      atomicAdd(&adjf[(int64_t)bb * R + ba], 1ull);
+    }
+  }
+}
+
+// labels with any pixel inside the mask (biofilm :1259-1262: debris = segmentation *
+// image_epithelial_area; debris_labels = its non-zero values)
+__global__ void label_overlap_kernel(const int32_t *__restrict__ lab, const uint8_t *__restrict__ mask, int64_t n,
+                                     int32_t maxlab, uint8_t *__restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t v = lab[p];
+    if (v > 0 && v <= maxlab && mask[p]) out[v] = 1;
+  }
+}
+
+// biofilm :1263-1269: a row is debris when area > area_max, its label overlaps the epithelial
+// area, or max_probability <= prob_min (a NaN probability compares false: stays a cell)
+__global__ void cell_typing_kernel(const int32_t *__restrict__ label, const double *__restrict__ area,
+                                   const double *__restrict__ maxprob, const uint8_t *__restrict__ overlap,
+                                   int32_t maxlab, int64_t n, double area_max, double prob_min,
+                                   uint8_t *__restrict__ is_cell) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t l = label[i];
+  const bool over = overlap && l > 0 && l <= maxlab && overlap[l];
+  is_cell[i] = !((area[i] > area_max) || over || (maxprob && maxprob[i] <= prob_min));
+}
+
 }  // namespace
 
 extern "C" {
@@ -71,6 +115,45 @@ hrf_status hrf_barcode_adjacency(const uint8_t *edge, int32_t maxlab, const int3
   const int64_t L = (int64_t)maxlab + 1;
   HRF_HIP(hipMemsetAsync(adj, 0, sizeof(int64_t) * (size_t)R * R, s));
   rag_count_kernel<<<hrf::stream_grid(L * L), 256, 0, s>>>(edge, L, bc_of_label, R, (unsigned long long *)adj);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_barcode_adjacency_filtered(const uint8_t *edge, int32_t maxlab, const int32_t *bc_of_label,
+                                          const uint8_t *keep_of_label, int32_t R, int64_t *adj, int64_t *adj_filtered,
+                                          hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(maxlab >= 0 && R >= 1 && edge && bc_of_label && keep_of_label && adj && adj_filtered,
+              "barcode_adjacency_filtered: bad arguments");
+  const int64_t L = (int64_t)maxlab + 1;
+  HRF_HIP(hipMemsetAsync(adj, 0, sizeof(int64_t) * (size_t)R * R, s));
+  HRF_HIP(hipMemsetAsync(adj_filtered, 0, sizeof(int64_t) * (size_t)R * R, s));
+  rag_count2_kernel<<<hrf::stream_grid(L * L), 256, 0, s>>>(edge, L, bc_of_label, keep_of_label, R,
+                                                             (unsigned long long *)adj,
+                                                             (unsigned long long *)adj_filtered);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_label_overlap(const int32_t *labels, const uint8_t *mask, int64_t H, int64_t W, int32_t maxlab,
+                             uint8_t *out, hrf_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  HRF_REQUIRE(maxlab >= 0 && out, "label_overlap: bad arguments");
+  HRF_HIP(hipMemsetAsync(out, 0, (size_t)maxlab + 1, s));
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(labels && mask, "label_overlap: null buffer");
+  label_overlap_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(labels, mask, H * W, maxlab, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_cell_typing(const int32_t *label, const double *area, const double *maxprob, const uint8_t *overlap,
+                           int32_t maxlab, int64_t n, double area_max, double prob_min, uint8_t *is_cell,
+                           hrf_stream_t stream) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(label && area && is_cell, "cell_typing: null buffer");
+  cell_typing_kernel<<<(unsigned)hrf::cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(
+      label, area, maxprob, overlap, maxlab, n, area_max, prob_min, is_cell);
   HRF_LAUNCHED();
   return HRF_OK;
 }

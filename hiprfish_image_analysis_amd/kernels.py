@@ -676,6 +676,41 @@ def barcode_adjacency(edge, bc_of_label, R):
     return adj
 
 
+def barcode_adjacency_filtered(edge, bc_of_label, keep_of_label, R):
+    """-> (raw, cell-filtered) (R, R) int64 adjacency counts in one pass"""
+    maxlab = edge.shape[0] - 1
+    bc = _i32(bc_of_label, "bc_of_label")
+    keep = _u8(keep_of_label, "keep_of_label")
+    if bc.numel() < maxlab + 1 or keep.numel() < maxlab + 1:
+        raise ValueError("barcode_adjacency_filtered: per-label arrays shorter than max label + 1")
+    adj = torch.empty((R, R), dtype=torch.int64, device=edge.device)
+    adjf = torch.empty((R, R), dtype=torch.int64, device=edge.device)
+    _lib.call("hrf_barcode_adjacency_filtered", _ptr(edge.contiguous()), maxlab, _ptr(bc), _ptr(keep), R, _ptr(adj),
+              _ptr(adjf), _stream())
+    return adj, adjf
+
+
+def label_overlap(labels, mask, maxlab):
+    l = _i32(labels, "labels")
+    m = _u8(mask, "mask")
+    H, W = l.shape
+    out = torch.empty(maxlab + 1, dtype=torch.uint8, device=l.device)
+    _lib.call("hrf_label_overlap", _ptr(l), _ptr(m), H, W, maxlab, _ptr(out), _stream())
+    return out
+
+
+def cell_typing(label, area, maxprob=None, overlap=None, maxlab=0, area_max=10000.0, prob_min=0.95):
+    lab = _i32(label, "label")
+    ar = _dev(area, torch.float64, "area")
+    mp = None if maxprob is None else _dev(maxprob, torch.float64, "maxprob")
+    ov = None if overlap is None else _u8(overlap, "overlap")
+    out = torch.empty(lab.numel(), dtype=torch.uint8, device=lab.device)
+    _lib.call("hrf_cell_typing", _ptr(lab), _ptr(ar), _ptr(mp) if mp is not None else None,
+              _ptr(ov) if ov is not None else None, int(maxlab), lab.numel(), float(area_max), float(prob_min),
+              _ptr(out), _stream())
+    return out
+
+
 def shape_filter(labels, props, maxlab, minor_lo=15.0, minor_hi=35.0):
     l = _i32(labels, "labels")
     H, W = l.shape
@@ -814,6 +849,24 @@ def svc_predict(x, model, out_column=None, want_dec=False):
               int(model.degree), _ptr(pred), _ptr(dec) if dec is not None else None,
               _ptr(vo) if vo is not None else None, vs, _ptr(model.class_values), _stream())
     return (pred, dec) if want_dec else pred
+
+
+def svc_predict_proba(x, model):
+    """sklearn SVC.predict_proba with the arrays of `model` (a backend.SvcModel carrying
+    probA / probB) -> (n, n_class) f64 in class order"""
+    if model.probA is None:
+        raise ValueError("svc_predict_proba: the model has no probA_ / probB_ (fitted without probability=True)")
+    if x.dtype != torch.float64 or not x.is_cuda or x.stride(1) != 1:
+        raise ValueError("svc_predict_proba: an f64 device table with contiguous rows expected")
+    n, f = x.shape
+    if f != model.sv.shape[1]:
+        raise ValueError("svc_predict_proba: %d features, the model has %d" % (f, model.sv.shape[1]))
+    nc = model.n_class
+    prob = torch.empty((n, nc), dtype=torch.float64, device=x.device)
+    _lib.call("hrf_svc_predict_proba", _ptr(x), n, x.stride(0), f, _ptr(model.sv), model.sv.shape[0],
+              _ptr(model.coef), _ptr(model.intercept), _ptr(model.start), nc, model.kernel, float(model.gamma),
+              float(model.coef0), int(model.degree), _ptr(model.probA), _ptr(model.probB), _ptr(prob), _stream())
+    return prob
 
 
 KNN_METRICS = {"euclidean": 0, "channel_cosine_intensity_7b_v2": 1, "channel_cosine_intensity_violet_derivative_v2": 2}

@@ -317,3 +317,52 @@ def allreduce_counts(counts: torch.Tensor, group=None) -> torch.Tensor:
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
     return counts
+
+
+def allreduce_adjacency(adj: torch.Tensor, group=None) -> torch.Tensor:
+    """the optional second exchange: the int64 (R, R) barcode adjacency summed over
+    ranks, one all-reduce of R*R*8 bytes per job"""
+    return allreduce_counts(adj, group)
+
+
+# --------------------------------------------------------------------------------------------
+# Biofilm cell typing and the filtered adjacency (biofilm_analysis.py:1259-1295, row f4)
+# --------------------------------------------------------------------------------------------
+@dataclass
+class CellTyping:
+    is_cell: torch.Tensor          # (N,) u8 per cell row: 1 'cell', 0 'debris'
+    debris_labels: torch.Tensor    # (maxlab + 1,) u8: labels overlapping the epithelial area
+    adjacency: torch.Tensor        # (R, R) int64
+    adjacency_filtered: torch.Tensor
+
+
+def biofilm_typing_and_adjacency(segmentation: torch.Tensor, adjacency_seg: torch.Tensor, bc_idx: torch.Tensor,
+                                 R: int, max_probability: torch.Tensor | None = None,
+                                 epithelial_area: torch.Tensor | None = None, area_max: float = 10000.0,
+                                 prob_min: float = 0.95) -> CellTyping:
+    """cell rows = the labels of `segmentation` in ascending order (regionprops), bc_idx their
+    barcode index in the (R, R) matrices (-1: not counted).  As the reference, row i stands for
+    node i + 1 of the adjacency graph of `adjacency_seg` (:1285-1290 index cell_info by
+    node - 1), so the labels are expected to be sequential."""
+    seg = segmentation.to(torch.int32).contiguous()
+    maxlab = int(seg.max().item()) if seg.numel() else 0
+    props = K.region_props(seg, maxlab)
+    present = props[1:, 7] > 0
+    labels = (torch.nonzero(present).flatten() + 1).to(torch.int32)
+    area = props[1:, 0][present].contiguous()
+    overlap = None
+    if epithelial_area is not None:
+        overlap = K.label_overlap(seg, epithelial_area, maxlab)                       # :1259-1262
+    is_cell = K.cell_typing(labels, area, max_probability, overlap, maxlab, area_max, prob_min)   # :1263-1269
+    aseg = adjacency_seg.to(torch.int32).contiguous()
+    amax = int(aseg.max().item()) if aseg.numel() else 0
+    edge = K.rag_edges(aseg, amax)                                                    # :1277-1278
+    n = labels.numel()
+    bc = torch.full((amax + 1,), -1, dtype=torch.int32, device=seg.device)
+    keep = torch.zeros(amax + 1, dtype=torch.uint8, device=seg.device)
+    m = min(n, amax)
+    bc[1:m + 1] = bc_idx[:m].to(torch.int32)
+    keep[1:m + 1] = is_cell[:m]
+    adj, adjf = K.barcode_adjacency_filtered(edge, bc, keep, R)                       # :1283-1295
+    return CellTyping(is_cell, overlap if overlap is not None else torch.zeros(maxlab + 1, dtype=torch.uint8,
+                                                                              device=seg.device), adj, adjf)

@@ -357,6 +357,15 @@ HRF_API hrf_status hrf_svc_predict(const double *x, int64_t n, int64_t ldx, int3
                                    int32_t n_class, int32_t kernel, double gamma, double coef0, int32_t degree,
                                    int32_t *pred, double *dec, double *val_out, int64_t val_stride,
                                    const double *class_values, hrf_stream_t stream);
+/* sklearn SVC.predict_proba (probability=True; libsvm svm_predict_probability): Platt sigmoids
+ * of the pair decision values with probA / probB (sklearn probA_ / probB_, n_pairs each), then
+ * libsvm's multiclass_probability coupling.  prob (n x n_class) in class order; n_class <= 128
+ * (biofilm_analysis.py:1229) */
+HRF_API hrf_status hrf_svc_predict_proba(const double *x, int64_t n, int64_t ldx, int32_t f, const double *sv,
+                                         int32_t nsv, const double *coef, const double *intercept,
+                                         const int32_t *start, int32_t n_class, int32_t kernel, double gamma,
+                                         double coef0, int32_t degree, const double *probA, const double *probB,
+                                         double *prob, hrf_stream_t stream);
 /* exact k nearest training rows (trainT: f x nt, feature-major) under metric 0 euclidean, 1
  * channel_cosine_intensity_7b_v2 (train_reference.py:993-1072), 2 the scalar of
  * channel_cosine_intensity_violet_derivative_v2 (:569-731); ascending distance, ties to the
@@ -390,6 +399,21 @@ HRF_API hrf_status hrf_rag_edges(const int32_t *labels, int64_t H, int64_t W, in
 /* barcode x barcode adjacency counts (biofilm :1283-1292): adj[R*R] int64 */
 HRF_API hrf_status hrf_barcode_adjacency(const uint8_t *edge, int32_t maxlab, const int32_t *bc_of_label, int32_t R,
                                          int64_t *adj, hrf_stream_t stream);
+
+/* raw and cell-filtered barcode adjacency in one pass (biofilm :1283-1295): adj_filtered counts
+ * an edge only when keep_of_label[a] and keep_of_label[b] (the rows typed 'cell') */
+HRF_API hrf_status hrf_barcode_adjacency_filtered(const uint8_t *edge, int32_t maxlab, const int32_t *bc_of_label,
+                                                  const uint8_t *keep_of_label, int32_t R, int64_t *adj,
+                                                  int64_t *adj_filtered, hrf_stream_t stream);
+/* out[l] = 1 when label l has a pixel inside mask (debris labels, biofilm :1259-1262);
+ * out[maxlab+1] u8 */
+HRF_API hrf_status hrf_label_overlap(const int32_t *labels, const uint8_t *mask, int64_t H, int64_t W, int32_t maxlab,
+                                     uint8_t *out, hrf_stream_t stream);
+/* per cell row: is_cell = !(area > area_max || overlap[label] || maxprob <= prob_min)
+ * (biofilm :1263-1269; overlap / maxprob may be NULL) */
+HRF_API hrf_status hrf_cell_typing(const int32_t *label, const double *area, const double *maxprob,
+                                   const uint8_t *overlap, int32_t maxlab, int64_t n, double area_max, double prob_min,
+                                   uint8_t *is_cell, hrf_stream_t stream);
 
 #ifdef __cplusplus
 }

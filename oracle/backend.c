@@ -75,6 +75,91 @@ void oracle_svc_predict(const double *x, int64_t n, int64_t ldx, int f, const do
   free(vote);
 }
 
+/* libsvm svm_predict_probability (C_SVC with probA / probB): sigmoid_predict per pair, clamp
+ * [1e-7, 1 - 1e-7], multiclass_probability (max(100, k) iterations, eps 0.005 / k) */
+static double sigmoid_predict(double dec, double A, double B) {
+  const double fApB = dec * A + B;
+  if (fApB >= 0) return exp(-fApB) / (1.0 + exp(-fApB));
+  return 1.0 / (1 + exp(fApB));
+}
+
+static void multiclass_probability(int k, double **r, double *p, double **Q, double *Qp) {
+  int t, j, iter, max_iter = k > 100 ? k : 100;
+  double pQp, eps = 0.005 / k;
+  for (t = 0; t < k; t++) {
+    p[t] = 1.0 / k;
+    Q[t][t] = 0;
+    for (j = 0; j < t; j++) {
+      Q[t][t] += r[j][t] * r[j][t];
+      Q[t][j] = Q[j][t];
+    }
+    for (j = t + 1; j < k; j++) {
+      Q[t][t] += r[j][t] * r[j][t];
+      Q[t][j] = -r[j][t] * r[t][j];
+    }
+  }
+  for (iter = 0; iter < max_iter; iter++) {
+    pQp = 0;
+    for (t = 0; t < k; t++) {
+      Qp[t] = 0;
+      for (j = 0; j < k; j++) Qp[t] += Q[t][j] * p[j];
+      pQp += p[t] * Qp[t];
+    }
+    double max_error = 0;
+    for (t = 0; t < k; t++) {
+      const double error = fabs(Qp[t] - pQp);
+      if (error > max_error) max_error = error;
+    }
+    if (max_error < eps) break;
+    for (t = 0; t < k; t++) {
+      const double diff = (-Qp[t] + pQp) / Q[t][t];
+      p[t] += diff;
+      pQp = (pQp + diff * (diff * Q[t][t] + 2 * Qp[t])) / (1 + diff) / (1 + diff);
+      for (j = 0; j < k; j++) {
+        Qp[j] = (Qp[j] + diff * Q[t][j]) / (1 + diff);
+        p[j] /= (1 + diff);
+      }
+    }
+  }
+}
+
+void oracle_svc_proba(const double *x, int64_t n, int64_t ldx, int f, const double *sv, int nsv, const double *coef,
+                      const double *intercept, const int32_t *start, int n_class, int kernel, double gamma,
+                      double coef0, int degree, const double *probA, const double *probB, double *prob) {
+  const int k = n_class, npair = k * (k - 1) / 2;
+  double *dec = (double *)malloc(sizeof(double) * (size_t)npair);
+  int32_t *pred = (int32_t *)malloc(sizeof(int32_t));
+  double **r = (double **)malloc(sizeof(double *) * (size_t)k), **Q = (double **)malloc(sizeof(double *) * (size_t)k);
+  double *rbuf = (double *)malloc(sizeof(double) * (size_t)k * k), *qbuf = (double *)malloc(sizeof(double) * (size_t)k * k);
+  double *Qp = (double *)malloc(sizeof(double) * (size_t)k);
+  for (int a = 0; a < k; ++a) {
+    r[a] = rbuf + (size_t)a * k;
+    Q[a] = qbuf + (size_t)a * k;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    oracle_svc_predict(x + i * ldx, 1, ldx, f, sv, nsv, coef, intercept, start, n_class, kernel, gamma, coef0, degree,
+                       pred, dec);
+    int q = 0;
+    for (int a = 0; a < k; ++a)
+      for (int b = a + 1; b < k; ++b, ++q) {
+        double v = sigmoid_predict(dec[q], probA[q], probB[q]);
+        v = v < 1e-7 ? 1e-7 : v;
+        v = v > 1 - 1e-7 ? 1 - 1e-7 : v;
+        r[a][b] = v;
+        r[b][a] = 1 - v;
+      }
+    /* sklearn's libsvm couples two classes too (no k == 2 shortcut) */
+    multiclass_probability(k, r, prob + i * k, Q, Qp);
+  }
+  free(dec);
+  free(pred);
+  free(r);
+  free(Q);
+  free(rbuf);
+  free(qbuf);
+  free(Qp);
+}
+
 static double seg_cos(const double *x, const double *y, int lo, int hi) {
   double result = 0.0, nx = 0.0, ny = 0.0;
   for (int i = lo; i < hi; ++i) {

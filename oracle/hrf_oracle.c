@@ -839,6 +839,9 @@ EXPORT void oracle_barcode_adjacency(const uint8_t *edge, int32_t nlab, const in
     for (int64_t a = 1; a < L; ++a)
         for (int64_t b = a + 1; b < L; ++b)
             if (edge[a * L + b]) {
+                /* a label whose row has no barcode in the lookup (bc < 0) is not counted (the
+                 * reference's .loc would raise KeyError there) */
+                if (bc[a] < 0 || bc[a] >= R || bc[b] < 0 || bc[b] >= R) continue;
                 adj[(int64_t)bc[a] * R + bc[b]] += 1;
                 adj[(int64_t)bc[b] * R + bc[a]] += 1;
             }

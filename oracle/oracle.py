@@ -433,6 +433,21 @@ def svc_predict(x, sv, coef, intercept, start, kernel, gamma=1.0, coef0=0.0, deg
     return (pred, dec) if want_dec else pred
 
 
+def svc_proba(x, sv, coef, intercept, start, kernel, gamma, coef0, degree, probA, probB):
+    """libsvm svm_predict_probability (coef / intercept in libsvm's sign convention)"""
+    x = _c(x, np.float64)
+    n, f = x.shape
+    start = _c(start, np.int32)
+    nc = len(start) - 1
+    prob = np.zeros((n, nc), np.float64)
+    sv, coef, intercept = _c(sv, np.float64), _c(coef, np.float64), _c(intercept, np.float64)
+    pa, pb = _c(probA, np.float64), _c(probB, np.float64)
+    lib().oracle_svc_proba(_p(x), I64(n), I64(f), f, _p(sv), sv.shape[0], _p(coef), _p(intercept), _p(start), nc,
+                           int(kernel), ctypes.c_double(gamma), ctypes.c_double(coef0), int(degree), _p(pa), _p(pb),
+                           _p(prob))
+    return prob
+
+
 def knn_metric(x, y, metric):
     x = _c(x, np.float64)
     y = _c(y, np.float64)

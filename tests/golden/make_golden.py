@@ -303,6 +303,30 @@ def main_backend():
         out[name + "_q"] = qs
         out[name + "_idx"] = i.astype(np.int32)
         out[name + "_dist"] = d
+    # SVC(probability=True): predict_proba (Platt pairs + libsvm's coupling) -- drawn after the
+    # cases above so their data stay as they were
+    for name, kw, ncls, f in [("prob2", dict(kernel="rbf", gamma=0.5, C=2.0), 2, 4),
+                              ("prob6", dict(kernel="rbf", gamma=0.3, C=4.0), 6, 5),
+                              ("prob30", dict(kernel="linear", C=1.0), 30, 3)]:
+        centres = rng.normal(0, 2.0, (ncls, f))
+        y = rng.integers(0, ncls, 900)
+        x = centres[y] + rng.normal(0, 1.0, (900, f))
+        clf = SVC(probability=True, random_state=0, **kw).fit(x, y)
+        xt = centres[rng.integers(0, ncls, 200)] + rng.normal(0, 1.3, (200, f))
+        out[name + "_sv"] = clf.support_vectors_
+        out[name + "_dual_coef"] = clf.dual_coef_
+        out[name + "_intercept"] = clf.intercept_
+        out[name + "_n_support"] = clf.n_support_.astype(np.int32)
+        out[name + "_classes"] = clf.classes_.astype(np.float64)
+        out[name + "_gamma"] = np.float64(clf._gamma)
+        out[name + "_coef0"] = np.float64(clf.coef0)
+        out[name + "_degree"] = np.int32(clf.degree)
+        out[name + "_kernel"] = np.int32({"linear": 0, "poly": 1, "rbf": 2, "sigmoid": 3}[kw["kernel"]])
+        out[name + "_probA"] = clf.probA_
+        out[name + "_probB"] = clf.probB_
+        out[name + "_x"] = xt
+        out[name + "_proba"] = clf.predict_proba(xt)
+        out[name + "_pred"] = clf.predict(xt).astype(np.float64)
     np.savez_compressed(os.path.join(HERE, "backend.npz"), **out)
     print("backend.npz written")
 

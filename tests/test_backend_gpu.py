@@ -205,3 +205,61 @@ def test_features_multi_with_scaler(orc):
         p = orc.svc_predict(sc[:, lo:hi], c.sv.cpu().numpy(), c.coef.cpu().numpy(), c.intercept.cpu().numpy(),
                             c.start.cpu().numpy(), c.kernel, c.gamma, c.coef0, c.degree)
         assert np.array_equal(feats[:, 63 + k], p.astype(np.float64))
+
+
+@pytest.mark.parametrize("name", ["prob2", "prob6", "prob30"])
+def test_svc_predict_proba(golden, orc, name):
+    """biofilm :1229 predict_proba against sklearn itself (its libsvm sums kernel values with
+    BLAS ddot, so agreement is to ~1e-15, not bit for bit) and the oracle's libsvm restatement"""
+    g = golden("backend")
+    m = model(g, name)
+    x = g[name + "_x"]
+    prob = m.predict_proba(dev(x)).cpu().numpy()
+    np.testing.assert_allclose(prob, g[name + "_proba"], rtol=0, atol=1e-12)
+    op = orc.svc_proba(x, m.sv.cpu().numpy(), m.coef.cpu().numpy(), m.intercept.cpu().numpy(), m.start.cpu().numpy(),
+                       m.kernel, m.gamma, m.coef0, m.degree, m.probA.cpu().numpy(), m.probB.cpu().numpy())
+    np.testing.assert_allclose(prob, op, rtol=0, atol=1e-13)
+    np.testing.assert_allclose(prob.sum(axis=1), 1.0, atol=1e-12)
+
+
+def test_biofilm_typing_and_filtered_adjacency(orc):
+    """biofilm :1259-1295: debris typing (area, epithelial overlap, max probability) and the raw
+    and cell-filtered barcode adjacency matrices, against the restatement (rag_boundary edges
+    counted from both endpoints; filtered = the same count over 'cell' rows only)"""
+    from hiprfish_image_analysis_amd import pipeline as P
+    H = W = 256
+    rng = np.random.default_rng(6)
+    # a packed biofilm-like field: nearest-seed cells, background where no seed is near
+    pts = rng.uniform(0, 256, (150, 2))
+    yy, xx = np.mgrid[0:H, 0:W]
+    d = (yy.ravel()[:, None] - pts[:, 0]) ** 2 + (xx.ravel()[:, None] - pts[:, 1]) ** 2
+    seg = (np.argmin(d, axis=1) + 1).astype(np.int32)
+    seg[np.min(d, axis=1) > 12.0 ** 2] = 0
+    seg = seg.reshape(H, W)
+    labs = np.unique(seg)
+    labs = labs[labs > 0]
+    remap = np.zeros(seg.max() + 1, np.int32)       # sequential labels, as the reference assumes
+    remap[labs] = np.arange(1, len(labs) + 1)
+    seg = remap[seg]
+    N = len(labs)
+    bc = rng.integers(0, 31, N).astype(np.int32)
+    prob = rng.uniform(0.8, 1.0, N)
+    prob[::7] = np.nan
+    epi = np.zeros((H, W), np.uint8)
+    epi[:40, :] = 1
+    area = np.bincount(seg.ravel(), minlength=N + 1)[1:].astype(np.float64)
+    area_max = float(np.percentile(area, 90))
+    res = P.biofilm_typing_and_adjacency(torch.from_numpy(seg).cuda(), torch.from_numpy(seg).cuda(),
+                                         torch.from_numpy(bc).cuda(), 31, dev(prob), torch.from_numpy(epi).cuda(),
+                                         area_max=area_max)
+    debris_labels = set(np.unique(seg * epi)) - {0}
+    want_cell = np.array([not (area[i] > area_max or (i + 1) in debris_labels or prob[i] <= 0.95)
+                          for i in range(N)])
+    assert np.array_equal(res.is_cell.cpu().numpy().astype(bool), want_cell)
+    assert 0 < want_cell.sum() < N
+    e = orc.rag_edges(seg, N)
+    bcl = np.concatenate([[-1], bc]).astype(np.int32)
+    assert np.array_equal(res.adjacency.cpu().numpy(), orc.barcode_adjacency(e, bcl, 31))
+    bcf = np.where(np.concatenate([[False], want_cell]), bcl, -1).astype(np.int32)
+    assert np.array_equal(res.adjacency_filtered.cpu().numpy(), orc.barcode_adjacency(e, bcf, 31))
+    assert res.adjacency_filtered.sum() < res.adjacency.sum()

@@ -120,3 +120,14 @@ def test_standard_scale_fixture(golden):
     g = golden("backend")
     np.testing.assert_allclose((g["scaler_x"] - g["scaler_mean"]) / g["scaler_scale"], g["scaler_out"], rtol=0,
                                atol=1e-15)
+
+
+@pytest.mark.parametrize("name", ["prob2", "prob6", "prob30"])
+def test_svc_proba_matches_sklearn(orc, golden, name):
+    """libsvm's svm_predict_probability restated (two classes coupled as sklearn's libsvm does);
+    sklearn sums its kernel values with BLAS ddot, hence ~1e-15 rather than bit equality"""
+    g = golden("backend")
+    sv, coef, inter, start = libsvm_arrays(g, name)
+    prob = orc.svc_proba(g[name + "_x"], sv, coef, inter, start, int(g[name + "_kernel"]), float(g[name + "_gamma"]),
+                         float(g[name + "_coef0"]), int(g[name + "_degree"]), g[name + "_probA"], g[name + "_probB"])
+    np.testing.assert_allclose(prob, g[name + "_proba"], rtol=0, atol=1e-13)

@@ -1,5 +1,6 @@
 """Multi-rank logic on CPU (gloo, world size 2): tile sharding and the per-barcode count
-all-reduce produce the same global counts as one process over all tiles."""
+all-reduce (and the optional barcode-adjacency all-reduce) produce the same global counts as
+one process over all tiles."""
 import os
 import socket
 
@@ -35,8 +36,17 @@ def _worker(rank, world, port, ntiles, R, out):
         local += O.barcode_counts(_tile_barcodes(t, R), R)
     c = torch.from_numpy(local)
     P.allreduce_counts(c)
-    out[rank] = c.numpy().copy()
+    # the optional adjacency exchange: each tile's (R', R') int64 matrix summed over ranks
+    adj = torch.from_numpy(sum((_tile_adjacency(t) for t in P.shard(ntiles, rank, world)), np.zeros((31, 31), np.int64)))
+    P.allreduce_adjacency(adj)
+    out[rank] = (c.numpy().copy(), adj.numpy().copy())
     dist.destroy_process_group()
+
+
+def _tile_adjacency(t):
+    rng = np.random.default_rng(2000 + t)
+    a = rng.integers(0, 5, (31, 31)).astype(np.int64)
+    return a + a.T
 
 
 def test_sharded_counts_allreduce_gloo():
@@ -55,8 +65,10 @@ def test_sharded_counts_allreduce_gloo():
         assert p.exitcode == 0
     import oracle as O
     ref = sum(O.barcode_counts(_tile_barcodes(t, R), R) for t in range(ntiles))
+    ref_adj = sum(_tile_adjacency(t) for t in range(ntiles))
     for r in range(world):
-        assert np.array_equal(out[r], ref)
+        assert np.array_equal(out[r][0], ref)
+        assert np.array_equal(out[r][1], ref_adj)
 
 
 def _run(rank, world, port, ntiles, R, out, path):

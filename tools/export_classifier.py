@@ -10,7 +10,7 @@ nothing here unpickles anything, and the .npz it writes loads with allow_pickle=
     export_bundle("ecoli_classifier.npz", umap_transform, clf_umap, clf, scaler=None)
 
 Keys (INTEGRATION.md lists them): n_checks; check{k}_* and svc_* (sv, dual_coef, intercept,
-n_support, classes, kernel, gamma, coef0, degree); scaler_mean / scaler_scale; umap_raw_data,
+n_support, classes, kernel, gamma, coef0, degree; probA / probB when fitted with probability=True); scaler_mean / scaler_scale; umap_raw_data,
 umap_embedding, umap_n_neighbors, umap_local_connectivity, umap_metric, umap_a, umap_b,
 umap_repulsion_strength, umap_negative_sample_rate, umap_n_epochs (-1 = umap's default rule),
 umap_initial_alpha.
@@ -36,7 +36,9 @@ def svc_arrays(clf, prefix):
             prefix + "kernel": np.int32(KERNEL_CODES[kernel]),
             prefix + "gamma": np.float64(clf._gamma),
             prefix + "coef0": np.float64(clf.coef0),
-            prefix + "degree": np.int32(clf.degree)}
+            prefix + "degree": np.int32(clf.degree),
+            **({prefix + "probA": np.asarray(clf.probA_, np.float64), prefix + "probB": np.asarray(clf.probB_, np.float64)}
+               if getattr(clf, "probability", False) else {})}
 
 
 def umap_arrays(um):
