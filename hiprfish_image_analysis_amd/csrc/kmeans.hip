@@ -1636,9 +1636,26 @@ hrf_status check_args(int32_t k, int64_t n, int32_t max_iter, int32_t n_init, in
   return HRF_OK;
 }
 
+// the final state of this thread's last hrf_kmeans_1d_sorted call (pinned host copy)
+KmState *&last_single_state() {
+  static thread_local KmState *fin = nullptr;
+  return fin;
+}
+
 }  // namespace
 
 extern "C" {
+
+hrf_status hrf_kmeans_last_runs(int32_t *iters, int32_t *relocations, int32_t *strict, int32_t n) {
+  KmState *f = last_single_state();
+  HRF_REQUIRE(f && n >= 1 && n <= NRUN && iters, "kmeans_last_runs: no hrf_kmeans_1d_sorted call on this thread yet");
+  for (int r = 0; r < n; ++r) {
+    iters[r] = f->run[r].iters;
+    if (relocations) relocations[r] = f->run[r].reloc;
+    if (strict) strict[r] = f->run[r].strict;
+  }
+  return HRF_OK;
+}
 
 int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n) {
   size_t tb = 0;
@@ -1673,7 +1690,7 @@ hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n
   if (hrf_status r = sort_tmp_bytes(n, &tb)) return r;
   const SortWs ws = carve(work, n, tb);
   hipStream_t s = (hipStream_t)stream;
-  static thread_local KmState *fin = nullptr;
+  KmState *&fin = last_single_state();
   if (!fin) HRF_HIP(hipHostMalloc((void **)&fin, sizeof(KmState), hipHostMallocDefault));
   if (hrf_status r = km_launch_k(k, x, valid, n, max_iter, n_init, top_rule, labels, top_mask, ws, reuse_sort, s, fin))
     return r;

@@ -174,6 +174,9 @@ HRF_API hrf_status hrf_nl_means_2d(const double *img, int64_t H, int64_t W, int3
  * bytes; reuse_sort != 0: `work` already holds the sort of this very x / valid from a
  * previous call (e.g. k = 2 then k = 3 on ecoli image_cn).  Synchronises the stream once. */
 HRF_API int64_t hrf_kmeans_sorted_workspace_bytes(int64_t n);
+/* diagnostics: per-run Lloyd iterations, empty-cluster relocations and strict convergence of
+ * this thread's last hrf_kmeans_1d_sorted call (n = its n_init) */
+HRF_API hrf_status hrf_kmeans_last_runs(int32_t *iters, int32_t *relocations, int32_t *strict, int32_t n);
 HRF_API hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n, int32_t k, int32_t max_iter,
                                         int32_t n_init, int32_t top_rule, int32_t *labels, uint8_t *top_mask,
                                         double *centers_host, int32_t *iters_host, void *work, int64_t work_bytes,
