@@ -94,12 +94,13 @@ __device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, b
 __global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
                                                            const int32_t *__restrict__ box,
                                                            const uint8_t *__restrict__ cls, int32_t want,
-                                                           int32_t area_max,
-                                                           int32_t min_obj, uint8_t *__restrict__ be_out) {
+                                                           int32_t area_max, int32_t min_obj,
+                                                           const uint8_t *__restrict__ ovf,
+                                                           uint8_t *__restrict__ be_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
-  if (r1 < r0 || c1 < c0 || cls[comp] != want) return;
+  if (r1 < r0 || c1 < c0 || !(cls[comp] == want || (ovf && ovf[comp]))) return;
   const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, n = bh * bw;
   uint8_t *fl = reinterpret_cast<uint8_t *>(lds);
   int32_t *par = reinterpret_cast<int32_t *>(lds + ((n + 15) & ~15));
@@ -148,6 +149,245 @@ __global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__res
       const int r = p / bw, c = p - r * bw;
       be_out[(int64_t)(r0 + r) * W + (c0 + c)] = 1;
     }
+}
+
+// ---- run-length variant -----------------------------------------------------------------------
+// The same per-component loop on a bit-packed box (one u64 word = 64 columns of a row) with
+// connected components over horizontal RUNS instead of pixels: a run is a node, runs of
+// adjacent rows that overlap (4-connected) or touch diagonally (8-connected) are united, a
+// component's size is the sum of its run lengths.  The erosion is word-parallel bit
+// arithmetic, freezing / sieving clears whole runs with LDS word atomics.  A box of a few
+// touching cells holds a few hundred runs against thousands of pixels, so an iteration is a
+// handful of short passes.  Run arrays have a fixed LDS capacity; a component whose run count
+// exceeds it at any iteration stops without writing and is flagged for the pixel kernel.
+constexpr int RS_T = 256;
+constexpr int RS_LDS = 32768;
+constexpr int RS_MIN_CAP = 96;
+
+struct RunBox {
+  uint64_t *m, *t, *sd;
+  int *off, *part;
+  uint16_t *c0, *c1, *row;
+  int *par, *sz;
+  int cap;
+};
+
+__host__ __device__ inline int rs_bytes_fixed(int bh, int w64) {
+  return 24 * bh * w64 + 4 * (bh + 1) + 4 * RS_T + 64;
+}
+
+__device__ __forceinline__ uint64_t rs_valid(int w, int w64, int bw) {
+  return (w < w64 - 1 || (bw & 63) == 0) ? ~0ull : ((1ull << (bw & 63)) - 1);
+}
+
+// block-wide exclusive scan of off[0..bh) in place; off[bh] = total.  Returns the total.
+__device__ int rs_scan_rows(int *off, int *part, int bh) {
+  const int t = threadIdx.x;
+  const int chunk = (bh + RS_T - 1) / RS_T;
+  const int lo = t * chunk, hi = min(bh, lo + chunk);
+  int acc = 0;
+  for (int r = lo; r < hi; ++r) acc += off[r];
+  part[t] = acc;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int i = 0; i < RS_T; ++i) {
+      const int v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    off[bh] = run;
+  }
+  __syncthreads();
+  int base = part[t];
+  for (int r = lo; r < hi; ++r) {
+    const int v = off[r];
+    off[r] = base;
+    base += v;
+  }
+  __syncthreads();
+  return off[bh];
+}
+
+// runs of the current mask, row-major, ascending columns within a row.  -1: over capacity.
+__device__ int rs_extract(RunBox &B, int bh, int w64) {
+  for (int r = threadIdx.x; r < bh; r += RS_T) {
+    int cnt = 0;
+    uint64_t prev = 0;
+    for (int w = 0; w < w64; ++w) {
+      const uint64_t x = B.m[r * w64 + w];
+      cnt += __popcll(x & ~((x << 1) | prev));
+      prev = x >> 63;
+    }
+    B.off[r] = cnt;
+  }
+  __syncthreads();
+  const int total = rs_scan_rows(B.off, B.part, bh);
+  if (total > B.cap) return -1;
+  for (int r = threadIdx.x; r < bh; r += RS_T) {
+    int k = B.off[r], start = 0;
+    uint64_t prev = 0;
+    for (int w = 0; w < w64; ++w) {
+      const uint64_t x = B.m[r * w64 + w];
+      const uint64_t nxt = w + 1 < w64 ? B.m[r * w64 + w + 1] : 0ull;
+      uint64_t st = x & ~((x << 1) | prev);
+      uint64_t en = x & ~((x >> 1) | (nxt << 63));
+      prev = x >> 63;
+      while (st | en) {
+        const int bs = st ? __ffsll((long long)st) - 1 : 64;
+        const int be = en ? __ffsll((long long)en) - 1 : 64;
+        if (bs <= be) {
+          start = w * 64 + bs;
+          st &= st - 1;
+        } else {
+          B.c0[k] = (uint16_t)start;
+          B.c1[k] = (uint16_t)(w * 64 + be);
+          B.row[k] = (uint16_t)r;
+          ++k;
+          en &= en - 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return total;
+}
+
+// union of runs in adjacent rows (d = 1: 8-connected, 0: 4-connected); par[i] = root,
+// sz[root] = pixels
+__device__ void rs_components(RunBox &B, int total, int d) {
+  for (int i = threadIdx.x; i < total; i += RS_T) {
+    B.par[i] = i;
+    B.sz[i] = 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < total; i += RS_T) {
+    const int r = B.row[i];
+    if (r == 0) continue;
+    int lo = B.off[r - 1], hi = B.off[r];
+    const int a = (int)B.c0[i] - d, b = (int)B.c1[i] + d;
+    while (lo < hi) {   // first run of the previous row ending at or after a
+      const int mid = (lo + hi) >> 1;
+      if ((int)B.c1[mid] < a) lo = mid + 1;
+      else hi = mid;
+    }
+    for (int j = lo; j < B.off[r] && (int)B.c0[j] <= b; ++j) sunion(B.par, i, j);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < total; i += RS_T) B.par[i] = sfind(B.par, i);
+  __syncthreads();
+  for (int i = threadIdx.x; i < total; i += RS_T) atomicAdd(&B.sz[B.par[i]], (int)B.c1[i] - (int)B.c0[i] + 1);
+  __syncthreads();
+}
+
+__device__ void rs_clear_run(uint64_t *m, uint64_t *sd, int base, int c0, int c1) {
+  for (int w = c0 >> 6; w <= (c1 >> 6); ++w) {
+    const int lo = w == (c0 >> 6) ? (c0 & 63) : 0;
+    const int hi = w == (c1 >> 6) ? (c1 & 63) : 63;
+    const uint64_t mask = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+    atomicAnd((unsigned long long *)&m[base + w], (unsigned long long)~mask);
+    if (sd) atomicOr((unsigned long long *)&sd[base + w], (unsigned long long)mask);
+  }
+}
+
+__global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *__restrict__ labels, int64_t H,
+                                                                 int64_t W, const int32_t *__restrict__ box,
+                                                                 const uint8_t *__restrict__ cls, int32_t area_max,
+                                                                 int32_t min_obj, uint8_t *__restrict__ ovf,
+                                                                 uint8_t *__restrict__ be_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int comp = blockIdx.x + 1;
+  if (cls[comp] != 0) return;
+  const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
+  if (r1 < r0 || c1 < c0) return;
+  const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, w64 = (bw + 63) >> 6, nw = bh * w64;
+  RunBox B;
+  B.m = reinterpret_cast<uint64_t *>(lds);
+  B.t = B.m + nw;
+  B.sd = B.t + nw;
+  B.off = reinterpret_cast<int *>(B.sd + nw);
+  B.part = B.off + bh + 1;
+  char *rp = reinterpret_cast<char *>(B.part + RS_T);
+  B.cap = (RS_LDS - rs_bytes_fixed(bh, w64)) / 14;
+  B.par = reinterpret_cast<int *>(rp);
+  B.sz = B.par + B.cap;
+  B.c0 = reinterpret_cast<uint16_t *>(B.sz + B.cap);
+  B.c1 = B.c0 + B.cap;
+  B.row = B.c1 + B.cap;
+  // the component's pixels as bits, one wave per (row, word)
+  const int lane = hrf::lane_id(), wave = threadIdx.x >> 6;
+  for (int q = wave; q < nw; q += RS_T / 64) {
+    const int r = q / w64, w = q - r * w64;
+    const int c = w * 64 + lane;
+    const bool in = c < bw && labels[(int64_t)(r0 + r) * W + (c0 + c)] == comp;
+    const uint64_t word = __ballot(in);
+    if (lane == 0) {
+      B.m[q] = word;
+      B.sd[q] = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t up_border = r0 == 0 ? ~0ull : 0ull, down_border = r1 == H - 1 ? ~0ull : 0ull;
+  const uint64_t left_border = c0 == 0 ? 1ull : 0ull, right_border = c1 == W - 1 ? 1ull : 0ull;
+  for (int it = 0; it < 4 * (bh + bw) + 8; ++it) {
+    // :102-106 regions (8-connected) below area_max become seeds
+    int total = rs_extract(B, bh, w64);
+    if (total < 0) break;
+    rs_components(B, total, 1);
+    for (int i = threadIdx.x; i < total; i += RS_T)
+      if (B.sz[B.par[i]] < area_max) rs_clear_run(B.m, B.sd, B.row[i] * w64, B.c0[i], B.c1[i]);
+    __syncthreads();
+    // :107 binary_erosion (cross; border True only at the image edge)
+    for (int q = threadIdx.x; q < nw; q += RS_T) {
+      const int r = q / w64, w = q - r * w64;
+      uint64_t x = B.m[q];
+      const uint64_t up = r > 0 ? B.m[q - w64] : up_border;
+      const uint64_t dn = r + 1 < bh ? B.m[q + w64] : down_border;
+      const uint64_t lft = (x << 1) | (w > 0 ? (B.m[q - 1] >> 63) : left_border);
+      uint64_t xe = x;
+      uint64_t nb;
+      if (w + 1 < w64) {
+        nb = B.m[q + 1] & 1ull;
+      } else if (bw & 63) {
+        xe |= right_border << (bw & 63);   // the column right of the box, as a padding bit
+        nb = 0;
+      } else {
+        nb = right_border;
+      }
+      const uint64_t rgt = (xe >> 1) | (nb << 63);
+      B.t[q] = x & up & dn & lft & rgt & rs_valid(w, w64, bw);
+    }
+    __syncthreads();
+    {
+      uint64_t *tmp = B.m;
+      B.m = B.t;
+      B.t = tmp;
+    }
+    // :108 remove_small_objects(., min_obj), 4-connected
+    total = rs_extract(B, bh, w64);
+    if (total < 0) break;
+    rs_components(B, total, 0);
+    int any = 0;
+    for (int i = threadIdx.x; i < total; i += RS_T) {
+      if (B.sz[B.par[i]] < min_obj) rs_clear_run(B.m, nullptr, B.row[i] * w64, B.c0[i], B.c1[i]);
+      else any = 1;
+    }
+    if (!__syncthreads_or(any)) {
+      // done: write the seeds
+      for (int q = threadIdx.x; q < nw; q += RS_T) {
+        uint64_t x = B.sd[q];
+        const int r = q / w64, w = q - r * w64;
+        while (x) {
+          const int b = __ffsll((long long)x) - 1;
+          x &= x - 1;
+          be_out[(int64_t)(r0 + r) * W + (c0 + w * 64 + b)] = 1;
+        }
+      }
+      return;
+    }
+  }
+  // over capacity (or the iteration cap): the pixel kernel redoes this component
+  if (threadIdx.x == 0) ovf[comp] = 1;
 }
 
 // crop (with padding) of the oversized components' pixels
@@ -260,15 +500,22 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
                                       hipStream_t s) {
   HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
   if (ncomp == 0) return HRF_OK;
-  std::vector<uint8_t> big((size_t)ncomp + 1, 0);  // 0: LDS 72 KB, 1: LDS 160 KB, 2: whole-image loop
+  // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
+  // Components the run kernel cannot hold (run arrays over capacity) are flagged in ovf and
+  // redone by the pixel kernel, so every box it may receive fits SEED_LDS_PX_MAX.
+  std::vector<uint8_t> big((size_t)ncomp + 1, 0);
   int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
-  int nmid = 0;
+  int npix = 0;
   for (int c = 1; c <= ncomp; ++c) {
     const int64_t bh = hb[c * 4 + 2] - hb[c * 4 + 0] + 1, bw = hb[c * 4 + 3] - hb[c * 4 + 1] + 1;
-    if (bh <= 0 || bw <= 0 || bh * bw <= SEED_LDS_PX) continue;
+    if (bh <= 0 || bw <= 0) continue;
     if (bh * bw <= SEED_LDS_PX_MAX) {
-      big[c] = 1;
-      ++nmid;
+      const bool runs_fit = bw <= 65535 && bh <= 65535 &&
+                            rs_bytes_fixed((int)bh, (int)((bw + 63) >> 6)) + 14 * RS_MIN_CAP <= RS_LDS;
+      if (!runs_fit) {
+        big[c] = 1;
+        ++npix;
+      }
       continue;
     }
     big[c] = 2;
@@ -277,15 +524,19 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     br1 = std::max<int64_t>(br1, hb[c * 4 + 2]);
     bc1 = std::max<int64_t>(bc1, hb[c * 4 + 3]);
   }
+  (void)npix;
   uint8_t *dbig = nullptr;
-  HRF_HIP(hipMallocAsync((void **)&dbig, big.size(), s));
-  HRF_HIP(hipMemcpyAsync(dbig, big.data(), big.size(), hipMemcpyHostToDevice, s));
-  const size_t shm = ((SEED_LDS_PX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX;
+  const size_t nb = big.size();
+  HRF_HIP(hipMallocAsync((void **)&dbig, 2 * nb, s));
+  uint8_t *dovf = dbig + nb;
+  HRF_HIP(hipMemcpyAsync(dbig, big.data(), nb, hipMemcpyHostToDevice, s));
+  HRF_HIP(hipMemsetAsync(dovf, 0, nb, s));
   const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
   hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_max);
-  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm, s>>>(labels, H, W, box, dbig, 0, area_max, min_obj, be_out);
-  if (nmid)
-    erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, dbig, 1, area_max, min_obj, be_out);
+  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, dbig, area_max, min_obj, dovf,
+                                                                 be_out);
+  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, dbig, 1, area_max, min_obj, dovf,
+                                                            be_out);
   HRF_LAUNCHED();
   hrf_status st = HRF_OK;
   if (br1 >= 0) {

@@ -460,7 +460,16 @@ def test_erosion_seeds_vs_oracle(K, orc, S, seed):
     m[0:3, 10:200] = True                 # touches the image border
     m[250:395, 250:415] = True            # box > 18176 px -> whole-image loop on the crop
     m[300:400, 0:200] = True              # a second one, on the image border
-    m[60:150, 300:410] = True             # 8192 < box <= 18176 -> 160 KB LDS launch
+    m[60:150, 300:410] = True             # 8192 < box <= 18176 -> run-length kernel (bits + runs)
+    # a comb: every other column of a 110 x 120 box plus its top row -- one 8-connected
+    # component with ~6600 runs, past the run kernel's capacity -> flagged, pixel kernel
+    m[160:270, 10:130] = False
+    m[160, 10:130] = True
+    m[161:270, 10:130:2] = True
+    # a tall thin box: one word per row, 390 rows
+    m[5:395, 180:183] = True
+    m[5:395, 178] = False
+    m[5:395, 184] = False
     ref = OP.erosion_seeds(m)
     got = host(K.erosion_seeds(dev(m))).astype(bool)
     assert np.array_equal(got, ref)
