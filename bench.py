@@ -222,9 +222,10 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
         if mode is not None:
             lib = P.Library(lib_main.spectra, lib_main.bounds, NBIT)
             lib._refx = K.classify_prepare(lib.spectra.to(torch.float32), lib.bounds, mode=mode)
-        sec = _timed_tiles(lambda t, lib=lib, pp=pp: P.process_tile(P.register_stack(t[0]), lib, calibration=t[1],
-                                                                     per_pixel=pp),
-                           tiles, T, streams, pool, steps, 2)
+        def job(t, lib=lib, pp=pp):
+            stack, cn = P.register_stack(t[0], want_cn=True)
+            return P.process_tile(stack, lib, calibration=t[1], per_pixel=pp, image_cn=cn)
+        sec = _timed_tiles(job, tiles, T, streams, pool, steps, 2)
         cfg3[name] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
                       "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
                       "classifier_mode": mode if pp else None}
@@ -341,8 +342,9 @@ def main():
 
     def tile_job(j, tile, timed):
         with torch.cuda.stream(streams[j]):
-            stack = P.register_stack(tile[0])                   # ecoli :45-70 (shifts stay on the device)
+            stack, cn = P.register_stack(tile[0], want_cn=True)  # ecoli :45-72 (shifts stay on the device)
             return P.process_tile(stack, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
+                                  image_cn=cn,
                                   pixel_events=ev if timed else None)
 
     def worker(j, first, nsteps, timed):

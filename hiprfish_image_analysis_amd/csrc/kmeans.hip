@@ -1533,6 +1533,14 @@ SortWs carve(void *work, int64_t n, size_t tmp_bytes) {
   return ws;
 }
 
+__global__ void km_state_init_kernel(KmState *st) {
+  static_assert(sizeof(KmState) % 8 == 0, "KmState is cleared in 8-byte words");
+  unsigned long long *w = reinterpret_cast<unsigned long long *>(st);
+  for (int i = threadIdx.x; i < (int)(sizeof(KmState) / 8); i += blockDim.x) w[i] = 0ull;
+  __syncthreads();
+  if (threadIdx.x == 0) st->lo_bits = ~0ull;
+}
+
 hrf_status scan_u32(unsigned *a, int64_t n, unsigned *bsum, hipStream_t s) {
   const int nb = (int)((n + KSC_B - 1) / KSC_B);
   km_scan_sum_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
@@ -1550,9 +1558,9 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   KmState *st = ws.st;
   const unsigned g = hrf::stream_grid(n);
   if (!reuse) {
-    KmState init{};
-    init.lo_bits = ~0ull;
-    HRF_HIP(hipMemcpyAsync(st, &init, sizeof(KmState), hipMemcpyHostToDevice, s));
+    // initial state written by a kernel: an asynchronous copy from a host stack object may run
+    // after this frame is gone
+    km_state_init_kernel<<<1, 256, 0, s>>>(st);
     if (n > 0) km_minmax_kernel<<<std::min<unsigned>(g, 512), 256, 0, s>>>(x, valid, n, st);
     km_scale_kernel<<<1, 1, 0, s>>>(st);
     HRF_LAUNCHED();

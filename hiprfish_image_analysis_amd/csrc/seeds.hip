@@ -14,6 +14,7 @@
 // background row/column wherever the crop edge is not the image edge (so the erosion's
 // border_value=True applies only at the true image border).
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -25,6 +26,36 @@ namespace {
 // (a clump of a few touching cells) run in a second launch using the whole 160 KB
 constexpr int SEED_LDS_PX = 8192;
 constexpr int SEED_LDS_PX_MAX = 18176;
+
+constexpr int RS_T = 256;
+constexpr int RS_LDS = 32768;
+constexpr int RS_MIN_CAP = 96;
+
+struct RunBox {
+  uint64_t *m, *t, *sd;
+  int *off, *part;
+  uint16_t *c0, *c1, *row;
+  int *par, *sz;
+  int cap;
+};
+
+__host__ __device__ inline int rs_bytes_fixed(int bh, int w64) {
+  return 24 * bh * w64 + 4 * (bh + 1) + 4 * RS_T + 64;
+}
+
+// 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop on a
+// crop; -1: no pixels.  Evaluated on the host (dispatch) and in the kernels from the same
+// boxes, so no class table travels host -> device.
+__host__ __device__ inline int seed_class(const int32_t *box, int comp, int use_runs) {
+  const int64_t bh = (int64_t)box[comp * 4 + 2] - box[comp * 4 + 0] + 1;
+  const int64_t bw = (int64_t)box[comp * 4 + 3] - box[comp * 4 + 1] + 1;
+  if (bh <= 0 || bw <= 0) return -1;
+  if (bh * bw > SEED_LDS_PX_MAX) return 2;
+  const bool runs_fit = use_runs && bw <= 65535 && bh <= 65535 &&
+                        rs_bytes_fixed((int)bh, (int)((bw + 63) >> 6)) + 14 * RS_MIN_CAP <= RS_LDS;
+  return runs_fit ? 0 : 1;
+}
+
 
 // find with path halving: a box is up to 18K px and the raster-order unions would otherwise
 // build parent chains as long as a row run (quadratic finds).  A halving store only ever
@@ -40,6 +71,20 @@ __device__ __forceinline__ int sfind(int32_t *par, int x) {
     v[x] = z;
     x = z;
   }
+}
+
+// read-only find for the flatten pass.  A flatten store (par[x] = root) racing with a
+// path-halving store from another thread's find (par[x] = a stale grandparent) could leave x
+// pointing at a non-root and its size counted there; with no halving during the flatten, every
+// store is a root and concurrent walks still end at it.
+__device__ __forceinline__ int sfind_ro(const int32_t *par, int x) {
+  const volatile int32_t *v = par;
+  int y = v[x];
+  while (y != x) {
+    x = y;
+    y = v[x];
+  }
+  return x;
 }
 
 __device__ __forceinline__ void sunion(int32_t *par, int a, int b) {
@@ -80,7 +125,7 @@ __device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, b
   }
   __syncthreads();
   for (int p = threadIdx.x; p < n; p += blockDim.x)
-    if (fl[p] & 1) par[p] = sfind(par, p);
+    if (fl[p] & 1) par[p] = sfind_ro(par, p);
   __syncthreads();
   const int n_up = (n + 63) & ~63;  // whole waves: one LDS atomic per distinct root per wave
   for (int p = threadIdx.x; p < n_up; p += blockDim.x) {
@@ -93,14 +138,14 @@ __device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, b
 // flags: bit0 = in play (dist_lab != 0), bit1 = seed (dist_be), bit2 = erosion result
 __global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
                                                            const int32_t *__restrict__ box,
-                                                           const uint8_t *__restrict__ cls, int32_t want,
+                                                           int32_t use_runs, int32_t want,
                                                            int32_t area_max, int32_t min_obj,
                                                            const uint8_t *__restrict__ ovf,
                                                            uint8_t *__restrict__ be_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
-  if (r1 < r0 || c1 < c0 || !(cls[comp] == want || (ovf && ovf[comp]))) return;
+  if (r1 < r0 || c1 < c0 || !(seed_class(box, comp, use_runs) == want || (ovf && ovf[comp]))) return;
   const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, n = bh * bw;
   uint8_t *fl = reinterpret_cast<uint8_t *>(lds);
   int32_t *par = reinterpret_cast<int32_t *>(lds + ((n + 15) & ~15));
@@ -160,22 +205,6 @@ __global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__res
 // touching cells holds a few hundred runs against thousands of pixels, so an iteration is a
 // handful of short passes.  Run arrays have a fixed LDS capacity; a component whose run count
 // exceeds it at any iteration stops without writing and is flagged for the pixel kernel.
-constexpr int RS_T = 256;
-constexpr int RS_LDS = 32768;
-constexpr int RS_MIN_CAP = 96;
-
-struct RunBox {
-  uint64_t *m, *t, *sd;
-  int *off, *part;
-  uint16_t *c0, *c1, *row;
-  int *par, *sz;
-  int cap;
-};
-
-__host__ __device__ inline int rs_bytes_fixed(int bh, int w64) {
-  return 24 * bh * w64 + 4 * (bh + 1) + 4 * RS_T + 64;
-}
-
 __device__ __forceinline__ uint64_t rs_valid(int w, int w64, int bw) {
   return (w < w64 - 1 || (bw & 63) == 0) ? ~0ull : ((1ull << (bw & 63)) - 1);
 }
@@ -274,7 +303,7 @@ __device__ void rs_components(RunBox &B, int total, int d) {
     for (int j = lo; j < B.off[r] && (int)B.c0[j] <= b; ++j) sunion(B.par, i, j);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < total; i += RS_T) B.par[i] = sfind(B.par, i);
+  for (int i = threadIdx.x; i < total; i += RS_T) B.par[i] = sfind_ro(B.par, i);
   __syncthreads();
   for (int i = threadIdx.x; i < total; i += RS_T) atomicAdd(&B.sz[B.par[i]], (int)B.c1[i] - (int)B.c0[i] + 1);
   __syncthreads();
@@ -292,12 +321,12 @@ __device__ void rs_clear_run(uint64_t *m, uint64_t *sd, int base, int c0, int c1
 
 __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *__restrict__ labels, int64_t H,
                                                                  int64_t W, const int32_t *__restrict__ box,
-                                                                 const uint8_t *__restrict__ cls, int32_t area_max,
+                                                                 int32_t use_runs, int32_t area_max,
                                                                  int32_t min_obj, uint8_t *__restrict__ ovf,
                                                                  uint8_t *__restrict__ be_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
-  if (cls[comp] != 0) return;
+  if (seed_class(box, comp, use_runs) != 0) return;
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
   if (r1 < r0 || c1 < c0) return;
   const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, w64 = (bw + 63) >> 6, nw = bh * w64;
@@ -391,15 +420,15 @@ __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *
 }
 
 // crop (with padding) of the oversized components' pixels
-__global__ void big_crop_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W, const uint8_t *__restrict__ big,
-                                int64_t r0, int64_t c0, int64_t h, int64_t w, uint8_t *__restrict__ m) {
+__global__ void big_crop_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W, const int32_t *__restrict__ box,
+                                int32_t ncomp, int64_t r0, int64_t c0, int64_t h, int64_t w, uint8_t *__restrict__ m) {
   const int64_t n = h * w;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = r0 + i / w, c = c0 + i % w;
     uint8_t v = 0;
     if (r >= 0 && r < H && c >= 0 && c < W) {
       const int32_t l = labels[r * W + c];
-      v = l > 0 && big[l] == 2;
+      v = l > 0 && l <= ncomp && seed_class(box, l, 1) == 2;
     }
     m[i] = v;
   }
@@ -503,39 +532,30 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
   // Components the run kernel cannot hold (run arrays over capacity) are flagged in ovf and
   // redone by the pixel kernel, so every box it may receive fits SEED_LDS_PX_MAX.
-  std::vector<uint8_t> big((size_t)ncomp + 1, 0);
+  static const int use_runs = [] {
+    const char *e = getenv("HRF_SEEDS_RUNS");
+    return e ? atoi(e) : 1;
+  }();
   int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
-  int npix = 0;
   for (int c = 1; c <= ncomp; ++c) {
-    const int64_t bh = hb[c * 4 + 2] - hb[c * 4 + 0] + 1, bw = hb[c * 4 + 3] - hb[c * 4 + 1] + 1;
-    if (bh <= 0 || bw <= 0) continue;
-    if (bh * bw <= SEED_LDS_PX_MAX) {
-      const bool runs_fit = bw <= 65535 && bh <= 65535 &&
-                            rs_bytes_fixed((int)bh, (int)((bw + 63) >> 6)) + 14 * RS_MIN_CAP <= RS_LDS;
-      if (!runs_fit) {
-        big[c] = 1;
-        ++npix;
-      }
-      continue;
-    }
-    big[c] = 2;
+    if (seed_class(hb, c, use_runs) != 2) continue;
     br0 = std::min<int64_t>(br0, hb[c * 4 + 0]);
     bc0 = std::min<int64_t>(bc0, hb[c * 4 + 1]);
     br1 = std::max<int64_t>(br1, hb[c * 4 + 2]);
     bc1 = std::max<int64_t>(bc1, hb[c * 4 + 3]);
   }
-  (void)npix;
-  uint8_t *dbig = nullptr;
-  const size_t nb = big.size();
-  HRF_HIP(hipMallocAsync((void **)&dbig, 2 * nb, s));
-  uint8_t *dovf = dbig + nb;
-  HRF_HIP(hipMemcpyAsync(dbig, big.data(), nb, hipMemcpyHostToDevice, s));
+  // overflow flags of the run kernel (device only: nothing is copied from host memory, whose
+  // lifetime an asynchronous copy would outlive)
+  uint8_t *dovf = nullptr;
+  const size_t nb = (size_t)ncomp + 1;
+  HRF_HIP(hipMallocAsync((void **)&dovf, nb, s));
   HRF_HIP(hipMemsetAsync(dovf, 0, nb, s));
   const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
-  hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm_max);
-  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, dbig, area_max, min_obj, dovf,
+  HRF_HIP(hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)shm_max));
+  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, use_runs, area_max, min_obj, dovf,
                                                                  be_out);
-  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, dbig, 1, area_max, min_obj, dovf,
+  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, use_runs, 1, area_max, min_obj, dovf,
                                                             be_out);
   HRF_LAUNCHED();
   hrf_status st = HRF_OK;
@@ -551,7 +571,7 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     int64_t *cnt_dev = nullptr;
     HRF_HIP(hipMallocAsync((void **)&cnt_dev, sizeof(int64_t), s));
     HRF_HIP(hipMemsetAsync(bec, 0, (size_t)n, s));
-    big_crop_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, H, W, dbig, r0, c0, h, w, m);
+    big_crop_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, H, W, box, ncomp, r0, c0, h, w, m);
     HRF_LAUNCHED();
     for (int64_t it = 0; it < 4 * (h + w) + 8; ++it) {
       int64_t cnt = 0;
@@ -571,6 +591,6 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     HRF_HIP(hipFreeAsync(cnt_dev, s));
     HRF_HIP(hipFreeAsync(ws, s));
   }
-  HRF_HIP(hipFreeAsync(dbig, s));
+  HRF_HIP(hipFreeAsync(dovf, s));
   return st;
 }

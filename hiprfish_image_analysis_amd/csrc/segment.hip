@@ -168,15 +168,13 @@ hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *c) {
   return HRF_OK;
 }
 
-hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int32_t *seg_out, int32_t *maxlab_host,
-                             hrf_stream_t stream) {
-  HRF_REQUIRE(c && stack && seg_out && maxlab_host && C >= 1, "segment_ecoli: bad arguments");
-  hipStream_t s = (hipStream_t)stream;
+// ecoli :73-127 from image_cn (f64, H x W)
+static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_t *seg_out, int32_t *maxlab_host,
+                                        hipStream_t s) {
   const int64_t H = c->H, W = c->W, n = c->n;
   uint8_t *rough = c->m[0], *interior = c->m[1], *a = c->m[2], *b = c->m[3], *d = c->m[4];
   int32_t *lab1 = c->l[0], *seeds = c->l[1], *ws = c->l[2], *lab3 = c->l[3];
-  HRF_TRY(hrf_channel_sum(stack, n, C, nullptr, 1, 0, c->cn, s));               // :71-72
-  HRF_TRY(hrf_kmeans_1d_sorted_pair(c->cn, nullptr, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes,
+  HRF_TRY(hrf_kmeans_1d_sorted_pair(cn, nullptr, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes,
                                     s));                                        // :73-94
   HRF_TRY(hrf_remove_small_holes(interior, H, W, 64, 1, a, c->parent, c->size, s));   // :95
   HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
@@ -203,7 +201,7 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
   HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
   int32_t passes = 0;
-  HRF_TRY(hrf_watershed(c->cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
+  HRF_TRY(hrf_watershed(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
   const int32_t nseeds = c->hpin[0];  // read back by the watershed's synchronisation
   HRF_TRY(ensure_labels(c, nseeds, s));
   HRF_TRY(hrf_remove_small_objects_labels(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114
@@ -213,6 +211,20 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   HRF_TRY(hrf_shape_filter(lab3, H, W, c->props, nseeds, 15.0, 35.0, seg_out, s));   // :117-126
   *maxlab_host = nseeds;
   return HRF_OK;
+}
+
+hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int32_t *seg_out, int32_t *maxlab_host,
+                             hrf_stream_t stream) {
+  HRF_REQUIRE(c && stack && seg_out && maxlab_host && C >= 1, "segment_ecoli: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  HRF_TRY(hrf_channel_sum(stack, c->n, C, nullptr, 1, 0, c->cn, s));            // :71-72
+  return segment_ecoli_from_cn(c, c->cn, seg_out, maxlab_host, s);
+}
+
+hrf_status hrf_segment_ecoli_cn(hrf_seg_ctx *c, const double *image_cn, int32_t *seg_out, int32_t *maxlab_host,
+                                hrf_stream_t stream) {
+  HRF_REQUIRE(c && image_cn && seg_out && maxlab_host, "segment_ecoli_cn: bad arguments");
+  return segment_ecoli_from_cn(c, image_cn, seg_out, maxlab_host, (hipStream_t)stream);
 }
 
 hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t C, const float *cal, int64_t cal_sp,

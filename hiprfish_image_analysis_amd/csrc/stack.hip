@@ -74,7 +74,8 @@ __global__ void assemble_kernel(Lasers L, int64_t H, int64_t W, int apply_mask, 
 // then written out as one contiguous 64 x C run with 16-byte stores.  32-bit index math only.
 constexpr int AS_P = 64;
 __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
-                                                           float *__restrict__ dst, int vec_ok) {
+                                                           float *__restrict__ dst, int vec_ok,
+                                                           double *__restrict__ cn_out, int cn_mode) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ uint8_t okp[AS_P];
   __shared__ int sdr[LMAX], sdc[LMAX];
@@ -134,6 +135,38 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
     for (int e = ((n >> 2) << 2) + tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
   } else {
     for (int e = tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
+  }
+  if (cn_out) {
+    // the channel sum of the assembled (masked) pixels, numpy's pairwise order as
+    // channel_sum_lds_kernel takes it (8 lanes per pixel), from the tile already in LDS:
+    // ecoli :71-72 image_cn without a second pass over the stack
+    const int j = tid & 7;
+    const int main_n = C < 8 ? 0 : C - (C % 8);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int pi = half * 32 + (tid >> 3);
+      const float *a = tile + (pi < np ? pi : 0) * C;
+      const bool ok = pi < np && (!apply_mask || okp[pi]);
+      double res = 0.0;
+      if (C >= 8) {
+        double rr = ok ? (double)a[j] : 0.0;
+        for (int i = 8; i < main_n; i += 8) rr += ok ? (double)a[i + j] : 0.0;
+        rr = rr + __shfl_xor(rr, 1, 64);
+        rr = rr + __shfl_xor(rr, 2, 64);
+        rr = rr + __shfl_xor(rr, 4, 64);
+        res = rr;
+        if (j == 0)
+          for (int i = main_n; i < C; ++i) res += ok ? (double)a[i] : 0.0;
+      } else if (j == 0) {
+        for (int i = 0; i < C; ++i) res += ok ? (double)a[i] : 0.0;
+      }
+      if (j == 0 && pi < np) {
+        double sv = 0.0 + res;
+        if (cn_mode == 1) sv = log(sv + 1e-2);
+        else if (cn_mode == 2) sv = log10(sv + 1.0);
+        cn_out[r * W + c0 + pi] = sv;
+      }
+    }
   }
 }
 
@@ -437,7 +470,8 @@ extern "C" {
 
 static hrf_status register_assemble(const float *const *src_host, const int32_t *channels_host,
                                     const int32_t *shifts_host, const int32_t *shifts_dev, int32_t nlaser, int64_t H,
-                                    int64_t W, int32_t apply_mask, float *dst, hrf_stream_t stream) {
+                                    int64_t W, int32_t apply_mask, float *dst, hrf_stream_t stream,
+                                    double *cn_out = nullptr, int32_t cn_mode = 0) {
   HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && (shifts_host || shifts_dev),
               "register_assemble: bad lasers");
   Lasers L{};
@@ -460,7 +494,8 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     // row runs start at pixel (r, 64 k): 16-byte aligned when W * C is a multiple of 4 floats
     const int vec_ok = ((W * C) % 4 == 0) && (((uintptr_t)dst & 15) == 0);
     dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
-    assemble_lds_kernel<<<grid, 256, sizeof(float) * AS_P * C, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, vec_ok);
+    assemble_lds_kernel<<<grid, 256, sizeof(float) * AS_P * C, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, vec_ok,
+                                                                                     cn_out, cn_mode);
   } else {
     assemble_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst);
   }
@@ -480,6 +515,22 @@ hrf_status hrf_register_assemble_dev(const float *const *src_host, const int32_t
                                      int32_t apply_mask, float *dst, hrf_stream_t stream) {
   HRF_REQUIRE(shifts_dev, "register_assemble: null device shifts");
   return register_assemble(src_host, channels_host, nullptr, shifts_dev, nlaser, H, W, apply_mask, dst, stream);
+}
+
+hrf_status hrf_register_assemble_cn_dev(const float *const *src_host, const int32_t *channels_host,
+                                        const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                        int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode,
+                                        hrf_stream_t stream) {
+  HRF_REQUIRE(shifts_dev && cn_out && cn_mode >= 0 && cn_mode <= 2, "register_assemble_cn: bad arguments");
+  int C = 0;
+  for (int i = 0; i < nlaser && channels_host; ++i) C += channels_host[i];
+  if (C <= 128 && H <= 65535)
+    return register_assemble(src_host, channels_host, nullptr, shifts_dev, nlaser, H, W, apply_mask, dst, stream, cn_out,
+                             cn_mode);
+  if (hrf_status r = register_assemble(src_host, channels_host, nullptr, shifts_dev, nlaser, H, W, apply_mask, dst,
+                                       stream))
+    return r;
+  return hrf_channel_sum(dst, H * W, C, nullptr, cn_mode, 0, cn_out, stream);
 }
 
 hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,

@@ -125,10 +125,12 @@ def _i32_host(seq):
 
 
 # ---- a1-a3 ----------------------------------------------------------------------------------
-def register_assemble(srcs, shifts, apply_mask=True):
+def register_assemble(srcs, shifts, apply_mask=True, cn_mode=None):
     """ecoli measurement.py:51-70: shift each (H,W,C_l) laser stack, concatenate on C.
     shifts: [(dr, dc), ...] on the host, or an (nlaser, 2) int32 device tensor (read by the
-    kernel: no synchronisation)."""
+    kernel: no synchronisation).  With cn_mode (device shifts only) also the channel sum of
+    the assembled stack from the same pass (0 sum, 1 log(sum + 1e-2) = image_cn, 2 log10(sum
+    + 1)) -> (stack, sum image f64)."""
     import ctypes
     srcs = [_dev(s, torch.float32, "laser stack") for s in srcs]
     H, W = srcs[0].shape[:2]
@@ -139,9 +141,16 @@ def register_assemble(srcs, shifts, apply_mask=True):
         sd = _dev(shifts, torch.int32, "shifts")
         if sd.numel() != 2 * len(srcs):
             raise ValueError("register_assemble: one (dr, dc) pair per laser expected")
+        if cn_mode is not None:
+            cn = torch.empty((H, W), dtype=torch.float64, device=out.device)
+            _lib.call("hrf_register_assemble_cn_dev", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd),
+                      len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _ptr(cn), int(cn_mode), _stream())
+            return out, cn
         _lib.call("hrf_register_assemble_dev", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd),
                   len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _stream())
         return out
+    if cn_mode is not None:
+        raise ValueError("register_assemble: cn_mode needs device shifts")
     sh = _i32_host([v for d in shifts for v in (int(d[0]), int(d[1]))])
     _lib.call("hrf_register_assemble", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, sh.ctypes.data,
               len(srcs), H, W, int(bool(apply_mask)), _ptr(out), _stream())
@@ -767,13 +776,22 @@ def _seg_ctx(dev, H, W):
     return h
 
 
-def segment_ecoli_native(stack):
-    """ecoli measurement.py:44-127 in one native call -> (segmentation int32, max label)"""
+def segment_ecoli_native(stack, image_cn=None):
+    """ecoli measurement.py:44-127 in one native call -> (segmentation int32, max label);
+    with image_cn (log(sum + 1e-2), f64 H x W, e.g. from register_assemble(cn_mode=1)) the
+    channel sum is not recomputed"""
     import ctypes
+    mx = ctypes.c_int32(0)
+    if image_cn is not None:
+        cn = _dev(image_cn, torch.float64, "image_cn")
+        H, W = cn.shape
+        seg = torch.empty((H, W), dtype=torch.int32, device=cn.device)
+        _lib.call("hrf_segment_ecoli_cn", _seg_ctx(cn.device, H, W), _ptr(cn), _ptr(seg), ctypes.addressof(mx),
+                  _stream())
+        return seg, mx.value
     stack = _dev(stack, torch.float32, "stack")
     H, W, C = stack.shape
     seg = torch.empty((H, W), dtype=torch.int32, device=stack.device)
-    mx = ctypes.c_int32(0)
     _lib.call("hrf_segment_ecoli", _seg_ctx(stack.device, H, W), _ptr(stack), C, _ptr(seg), ctypes.addressof(mx),
               _stream())
     return seg, mx.value

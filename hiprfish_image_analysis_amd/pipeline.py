@@ -44,11 +44,13 @@ def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: in
 NATIVE_SEG = os.environ.get("HRF_NATIVE_SEG", "1") != "0"
 
 
-def segment_ecoli(stack: torch.Tensor, keep: dict | None = None):
-    """ecoli measurement.py:44-127 on the registered stack.  -> (segmentation int32, max label)"""
+def segment_ecoli(stack: torch.Tensor, keep: dict | None = None, image_cn: torch.Tensor | None = None):
+    """ecoli measurement.py:44-127 on the registered stack.  -> (segmentation int32, max label)
+    image_cn: the stack's log(sum + 1e-2) when already computed (register_stack(want_cn=True))"""
     if keep is None and NATIVE_SEG:
-        return K.segment_ecoli_native(stack)
-    image_cn = K.channel_sum(stack, mode=1)                              # :71-72 log(sum + 1e-2)
+        return K.segment_ecoli_native(stack, image_cn)
+    if image_cn is None:
+        image_cn = K.channel_sum(stack, mode=1)                          # :71-72 log(sum + 1e-2)
     share = {}                                                           # one sort for both fits
     _, rough_mask, _, _ = K.kmeans_1d(image_cn, 2, want_labels=False, share=share, rule=2)  # :73-84 brighter
     _, interior, _, _ = K.kmeans_1d(image_cn, 3, want_labels=False, share=share, rule=0)    # :85-94 brightest
@@ -78,10 +80,11 @@ class Measurement:
     extras: dict = field(default_factory=dict)
 
 
-def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, keep: dict | None = None):
+def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, keep: dict | None = None,
+                  image_cn: torch.Tensor | None = None):
     """ecoli measurement.py:142-162: segment, flat-field channels 0..31 (load_calibration_images
     :33-38 puts the calibration image on channels 0-31 and 1.0 elsewhere), per-cell means."""
-    seg, maxlab = segment_ecoli(stack, keep)
+    seg, maxlab = segment_ecoli(stack, keep, image_cn)
     sums, counts = K.label_sums(stack, seg, maxlab, cal=calibration,
                                 cal_range=(0, 32) if calibration is not None else None)   # :147-155
     _, lor, avgint, avgint_norm = K.cell_table(sums, counts, maxlab)                      # :151-157
@@ -112,11 +115,15 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
     return shifts
 
 
-def register_stack(lasers, reduce: str = "max", clamp: int | None = 15, apply_mask: bool = True):
+def register_stack(lasers, reduce: str = "max", clamp: int | None = 15, apply_mask: bool = True,
+                   want_cn: bool = False):
     """ecoli measurement.py:44-70 (-c T: plus load_calibration_images :33-38, applied to the
     per-cell spectra by measure_ecoli): shift estimate on the per-laser projections, then the
-    registered, concatenated (H, W, C) stack -- one stream, no synchronisation."""
-    return K.register_assemble(lasers, estimate_shifts(lasers, reduce, clamp, device=True), apply_mask)
+    registered, concatenated (H, W, C) stack -- one stream, no synchronisation.  want_cn: also
+    image_cn = log(sum + 1e-2) of the registered stack (:71-72) from the assembly pass
+    -> (stack, image_cn)."""
+    return K.register_assemble(lasers, estimate_shifts(lasers, reduce, clamp, device=True), apply_mask,
+                               cn_mode=1 if want_cn else None)
 
 
 # --------------------------------------------------------------------------------------------
@@ -259,7 +266,7 @@ def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
 
 
 def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0,
-                 overlap: bool = True, pixel_events: list | None = None, measure=None):
+                 overlap: bool = True, pixel_events: list | None = None, measure=None, image_cn=None):
     """One tile of the hot path: measure (segment + per-cell spectra) + classify + count.
 
     The per-pixel classification does not depend on the segmentation, so with `overlap` it
@@ -268,7 +275,8 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
     idle; the caller's stream joins it before returning.  `pixel_events`, if given, receives
     the (start, end) events recorded around the classification on the stream it ran on.
     `measure` selects the measurement chain (default measure_ecoli; measure_multispecies for
-    the synthetic-community pipeline)."""
+    the synthetic-community pipeline); `image_cn` hands measure_ecoli the log-sum image the
+    registration pass already produced."""
     main = torch.cuda.current_stream(stack.device)
     pix = None
     if per_pixel:
@@ -288,7 +296,10 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
         if overlap:
             stack.record_stream(side)
             refx.record_stream(side)
-    meas = (measure or measure_ecoli)(stack, calibration)
+    if image_cn is not None:
+        meas = (measure or measure_ecoli)(stack, calibration, image_cn=image_cn)
+    else:
+        meas = (measure or measure_ecoli)(stack, calibration)
     idx, dist = classify_cells(meas.avgint_norm, lib, variant)
     counts = K.barcode_counts(idx, lib.R)                       # collect_measurement_results.py:92-98
     ident = K.paint_ids(meas.segmentation, idx + 1)             # image_classification.py:65-71

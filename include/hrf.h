@@ -102,6 +102,13 @@ HRF_API hrf_status hrf_register_assemble(const float *const *src_host, const int
 HRF_API hrf_status hrf_register_assemble_dev(const float *const *src_host, const int32_t *channels_host,
                                              const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
                                              int32_t apply_mask, float *dst, hrf_stream_t stream);
+/* the same, also writing the channel sum of the assembled stack (numpy pairwise order, f64;
+ * cn_mode 0 sum, 1 log(sum + 1e-2) = ecoli :71-72 image_cn, 2 log10(sum + 1)) from the tile
+ * the assembly already holds -- no second pass over the stack.  cn_out (H x W) f64 */
+HRF_API hrf_status hrf_register_assemble_cn_dev(const float *const *src_host, const int32_t *channels_host,
+                                                const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                                int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode,
+                                                hrf_stream_t stream);
 /* per-pixel sum over C in numpy pairwise order (== np.sum(stack, axis=2) in f64);
  * mode 0: sum, 1: log(sum + 1e-2) (ecoli :72), 2: log10(sum + 1) (biofilm :831);
  * mask (nullable) zeroes the sum; negate flips the sign (watershed input). */
@@ -276,6 +283,10 @@ HRF_API hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *ctx);
 /* ecoli measurement.py:44-127: seg_out (H*W int32, labels not re-sequenced), *maxlab_host */
 HRF_API hrf_status hrf_segment_ecoli(hrf_seg_ctx *ctx, const float *stack, int32_t C, int32_t *seg_out,
                                      int32_t *maxlab_host, hrf_stream_t stream);
+/* the same chain from a precomputed image_cn = log(sum + 1e-2) (H x W f64, e.g. written by
+ * hrf_register_assemble_cn_dev) */
+HRF_API hrf_status hrf_segment_ecoli_cn(hrf_seg_ctx *ctx, const double *image_cn, int32_t *seg_out,
+                                        int32_t *maxlab_host, hrf_stream_t stream);
 /* multispecies measurement.py:102-157 (calibration as hrf_channel_sum_cal, cal may be NULL):
  * seg_out relabelled 1..*nlab_host; image_sum_out / final_bkg_out (nullable, H*W f64) receive
  * the calibrated channel sum (:105) and the background-filtered enhanced image (:150). */

@@ -114,3 +114,29 @@ def test_pad_edge_3d(K):
     for w in (0, 1, 5):
         got = K.pad_edge_3d(torch.from_numpy(a).cuda(), w).cpu().numpy()
         assert np.array_equal(got, np.pad(a, w, mode="edge"))
+
+
+@pytest.mark.parametrize("mask", [True, False])
+def test_assembly_with_image_cn(K, mask):
+    """register_assemble(cn_mode=...) writes the registered stack and, from the same pass, its
+    channel sum in numpy's order: bit-equal to channel_sum on the written stack; the native
+    E. coli chain from that image_cn equals the chain from the stack"""
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    st, _, _, _ = S.tile(320, 352, seed=77)
+    lasers = S.laser_split(st)
+    sh = P.estimate_shifts(lasers, device=True)
+    plain = K.register_assemble(lasers, sh, apply_mask=mask)
+    for mode in (0, 1, 2):
+        stack, cn = K.register_assemble(lasers, sh, apply_mask=mask, cn_mode=mode)
+        assert torch.equal(stack, plain)
+        assert torch.equal(cn, K.channel_sum(plain, mode=mode))
+    stack, cn = P.register_stack(lasers, want_cn=True)
+    a = P.segment_ecoli(stack)
+    b = P.segment_ecoli(stack, image_cn=cn)
+    assert a[1] == b[1] and torch.equal(a[0], b[0])
+    # odd channel counts (C < 8 and a ragged tail) through the fused sum
+    few = [l[:, :, :3].contiguous() for l in lasers[:2]]
+    sh2 = P.estimate_shifts(few, device=True)
+    st2, cn2 = K.register_assemble(few, sh2, apply_mask=mask, cn_mode=1)
+    assert torch.equal(cn2, K.channel_sum(st2, mode=1))
