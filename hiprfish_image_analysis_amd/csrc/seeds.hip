@@ -136,16 +136,12 @@ __device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, b
 }
 
 // flags: bit0 = in play (dist_lab != 0), bit1 = seed (dist_be), bit2 = erosion result
-__global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
-                                                           const int32_t *__restrict__ box,
-                                                           int32_t use_runs, int32_t want,
-                                                           int32_t area_max, int32_t min_obj,
-                                                           const uint8_t *__restrict__ ovf,
-                                                           uint8_t *__restrict__ be_out) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int comp = blockIdx.x + 1;
+// one component in LDS (box <= SEED_LDS_PX_MAX pixels)
+__device__ void seed_component_px(char *lds, const int32_t *__restrict__ labels, int64_t H, int64_t W,
+                                  const int32_t *__restrict__ box, int comp, int32_t area_max, int32_t min_obj,
+                                  uint8_t *__restrict__ be_out) {
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
-  if (r1 < r0 || c1 < c0 || !(seed_class(box, comp, use_runs) == want || (ovf && ovf[comp]))) return;
+  if (r1 < r0 || c1 < c0) return;
   const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, n = bh * bw;
   uint8_t *fl = reinterpret_cast<uint8_t *>(lds);
   int32_t *par = reinterpret_cast<int32_t *>(lds + ((n + 15) & ~15));
@@ -194,6 +190,21 @@ __global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__res
       const int r = p / bw, c = p - r * bw;
       be_out[(int64_t)(r0 + r) * W + (c0 + c)] = 1;
     }
+}
+
+// the components the run kernel hands over (class 1, or over its run capacity), listed on the
+// device: a few workgroups walk the list, so no 160 KB-LDS grid is launched per component
+__global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
+                                                           const int32_t *__restrict__ box,
+                                                           const int32_t *__restrict__ list,
+                                                           const int32_t *__restrict__ count, int32_t area_max,
+                                                           int32_t min_obj, uint8_t *__restrict__ be_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int n = *count;
+  for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
+    seed_component_px(lds, labels, H, W, box, list[idx], area_max, min_obj, be_out);
+    __syncthreads();
+  }
 }
 
 // ---- run-length variant -----------------------------------------------------------------------
@@ -322,11 +333,14 @@ __device__ void rs_clear_run(uint64_t *m, uint64_t *sd, int base, int c0, int c1
 __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *__restrict__ labels, int64_t H,
                                                                  int64_t W, const int32_t *__restrict__ box,
                                                                  int32_t use_runs, int32_t area_max,
-                                                                 int32_t min_obj, uint8_t *__restrict__ ovf,
+                                                                 int32_t min_obj, int32_t *__restrict__ list,
+                                                                 int32_t *__restrict__ count,
                                                                  uint8_t *__restrict__ be_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
-  if (seed_class(box, comp, use_runs) != 0) return;
+  const int cls = seed_class(box, comp, use_runs);
+  if (cls == 1 && threadIdx.x == 0) list[atomicAdd(count, 1)] = comp;
+  if (cls != 0) return;
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
   if (r1 < r0 || c1 < c0) return;
   const int bh = r1 - r0 + 1, bw = c1 - c0 + 1, w64 = (bw + 63) >> 6, nw = bh * w64;
@@ -416,7 +430,7 @@ __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *
     }
   }
   // over capacity (or the iteration cap): the pixel kernel redoes this component
-  if (threadIdx.x == 0) ovf[comp] = 1;
+  if (threadIdx.x == 0) list[atomicAdd(count, 1)] = comp;
 }
 
 // crop (with padding) of the oversized components' pixels
@@ -530,8 +544,8 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
   if (ncomp == 0) return HRF_OK;
   // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
-  // Components the run kernel cannot hold (run arrays over capacity) are flagged in ovf and
-  // redone by the pixel kernel, so every box it may receive fits SEED_LDS_PX_MAX.
+  // Components the run kernel cannot hold (run arrays over capacity) are listed with the
+  // class-1 ones and redone by the pixel kernel, so every box it receives fits SEED_LDS_PX_MAX.
   static const int use_runs = [] {
     const char *e = getenv("HRF_SEEDS_RUNS");
     return e ? atoi(e) : 1;
@@ -544,19 +558,20 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     br1 = std::max<int64_t>(br1, hb[c * 4 + 2]);
     bc1 = std::max<int64_t>(bc1, hb[c * 4 + 3]);
   }
-  // overflow flags of the run kernel (device only: nothing is copied from host memory, whose
-  // lifetime an asynchronous copy would outlive)
-  uint8_t *dovf = nullptr;
-  const size_t nb = (size_t)ncomp + 1;
-  HRF_HIP(hipMallocAsync((void **)&dovf, nb, s));
-  HRF_HIP(hipMemsetAsync(dovf, 0, nb, s));
+  // the run kernel lists, on the device, the components it hands to the pixel kernel (nothing
+  // is copied from host memory, whose lifetime an asynchronous copy would outlive)
+  int32_t *dlist = nullptr;
+  const size_t nl = (size_t)ncomp + 2;
+  HRF_HIP(hipMallocAsync((void **)&dlist, sizeof(int32_t) * nl, s));
+  int32_t *dcount = dlist + ncomp + 1;
+  HRF_HIP(hipMemsetAsync(dcount, 0, sizeof(int32_t), s));
   const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
   HRF_HIP(hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)shm_max));
-  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, use_runs, area_max, min_obj, dovf,
-                                                                 be_out);
-  erosion_seed_kernel<<<(unsigned)ncomp, 1024, shm_max, s>>>(labels, H, W, box, use_runs, 1, area_max, min_obj, dovf,
-                                                            be_out);
+                              (int)shm_max));
+  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, use_runs, area_max, min_obj, dlist,
+                                                                 dcount, be_out);
+  erosion_seed_kernel<<<(unsigned)std::min(ncomp, 16), 1024, shm_max, s>>>(labels, H, W, box, dlist, dcount, area_max,
+                                                                          min_obj, be_out);
   HRF_LAUNCHED();
   hrf_status st = HRF_OK;
   if (br1 >= 0) {
@@ -591,6 +606,6 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     HRF_HIP(hipFreeAsync(cnt_dev, s));
     HRF_HIP(hipFreeAsync(ws, s));
   }
-  HRF_HIP(hipFreeAsync(dovf, s));
+  HRF_HIP(hipFreeAsync(dlist, s));
   return st;
 }
