@@ -14,7 +14,7 @@ run() {  # name, counters...
     python3 tools/time_classify.py $mode 1023 > $out/$name.log 2>&1
 }
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- \
-  python3 tools/time_classify.py $mode 64 1023 > $out/kt.log 2>&1 &&
+  python3 tools/time_classify.py $mode 1023 > $out/kt.log 2>&1 &&
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
 run sq1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE &&
