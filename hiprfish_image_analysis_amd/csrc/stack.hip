@@ -442,6 +442,65 @@ __global__ __launch_bounds__(256) void channel_max_lds_kernel(const float *__res
   }
 }
 
+// All lasers' channel-max projections in one launch (ecoli :45, one per laser before the shift
+// estimate): workgroups are split between the lasers in proportion to their channel counts and
+// each walks its laser's 64-pixel chunks as channel_max_lds_kernel does.
+struct MaxJob {
+  const float *src[LMAX];
+  double *out[LMAX];
+  int32_t C[LMAX];
+  int32_t wg0[LMAX + 1];  // first workgroup of each laser; wg0[n] = grid size
+  int32_t n;
+};
+
+__global__ __launch_bounds__(256) void channel_max_multi_kernel(MaxJob J, int64_t npix) {
+  extern __shared__ __attribute__((aligned(16))) float sb[];
+  int l = 0;
+#pragma unroll
+  for (int q = 1; q < LMAX; ++q)
+    if (q < J.n && (int)blockIdx.x >= J.wg0[q]) l = q;
+  const int C = J.C[l];
+  const float *stack = J.src[l];
+  double *out = J.out[l];
+  const int nwg = J.wg0[l + 1] - J.wg0[l], wg = (int)blockIdx.x - J.wg0[l];
+  const int vec_ok = ((uintptr_t)stack & 15) == 0 && (CM_P * C) % 4 == 0;
+  const int tid = threadIdx.x, pi = tid >> 2, q = tid & 3;
+  for (int64_t ch = wg; ch * CM_P < npix; ch += nwg) {
+    const int64_t p0 = ch * CM_P;
+    const int np = (int)min((int64_t)CM_P, npix - p0);
+    const int nel = np * C;
+    const float *src = stack + p0 * C;
+    int e0 = 0;
+    if (vec_ok) {
+      for (int v = tid; v < (nel >> 2); v += 256) reinterpret_cast<float4 *>(sb)[v] = reinterpret_cast<const float4 *>(src)[v];
+      e0 = (nel >> 2) << 2;
+    }
+    for (int e = e0 + tid; e < nel; e += 256) sb[e] = src[e];
+    __syncthreads();
+    float m = -__builtin_inff();
+    bool any = false;
+    if (pi < np) {
+      const float *a = sb + pi * C;
+      for (int c = q; c < C; c += 4) {
+        const float v = a[c];
+        m = (!any || v > m || v != v) ? v : m;
+        any = true;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o <= 2; o <<= 1) {
+      const float v = __shfl_xor(m, o, 64);
+      const bool va = __shfl_xor((int)any, o, 64) != 0;
+      if (va) {
+        m = (!any || v > m || v != v || m != m) ? (m != m ? m : v) : m;
+        any = true;
+      }
+    }
+    if (q == 0 && pi < np) out[p0 + pi] = (double)m;
+    __syncthreads();
+  }
+}
+
 __global__ void and_u8_kernel(const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, int64_t n,
                               uint8_t *__restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -581,6 +640,40 @@ hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *
   } else {
     channel_max_kernel<<<hrf::stream_grid(npix), 256, 0, (hipStream_t)stream>>>(stack, npix, C, out);
   }
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *channels_host, int32_t nlaser,
+                                 int64_t npix, double *const *out_host, hrf_stream_t stream) {
+  HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && out_host, "channel_max_multi: bad lasers");
+  if (npix == 0) return HRF_OK;
+  MaxJob J{};
+  J.n = nlaser;
+  int ctot = 0, cmax = 0;
+  for (int i = 0; i < nlaser; ++i) {
+    HRF_REQUIRE(src_host[i] && out_host[i] && channels_host[i] >= 1, "channel_max_multi: laser %d empty", i);
+    if (channels_host[i] > 256)
+      for (int k = 0; k < nlaser; ++k)   // wide stacks: one launch each
+        if (hrf_status r = hrf_channel_max(src_host[k], npix, channels_host[k], out_host[k], stream)) return r;
+    if (channels_host[i] > 256) return HRF_OK;
+    J.src[i] = src_host[i];
+    J.out[i] = out_host[i];
+    J.C[i] = channels_host[i];
+    ctot += channels_host[i];
+    cmax = std::max(cmax, (int)channels_host[i]);
+  }
+  const int64_t chunks = hrf::cdiv(npix, CM_P);
+  const int64_t total = std::min<int64_t>(chunks * nlaser, 4096);
+  int wg = 0;
+  for (int i = 0; i < nlaser; ++i) {
+    J.wg0[i] = wg;
+    int64_t share = std::max<int64_t>(1, (total * J.C[i] + ctot - 1) / ctot);
+    share = std::min<int64_t>(share, chunks);
+    wg += (int)share;
+  }
+  for (int i = nlaser; i <= LMAX; ++i) J.wg0[i] = wg;
+  channel_max_multi_kernel<<<(unsigned)wg, 256, sizeof(float) * CM_P * cmax, (hipStream_t)stream>>>(J, npix);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -199,6 +199,22 @@ def channel_max(stack):
     return out
 
 
+def channel_max_multi(stacks):
+    """[np.max(s, axis=2) for s in stacks] (f64) in one launch; the stacks share H x W"""
+    import ctypes
+    stacks = [_dev(s, torch.float32, "stack") for s in stacks]
+    H, W = stacks[0].shape[:2]
+    if any(s.shape[:2] != (H, W) for s in stacks):
+        raise ValueError("channel_max_multi: the stacks must share H x W")
+    outs = [torch.empty((H, W), dtype=torch.float64, device=stacks[0].device) for _ in stacks]
+    src = (ctypes.c_void_p * len(stacks))(*[s.data_ptr() for s in stacks])
+    dst = (ctypes.c_void_p * len(stacks))(*[o.data_ptr() for o in outs])
+    ch = _i32_host([s.shape[2] for s in stacks])
+    _lib.call("hrf_channel_max_multi", ctypes.cast(src, ctypes.c_void_p), ch.ctypes.data, len(stacks), H * W,
+              ctypes.cast(dst, ctypes.c_void_p), _stream())
+    return outs
+
+
 def calibrate(stack, cal, cal_range=None):
     """stack / cal as f64 (multispecies measurement.py:104, saved as _registered.npy :166)"""
     stack = _dev(stack, torch.float32, "stack")

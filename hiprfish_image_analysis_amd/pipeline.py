@@ -102,7 +102,10 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
     -> [(0, 0), (dr_1, dc_1), ...] ready for kernels.register_assemble; with `device` an
     (nlaser, 2) int32 device tensor instead (no host synchronisation; register_assemble reads
     it on the device)."""
-    proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
+    if reduce == "max" and len(lasers) <= 8:
+        proj = K.channel_max_multi(lasers)                               # one launch for all lasers
+    else:
+        proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
     if device:
         return K.register_translations_dev(proj[0], proj[1:], clamp)
     shifts = [(0, 0)]

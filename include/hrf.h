@@ -123,6 +123,10 @@ HRF_API hrf_status hrf_channel_sum_cal(const float *stack, int64_t npix, int32_t
                                        hrf_stream_t stream);
 /* np.max(stack, axis=2) as f64 (ecoli :45, the per-laser registration images) */
 HRF_API hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *out, hrf_stream_t stream);
+/* every laser's np.max(stack, axis=2) projection (ecoli :45) in one launch: src / out per laser
+ * ((npix x C_l) f32 -> npix f64) */
+HRF_API hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *channels_host, int32_t nlaser,
+                                         int64_t npix, double *const *out_host, hrf_stream_t stream);
 /* the calibrated stack as f64, out (npix, C) (multispecies :104 image_channel / :166 _registered.npy) */
 HRF_API hrf_status hrf_calibrate_f64(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
                                      int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, double *out,

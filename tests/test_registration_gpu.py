@@ -140,3 +140,16 @@ def test_assembly_with_image_cn(K, mask):
     sh2 = P.estimate_shifts(few, device=True)
     st2, cn2 = K.register_assemble(few, sh2, apply_mask=mask, cn_mode=1)
     assert torch.equal(cn2, K.channel_sum(st2, mode=1))
+
+
+def test_channel_max_multi_equals_per_laser(K):
+    from hiprfish_image_analysis_amd import synthetic as S
+    st, _, _, _ = S.tile(200, 264, seed=78)
+    lasers = S.laser_split(st)
+    lasers[2][5, 7, 3] = float("nan")            # numpy's max propagates NaN
+    outs = K.channel_max_multi(lasers)
+    for l, o in zip(lasers, outs):
+        want = K.channel_max(l)
+        assert torch.equal(torch.isnan(o), torch.isnan(want))
+        assert torch.equal(torch.nan_to_num(o), torch.nan_to_num(want))
+    assert torch.isnan(outs[2][5, 7])
