@@ -235,6 +235,18 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
         cfg3[name] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
                       "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
                       "classifier_mode": mode if pp else None}
+    # round 1's definition of the line, for continuity: the timed path starting from an
+    # assembled, registered stack without the flat field (no registration, no calibration)
+    # (the rolls laser_split applied come back whole without the coverage mask: the original,
+    # round-1-style synthetic stack)
+    pre = [(P.register_stack(t[0], apply_mask=False),) for t in tiles]
+    torch.cuda.synchronize()
+    sec = _timed_tiles(lambda t: P.process_tile(t[0], lib_main), pre, T, streams, pool, steps, 2)
+    cfg3["preassembled_uncalibrated"] = {"value": round(H * W * steps * T / sec / 1e6, 3),
+                                         "unit": "Mpixel-spectra/s", "ms_per_step": round(sec / steps * 1e3, 3),
+                                         "steps": steps, "concurrent": T, "classifier_mode": 2,
+                                         "note": "round 1's timed path (BENCH_r01.json 1044.5)"}
+    del pre
     out["cfg3"] = cfg3
     # cfg2: synthetic-community tiles
     b = S.MULTI_BOUNDS
