@@ -1,3 +1,4 @@
+#include <cstdlib>
 // stack.hip -- spectral stack assembly and per-pixel channel reductions (a1-a3), plus the
 // small elementwise steps between pipeline stages.
 //
@@ -160,6 +161,118 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
       } else if (j == 0) {
         for (int i = 0; i < C; ++i) res += ok ? (double)a[i] : 0.0;
       }
+      if (j == 0 && pi < np) {
+        double sv = 0.0 + res;
+        if (cn_mode == 1) sv = log(sv + 1e-2);
+        else if (cn_mode == 2) sv = log10(sv + 1.0);
+        cn_out[r * W + c0 + pi] = sv;
+      }
+    }
+  }
+}
+
+// E. coli layout (lasers of 32, 23, 20, 14, 6 channels) specialised: every laser's source run
+// of the strip is loaded with all reads in flight (25 per thread, divisions by compile-time
+// channel counts), then scattered into the tile; the rest as assemble_lds_kernel.
+template <int Q>
+struct EcoliLasers {
+  static constexpr int n = 5;
+  static constexpr int cl(int q) { return q == 0 ? 32 : q == 1 ? 23 : q == 2 ? 20 : q == 3 ? 14 : 6; }
+  static constexpr int off(int q) { return q == 0 ? 0 : off(q - 1) + cl(q - 1); }
+  static constexpr int C = 95;
+};
+
+template <int q, int NL>
+__device__ __forceinline__ void lay_load(const Lasers &L, const int *sdr, const int *sdc, int64_t r, int64_t c0,
+                                         int64_t H, int64_t W, int tid, float *v) {
+  constexpr int cl = EcoliLasers<0>::cl(q);
+  constexpr int U = (AS_P * cl + 255) / 256;
+  const int dr = sdr[q], dc = sdc[q];
+  const bool row_ok = r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0);
+  const int64_t cmin = dc > 0 ? dc : 0, cmax = W + (dc < 0 ? dc : 0);
+  const float *src = L.src[q] + ((r - dr) * W + (c0 - dc)) * (int64_t)cl;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + 256 * u;
+    const int pp = e / cl;
+    const int64_t c = c0 + pp;
+    v[u] = (e < AS_P * cl && row_ok && c >= cmin && c < cmax && c < W) ? src[e] : 0.0f;
+  }
+  if constexpr (q + 1 < NL) lay_load<q + 1, NL>(L, sdr, sdc, r, c0, H, W, tid, v + U);
+}
+
+template <int q, int NL>
+__device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) {
+  constexpr int cl = EcoliLasers<0>::cl(q), off = EcoliLasers<0>::off(q);
+  constexpr int U = (AS_P * cl + 255) / 256;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + 256 * u;
+    if (e < AS_P * cl) {
+      const int pp = e / cl;
+      tile[pp * EcoliLasers<0>::C + off + (e - pp * cl)] = v[u];
+    }
+  }
+  if constexpr (q + 1 < NL) lay_store<q + 1, NL>(tile, tid, v + U);
+}
+
+__global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+                                                             float *__restrict__ dst, double *__restrict__ cn_out,
+                                                             int cn_mode) {
+  constexpr int C = EcoliLasers<0>::C;
+  __shared__ __attribute__((aligned(16))) float tile[AS_P * C];
+  __shared__ uint8_t okp[AS_P];
+  __shared__ int sdr[LMAX], sdc[LMAX];
+  load_shifts(L, sdr, sdc);
+  const int tid = threadIdx.x;
+  const int64_t r = blockIdx.y;
+  const int64_t c0 = (int64_t)blockIdx.x * AS_P;
+  const int np = (int)min((int64_t)AS_P, W - c0);
+  if (tid < AS_P) {
+    bool ok = tid < np;
+    if (apply_mask)
+      for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, sdr[q], sdc[q]);
+    okp[tid] = (uint8_t)ok;
+  }
+  constexpr int UT = 8 + 6 + 5 + 4 + 2;
+  float v[UT];
+  lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
+  lay_store<0, 5>(tile, tid, v);
+  __syncthreads();
+  float *out = dst + (r * W + c0) * (int64_t)C;
+  const int n = np * C;
+  if (np == AS_P) {   // a full strip: 64 x 95 floats, 16-byte aligned (W multiple of 64)
+    for (int vv = tid; vv < (n >> 2); vv += 256) {
+      const int e = vv << 2;
+      float4 x = reinterpret_cast<const float4 *>(tile)[vv];
+      if (apply_mask) {
+        x.x = okp[e / C] ? x.x : 0.0f;
+        x.y = okp[(e + 1) / C] ? x.y : 0.0f;
+        x.z = okp[(e + 2) / C] ? x.z : 0.0f;
+        x.w = okp[(e + 3) / C] ? x.w : 0.0f;
+      }
+      reinterpret_cast<float4 *>(out)[vv] = x;
+    }
+  } else {
+    for (int e = tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
+  }
+  if (cn_out) {
+    const int j = tid & 7;
+    constexpr int main_n = C - (C % 8);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int pi = half * 32 + (tid >> 3);
+      const float *a = tile + (pi < np ? pi : 0) * C;
+      const bool ok = pi < np && (!apply_mask || okp[pi]);
+      double rr = ok ? (double)a[j] : 0.0;
+#pragma unroll
+      for (int i = 8; i < main_n; i += 8) rr += ok ? (double)a[i + j] : 0.0;
+      rr = rr + __shfl_xor(rr, 1, 64);
+      rr = rr + __shfl_xor(rr, 2, 64);
+      rr = rr + __shfl_xor(rr, 4, 64);
+      double res = rr;
+      if (j == 0)
+        for (int i = main_n; i < C; ++i) res += ok ? (double)a[i] : 0.0;
       if (j == 0 && pi < np) {
         double sv = 0.0 + res;
         if (cn_mode == 1) sv = log(sv + 1e-2);
@@ -501,6 +614,56 @@ __global__ __launch_bounds__(256) void channel_max_multi_kernel(MaxJob J, int64_
   }
 }
 
+// The same for C <= 32 and whole 128-pixel chunks, software-pipelined: the next chunk's
+// 16-byte loads (at most 4 per thread) are in flight in registers while this chunk is reduced
+// from LDS; two lanes per pixel.
+constexpr int CM_P2 = 128;
+__global__ __launch_bounds__(256) void channel_max_multi_pf_kernel(MaxJob J, int64_t npix) {
+  __shared__ __attribute__((aligned(16))) float sb[CM_P2 * 32];
+  int l = 0;
+#pragma unroll
+  for (int q = 1; q < LMAX; ++q)
+    if (q < J.n && (int)blockIdx.x >= J.wg0[q]) l = q;
+  const int C = J.C[l];
+  const float4 *g = reinterpret_cast<const float4 *>(J.src[l]);
+  double *out = J.out[l];
+  const int nwg = J.wg0[l + 1] - J.wg0[l], wg = (int)blockIdx.x - J.wg0[l];
+  const int tid = threadIdx.x, pi = tid >> 1, h = tid & 1;
+  const int nv = CM_P2 * C / 4;          // float4 per chunk
+  const int64_t nch = npix / CM_P2;
+  float4 r0, r1, r2, r3;
+  auto fetch = [&](int64_t ch) {
+    if (ch >= nch) return;
+    const float4 *s = g + ch * nv;
+    if (tid < nv) r0 = s[tid];
+    if (tid + 256 < nv) r1 = s[tid + 256];
+    if (tid + 512 < nv) r2 = s[tid + 512];
+    if (tid + 768 < nv) r3 = s[tid + 768];
+  };
+  fetch(wg);
+  for (int64_t ch = wg; ch < nch; ch += nwg) {
+    float4 *d = reinterpret_cast<float4 *>(sb);
+    if (tid < nv) d[tid] = r0;
+    if (tid + 256 < nv) d[tid + 256] = r1;
+    if (tid + 512 < nv) d[tid + 512] = r2;
+    if (tid + 768 < nv) d[tid + 768] = r3;
+    __syncthreads();
+    fetch(ch + nwg);
+    const float *a = sb + pi * C;
+    float m = a[h];
+    for (int c = h + 2; c < C; c += 2) {
+      const float v = a[c];
+      m = (v > m || v != v) ? v : m;
+    }
+    if (C > 1) {
+      const float v = __shfl_xor(m, 1, 64);
+      m = (m != m) ? m : ((v > m || v != v) ? v : m);
+    }
+    if (h == 0) out[ch * CM_P2 + pi] = (double)m;
+    __syncthreads();
+  }
+}
+
 __global__ void and_u8_kernel(const uint8_t *__restrict__ a, const uint8_t *__restrict__ b, int64_t n,
                               uint8_t *__restrict__ o) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -553,6 +716,13 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     // row runs start at pixel (r, 64 k): 16-byte aligned when W * C is a multiple of 4 floats
     const int vec_ok = ((W * C) % 4 == 0) && (((uintptr_t)dst & 15) == 0);
     dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
+    bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
+    for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
+    if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
+      assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode);
+      HRF_LAUNCHED();
+      return HRF_OK;
+    }
     assemble_lds_kernel<<<grid, 256, sizeof(float) * AS_P * C, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, vec_ok,
                                                                                      cn_out, cn_mode);
   } else {
@@ -673,7 +843,12 @@ hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *ch
     wg += (int)share;
   }
   for (int i = nlaser; i <= LMAX; ++i) J.wg0[i] = wg;
-  channel_max_multi_kernel<<<(unsigned)wg, 256, sizeof(float) * CM_P * cmax, (hipStream_t)stream>>>(J, npix);
+  bool pf = cmax <= 32 && npix % CM_P2 == 0;
+  for (int i = 0; i < nlaser && pf; ++i) pf = ((uintptr_t)src_host[i] & 15) == 0;
+  if (pf)
+    channel_max_multi_pf_kernel<<<(unsigned)wg, 256, 0, (hipStream_t)stream>>>(J, npix);
+  else
+    channel_max_multi_kernel<<<(unsigned)wg, 256, sizeof(float) * CM_P * cmax, (hipStream_t)stream>>>(J, npix);
   HRF_LAUNCHED();
   return HRF_OK;
 }
