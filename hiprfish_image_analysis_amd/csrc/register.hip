@@ -19,8 +19,13 @@
 
 namespace {
 
+// One plan pair per (device, size), shared by every stream.  The plans' work areas are NOT
+// allocated by hipFFT: each call binds a region of its own caller-provided workspace (under
+// the mutex, right before it enqueues), so transforms of concurrent tiles on different streams
+// never share scratch memory.
 struct Plans {
   hipfftHandle fwd, inv;
+  size_t work;   // bytes of work area either plan needs
 };
 std::mutex g_plan_mu;
 std::map<std::tuple<int, int64_t, int64_t>, Plans> g_plans;
@@ -45,8 +50,14 @@ hrf_status get_plans(int64_t H, int64_t W, Plans *out) {
     return HRF_OK;
   }
   Plans p{};
-  HRF_FFT(hipfftPlan2d(&p.fwd, (int)H, (int)W, HIPFFT_D2Z));
-  HRF_FFT(hipfftPlan2d(&p.inv, (int)H, (int)W, HIPFFT_Z2D));
+  size_t wf = 0, wi = 0;
+  HRF_FFT(hipfftCreate(&p.fwd));
+  HRF_FFT(hipfftCreate(&p.inv));
+  HRF_FFT(hipfftSetAutoAllocation(p.fwd, 0));
+  HRF_FFT(hipfftSetAutoAllocation(p.inv, 0));
+  HRF_FFT(hipfftMakePlan2d(p.fwd, (int)H, (int)W, HIPFFT_D2Z, &wf));
+  HRF_FFT(hipfftMakePlan2d(p.inv, (int)H, (int)W, HIPFFT_Z2D, &wi));
+  p.work = std::max(wf, wi);
   g_plans[key] = p;
   *out = p;
   return HRF_OK;
@@ -140,12 +151,15 @@ hrf_status xcorr_peak(const double *src, const double *target, int64_t H, int64_
   double *cc = (double *)(fp + nc);
   Best *part = (Best *)(cc + H * W);
   int64_t *bidx = (int64_t *)(part + AM_BLOCKS);
+  char *fft_work = (char *)(((uintptr_t)(bidx + 1) + 255) & ~(uintptr_t)255);
   {
-    std::lock_guard<std::mutex> lk(g_plan_mu);  // plan handles are shared; bind the stream and run
+    std::lock_guard<std::mutex> lk(g_plan_mu);  // plan handles are shared; bind stream + work area, run
     Plans p{};
     if (hrf_status st = get_plans(H, W, &p)) return st;
     HRF_FFT(hipfftSetStream(p.fwd, s));
     HRF_FFT(hipfftSetStream(p.inv, s));
+    HRF_FFT(hipfftSetWorkArea(p.fwd, fft_work));
+    HRF_FFT(hipfftSetWorkArea(p.inv, fft_work));
     // hipFFT's real-to-complex transform does not modify its input
     if (!src_fft_ready) HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(src), fa));
     HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(target), fb));
@@ -166,9 +180,15 @@ hrf_status xcorr_peak(const double *src, const double *target, int64_t H, int64_
 extern "C" {
 
 int64_t hrf_register_workspace_bytes(int64_t H, int64_t W) {
+  if (H < 1 || W < 1 || H > (1 << 20) || W > (1 << 20)) return -1;
   const int64_t nc = H * (W / 2 + 1);
+  Plans p{};
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if (get_plans(H, W, &p) != HRF_OK) return -1;
+  }
   return 3 * nc * (int64_t)sizeof(hipfftDoubleComplex) + H * W * (int64_t)sizeof(double) +
-         AM_BLOCKS * (int64_t)sizeof(Best) + 64;
+         AM_BLOCKS * (int64_t)sizeof(Best) + 64 + 256 + (int64_t)p.work;
 }
 
 hrf_status hrf_register_translation_dev(const double *src, const double *target, int64_t H, int64_t W, void *work,

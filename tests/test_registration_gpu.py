@@ -153,3 +153,36 @@ def test_channel_max_multi_equals_per_laser(K):
         assert torch.equal(torch.isnan(o), torch.isnan(want))
         assert torch.equal(torch.nan_to_num(o), torch.nan_to_num(want))
     assert torch.isnan(outs[2][5, 7])
+
+
+def test_concurrent_registrations_equal_serial(K):
+    """four tiles registered at once on four streams from four host threads (as bench.py runs
+    them): the FFT plans are shared, their work areas come from each call's own workspace, so
+    the shifts and assembled stacks equal serial runs"""
+    import threading
+
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    shifts = [((0, 0), (2, -1), (0, 3), (-1, 0), (1, 1)), ((0, 0), (-3, 2), (1, -1), (2, 2), (0, -2)),
+              ((0, 0), (1, 1), (-2, 0), (0, 4), (3, -3)), ((0, 0), (0, -4), (4, 0), (-1, -1), (2, 0))]
+    tiles = [S.laser_split(S.tile(512, 512, seed=90 + i)[0], shifts=shifts[i]) for i in range(4)]
+    want = [P.register_stack(t, want_cn=True) for t in tiles]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in tiles]
+    got = [None] * 4
+
+    def run(i):
+        with torch.cuda.stream(streams[i]):
+            for _ in range(3):
+                got[i] = P.register_stack(tiles[i], want_cn=True)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    for i in range(4):
+        assert torch.equal(got[i][0], want[i][0]) and torch.equal(got[i][1], want[i][1])
+        sh = P.estimate_shifts(tiles[i], device=True).cpu().tolist()
+        assert [tuple(v) for v in sh] == list(shifts[i])
