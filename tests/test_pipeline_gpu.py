@@ -265,3 +265,44 @@ def test_multispecies_quantised_parity(mods, H, q, seed):
     assert np.array_equal(host(native[0]), oseg)
     assert np.array_equal(host(m.labels), olabs) and len(olabs) >= 1
     np.testing.assert_allclose(host(m.avgint), oavg, rtol=1e-12)
+
+
+def test_concurrent_registered_tiles_equal_isolated(mods):
+    """bench.py's current configuration: four tiles in flight, each on its own high-priority
+    stream and host thread, starting from the five per-laser acquisitions and the flat field
+    (registration with image_cn, calibrated spectra), classifiers on side streams.  Every
+    output equals the tile processed alone."""
+    P, S, OP = mods
+    from concurrent.futures import ThreadPoolExecutor
+    ref = S.reference_library(10, S.ECOLI_BOUNDS)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), S.ECOLI_BOUNDS, 10)
+    lib.refx()
+    cal = S.flat_field(768, 768)
+    tiles = [S.laser_split(S.tile(768, 768, seed=160 + t)[0]) for t in range(8)]
+
+    def run(t):
+        stack, cn = P.register_stack(t, want_cn=True)
+        r = P.process_tile(stack, lib, calibration=cal, image_cn=cn)
+        return [x.clone() for x in (r.pixel_idx, r.pixel_dist, r.cell_idx, r.counts, r.meas.segmentation,
+                                    r.identification, r.meas.avgint)]
+
+    alone = [run(t) for t in tiles]
+    torch.cuda.synchronize()
+    hi = torch.cuda.Stream.priority_range()[1]
+    streams = [torch.cuda.Stream(priority=hi) for _ in range(4)]
+
+    def worker(j):
+        res = []
+        with torch.cuda.stream(streams[j]):
+            for i in range(j, len(tiles), 4):
+                res.append((i, run(tiles[i])))
+        streams[j].synchronize()
+        return res
+    for rep in range(2):
+        with ThreadPoolExecutor(4) as ex:
+            got = [r for f in [ex.submit(worker, j) for j in range(4)] for r in f.result()]
+        torch.cuda.synchronize()
+        for i, outs in got:
+            for a, b in zip(outs[:-1], alone[i][:-1]):
+                assert torch.equal(a, b), (rep, i)
+            torch.testing.assert_close(outs[-1], alone[i][-1], rtol=1e-12, atol=0)
