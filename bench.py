@@ -472,7 +472,11 @@ def main():
                            "overlapped_with_segmentation": not args.no_overlap,
                            "isolated_kernel_ms": round(ms_iso, 4),
                            "isolated_achieved": round(flops / (ms_iso * 1e-3) / 1e12, 2),
-                           "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4)}
+                           "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4),
+                           "note": ("kernel_ms: mean launch time on the classifier's side stream inside the timed "
+                                    "region, where %d tiles are in flight and the segmentation streams run at higher "
+                                    "priority (the classifier yields to them); isolated_*: the same launch alone "
+                                    "after the timed region" % T)}
     if world == 1 and not args.no_extras:
         out["extras"] = _extras(dev, T, streams, pool, tiles, lib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
