@@ -472,11 +472,13 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
 // maps.  Every B-operand column's segment is then known at compile time, so the operand build
 // is straight-line code (a select only where the two lane halves straddle a segment bound)
 // with no LDS table lookups, and K = C + 1 (channels + the validity-bias column) instead of
-// C + nseg + 1: the zero-segment indicator terms (+1 for a segment that is zero in both the
-// pixel and the reference row) are added in the argmax epilogue, and only by a wave holding a
-// pixel with an all-zero segment (wave-uniform branch to a second copy of the sweep; each
-// prepared row carries its zero-segment mask in its pad bytes).  95 -> 96 columns: 6 k-steps
-// per 32-row block instead of 7.
+// C + nseg + 1.  The zero-segment indicator terms (+1 for a segment that is zero in both the
+// pixel and the reference row) are one extra hi-only k-step, run only by workgroups holding a
+// pixel with an all-zero segment (workgroup-uniform branch to a second copy of the sweep): its
+// A operand is the row's pad, which holds the row's indicators as fp16 1/0 (exact products, so
+// the sum equals adding the integer count after the products); its B operand is the pixel's
+// indicators.  95 -> 96 columns: 6 k-steps per 32-row block instead of 7, 19 MFMAs instead of
+// 18 in the zero-segment copy.
 struct LayEcoli {
   static constexpr int C = 95, NSEG = 5;
   __host__ __device__ static constexpr int b(int s) {
@@ -605,13 +607,15 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
 }
 
 // The library sweep of one workgroup (see classify_pixels_f16_kernel).  ZS adds the
-// zero-segment indicator terms popcount(zx & zr) to every score.  KEYED (all scores >= 0:
+// zero-segment indicator terms popcount(zx & zr) to every score, as a seventh MFMA per pixel
+// group and block: A = the row's indicator fp16s in its pad (every lane reads its row's pad;
+// the h = 1 half meets B = 0), B = the pixel's indicators (h = 0 lanes, k < NSEG).  KEYED (all scores >= 0:
 // no negative value in the workgroup's pixels or the library) runs the argmax on integer
 // keys: score bits with the low 4 mantissa bits replaced by 15 - register (so the max also
 // names the register, lower rows winning ties), a max tree per block and one compare per
 // block -- about half the VALU of a compare-and-select per score.  The 4 dropped bits are
 // <= 2^-19 relative (< 1e-5 of a distance); blocks still compete in row order.
-template <int KS16, int ROWB, int NW, bool ZS, bool KEYED>
+template <int KS16, int ROWB, int NW, int NSEG, bool ZS, bool KEYED>
 __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w, int h,
                                           const h8 (&bh0)[KS16], const h8 (&bl0)[KS16], const h8 (&bh1)[KS16],
                                           const h8 (&bl1)[KS16], uint32_t zx0, uint32_t zx1, float &best0,
@@ -631,21 +635,19 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
 #pragma unroll
   for (int reg = 0; reg < 16; ++reg) pv0[reg] = pv1[reg] = -__builtin_inff();
   int pr = 0;  // first row of the pending block
-  // ZS: the pending block's 16 row zero-segment masks (this lane's rows), packed 4 per word; read
-  // from the LDS chunk when the block's MFMAs are issued (the chunk may be gone by its epilogue)
-  uint32_t pz[4] = {0u, 0u, 0u, 0u};
+  h8 bz0, bz1;  // ZS: the pixels' zero-segment indicators (B operand of the extra k-step)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    bz0[q] = (_Float16)((h == 0 && q < NSEG && ((zx0 >> q) & 1u)) ? 1.0f : 0.0f);
+    bz1[q] = (_Float16)((h == 0 && q < NSEG && ((zx1 >> q) & 1u)) ? 1.0f : 0.0f);
+  }
   int bk0 = INT32_MIN, bk1 = INT32_MIN;        // KEYED: the pending block's keys
   int key0 = INT32_MIN, key1 = INT32_MIN;      // KEYED: best keys so far
   auto epi = [&](int lo, int hi) {
 #pragma unroll
     for (int reg = lo; reg < hi; ++reg) {
       const int r = pr + (reg & 3) + 8 * (reg >> 2);
-      float s0 = pv0[reg], s1 = pv1[reg];
-      if (ZS) {
-        const uint32_t zr = (pz[reg >> 2] >> (8 * (reg & 3))) & 0xffu;
-        s0 += (float)__popc(zx0 & zr);
-        s1 += (float)__popc(zx1 & zr);
-      }
+      const float s0 = pv0[reg], s1 = pv1[reg];
       if (KEYED) {
         bk0 = max(bk0, (__float_as_int(s0) & -16) | (15 - reg));
         bk1 = max(bk1, (__float_as_int(s1) & -16) | (15 - reg));
@@ -683,14 +685,9 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
 #pragma unroll
     for (int rb = 0; rb < RCH; rb += 32) {
       f32x16 acc0 = {0}, acc1 = {0};
-      uint32_t cz[4] = {0u, 0u, 0u, 0u};
-      if (ZS) {
-        const unsigned char *zl = reinterpret_cast<const unsigned char *>(buf) + (rb + 4 * h) * ROWB + 4 * KP;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg)
-          cz[reg >> 2] |= (uint32_t)zl[((reg & 3) + 8 * (reg >> 2)) * ROWB] << (8 * (reg & 3));
-      }
       const char *row = buf + (rb + j) * ROWB + 16 * h;
+      h8 az;
+      if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + j) * ROWB + 4 * KP);
 #pragma unroll
       for (int s = 0; s < KS16; ++s) {
         const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
@@ -703,12 +700,12 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
         epi((16 * s) / KS16, (16 * (s + 1)) / KS16);  // previous block, slice s
       }
+      if (ZS) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(az, bz0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(az, bz1, acc1, 0, 0, 0);
+      }
       pv0 = acc0;
       pv1 = acc1;
-      if (ZS) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pz[q] = cz[q];
-      }
       pr = c * RCH + rb;
     }
   }
@@ -731,6 +728,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   constexpr int KP = 16 * KS16;
   constexpr int ROWB = 4 * KP + 16;
   static_assert((RCH * ROWB) % 1024 == 0, "chunk must be whole 1 KiB pieces");
+  static_assert(L::NSEG <= 6, "the pad holds 6 indicators (fp16 6-7 of row 0: the negative flag)");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j = lane & 31, h = lane >> 5;
@@ -747,7 +745,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
     build_b_lay<L, KS16>(v1, stg, lane, j, h, bh1, bl1, zx1, ng1);
   }
   // the library's "has a negative value" flag sits in row 0's pad (ref_negflag_kernel)
-  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 4);
+  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
   float best0 = -__builtin_inff(), best1 = -__builtin_inff();
   int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
   const char *gref = reinterpret_cast<const char *>(refh);
@@ -757,7 +755,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   const bool zs = __syncthreads_or((zx0 | zx1) != 0);
   const bool keyed = !libneg && !__syncthreads_or((ng0 | ng1) != 0);
 #define HRF_SWEEP(Z, K) \
-  lay_sweep<KS16, ROWB, NW, Z, K>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1)
+  lay_sweep<KS16, ROWB, NW, L::NSEG, Z, K>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1)
   if (keyed) {
     if (zs) HRF_SWEEP(true, true);
     else HRF_SWEEP(false, true);
@@ -785,8 +783,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
 }
 
 // mode-2 table: {hi[KP], lo[KP], pad 16 B} fp16 per row, KP = 16 * ceil((C + 1) / 16); column C
-// is the validity bias (0 real rows, -1024 padding rows); byte 4*KP of the row holds the row's
-// zero-segment mask.
+// is the validity bias (0 real rows, -1024 padding rows); pad fp16 s (s < nseg) = 1 when the row's
+// segment s is all zero (the indicator k-step's A operand), fp16 6-7 of row 0 = the library's
+// negative-value flag.
 __global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
                                     int32_t Rpad, _Float16 *__restrict__ refh) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -797,7 +796,6 @@ __global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, in
   hi[C] = (_Float16)(r < R ? 0.0f : -1024.0f);
   if (r >= R) return;
   const float *x = ref + r * C;
-  uint8_t zr = 0;
   for (int s = 0; s < bd.nseg; ++s) {
     double nn = 0.0;
     for (int c = bd.b[s]; c < bd.b[s + 1]; ++c) nn += (double)x[c] * (double)x[c];
@@ -808,19 +806,18 @@ __global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, in
       hi[c] = h;
       lo[c] = (_Float16)(v - (float)h);
     }
-    if (!(nn > 0)) zr |= (uint8_t)(1u << s);
+    if (!(nn > 0)) hi[2 * KP + s] = (_Float16)1.0f;
   }
-  reinterpret_cast<uint8_t *>(hi + 2 * KP)[0] = zr;
 }
 
-// row 0's pad word (byte 4*KP + 4) = 1 when any library value is negative (the keyed argmax
+// row 0's last pad word (byte 4*KP + 12) = 1 when any library value is negative (the keyed argmax
 // needs every score >= 0); one workgroup, after ref_prep_lay_kernel
 __global__ __launch_bounds__(256) void ref_negflag_kernel(const float *__restrict__ ref, int64_t n, int32_t KP,
                                                           _Float16 *__restrict__ refh) {
   int neg = 0;
   for (int64_t i = threadIdx.x; i < n; i += 256) neg |= ref[i] < 0.0f;
   neg = __syncthreads_or(neg);
-  if (threadIdx.x == 0) *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(refh) + 4 * KP + 4) = (uint32_t)neg;
+  if (threadIdx.x == 0) *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(refh) + 4 * KP + 12) = (uint32_t)neg;
 }
 
 // 1 = E. coli layout, 2 = synthetic-community layout, 0 = other

@@ -335,6 +335,9 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
     ref = S.reference_library(nbit, bounds) if len(bounds) > 2 else \
         np.abs(np.random.default_rng(0).normal(size=(31, 32))).astype(np.float32)
     R, C = ref.shape
+    ref = ref.copy()
+    ref[3, bounds[0]:bounds[1]] = 0.0     # library rows with a zero segment: the indicator terms
+    ref[5, bounds[-2]:bounds[-1]] = 0.0   # meet the pixels' zero segments below
     stack, truth, lay, _ = S.tile(96, 80, nbit=max(nbit, 2), bounds=bounds, seed=3, ncells=8) if len(bounds) > 2 \
         else (None, None, None, None)
     if stack is None:
@@ -350,7 +353,7 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
 
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
 def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
-    """mode 2 (indicator terms in the epilogue) vs mode 1 (indicator columns) on a 512x384
+    """mode 2 (indicator terms as an extra k-step) vs mode 1 (indicator columns) on a 512x384
     tile whose first rows carry zero segments; the cell pixels checked exactly against the
     restatement"""
     stack, truth, lay, ref = S.tile(512, 384, nbit=nbit, bounds=bounds, seed=21)
