@@ -227,19 +227,20 @@ __device__ int rs_scan_rows(int *off, int *part, int bh) {
   const int lo = t * chunk, hi = min(bh, lo + chunk);
   int acc = 0;
   for (int r = lo; r < hi; ++r) acc += off[r];
-  part[t] = acc;
+  // exclusive scan of the per-thread sums: shuffles within each wave, wave totals in part[]
+  const int incl = hrf::wave_inclusive_scan(acc);
+  const int wave = t >> 6;
+  if ((t & 63) == 63) part[wave] = incl;
   __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int i = 0; i < RS_T; ++i) {
-      const int v = part[i];
-      part[i] = run;
-      run += v;
-    }
-    off[bh] = run;
+  int wbase = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < RS_T / 64; ++i) {
+    const int v = part[i];
+    wbase += i < wave ? v : 0;
+    all += v;
   }
-  __syncthreads();
-  int base = part[t];
+  if (t == 0) off[bh] = all;
+  int base = wbase + incl - acc;
   for (int r = lo; r < hi; ++r) {
     const int v = off[r];
     off[r] = base;

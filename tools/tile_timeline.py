@@ -12,7 +12,7 @@ if len(sys.argv) > 1 and sys.argv[1].endswith(".db"):
     import sqlite3
     c = sqlite3.connect(sys.argv[1])
     rows = list(c.execute("select name, start, end from kernels order by start"))
-    idx = [i for i, r in enumerate(rows) if "channel_max_multi_kernel" in r[0]]   # a tile's first kernel
+    idx = [i for i, r in enumerate(rows) if "channel_max_multi" in r[0]]   # a tile's first kernel
     seq = rows[idx[-1]:]
     agg = collections.defaultdict(lambda: [0, 0.0])
     for n, s, e in seq:
