@@ -353,7 +353,10 @@ def main():
     # default-priority side streams (+5 % end to end with four tiles in flight, interleaved A/B;
     # the classifier then fills the gaps, so its in-bench launch time includes the yielding).
     # HRF_PRIORITY=0 turns it off.
-    prio = torch.cuda.Stream.priority_range()[1] if os.environ.get("HRF_PRIORITY", "1") == "1" else 0
+    pmode = os.environ.get("HRF_PRIORITY", "1")
+    prio = torch.cuda.Stream.priority_range()[1] if pmode == "1" else 0
+    if pmode == "2":          # the reverse: classifier side streams high, segmentation default
+        P.SIDE_PRIORITY = torch.cuda.Stream.priority_range()[1]
     streams = [torch.cuda.Stream(device=dev, priority=prio) for _ in range(T)]
     pool = None
     if T > 1:

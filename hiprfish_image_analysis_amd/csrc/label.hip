@@ -95,21 +95,36 @@ __global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t
     const int64_t gr = r0 + lr, gc = c0 + lc;
     const int32_t v = (gr < H && gc < W) ? val(gr * W + gc) : 0;
     lv[li] = v;
-    lp[li] = v ? li : -1;
   }
   __syncthreads();
+  // Horizontal runs come from a ballot: a wave holds two tile rows (lanes 0-31, 32-63); a
+  // pixel's initial parent is the start of its run (the run's least index), so no union is
+  // spent inside a run.
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int li = tid + 256 * k, lc = li & 31;
+    const int32_t v = lv[li];
+    const unsigned long long join = __ballot(v && lc > 0 && lv[li - 1] == v);
+    const unsigned row = (unsigned)(join >> (threadIdx.x & 32));
+    const unsigned starts = ~row & (lc == 31 ? 0xffffffffu : ((2u << lc) - 1u));  // bit 0 never joins
+    lp[li] = v ? (li - lc) + (31 - __builtin_clz(starts)) : -1;
+  }
+  __syncthreads();
+  // Vertical links: once per overlap segment of two runs (its first column); a diagonal link
+  // only where neither the pixel's own run nor the other row's run already implies it through
+  // a vertical one.  Every adjacency of equal values ends up linked, with ~one union per
+  // (run, run) contact instead of one per neighbour pair.
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int li = tid + 256 * k, lr = li >> 5, lc = li & 31;
     const int32_t v = lv[li];
-    if (!v) continue;
-    if (lc > 0 && lv[li - 1] == v) union_lds(lp, li, li - 1);
-    if (lr > 0) {
-      if (lv[li - 32] == v) union_lds(lp, li, li - 32);
-      if (CONN == 2) {
-        if (lc > 0 && lv[li - 33] == v) union_lds(lp, li, li - 33);
-        if (lc < 31 && lv[li - 31] == v) union_lds(lp, li, li - 31);
-      }
+    if (!v || lr == 0) continue;
+    const bool l = lc > 0 && lv[li - 1] == v, u = lv[li - 32] == v;
+    const bool ul = lc > 0 && lv[li - 33] == v, ur = lc < 31 && lv[li - 31] == v;
+    if (u && !(l && ul)) union_lds(lp, li, li - 32);
+    if (CONN == 2) {
+      if (ul && !l && !u) union_lds(lp, li, li - 33);
+      if (ur && !u && !(lc < 31 && lv[li + 1] == v)) union_lds(lp, li, li - 31);
     }
   }
   __syncthreads();
@@ -564,9 +579,11 @@ hrf_status hrf_fill_holes(const uint8_t *mask, int64_t H, int64_t W, uint8_t *ou
                           int32_t *flag_ws, hrf_stream_t stream) {
   const int64_t n = H * W;
   hipStream_t s = (hipStream_t)stream;
-  if (hrf_status st = hrf_cc_roots(mask, 2, H, W, 1, parent_ws, stream)) return st;
+  if (hrf_status st = check_hw(H, W, "fill_holes")) return st;
   if (n == 0) return HRF_OK;
-  HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * n, s));
+  HRF_REQUIRE(mask && out && parent_ws && flag_ws, "fill_holes: null buffer");
+  // the compression pass clears the root flags (no memset launch)
+  if (hrf_status st = run_cc(MaskV{mask, 1}, H, W, 1, parent_ws, s, flag_ws)) return st;
   border_roots_kernel<<<hrf::stream_grid(2 * (H + W)), 256, 0, s>>>(parent_ws, H, W, flag_ws);
   fill_holes_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(mask, parent_ws, flag_ws, n, out);
   HRF_LAUNCHED();
@@ -577,9 +594,10 @@ hrf_status hrf_clear_border(const int32_t *labels, int64_t H, int64_t W, int32_t
                             int32_t *flag_ws, hrf_stream_t stream) {
   const int64_t n = H * W;
   hipStream_t s = (hipStream_t)stream;
-  if (hrf_status st = hrf_cc_roots(labels, 1, H, W, 2, parent_ws, stream)) return st;
+  if (hrf_status st = check_hw(H, W, "clear_border")) return st;
   if (n == 0) return HRF_OK;
-  HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * n, s));
+  HRF_REQUIRE(labels && out && parent_ws && flag_ws, "clear_border: null buffer");
+  if (hrf_status st = run_cc(LabelV{labels}, H, W, 2, parent_ws, s, flag_ws)) return st;
   border_roots_kernel<<<hrf::stream_grid(2 * (H + W)), 256, 0, s>>>(parent_ws, H, W, flag_ws);
   clear_border_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, parent_ws, flag_ws, n, out);
   HRF_LAUNCHED();

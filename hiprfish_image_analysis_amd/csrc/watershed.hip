@@ -47,19 +47,39 @@ struct WsState {
   int32_t *dst;  // basin distance (relaxation tie-break only, see ws_pass_kernel)
 };
 
-__global__ void ws_init_kernel(const double *__restrict__ f, int negate, const int32_t *__restrict__ markers,
-                               const uint8_t *__restrict__ mask, int64_t n, double *__restrict__ lam,
-                               int32_t *__restrict__ hop, int32_t *__restrict__ lab, int32_t *__restrict__ dst,
-                               int32_t *__restrict__ ptr) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+// One workgroup per 32x32 tile: both ping-pong buffers get the initial state (so a tile that
+// never runs keeps a valid copy in each), and tile_work[t] = 1 iff the tile holds a pixel the
+// relaxation can change (in the mask and not a marker).  Tiles without one -- the background
+// beyond the rough mask, about a quarter of an E. coli tile -- are skipped by every pass.
+__global__ __launch_bounds__(256) void ws_init_kernel(const double *__restrict__ f, int negate,
+                                                      const int32_t *__restrict__ markers,
+                                                      const uint8_t *__restrict__ mask, int64_t H, int64_t W,
+                                                      WsState a, WsState b, int32_t *__restrict__ ptr,
+                                                      int32_t *__restrict__ tile_work) {
+  const int tid = threadIdx.x;
+  int work = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t gr = (int64_t)blockIdx.y * WT + (tid >> 5) + 8 * k, gc = (int64_t)blockIdx.x * WT + (tid & 31);
+    if (gr >= H || gc >= W) continue;
+    const int64_t i = gr * W + gc;
     const bool in = !mask || mask[i];
     const int32_t m = in ? markers[i] : 0;
-    lam[i] = m ? (negate ? -f[i] : f[i]) : __builtin_inf();
-    hop[i] = m ? 0 : HOP_INF;
-    dst[i] = m ? 0 : HOP_INF;
-    lab[i] = m;
+    const double l = m ? (negate ? -f[i] : f[i]) : __builtin_inf();
+    const int32_t h = m ? 0 : HOP_INF;
+    a.lam[i] = l;
+    b.lam[i] = l;
+    a.hop[i] = h;
+    b.hop[i] = h;
+    a.dst[i] = h;
+    b.dst[i] = h;
+    a.lab[i] = m;
+    b.lab[i] = m;
     ptr[i] = -1;
+    work |= in && !m;
   }
+  work = __syncthreads_or(work);
+  if (tid == 0) tile_work[blockIdx.y * gridDim.x + blockIdx.x] = work;
 }
 
 __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_t b1, double l2, int32_t h2,
@@ -85,7 +105,8 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
                                                       int32_t *__restrict__ changed,
                                                       const int32_t *__restrict__ prev_tile,
                                                       int32_t *__restrict__ cur_tile,
-                                                      int32_t *__restrict__ next_tile) {
+                                                      int32_t *__restrict__ next_tile,
+                                                      const int32_t *__restrict__ tile_work) {
   __shared__ double sl[WL * WL];
   __shared__ double sf[WL * WL];
   __shared__ int32_t sh[WL * WL];
@@ -98,6 +119,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   // next for the following pass (last read as prev by the pass before this one, which has
   // finished), so no memset is needed between passes.
   if (tid == 0) next_tile[blockIdx.y * gridDim.x + blockIdx.x] = 0;
+  if (!tile_work[blockIdx.y * gridDim.x + blockIdx.x]) return;  // nothing relaxable: state fixed
   // A tile whose 3x3 tile neighbourhood did not change in the previous pass is skipped: its
   // own state did not change either, so both ping-pong buffers already hold it.
   if (prev_tile) {
@@ -319,7 +341,7 @@ int64_t walker_bytes(int32_t cap, int32_t hcap, int32_t gcap) {
 
 struct WsBuffers {
   WsState a, b;
-  int32_t *ptr, *list, *retry, *tf;
+  int32_t *ptr, *list, *retry, *tf, *tw;
 };
 
 WsBuffers carve(void *state_ws, int64_t n, int64_t ntiles) {
@@ -331,7 +353,7 @@ WsBuffers carve(void *state_ws, int64_t n, int64_t ntiles) {
   B.list = (int32_t *)(ws + 48 * n);
   B.retry = (int32_t *)(ws + 52 * n);
   B.tf = (int32_t *)(ws + 56 * n);
-  (void)ntiles;
+  B.tw = B.tf + 3 * ntiles;
   return B;
 }
 
@@ -342,7 +364,7 @@ extern "C" {
 int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W) {
   if (H < 0 || W < 0) return -1;
   const int64_t ntiles = hrf::cdiv(W, WT) * hrf::cdiv(H, WT);
-  return 56 * H * W + 12 * ntiles + 256;
+  return 56 * H * W + 16 * ntiles + 256;
 }
 
 // flag_ws (>= 8 int32): [0] change flag of a batch's last pass, [1] the other passes',
@@ -362,8 +384,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   const int64_t ntiles = (int64_t)grid.x * grid.y;
   WsBuffers B = carve(state_ws, n, ntiles);
   WsState a = B.a, b = B.b;
-  ws_init_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(image, negate, markers, mask, n, a.lam, a.hop, a.lab, a.dst,
-                                                      B.ptr);
+  ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw);
   HRF_LAUNCHED();
   int32_t *tf = B.tf;  // per-tile change flags, three rotating generations
   int32_t hflag[4] = {0, 0, 0, 0};  // host copies of flag_ws[0..3]
@@ -386,10 +407,10 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
         int32_t *chg = flag_ws + (k == batch - 1 ? 0 : 1);
         if (relabel)
           ws_pass_kernel<true><<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev, cur,
-                                                    next);
+                                                    next, B.tw);
         else
           ws_pass_kernel<false><<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev, cur,
-                                                     next);
+                                                     next, B.tw);
         WsState t = a;
         a = b;
         b = t;

@@ -256,15 +256,16 @@ class TileResult:
 
 
 _SIDE_STREAMS: dict = {}
+SIDE_PRIORITY = 0   # stream priority of the classifier side streams (torch convention: lower = higher)
 
 
 def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
     """the side stream paired with `main` (one per caller stream, so concurrent tiles on
     different streams do not serialise on a shared one)"""
-    key = (main.device, main.cuda_stream)
+    key = (main.device, main.cuda_stream, SIDE_PRIORITY)
     s = _SIDE_STREAMS.get(key)
     if s is None:
-        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=main.device)
+        s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=main.device, priority=SIDE_PRIORITY)
     return s
 
 

@@ -70,6 +70,15 @@ def main():
         ms = timed(lambda: K.label_sums(stack, seg, maxlab))
         print("label_sums (%d labels, %.0f %% fg): %.3f ms  %.0f GB/s algorithmic" % (maxlab, 100.0 * fg / H / W, ms,
                                                                                       nb2 / ms / 1e6))
+        # counter calibration for this access width (MI355X_MICROARCH.md: widths other than 16 B
+        # per lane are uncalibrated): every pixel labelled (16x16 blocks), so the algorithmic
+        # bytes are the whole stack + the label map and FETCH_SIZE / them is the width's factor
+        rr = torch.arange(H, device="cuda", dtype=torch.int32)[:, None] // 16
+        cc = torch.arange(W, device="cuda", dtype=torch.int32)[None, :] // 16
+        dense = (1 + rr * (W // 16) + cc).contiguous()
+        nbd = H * W * (4 * C + 4)
+        ms = timed(lambda: K.label_sums(stack, dense, int(dense.max())))
+        print("label_sums dense calibration map: %.3f ms  %.0f GB/s (%.0f bytes)" % (ms, nbd / ms / 1e6, nbd))
         calp = (0.5 + torch.rand((H, W), device="cuda"))
         ms = timed(lambda: K.label_sums(stack, seg, maxlab, cal=calp, cal_range=(0, 32)))
         print("label_sums plane cal: %.3f ms  %.0f GB/s algorithmic" % (ms, nb2 / ms / 1e6))
