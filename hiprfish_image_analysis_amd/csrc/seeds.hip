@@ -477,19 +477,31 @@ __global__ void box_kernel(const int32_t *__restrict__ lab, int64_t H, int64_t W
     const int32_t l = p < n ? lab[p] : 0;
     bool active = l > 0 && l <= maxlab;
     const int32_t r = (int32_t)(p / W), c = (int32_t)(p - (p / W) * W);
+    // the wave's 64 pixels on one image row (always, when 64 divides W): a label's box within
+    // the wave is its first and last lane -- no reductions
+    const int64_t pb = p - lane, rb = pb / W;
+    const bool one_row = pb + 63 < n && (pb + 63) / W == rb;
     unsigned long long pending = __ballot(active);
     while (pending) {
       const int leader = __ffsll((long long)pending) - 1;
       const int32_t k = __shfl(l, leader, 64);
       const bool m = active && l == k;
       const unsigned long long same = __ballot(m);
-      int32_t rmin = m ? r : 0x7fffffff, cmin = m ? c : 0x7fffffff, rmax = m ? r : -1, cmax = m ? c : -1;
+      int32_t rmin, cmin, rmax, cmax;
+      if (one_row) {
+        const int32_t cb = (int32_t)(pb - rb * W);
+        rmin = rmax = (int32_t)rb;
+        cmin = cb + leader;
+        cmax = cb + 63 - __builtin_clzll(same);
+      } else {
+        rmin = m ? r : 0x7fffffff, cmin = m ? c : 0x7fffffff, rmax = m ? r : -1, cmax = m ? c : -1;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        rmin = min(rmin, __shfl_xor(rmin, o, 64));
-        cmin = min(cmin, __shfl_xor(cmin, o, 64));
-        rmax = max(rmax, __shfl_xor(rmax, o, 64));
-        cmax = max(cmax, __shfl_xor(cmax, o, 64));
+        for (int o = 32; o > 0; o >>= 1) {
+          rmin = min(rmin, __shfl_xor(rmin, o, 64));
+          cmin = min(cmin, __shfl_xor(cmin, o, 64));
+          rmax = max(rmax, __shfl_xor(rmax, o, 64));
+          cmax = max(cmax, __shfl_xor(cmax, o, 64));
+        }
       }
       if (lane == leader) {
         atomicMin(&box[k * 4 + 0], rmin);

@@ -268,21 +268,49 @@ __global__ void moments_kernel(const int32_t *__restrict__ lab, int64_t H, int64
     const bool ok = l > 0 && l <= maxlab;
     const int64_t r = p / W, c = p - (p / W) * W;
     const int64_t key = ok ? (int64_t)l * 6 : 0;
-    // six aggregated adds, one per moment, keyed by the label
+    // six aggregated adds, one per moment, keyed by the label.  When the wave's 64 pixels lie on
+    // one image row (always, when 64 divides W), r is uniform: the count is a popcount, the
+    // row moments follow from it, and a label's lanes usually form one run [c0, c1] whose column
+    // sums have closed forms -- no reductions; otherwise wave sums as before.
     unsigned long long pending = __ballot(ok);
     bool active = ok;
     const int lane = hrf::lane_id();
+    const int64_t pb = p - lane, rb = pb / W;
+    const bool one_row = pb + 63 < n && (pb + 63) / W == rb;
     while (pending) {
       const int leader = __ffsll((long long)pending) - 1;
       const int64_t k = __shfl(key, leader, 64);
       const bool m = active && key == k;
       const unsigned long long same = __ballot(m);
-      const unsigned long long a0 = hrf::wave_sum<unsigned long long>(m ? 1ull : 0ull);
-      const unsigned long long a1 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)r : 0ull);
-      const unsigned long long a2 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)c : 0ull);
-      const unsigned long long a3 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(r * r) : 0ull);
-      const unsigned long long a4 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(c * c) : 0ull);
-      const unsigned long long a5 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(r * c) : 0ull);
+      unsigned long long a0, a1, a2, a3, a4, a5;
+      if (one_row) {
+        const unsigned long long cnt = (unsigned long long)__popcll(same);
+        const unsigned long long cb = (unsigned long long)(pb - rb * W), rr = (unsigned long long)rb;
+        const int hi = 63 - __builtin_clzll(same);
+        unsigned long long sc, scc;
+        if ((int)cnt == hi - leader + 1) {  // one run: closed forms over [c0, c1]
+          const unsigned long long c0 = cb + leader, c1 = cb + hi;
+          sc = (c0 + c1) * cnt / 2;
+          auto sq = [](unsigned long long x) { return x * (x + 1) * (2 * x + 1) / 6; };
+          scc = sq(c1) - (c0 ? sq(c0 - 1) : 0ull);
+        } else {
+          sc = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)c : 0ull);
+          scc = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(c * c) : 0ull);
+        }
+        a0 = cnt;
+        a1 = cnt * rr;
+        a2 = sc;
+        a3 = cnt * rr * rr;
+        a4 = scc;
+        a5 = rr * sc;
+      } else {
+        a0 = hrf::wave_sum<unsigned long long>(m ? 1ull : 0ull);
+        a1 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)r : 0ull);
+        a2 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)c : 0ull);
+        a3 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(r * r) : 0ull);
+        a4 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(c * c) : 0ull);
+        a5 = hrf::wave_sum<unsigned long long>(m ? (unsigned long long)(r * c) : 0ull);
+      }
       if (lane == leader) {
         atomicAdd(mom + k + 0, a0);
         atomicAdd(mom + k + 1, a1);

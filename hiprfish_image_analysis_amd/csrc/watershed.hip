@@ -383,6 +383,10 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   dim3 grid((unsigned)hrf::cdiv(W, WT), (unsigned)hrf::cdiv(H, WT));
   const int64_t ntiles = (int64_t)grid.x * grid.y;
   WsBuffers B = carve(state_ws, n, ntiles);
+  // Buffer a's labels live in out_labels: every batch runs an even number of passes, so the
+  // converged labels end in a, and no final copy is needed (kept as a fallback below).
+  HRF_REQUIRE(out_labels != markers, "watershed: out_labels must not alias markers");
+  B.a.lab = out_labels;
   WsState a = B.a, b = B.b;
   ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw);
   HRF_LAUNCHED();
@@ -496,7 +500,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       ties_host[2] = hflag[3];
     }
   }
-  HRF_HIP(hipMemcpyAsync(out_labels, a.lab, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  if (a.lab != out_labels) HRF_HIP(hipMemcpyAsync(out_labels, a.lab, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
   if (passes_host) *passes_host = passes;
   return HRF_OK;
 }
