@@ -44,7 +44,8 @@ F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (mo
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (modes 1, 2)
 F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
-               2: "classify_pixels_lay_kernel<LayEcoli>"}
+               2: ("classify_pixels_lay_kernel<LayEcoli>" if os.environ.get("HRF_CLASSIFY_MFMA16") == "0"
+                   else "classify_pixels_lay16_kernel<LayEcoli>")}
 # algorithmic work (DESIGN.md "Measurement"):
 NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixel, ~20 f64 ops each
 E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort
@@ -470,7 +471,9 @@ def main():
                            "kernel": KERNEL_NAME[mode],
                            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                            "frac": round(ach / peak, 4), "traffic": traffic, "kernel_ms": round(ms, 4),
-                           "mfma_dtype": "f16 (split hi/lo, 3 MFMA per f32 product)" if mode else "f32",
+                           "mfma_dtype": ("f16 (split hi/lo, 3 MFMA per f32 product; v_mfma_f32_%s_f16)" %
+                                          ("32x32x16" if "lay_kernel" in KERNEL_NAME[mode] else "16x16x32")
+                                          if mode else "f32"),
                            "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4),
                            "overlapped_with_segmentation": not args.no_overlap,
                            "isolated_kernel_ms": round(ms_iso, 4),

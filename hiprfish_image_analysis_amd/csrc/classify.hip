@@ -481,12 +481,14 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
 // 18 in the zero-segment copy.
 struct LayEcoli {
   static constexpr int C = 95, NSEG = 5;
+  static constexpr int PADB = 32;  // row pad bytes: 416-byte rows (see lay_sweep16's bank note)
   __host__ __device__ static constexpr int b(int s) {
     return s <= 0 ? 0 : s == 1 ? 32 : s == 2 ? 55 : s == 3 ? 75 : s == 4 ? 89 : 95;
   }
 };
 struct LayMulti {
   static constexpr int C = 63, NSEG = 4;
+  static constexpr int PADB = 16;
   __host__ __device__ static constexpr int b(int s) { return s <= 0 ? 0 : s == 1 ? 23 : s == 2 ? 43 : s == 3 ? 57 : 63; }
 };
 
@@ -726,7 +728,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
                                                                      float *__restrict__ best_dist) {
   constexpr int KS16 = lay_ks16<L>();
   constexpr int KP = 16 * KS16;
-  constexpr int ROWB = 4 * KP + 16;
+  constexpr int ROWB = 4 * KP + L::PADB;
   static_assert((RCH * ROWB) % 1024 == 0, "chunk must be whole 1 KiB pieces");
   static_assert(L::NSEG <= 6, "the pad holds 6 indicators (fp16 6-7 of row 0: the negative flag)");
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -782,17 +784,291 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   }
 }
 
+// ---- the same sweep on v_mfma_f32_16x16x32_f16 -------------------------------------------
+// Same table, same split-fp16 products, same argmax rules; the MFMA shape differs: A = 16
+// library rows x 32 columns (lane: row lane & 15, columns 32t + 8Q..+7, Q = lane >> 4), B = 32
+// columns x 16 pixels (lane: pixel lane & 15, the same columns), C = 16 x 16 (lane: pixel lane &
+// 15, rows 4Q..4Q+3).  A wave holds four 16-pixel groups.  At equal cycles per flop, this
+// shape holds a higher clock than 32x32x16 under load (MI355X_MICROARCH.md, matrix-core DVFS).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// B operand of the 16-pixel sub-group g (0/1) of a staged 32-pixel group: lane pixel
+// jj = (lane & 15) + 16 g, columns 32t + 8Q + q.  The four quarter-lanes of a pixel split its
+// columns; segment norms are summed over them (two shuffles).  Arithmetic as build_b_lay.
+template <class L, int KT>
+__device__ __forceinline__ void build_b_lay16(const float *stg, int lane, int g, h8 (&bh)[KT], h8 (&bl)[KT],
+                                              uint32_t &zx, uint32_t &neg) {
+  const int jj = (lane & 15) + 16 * g, Q = lane >> 4;
+  const float *pc = stg + jj * L::C + 8 * Q;
+  float raw[KT][8];
+  int sg[KT][8];
+  float nn[L::NSEG];
+  uint32_t nzs[L::NSEG];
+  uint32_t sgn = 0;
+#pragma unroll
+  for (int s = 0; s < L::NSEG; ++s) {
+    nn[s] = 0.0f;
+    nzs[s] = 0u;
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 32 * t + 8 * Q + q;
+      int seg = -2;
+      if (k == L::C) seg = -1;
+      else if (k < L::C) {
+        seg = 0;
+#pragma unroll
+        for (int u = 1; u < L::NSEG; ++u) seg += k >= L::b(u) ? 1 : 0;
+      }
+      sg[t][q] = seg;
+      const float r = pc[32 * t + q];  // past the row end: another pixel's value, masked here
+      const float x = seg >= 0 ? r : 0.0f;
+      raw[t][q] = x;
+      const uint32_t xb = __float_as_uint(x);
+      sgn |= xb;
+      const float x2 = x * x;
+#pragma unroll
+      for (int s = 0; s < L::NSEG; ++s) {
+        nn[s] += seg == s ? x2 : 0.0f;
+        nzs[s] |= seg == s ? (xb << 1) : 0u;
+      }
+    }
+  neg = sgn >> 31;
+  float inv[L::NSEG];
+  zx = 0;
+#pragma unroll
+  for (int s = 0; s < L::NSEG; ++s) {
+    float t = nn[s] + __shfl_xor(nn[s], 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    uint32_t nz = nzs[s] | __shfl_xor(nzs[s], 16, 64);
+    nz |= __shfl_xor(nz, 32, 64);
+    inv[s] = nz ? rsqrtf(t) : 0.0f;
+    zx |= (nz ? 0u : 1u) << s;
+    if (nz && !(t >= 1e-30f)) {  // f32 underflow: redo in f64
+      double td = 0.0;
+#pragma unroll
+      for (int tt = 0; tt < KT; ++tt)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (sg[tt][q] == s) td += (double)raw[tt][q] * (double)raw[tt][q];
+      td += __shfl_xor(td, 16, 64);
+      td += __shfl_xor(td, 32, 64);
+      inv[s] = (float)(1.0 / sqrt(td));
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    h8 vh, vl;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int seg = sg[t][q];
+      float m = seg == -1 ? 1.0f : 0.0f;
+#pragma unroll
+      for (int s = 0; s < L::NSEG; ++s) m = seg == s ? inv[s] : m;
+      float x = seg >= 0 ? raw[t][q] * m : m;
+      asm volatile("" : "+v"(x));  // round to f32 first: no fused multiply-to-f16
+      const _Float16 hv = (_Float16)x;
+      vh[q] = hv;
+      vl[q] = (_Float16)(x - (float)hv);
+    }
+    bh[t] = vh;
+    bl[t] = vl;
+  }
+}
+
+template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED>
+__device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
+                                            const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t (&zx)[4],
+                                            float (&best)[4], int (&bi)[4]) {
+  constexpr int KP = 32 * KT;
+  constexpr int CHB = RCH * ROWB;
+  constexpr int NPC = CHB / 1024;
+  const int rl = lane & 15, Q = lane >> 4;
+  // three chunk buffers: chunk c + 2 streams in while c feeds the MFMAs and c + 1 lands
+  auto issue = [&](int c) {
+    const char *g = gref + (int64_t)c * CHB + lane * 16;
+    char *l = ldsb + (c % 3) * CHB;
+    for (int q = w; q < NPC; q += NW)
+      __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
+  };
+  constexpr int MINE_LO = NPC / NW;                  // pieces per wave: MINE_LO or MINE_LO + 1
+  const int mine = (NPC - w + NW - 1) / NW;
+  issue(0);
+  if (nch > 1) issue(1);
+  f32x4 pv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pv[g][i] = -__builtin_inff();
+  int pr = 0;  // first row of the pending block
+  h8 bz[4];    // ZS: the pixels' zero-segment indicators (Q == 0 lanes, k < NSEG)
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bz[g][q] = (_Float16)((Q == 0 && q < NSEG && ((zx[g] >> q) & 1u)) ? 1.0f : 0.0f);
+  int key[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) key[g] = INT32_MIN;
+  // epilogue of the pending block, groups [g0, g1): this lane's rows pr + 4Q + i
+  auto epi = [&](int g0, int g1) {
+#pragma unroll
+    for (int g = g0; g < g1; ++g) {
+      if (KEYED) {
+        int bk = INT32_MIN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bk = max(bk, (__float_as_int(pv[g][i]) & -16) | (15 - i));
+        if (bk > key[g]) {
+          key[g] = bk;
+          bi[g] = pr;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (pv[g][i] > best[g]) {
+            best[g] = pv[g][i];
+            bi[g] = pr + i;
+          }
+      }
+    }
+  };
+  for (int c = 0; c < nch; ++c) {
+    // chunk c landed for this wave: only chunk c + 1's pieces may still be outstanding (loads
+    // retire in order; hipcc does not count LDS-DMA before the barrier, see lay_sweep)
+    if (c + 1 >= nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (mine > MINE_LO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO) : "memory");
+    __syncthreads();  // every wave's pieces of c landed; everyone is past chunk c - 1
+    if (c + 2 < nch) issue(c + 2);
+    const char *buf = ldsb + (c % 3) * CHB;
+#pragma unroll
+    for (int rb = 0; rb < RCH; rb += 16) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char *row = buf + (rb + rl) * ROWB + 16 * Q;
+      h8 az;
+      if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + rl) * ROWB + 4 * KP);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
+        const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 64 * t);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
+        epi((4 * t) / KT, (4 * (t + 1)) / KT);  // previous block, slice t
+      }
+      if (ZS) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz[g], acc[g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pv[g] = acc[g];
+      pr = c * RCH + rb;
+    }
+  }
+  epi(0, 4);  // the last block
+  if (KEYED) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bi[g] += 15 - (key[g] & 15);
+      best[g] = __int_as_float(key[g] & -16);
+    }
+  }
+}
+
+template <class L, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(const float *__restrict__ stack,
+                                                                       int64_t P, const _Float16 *__restrict__ refh,
+                                                                       int32_t R, int32_t Rpad,
+                                                                       int32_t *__restrict__ best_idx,
+                                                                       float *__restrict__ best_dist) {
+  constexpr int KT = (L::C + 1 + 31) / 32;
+  constexpr int KP = 32 * KT;
+  static_assert(KP == 16 * lay_ks16<L>(), "the 16x16x32 path needs K padded to a multiple of 32");
+  constexpr int ROWB = 4 * KP + L::PADB;
+  static_assert((RCH * ROWB) % 1024 == 0, "chunk must be whole 1 KiB pieces");
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
+  h8 bh[4][KT], bl[4][KT];
+  uint32_t zx[4], ng[4];
+  float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
+  {
+    float4 v[LDV];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      load_group(stack, P, L::C, pbase + 32 * half, lane, v);
+#pragma unroll
+      for (int i = 0; i < LDV; ++i) {
+        const int e4 = lane + 64 * i;
+        if (e4 < 8 * L::C) reinterpret_cast<float4 *>(stg)[e4] = v[i];
+      }
+      __syncthreads();
+      build_b_lay16<L, KT>(stg, lane, 0, bh[2 * half], bl[2 * half], zx[2 * half], ng[2 * half]);
+      build_b_lay16<L, KT>(stg, lane, 1, bh[2 * half + 1], bl[2 * half + 1], zx[2 * half + 1], ng[2 * half + 1]);
+      __syncthreads();
+    }
+  }
+  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
+  float best[4];
+  int bi[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    best[g] = -__builtin_inff();
+    bi[g] = 0;
+  }
+  const char *gref = reinterpret_cast<const char *>(refh);
+  char *ldsb = reinterpret_cast<char *>(lds);
+  const int nch = Rpad / RCH;
+  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
+  const bool keyed = !libneg && !__syncthreads_or((ng[0] | ng[1] | ng[2] | ng[3]) != 0);
+#define HRF_SWEEP16(Z, K) lay_sweep16<KT, ROWB, NW, L::NSEG, Z, K>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+  if (keyed) {
+    if (zs) HRF_SWEEP16(true, true);
+    else HRF_SWEEP16(false, true);
+  } else {
+    if (zs) HRF_SWEEP16(true, false);
+    else HRF_SWEEP16(false, false);
+  }
+#undef HRF_SWEEP16
+  const int Q = lane >> 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float b = best[g];
+    int idx = bi[g] + 4 * Q;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ob = __shfl_xor(b, o, 64);
+      const int oi = __shfl_xor(idx, o, 64);
+      if (ob > b || (ob == b && oi < idx)) {
+        b = ob;
+        idx = oi;
+      }
+    }
+    const int64_t p = pbase + 16 * g + (lane & 15);
+    if (Q == 0 && p < P) {
+      best_idx[p] = idx;
+      best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
+    }
+  }
+}
+
 // mode-2 table: {hi[KP], lo[KP], pad 16 B} fp16 per row, KP = 16 * ceil((C + 1) / 16); column C
 // is the validity bias (0 real rows, -1024 padding rows); pad fp16 s (s < nseg) = 1 when the row's
 // segment s is all zero (the indicator k-step's A operand), fp16 6-7 of row 0 = the library's
 // negative-value flag.
 __global__ void ref_prep_lay_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
-                                    int32_t Rpad, _Float16 *__restrict__ refh) {
+                                    int32_t Rpad, int32_t rowh, _Float16 *__restrict__ refh) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= Rpad) return;
-  _Float16 *hi = refh + r * (2 * KP + 8);
+  _Float16 *hi = refh + r * rowh;
   _Float16 *lo = hi + KP;
-  for (int k = 0; k < 2 * KP + 8; ++k) hi[k] = (_Float16)0.0f;
+  for (int k = 0; k < rowh; ++k) hi[k] = (_Float16)0.0f;
   hi[C] = (_Float16)(r < R ? 0.0f : -1024.0f);
   if (r >= R) return;
   const float *x = ref + r * C;
@@ -832,6 +1108,12 @@ int layout_id(const Bounds &bd, int C) {
   if (is_layout<LayEcoli>(bd, C)) return 1;
   if (is_layout<LayMulti>(bd, C)) return 2;
   return 0;
+}
+// bytes per row of a mode-1/2 table: hi | lo | pad (the reference layouts' pads differ)
+int64_t table_rowb(int mode, int lay, int kp) {
+  if (mode == 2 && lay == 1) return 4 * kp + LayEcoli::PADB;
+  if (mode == 2 && lay == 2) return 4 * kp + LayMulti::PADB;
+  return 4 * kp + 16;
 }
 
 // ---- per cell, f64, gated variants; one workgroup per cell ----
@@ -962,6 +1244,17 @@ hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mod
   return HRF_OK;
 }
 
+hrf_status hrf_classify_table_row_bytes(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t mode,
+                                        int32_t *row_bytes_host) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, 1, mode, &kp, &rpad)) return s;
+  HRF_REQUIRE(row_bytes_host, "classify_table_row_bytes: null output");
+  *row_bytes_host = (int32_t)(mode == 0 ? 4 * kp : table_rowb(mode, layout_id(bd, C), kp));
+  return HRF_OK;
+}
+
 hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg,
                                      int32_t mode, void *refx, hrf_stream_t stream) {
   Bounds bd;
@@ -972,8 +1265,8 @@ hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, con
   HRF_REQUIRE(mode != 2 || layout_id(bd, C) != 0,
               "classify: mode 2 needs the E. coli (0,32,55,75,89,95) or multispecies (0,23,43,57,63) layout");
   if (mode == 2) {
-    ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
-                                                                                          (_Float16 *)refx);
+    ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(
+        ref, R, C, bd, kp, rpad, (int32_t)(table_rowb(2, layout_id(bd, C), kp) / 2), (_Float16 *)refx);
     ref_negflag_kernel<<<1, 256, 0, (hipStream_t)stream>>>(ref, (int64_t)R * C, kp, (_Float16 *)refx);
   } else if (mode == 0)
     ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
@@ -1001,13 +1294,35 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
     HRF_REQUIRE(lay != 0, "classify: mode 2 needs the E. coli or multispecies channel layout");
     // waves per workgroup: the library chunks streamed through LDS are shared by NW*64 pixels
     static const int nw = getenv("HRF_CLASSIFY_NW") ? atoi(getenv("HRF_CLASSIFY_NW")) : 4;
-    const size_t shm = std::max<size_t>((size_t)2 * RCH * (4 * kp + 16), sizeof(float) * nw * 32 * C);
+    const size_t rowb = (size_t)table_rowb(2, lay, kp);
+    const size_t shm = std::max<size_t>((size_t)2 * RCH * rowb, sizeof(float) * nw * 32 * C);
 #define HRF_LAY(LAY, NWV)                                                                                      \
   (void)hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LAY, NWV>,                                \
                             hipFuncAttributeMaxDynamicSharedMemorySize,                                       \
                             (int)shm);                                                                        \
   classify_pixels_lay_kernel<LAY, NWV><<<(unsigned)hrf::cdiv(P, 64 * NWV), 64 * NWV, shm, s>>>(                 \
       stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
+    // the 16x16x32 MFMA form of the same sweep, default for the E. coli layout (R = 1023: +2 %
+    // end to end in interleaved A/B pairs; isolated within 1 %); the 32x32x16 form for the
+    // community layout (R = 127, where it is 25 % faster).  HRF_CLASSIFY_MFMA16=0/1 forces one.
+    static const int m16_env = getenv("HRF_CLASSIFY_MFMA16") ? atoi(getenv("HRF_CLASSIFY_MFMA16")) : -1;
+    const int m16 = m16_env >= 0 ? m16_env : (lay == 1);
+    const size_t shm16 = std::max<size_t>((size_t)3 * RCH * rowb, sizeof(float) * 4 * 32 * C);
+#define HRF_LAY16(LAY)                                                                                         \
+  (void)hipFuncSetAttribute((const void *)classify_pixels_lay16_kernel<LAY, 4>,                                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm16);                           \
+  classify_pixels_lay16_kernel<LAY, 4><<<(unsigned)hrf::cdiv(P, 256), 256, shm16, s>>>(                          \
+      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
+    if (m16) {
+      if (lay == 1) {
+        HRF_LAY16(LayEcoli);
+      } else {
+        HRF_LAY16(LayMulti);
+      }
+      HRF_LAUNCHED();
+      return HRF_OK;
+    }
+#undef HRF_LAY16
     if (lay == 1) {
       if (nw == 8) {
         HRF_LAY(LayEcoli, 8);

@@ -628,6 +628,14 @@ def classify_geometry(C, nseg, R, mode=1):
     return kp.value, rp.value
 
 
+def classify_table_row_bytes(C, bounds, mode):
+    import ctypes
+    b = _i32_host(bounds)
+    rb = ctypes.c_int32(0)
+    _lib.call("hrf_classify_table_row_bytes", C, b.ctypes.data, len(b) - 1, mode, ctypes.addressof(rb))
+    return rb.value
+
+
 def classify_prepare(ref, bounds, mode=None):
     """-> prepared reference table for classify_pixels (mode 0: f32; 1: fp16 hi/lo with
     zero-segment indicator columns; 2: fp16 hi/lo, reference layouts, indicators in the epilogue)"""
@@ -639,7 +647,8 @@ def classify_prepare(ref, bounds, mode=None):
     if mode == 0:
         refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
     else:
-        refx = torch.empty((rp, 2 * kp + 8), dtype=torch.float16, device=ref.device)  # hi | lo | pad
+        rowh = classify_table_row_bytes(C, bounds, mode) // 2                            # hi | lo | pad
+        refx = torch.empty((rp, rowh), dtype=torch.float16, device=ref.device)
     _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, mode, _ptr(refx), _stream())
     return refx
 
@@ -649,8 +658,7 @@ def refx_mode(refx, C, bounds):
     if refx.dtype == torch.float32:
         return 0
     if 2 in classify_modes(bounds):
-        kp2, _ = classify_geometry(C, len(bounds) - 1, 1, 2)
-        if refx.shape[1] == 2 * kp2 + 8:
+        if refx.shape[1] * 2 == classify_table_row_bytes(C, bounds, 2):
             return 2
     return 1
 

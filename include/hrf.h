@@ -341,6 +341,10 @@ HRF_API hrf_status hrf_paint_ids(const int32_t *labels, int64_t n, const int32_t
 HRF_API hrf_status hrf_classify_geometry(int32_t C, int32_t nseg, int32_t R, int32_t mode, int32_t *kp_host,
                                          int32_t *rpad_host);
 /* segment-normalised references + zero-segment indicator columns, padded */
+/* bytes per row of the prepared table of `mode` (mode 0: f32 [kp]; 1/2: fp16 hi | lo | pad, the
+ * pad 16 B, or 32 B for mode 2 on the E. coli layout) */
+HRF_API hrf_status hrf_classify_table_row_bytes(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t mode,
+                                                int32_t *row_bytes_host);
 HRF_API hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host,
                                              int32_t nseg, int32_t mode, void *refx, hrf_stream_t stream);
 /* per pixel (north_star mode): best_idx[p] = argmin_r ungated distance, best_dist[p] */

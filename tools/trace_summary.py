@@ -30,12 +30,15 @@ def main():
         n[k] += 1
     for k, v in d.most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 30):
         print("%-60s %6.1f/step %8.3f ms/step" % (k, n[k] / nst, v / nst / 1e6))
-    gap = 0
-    for x, y in zip(seg, seg[1:]):
-        g = int(y["Start_Timestamp"]) - int(x["End_Timestamp"])
-        if g > 0:
-            gap += g
-    print("idle between kernels: %.3f ms/step" % (gap / nst / 1e6))
+    # time with no kernel running at all (union of the kernels' intervals; with concurrent
+    # streams a gap between two consecutive starts is not idle if a third kernel spans it)
+    gap, reach = 0, int(seg[0]["Start_Timestamp"])
+    for r in seg:
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if a > reach:
+            gap += a - reach
+        reach = max(reach, b)
+    print("idle (no kernel running): %.3f ms/step, %.1f %% of wall" % (gap / nst / 1e6, 100.0 * gap / (t1 - t0)))
 
 
 if __name__ == "__main__":
