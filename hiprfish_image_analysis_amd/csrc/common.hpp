@@ -91,6 +91,6 @@ int lp_table_3d(int patch, int ntheta, int nphi, int32_t *off /*[ndir][patch][3]
 // hrf_erosion_seeds with the component boxes already read back to the host (seeds.hip)
 hrf_status erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
                                  const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
-                                 hipStream_t s);
+                                 hipStream_t s, int32_t *ovf_dev);
 
 }  // namespace hrf

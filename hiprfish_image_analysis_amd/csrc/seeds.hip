@@ -45,14 +45,20 @@ __host__ __device__ inline int rs_bytes_fixed(int bh, int w64) {
 
 // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop on a
 // crop; -1: no pixels.  Evaluated on the host (dispatch) and in the kernels from the same
-// boxes, so no class table travels host -> device.
-__host__ __device__ inline int seed_class(const int32_t *box, int comp, int use_runs) {
+// boxes, so no class table travels host -> device.  mode bit 0: the run kernel is in use
+// (HRF_SEEDS_RUNS); bit 1 (SEED_BIG_RUNS): a box above the pixel kernel's capacity still goes
+// to the run kernel when its bit planes fit -- a clump of cells on a diagonal has a large box
+// but few pixels and runs.  Should such a component overflow its run arrays, the run kernel
+// counts it (it has no device fallback) and the caller redoes the stage without bit 1.
+constexpr int SEED_BIG_RUNS = 2;
+__host__ __device__ inline int seed_class(const int32_t *box, int comp, int mode) {
   const int64_t bh = (int64_t)box[comp * 4 + 2] - box[comp * 4 + 0] + 1;
   const int64_t bw = (int64_t)box[comp * 4 + 3] - box[comp * 4 + 1] + 1;
   if (bh <= 0 || bw <= 0) return -1;
-  if (bh * bw > SEED_LDS_PX_MAX) return 2;
-  const bool runs_fit = use_runs && bw <= 65535 && bh <= 65535 &&
+  const bool runs_fit = (mode & 1) && bw <= 65535 && bh <= 65535 &&
                         rs_bytes_fixed((int)bh, (int)((bw + 63) >> 6)) + 14 * RS_MIN_CAP <= RS_LDS;
+  if (runs_fit && (mode & SEED_BIG_RUNS)) return 0;
+  if (bh * bw > SEED_LDS_PX_MAX) return 2;
   return runs_fit ? 0 : 1;
 }
 
@@ -333,13 +339,13 @@ __device__ void rs_clear_run(uint64_t *m, uint64_t *sd, int base, int c0, int c1
 
 __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *__restrict__ labels, int64_t H,
                                                                  int64_t W, const int32_t *__restrict__ box,
-                                                                 int32_t use_runs, int32_t area_max,
+                                                                 int32_t mode, int32_t area_max,
                                                                  int32_t min_obj, int32_t *__restrict__ list,
                                                                  int32_t *__restrict__ count,
                                                                  uint8_t *__restrict__ be_out) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
-  const int cls = seed_class(box, comp, use_runs);
+  const int cls = seed_class(box, comp, mode);
   if (cls == 1 && threadIdx.x == 0) list[atomicAdd(count, 1)] = comp;
   if (cls != 0) return;
   const int r0 = box[comp * 4 + 0], c0 = box[comp * 4 + 1], r1 = box[comp * 4 + 2], c1 = box[comp * 4 + 3];
@@ -430,20 +436,25 @@ __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *
       return;
     }
   }
-  // over capacity (or the iteration cap): the pixel kernel redoes this component
-  if (threadIdx.x == 0) list[atomicAdd(count, 1)] = comp;
+  // over capacity (or the iteration cap): the pixel kernel redoes this component -- unless its
+  // box exceeds the pixel kernel's capacity (SEED_BIG_RUNS): then count[1] tells the caller
+  if (threadIdx.x == 0) {
+    if ((int64_t)bh * bw > SEED_LDS_PX_MAX) atomicAdd(count + 1, 1);
+    else list[atomicAdd(count, 1)] = comp;
+  }
 }
 
 // crop (with padding) of the oversized components' pixels
 __global__ void big_crop_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W, const int32_t *__restrict__ box,
-                                int32_t ncomp, int64_t r0, int64_t c0, int64_t h, int64_t w, uint8_t *__restrict__ m) {
+                                int32_t ncomp, int mode, int64_t r0, int64_t c0, int64_t h, int64_t w,
+                                uint8_t *__restrict__ m) {
   const int64_t n = h * w;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = r0 + i / w, c = c0 + i % w;
     uint8_t v = 0;
     if (r >= 0 && r < H && c >= 0 && c < W) {
       const int32_t l = labels[r * W + c];
-      v = l > 0 && l <= ncomp && seed_class(box, l, 1) == 2;
+      v = l > 0 && l <= ncomp && seed_class(box, l, mode) == 2;
     }
     m[i] = v;
   }
@@ -543,7 +554,18 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   std::vector<int32_t> hb((size_t)(ncomp + 1) * 4);
   HRF_HIP(hipMemcpyAsync(hb.data(), box, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));
-  return ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s);
+  int32_t *ovf = nullptr;
+  HRF_HIP(hipMallocAsync((void **)&ovf, sizeof(int32_t), s));
+  hrf_status st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, ovf);
+  int32_t novf = 0;
+  if (st == HRF_OK) {
+    HRF_HIP(hipMemcpyAsync(&novf, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+  }
+  HRF_HIP(hipFreeAsync(ovf, s));
+  if (st == HRF_OK && novf > 0)  // a large-box component overflowed the run kernel: redo the classic way
+    st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, nullptr);
+  return st;
 }
 
 }  // extern "C"
@@ -553,8 +575,9 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
 // synchronisation instead of a second one here.
 hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
                                       const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
-                                      hipStream_t s) {
+                                      hipStream_t s, int32_t *ovf_dev) {
   HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+  if (ovf_dev) HRF_HIP(hipMemsetAsync(ovf_dev, 0, sizeof(int32_t), s));
   if (ncomp == 0) return HRF_OK;
   // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
   // Components the run kernel cannot hold (run arrays over capacity) are listed with the
@@ -563,9 +586,12 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     const char *e = getenv("HRF_SEEDS_RUNS");
     return e ? atoi(e) : 1;
   }();
+  // ovf_dev given: large boxes may go to the run kernel; ovf_dev receives the number of those
+  // that overflowed it (then the caller redoes the stage with ovf_dev == nullptr)
+  const int mode = (use_runs ? 1 : 0) | (ovf_dev ? SEED_BIG_RUNS : 0);
   int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
   for (int c = 1; c <= ncomp; ++c) {
-    if (seed_class(hb, c, use_runs) != 2) continue;
+    if (seed_class(hb, c, mode) != 2) continue;
     br0 = std::min<int64_t>(br0, hb[c * 4 + 0]);
     bc0 = std::min<int64_t>(bc0, hb[c * 4 + 1]);
     br1 = std::max<int64_t>(br1, hb[c * 4 + 2]);
@@ -574,15 +600,16 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   // the run kernel lists, on the device, the components it hands to the pixel kernel (nothing
   // is copied from host memory, whose lifetime an asynchronous copy would outlive)
   int32_t *dlist = nullptr;
-  const size_t nl = (size_t)ncomp + 2;
+  const size_t nl = (size_t)ncomp + 3;
   HRF_HIP(hipMallocAsync((void **)&dlist, sizeof(int32_t) * nl, s));
-  int32_t *dcount = dlist + ncomp + 1;
-  HRF_HIP(hipMemsetAsync(dcount, 0, sizeof(int32_t), s));
+  int32_t *dcount = dlist + ncomp + 1;  // [0] pixel-kernel list length, [1] large-box overflows
+  HRF_HIP(hipMemsetAsync(dcount, 0, 2 * sizeof(int32_t), s));
   const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
   HRF_HIP(hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)shm_max));
-  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, use_runs, area_max, min_obj, dlist,
+  erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, mode, area_max, min_obj, dlist,
                                                                  dcount, be_out);
+  if (ovf_dev) HRF_HIP(hipMemcpyAsync(ovf_dev, dcount + 1, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   erosion_seed_kernel<<<(unsigned)std::min(ncomp, 16), 1024, shm_max, s>>>(labels, H, W, box, dlist, dcount, area_max,
                                                                           min_obj, be_out);
   HRF_LAUNCHED();
@@ -599,7 +626,7 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
     int64_t *cnt_dev = nullptr;
     HRF_HIP(hipMallocAsync((void **)&cnt_dev, sizeof(int64_t), s));
     HRF_HIP(hipMemsetAsync(bec, 0, (size_t)n, s));
-    big_crop_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, H, W, box, ncomp, r0, c0, h, w, m);
+    big_crop_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, H, W, box, ncomp, mode, r0, c0, h, w, m);
     HRF_LAUNCHED();
     for (int64_t it = 0; it < 4 * (h + w) + 8; ++it) {
       int64_t cnt = 0;

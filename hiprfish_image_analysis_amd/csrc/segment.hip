@@ -197,11 +197,19 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
     HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)ncomp + 1), hipMemcpyDeviceToHost, s));
     HRF_HIP(hipStreamSynchronize(s));
   }
-  HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s));
-  HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
-  HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
-  int32_t passes = 0;
-  HRF_TRY(hrf_watershed(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
+  // Large-box components go to the run kernel too; how many overflowed it lands in hpin[2]
+  // at the watershed's synchronisation, and in that (rare) case the seeds and everything
+  // after them are redone with those components in the whole-image loop.
+  for (int attempt = 0;; ++attempt) {
+    HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s,
+                                         attempt == 0 ? c->dint + 8 : nullptr));
+    if (attempt == 0) HRF_HIP(hipMemcpyAsync(c->hpin + 2, c->dint + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
+    HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
+    int32_t passes = 0;
+    HRF_TRY(hrf_watershed(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
+    if (attempt > 0 || c->hpin[2] == 0) break;
+  }
   const int32_t nseeds = c->hpin[0];  // read back by the watershed's synchronisation
   HRF_TRY(ensure_labels(c, nseeds, s));
   HRF_TRY(hrf_remove_small_objects_labels(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114

@@ -480,6 +480,23 @@ def test_erosion_seeds_vs_oracle(K, orc, S, seed):
     assert np.array_equal(glob, ref)
 
 
+def test_erosion_seeds_large_boxes(K):
+    """boxes above the pixel kernel's capacity: a diagonal clump with few runs stays in the run
+    kernel; a comb with thousands of runs overflows it and the stage is redone with it in the
+    whole-image loop -- both equal to the restatement"""
+    import pipeline as OP
+    H, W = 420, 440
+    m = np.zeros((H, W), bool)
+    for k in range(12):                              # a diagonal chain of 14x14 blobs: box 178x178
+        m[10 + 14 * k:24 + 14 * k, 10 + 14 * k:24 + 14 * k] = True
+    m[230:400, 200:410:4] = True                     # a comb: 53 teeth, one px wide
+    m[230:233, 200:410] = True                       # its bar: box 170 x 210, ~9000 runs
+    m[300:340, 20:60] = True                         # an ordinary solid box
+    ref = OP.erosion_seeds(m)
+    got = host(K.erosion_seeds(dev(m))).astype(bool)
+    assert np.array_equal(got, ref)
+
+
 def test_label_boxes(K):
     lab = np.zeros((50, 60), np.int32)
     lab[3:9, 5:20] = 1

@@ -170,6 +170,27 @@ def test_native_segmentation_equals_composed(mods, H, W, seed):
     assert torch.equal(seg_n2, seg_n)
 
 
+def test_native_segmentation_run_overflow(mods):
+    """a bright comb whose 8-connected component has a box above the pixel kernel's capacity and
+    more runs than the run kernel holds: the native driver finds the overflow at the
+    watershed's synchronisation and redoes the seeds; equal to the composition and the oracle"""
+    P, S, OP = mods
+    stack, _, _, _ = S.tile(512, 512, seed=24)
+    st = host(stack).copy()
+    peak = float(st.sum(axis=2).max())
+    teeth = np.zeros((512, 512), bool)
+    for c in range(250, 480, 6):
+        teeth[280:470, c:c + 3] = True
+    teeth[280:284, 250:480] = True
+    st[teeth] = (3.0 * peak / st.shape[2]) * (1.0 + 0.05 * np.random.default_rng(5).random((int(teeth.sum()), 1)))
+    dstack = torch.from_numpy(st).cuda()
+    seg_n, mx_n = P.segment_ecoli(dstack)
+    seg_c, mx_c = P.segment_ecoli(dstack, keep={})
+    assert mx_n == mx_c and torch.equal(seg_n, seg_c)
+    oseg, _ = OP.segment_ecoli(st)
+    assert np.array_equal(host(seg_n), oseg)
+
+
 # ---- degenerate tiles: empty, constant, tiny, ragged -----------------------------------------
 def _degenerate_tiles(S, C):
     rng = np.random.default_rng(40)
