@@ -93,4 +93,7 @@ hrf_status erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, in
                                  const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
                                  hipStream_t s, int32_t *ovf_dev);
 
+hrf_status kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32_t k1, int32_t k2, int32_t max_iter,
+                                          int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1, uint8_t *top2,
+                                          void *work, int64_t work_bytes, hipStream_t s, int32_t *err_pinned);
 }  // namespace hrf

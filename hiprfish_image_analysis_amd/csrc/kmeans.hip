@@ -1710,6 +1710,30 @@ hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n
   return HRF_OK;
 }
 
+}  // extern "C"
+
+// The pair without its synchronisation (the native E. coli driver): the NaN flag lands in
+// *err_pinned (pinned host memory) and the caller checks it after its next synchronisation.
+hrf_status hrf::kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32_t k1, int32_t k2, int32_t max_iter,
+                                               int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1,
+                                               uint8_t *top2, void *work, int64_t work_bytes, hipStream_t s,
+                                               int32_t *err_pinned) {
+  if (hrf_status r = check_args(k1, n, max_iter, n_init, rule1, work, x)) return r;
+  if (hrf_status r = check_args(k2, n, max_iter, n_init, rule2, work, x)) return r;
+  HRF_REQUIRE(err_pinned, "kmeans_1d_pair: null error slot");
+  const int64_t need = hrf_kmeans_sorted_workspace_bytes(n);
+  HRF_REQUIRE(need > 0 && work_bytes >= need, "kmeans_1d_pair: workspace too small");
+  size_t tb = 0;
+  if (hrf_status r = sort_tmp_bytes(n, &tb)) return r;
+  const SortWs ws = carve(work, n, tb);
+  if (hrf_status r = km_launch_k(k1, x, nullptr, n, max_iter, n_init, rule1, nullptr, top1, ws, 0, s, nullptr)) return r;
+  if (hrf_status r = km_launch_k(k2, x, nullptr, n, max_iter, n_init, rule2, nullptr, top2, ws, 1, s, nullptr)) return r;
+  HRF_HIP(hipMemcpyAsync(err_pinned, &ws.st->error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  return HRF_OK;
+}
+
+extern "C" {
+
 hrf_status hrf_kmeans_1d_sorted_pair(const double *x, const uint8_t *valid, int64_t n, int32_t k1, int32_t k2,
                                      int32_t max_iter, int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1,
                                      uint8_t *top2, void *work, int64_t work_bytes, hrf_stream_t stream) {

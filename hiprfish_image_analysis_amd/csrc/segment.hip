@@ -174,8 +174,9 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   const int64_t H = c->H, W = c->W, n = c->n;
   uint8_t *rough = c->m[0], *interior = c->m[1], *a = c->m[2], *b = c->m[3], *d = c->m[4];
   int32_t *lab1 = c->l[0], *seeds = c->l[1], *ws = c->l[2], *lab3 = c->l[3];
-  HRF_TRY(hrf_kmeans_1d_sorted_pair(cn, nullptr, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes,
-                                    s));                                        // :73-94
+  // :73-94; the NaN check (sklearn raises) is read at the component-count synchronisation below
+  HRF_TRY(::hrf::kmeans_1d_sorted_pair_deferred(cn, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes, s,
+                                                c->hpin + 3));
   HRF_TRY(hrf_remove_small_holes(interior, H, W, 64, 1, a, c->parent, c->size, s));   // :95
   HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
   HRF_TRY(hrf_binary_dilation(b, H, W, d, s));
@@ -190,6 +191,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   HRF_TRY(hrf_label_boxes(lab1, H, W, guess, c->box, s));
   HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)guess + 1), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));
+  HRF_REQUIRE(!c->hpin[3], "kmeans_1d_pair: input contains NaN (sklearn KMeans raises ValueError)");
   const int32_t ncomp = c->hpin[1];
   if (ncomp > guess) {
     HRF_TRY(ensure_labels(c, ncomp, s));

@@ -191,6 +191,23 @@ def test_native_segmentation_run_overflow(mods):
     assert np.array_equal(host(seg_n), oseg)
 
 
+def test_ecoli_nan_input_raises(mods):
+    """a NaN in the stack makes image_cn NaN and sklearn's KMeans raise (:73); the native driver
+    reads the flag at its next synchronisation and raises the same ValueError; the context
+    stays usable"""
+    P, S, OP = mods
+    stack, _, _, _ = S.tile(128, 160, seed=25)
+    bad = stack.clone()
+    bad[7, 9, 3] = float("nan")
+    with pytest.raises(ValueError):
+        P.segment_ecoli(bad)
+    with pytest.raises(ValueError):
+        P.segment_ecoli(bad, keep={})
+    seg_n, mx_n = P.segment_ecoli(stack)
+    seg_c, mx_c = P.segment_ecoli(stack, keep={})
+    assert mx_n == mx_c and torch.equal(seg_n, seg_c)
+
+
 # ---- degenerate tiles: empty, constant, tiny, ragged -----------------------------------------
 def _degenerate_tiles(S, C):
     rng = np.random.default_rng(40)
