@@ -175,9 +175,155 @@ hrf_status xcorr_peak(const double *src, const double *target, int64_t H, int64_
   return HRF_OK;
 }
 
+// ---- all targets of one reference in one batch ------------------------------------------
+// One batched D2Z over the nimg images (reference first), one product launch for the nimg - 1
+// targets, one batched Z2D, one argmax pass over every correlation surface and one kernel for
+// the shifts: a dozen launches per tile set instead of ten per target, and FFT grids nimg
+// times larger.
+struct BatchPlans {
+  hipfftHandle fwd, inv;
+  size_t work;
+};
+std::map<std::tuple<int, int64_t, int64_t, int>, BatchPlans> g_bplans;
+
+hrf_status get_batch_plans(int64_t H, int64_t W, int nimg, BatchPlans *out) {
+  int dev = 0;
+  HRF_HIP(hipGetDevice(&dev));
+  auto key = std::make_tuple(dev, H, W, nimg);
+  auto it = g_bplans.find(key);
+  if (it != g_bplans.end()) {
+    *out = it->second;
+    return HRF_OK;
+  }
+  BatchPlans p{};
+  int n[2] = {(int)H, (int)W};
+  size_t wf = 0, wi = 0;
+  const int real_dist = (int)(H * W), cplx_dist = (int)(H * (W / 2 + 1));
+  HRF_FFT(hipfftCreate(&p.fwd));
+  HRF_FFT(hipfftCreate(&p.inv));
+  HRF_FFT(hipfftSetAutoAllocation(p.fwd, 0));
+  HRF_FFT(hipfftSetAutoAllocation(p.inv, 0));
+  HRF_FFT(hipfftMakePlanMany(p.fwd, 2, n, nullptr, 1, real_dist, nullptr, 1, cplx_dist, HIPFFT_D2Z, nimg, &wf));
+  HRF_FFT(hipfftMakePlanMany(p.inv, 2, n, nullptr, 1, cplx_dist, nullptr, 1, real_dist, HIPFFT_Z2D, nimg - 1, &wi));
+  p.work = std::max(wf, wi);
+  g_bplans[key] = p;
+  *out = p;
+  return HRF_OK;
+}
+
+// o[t] = F[0] * conj(F[1 + t]) for every target t
+__global__ void xcorr_product_batch_kernel(const hipfftDoubleComplex *__restrict__ F, int64_t nc, int ntgt,
+                                           hipfftDoubleComplex *__restrict__ o) {
+  const int64_t total = nc * ntgt;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = i / nc, j = i - t * nc;
+    const hipfftDoubleComplex x = F[j], y = F[(1 + t) * nc + j];
+    o[i] = make_hipDoubleComplex(x.x * y.x + x.y * y.y, x.y * y.x - x.x * y.y);
+  }
+}
+
+// blockIdx.y = surface; AM_BLOCKS partials per surface
+__global__ __launch_bounds__(256) void abs_argmax_partial_batch_kernel(const double *__restrict__ cc, int64_t n,
+                                                                       Best *__restrict__ part) {
+  const double *c = cc + (int64_t)blockIdx.y * n;
+  Best b{-1.0, INT64_MAX};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = fabs(c[i]);
+    if (v > b.v) b = Best{v, i};
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best q{__shfl_xor(b.v, o, 64), (int64_t)__shfl_xor((long long)b.i, o, 64)};
+    b = better(b, q);
+  }
+  __shared__ Best red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) b = better(b, red[q]);
+    part[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = b;
+  }
+}
+
+// one workgroup per surface: its peak -> shift[1 + t] (row 0, the reference, = (0, 0))
+__global__ __launch_bounds__(256) void shifts_batch_kernel(const Best *__restrict__ part, int nparts, int64_t H,
+                                                           int64_t W, int32_t clamp, int32_t *__restrict__ shift) {
+  const Best *p = part + (int64_t)blockIdx.x * nparts;
+  Best b{-1.0, INT64_MAX};
+  for (int i = threadIdx.x; i < nparts; i += 256) b = better(b, p[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best q{__shfl_xor(b.v, o, 64), (int64_t)__shfl_xor((long long)b.i, o, 64)};
+    b = better(b, q);
+  }
+  __shared__ Best red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) b = better(b, red[q]);
+    int64_t r = b.i / W, c = b.i % W;
+    if (r > H / 2) r -= H;
+    if (c > W / 2) c -= W;
+    if (clamp >= 0) {
+      r = (r > clamp || r < -clamp) ? 0 : r;
+      c = (c > clamp || c < -clamp) ? 0 : c;
+    }
+    shift[2 * (1 + blockIdx.x)] = (int32_t)r;
+    shift[2 * (1 + blockIdx.x) + 1] = (int32_t)c;
+    if (blockIdx.x == 0) shift[0] = shift[1] = 0;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int64_t hrf_register_batch_workspace_bytes(int32_t nimg, int64_t H, int64_t W) {
+  if (nimg < 2 || nimg > 64 || H < 1 || W < 1 || H > (1 << 15) || W > (1 << 15)) return -1;
+  const int64_t nc = H * (W / 2 + 1);
+  BatchPlans p{};
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    if (get_batch_plans(H, W, nimg, &p) != HRF_OK) return -1;
+  }
+  const int64_t spectra = (2 * (int64_t)nimg - 1) * nc * (int64_t)sizeof(hipfftDoubleComplex);
+  const int64_t surfaces = ((int64_t)nimg - 1) * H * W * (int64_t)sizeof(double);
+  const int64_t parts = ((int64_t)nimg - 1) * AM_BLOCKS * (int64_t)sizeof(Best);
+  return spectra + surfaces + parts + 512 + (int64_t)p.work;
+}
+
+hrf_status hrf_register_translations_batch_dev(const double *imgs, int32_t nimg, int64_t H, int64_t W, void *work,
+                                               int32_t clamp, int32_t *shifts_dev, hrf_stream_t stream) {
+  HRF_REQUIRE(nimg >= 2 && nimg <= 64 && H >= 1 && W >= 1 && H <= (1 << 15) && W <= (1 << 15),
+              "register_translations_batch: bad sizes");
+  HRF_REQUIRE(imgs && work && shifts_dev, "register_translations_batch: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nc = H * (W / 2 + 1), n = H * W;
+  char *w = (char *)work;
+  hipfftDoubleComplex *F = (hipfftDoubleComplex *)w;           // nimg spectra
+  hipfftDoubleComplex *Pr = F + (int64_t)nimg * nc;              // nimg - 1 products
+  double *cc = (double *)(Pr + (int64_t)(nimg - 1) * nc);        // nimg - 1 surfaces
+  Best *part = (Best *)(cc + (int64_t)(nimg - 1) * n);
+  char *fft_work = (char *)(((uintptr_t)(part + (int64_t)(nimg - 1) * AM_BLOCKS) + 255) & ~(uintptr_t)255);
+  {
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    BatchPlans p{};
+    if (hrf_status st = get_batch_plans(H, W, nimg, &p)) return st;
+    HRF_FFT(hipfftSetStream(p.fwd, s));
+    HRF_FFT(hipfftSetStream(p.inv, s));
+    HRF_FFT(hipfftSetWorkArea(p.fwd, fft_work));
+    HRF_FFT(hipfftSetWorkArea(p.inv, fft_work));
+    HRF_FFT(hipfftExecD2Z(p.fwd, const_cast<double *>(imgs), F));
+    xcorr_product_batch_kernel<<<hrf::stream_grid(nc * (nimg - 1)), 256, 0, s>>>(F, nc, nimg - 1, Pr);
+    HRF_LAUNCHED();
+    HRF_FFT(hipfftExecZ2D(p.inv, Pr, cc));  // unnormalised: a positive scale leaves the argmax
+  }
+  const unsigned nb = (unsigned)std::min<int64_t>(AM_BLOCKS, hrf::cdiv(n, 256));
+  abs_argmax_partial_batch_kernel<<<dim3(nb, (unsigned)(nimg - 1)), 256, 0, s>>>(cc, n, part);
+  shifts_batch_kernel<<<(unsigned)(nimg - 1), 256, 0, s>>>(part, (int)nb, H, W, clamp, shifts_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
 
 int64_t hrf_register_workspace_bytes(int64_t H, int64_t W) {
   if (H < 1 || W < 1 || H > (1 << 20) || W > (1 << 20)) return -1;

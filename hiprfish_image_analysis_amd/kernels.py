@@ -199,20 +199,22 @@ def channel_max(stack):
     return out
 
 
-def channel_max_multi(stacks):
-    """[np.max(s, axis=2) for s in stacks] (f64) in one launch; the stacks share H x W"""
+def channel_max_multi(stacks, stacked=False):
+    """[np.max(s, axis=2) for s in stacks] (f64) in one launch; the stacks share H x W.
+    stacked: return them as one (n, H, W) tensor instead of a list"""
     import ctypes
     stacks = [_dev(s, torch.float32, "stack") for s in stacks]
     H, W = stacks[0].shape[:2]
     if any(s.shape[:2] != (H, W) for s in stacks):
         raise ValueError("channel_max_multi: the stacks must share H x W")
-    outs = [torch.empty((H, W), dtype=torch.float64, device=stacks[0].device) for _ in stacks]
+    buf = torch.empty((len(stacks), H, W), dtype=torch.float64, device=stacks[0].device)
+    outs = list(buf.unbind(0))
     src = (ctypes.c_void_p * len(stacks))(*[s.data_ptr() for s in stacks])
     dst = (ctypes.c_void_p * len(stacks))(*[o.data_ptr() for o in outs])
     ch = _i32_host([s.shape[2] for s in stacks])
     _lib.call("hrf_channel_max_multi", ctypes.cast(src, ctypes.c_void_p), ch.ctypes.data, len(stacks), H * W,
               ctypes.cast(dst, ctypes.c_void_p), _stream())
-    return outs
+    return buf if stacked else outs
 
 
 def calibrate(stack, cal, cal_range=None):
@@ -261,6 +263,23 @@ def register_translations_dev(ref, targets, clamp=None):
             raise ValueError("register_translation: two equal-shape 2-D images expected")
         _lib.call("hrf_register_translation_dev", _ptr(ref) if i == 0 else None, _ptr(t), H, W, _ptr(work), cl,
                   _ptr(out[1 + i]), _stream())
+    return out
+
+
+def register_translations_batch_dev(imgs, clamp=None):
+    """register_translations_dev(imgs[0], imgs[1:], clamp) from one (n, H, W) f64 tensor in one
+    batch (batched hipFFT transforms, one product, argmax and shift launch each)"""
+    imgs = _dev(imgs, torch.float64, "imgs")
+    n, H, W = imgs.shape
+    if n < 2:
+        raise ValueError("register_translations_batch: a reference and at least one target expected")
+    nb = int(_lib.lib().hrf_register_batch_workspace_bytes(n, H, W))
+    if nb <= 0:
+        raise ValueError("register_translations_batch: unsupported size")
+    work = torch.empty(nb, dtype=torch.uint8, device=imgs.device)
+    out = torch.empty((n, 2), dtype=torch.int32, device=imgs.device)
+    _lib.call("hrf_register_translations_batch_dev", _ptr(imgs), n, H, W, _ptr(work), -1 if clamp is None else int(clamp),
+              _ptr(out), _stream())
     return out
 
 

@@ -42,6 +42,10 @@ def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: in
 # The segmentation chains run as one native call (segment.hip, same calls in the same order)
 # unless intermediates are requested (`keep`) or HRF_NATIVE_SEG=0.
 NATIVE_SEG = os.environ.get("HRF_NATIVE_SEG", "1") != "0"
+# the registration estimate of all lasers as one batch of FFTs (HRF_BATCH_REG=1).  Off by default:
+# with four tiles in flight the batched transforms cost 1-7 % end to end against one transform
+# pair per target (4 of 4 interleaved pairs; DESIGN.md "Tried and not kept")
+BATCH_REGISTRATION = os.environ.get("HRF_BATCH_REG", "0") == "1"
 
 
 def segment_ecoli(stack: torch.Tensor, keep: dict | None = None, image_cn: torch.Tensor | None = None):
@@ -103,7 +107,10 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
     (nlaser, 2) int32 device tensor instead (no host synchronisation; register_assemble reads
     it on the device)."""
     if reduce == "max" and len(lasers) <= 8:
-        proj = K.channel_max_multi(lasers)                               # one launch for all lasers
+        proj = K.channel_max_multi(lasers, stacked=True)                 # one launch for all lasers
+        if device and len(lasers) >= 2 and BATCH_REGISTRATION:
+            return K.register_translations_batch_dev(proj, clamp)       # batched FFTs
+        proj = list(proj.unbind(0))
     else:
         proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
     if device:

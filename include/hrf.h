@@ -161,6 +161,13 @@ HRF_API hrf_status hrf_register_translation(const double *src, const double *tar
  * reference image's transform already in `work` from the previous call on that workspace. */
 HRF_API hrf_status hrf_register_translation_dev(const double *src, const double *target, int64_t H, int64_t W,
                                                 void *work, int32_t clamp, int32_t *shift_dev, hrf_stream_t stream);
+/* every target against the reference in one batch: imgs = nimg contiguous H x W f64 images
+ * (reference first, 2 <= nimg <= 64), shifts_dev = nimg x 2 int32 (row 0 = (0, 0)); clamp as
+ * hrf_register_translation_dev; work: hrf_register_batch_workspace_bytes(nimg, H, W) bytes */
+HRF_API int64_t hrf_register_batch_workspace_bytes(int32_t nimg, int64_t H, int64_t W);
+HRF_API hrf_status hrf_register_translations_batch_dev(const double *imgs, int32_t nimg, int64_t H, int64_t W,
+                                                       void *work, int32_t clamp, int32_t *shifts_dev,
+                                                       hrf_stream_t stream);
 
 /* ==== a4: non-local means (nlmeans.hip) ==================================================
  * skimage.restoration.denoise_nl_means(img, patch_size, patch_distance, h, fast_mode=True,

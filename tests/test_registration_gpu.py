@@ -108,6 +108,24 @@ def test_estimate_shifts_on_device_equals_host(K):
     assert tuple(unclamped[3]) == (-20, 1) and [tuple(r) for r in unclamped] == P.estimate_shifts(lasers, clamp=None)
 
 
+@pytest.mark.parametrize("n,H,W", [(2, 64, 80), (5, 160, 144), (5, 257, 96)])
+def test_batched_registration_equals_per_target(K, orc, n, H, W):
+    """the batched estimate (one batched D2Z / Z2D) == one transform pair per target, and the
+    numpy restatement, clamped and unclamped, odd sizes included"""
+    rng = np.random.default_rng(n * 1000 + H)
+    base = smooth_image(H, W, 30)
+    imgs = [np.roll(base, (int(rng.integers(-20, 21)), int(rng.integers(-20, 21))), (0, 1))
+            + 0.05 * rng.random((H, W)) for _ in range(n)]
+    stackd = torch.from_numpy(np.stack(imgs)).cuda()
+    for clamp in (15, None):
+        got = K.register_translations_batch_dev(stackd, clamp).cpu().tolist()
+        want = K.register_translations_dev(stackd[0], list(stackd[1:]), clamp).cpu().tolist()
+        assert got == want
+        assert tuple(got[0]) == (0, 0)
+    for i in range(1, n):
+        assert tuple(got[i]) == tuple(int(v) for v in orc.register_translation(imgs[0], imgs[i]))
+
+
 def test_pad_edge_3d(K):
     rng = np.random.default_rng(2)
     a = rng.random((7, 5, 9))
