@@ -83,8 +83,11 @@ __device__ __forceinline__ void union_g(int32_t *par, int32_t a, int32_t b) {
   }
 }
 
+// zero != nullptr: also clears that per-pixel array (the component sizes the fused
+// compression pass counts into)
 template <class V, int CONN>
-__global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent) {
+__global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent,
+                                                       int32_t *__restrict__ zero) {
   __shared__ int32_t lp[CC_T * CC_T];
   __shared__ int32_t lv[CC_T * CC_T];
   const int tid = threadIdx.x;
@@ -139,6 +142,7 @@ __global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t
       g = (int32_t)((r0 + (rt >> 5)) * W + c0 + (rt & 31));
     }
     parent[gr * W + gc] = g;
+    if (zero) zero[gr * W + gc] = 0;
   }
 }
 
@@ -177,6 +181,25 @@ __global__ void cc_compress_kernel(int32_t *__restrict__ parent, int64_t n, int3
     if (q >= 0 && q != p) parent[p] = find_g(parent, q);
     if (zero) zero[p] = 0;
   }
+}
+
+// compression fused with the size count: each wave compresses RUN_PX consecutive pixels and
+// counts them at their roots (wave_run_count); size[] was cleared by the tile pass.  The finds
+// read ancestors while other waves store roots -- every store is a root, as in cc_compress.
+constexpr int RUN = 32;
+constexpr int64_t RUN_PX = RUN * 64;
+__global__ void cc_compress_sizes_kernel(int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ size) {
+  const int64_t nw = (n + RUN_PX - 1) / RUN_PX;
+  const int64_t wpb = blockDim.x >> 6;
+  for (int64_t w = (int64_t)blockIdx.x * wpb + (threadIdx.x >> 6); w < nw; w += (int64_t)gridDim.x * wpb)
+    hrf::wave_run_count<RUN>(size, w * RUN_PX, n, [&](int64_t e) {
+      int32_t q = parent[e];
+      if (q >= 0 && q != e) {
+        q = find_g(parent, q);
+        parent[e] = q;
+      }
+      return q;
+    });
 }
 
 // Numbering.  Block = 256 threads x 4 pixels = 1024 consecutive raster pixels.
@@ -265,8 +288,6 @@ __global__ void cc_fill_kernel(const int32_t *__restrict__ parent, int64_t n, in
 
 // component sizes at the root index (size[] zeroed by the caller); each wave counts RUN*64
 // consecutive pixels (wave_run_count) so a giant component is one atomic per wave
-constexpr int RUN = 32;
-constexpr int64_t RUN_PX = RUN * 64;
 __global__ void cc_sizes_kernel(const int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ size) {
   const int64_t nw = (n + RUN_PX - 1) / RUN_PX;
   const int64_t wpb = blockDim.x >> 6;
@@ -451,18 +472,25 @@ __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t
   }
 }
 
+// zero: an array the compression pass clears; sizes: component sizes counted at the roots by
+// the compression pass itself (cleared by the tile pass)
 template <class V>
-hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s, int32_t *zero = nullptr) {
+hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s, int32_t *zero = nullptr,
+                  int32_t *sizes = nullptr) {
   dim3 g((unsigned)hrf::cdiv(W, CC_T), (unsigned)hrf::cdiv(H, CC_T));
   const unsigned gb = (unsigned)hrf::cdiv(hrf::cdiv(W, CC_T) * hrf::cdiv(H, CC_T) * CC_BORDER_PX, 256);
   if (conn == 2) {
-    cc_local_kernel<V, 2><<<g, 256, 0, s>>>(val, H, W, parent);
+    cc_local_kernel<V, 2><<<g, 256, 0, s>>>(val, H, W, parent, sizes);
     cc_border_kernel<V, 2><<<gb, 256, 0, s>>>(val, H, W, parent);
   } else {
-    cc_local_kernel<V, 1><<<g, 256, 0, s>>>(val, H, W, parent);
+    cc_local_kernel<V, 1><<<g, 256, 0, s>>>(val, H, W, parent, sizes);
     cc_border_kernel<V, 1><<<gb, 256, 0, s>>>(val, H, W, parent);
   }
-  cc_compress_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(parent, H * W, zero);
+  if (sizes)
+    cc_compress_sizes_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(H * W, RUN_PX * 4), 4096), 256, 0, s>>>(
+        parent, H * W, sizes);
+  else
+    cc_compress_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(parent, H * W, zero);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -533,11 +561,7 @@ hrf_status cc_roots_sizes(const uint8_t *mask, int dtype, int64_t H, int64_t W, 
   HRF_REQUIRE(conn == 1 || conn == 2, "cc_roots: connectivity must be 1 or 2");
   if (H * W == 0) return HRF_OK;
   HRF_REQUIRE(mask && parent && size, "cc_roots: null buffer");
-  if (hrf_status st = run_cc(MaskV{mask, dtype == 2}, H, W, conn, parent, s, size)) return st;
-  cc_sizes_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(H * W, RUN_PX * 4), 4096), 256, 0, s>>>(parent, H * W,
-                                                                                                  size);
-  HRF_LAUNCHED();
-  return HRF_OK;
+  return run_cc(MaskV{mask, dtype == 2}, H, W, conn, parent, s, nullptr, size);
 }
 }  // namespace
 
