@@ -51,13 +51,17 @@ struct WsState {
 // never runs keeps a valid copy in each), and tile_work[t] = 1 iff the tile holds a pixel the
 // relaxation can change (in the mask and not a marker).  Tiles without one -- the background
 // beyond the rough mask, about a quarter of an E. coli tile -- are skipped by every pass.
+// tile_marker[t] = 1 iff the tile holds a marker: the first pass of a relaxation (labels only
+// flow out of markers then) takes these flags as "changed in the previous pass", so tiles with
+// no marker in their 3x3 tile neighbourhood skip it.
 __global__ __launch_bounds__(256) void ws_init_kernel(const double *__restrict__ f, int negate,
                                                       const int32_t *__restrict__ markers,
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
                                                       WsState a, WsState b, int32_t *__restrict__ ptr,
-                                                      int32_t *__restrict__ tile_work) {
+                                                      int32_t *__restrict__ tile_work,
+                                                      int32_t *__restrict__ tile_marker) {
   const int tid = threadIdx.x;
-  int work = 0;
+  int work = 0, mark = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t gr = (int64_t)blockIdx.y * WT + (tid >> 5) + 8 * k, gc = (int64_t)blockIdx.x * WT + (tid & 31);
@@ -77,9 +81,14 @@ __global__ __launch_bounds__(256) void ws_init_kernel(const double *__restrict__
     b.lab[i] = m;
     ptr[i] = -1;
     work |= in && !m;
+    mark |= m != 0;
   }
   work = __syncthreads_or(work);
-  if (tid == 0) tile_work[blockIdx.y * gridDim.x + blockIdx.x] = work;
+  mark = __syncthreads_or(mark);
+  if (tid == 0) {
+    tile_work[blockIdx.y * gridDim.x + blockIdx.x] = work;
+    tile_marker[blockIdx.y * gridDim.x + blockIdx.x] = mark;
+  }
 }
 
 __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_t b1, double l2, int32_t h2,
@@ -341,7 +350,7 @@ int64_t walker_bytes(int32_t cap, int32_t hcap, int32_t gcap) {
 
 struct WsBuffers {
   WsState a, b;
-  int32_t *ptr, *list, *retry, *tf, *tw;
+  int32_t *ptr, *list, *retry, *tf, *tw, *tm;
 };
 
 WsBuffers carve(void *state_ws, int64_t n, int64_t ntiles) {
@@ -354,6 +363,7 @@ WsBuffers carve(void *state_ws, int64_t n, int64_t ntiles) {
   B.retry = (int32_t *)(ws + 52 * n);
   B.tf = (int32_t *)(ws + 56 * n);
   B.tw = B.tf + 3 * ntiles;
+  B.tm = B.tw + ntiles;
   return B;
 }
 
@@ -364,7 +374,7 @@ extern "C" {
 int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W) {
   if (H < 0 || W < 0) return -1;
   const int64_t ntiles = hrf::cdiv(W, WT) * hrf::cdiv(H, WT);
-  return 56 * H * W + 16 * ntiles + 256;
+  return 56 * H * W + 20 * ntiles + 256;
 }
 
 // flag_ws (>= 8 int32): [0] change flag of a batch's last pass, [1] the other passes',
@@ -388,7 +398,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   HRF_REQUIRE(out_labels != markers, "watershed: out_labels must not alias markers");
   B.a.lab = out_labels;
   WsState a = B.a, b = B.b;
-  ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw);
+  ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw, B.tm);
   HRF_LAUNCHED();
   int32_t *tf = B.tf;  // per-tile change flags, three rotating generations
   int32_t hflag[4] = {0, 0, 0, 0};  // host copies of flag_ws[0..3]
@@ -406,7 +416,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 3, s));
       for (int k = 0; k < batch; ++k) {
         int32_t *cur = tf + (local % 3) * ntiles;
-        const int32_t *prev = local == 0 ? nullptr : tf + ((local + 2) % 3) * ntiles;
+        const int32_t *prev = local == 0 ? B.tm : tf + ((local + 2) % 3) * ntiles;
         int32_t *next = tf + ((local + 1) % 3) * ntiles;
         int32_t *chg = flag_ws + (k == batch - 1 ? 0 : 1);
         if (relabel)
