@@ -878,7 +878,7 @@ __device__ __forceinline__ void build_b_lay16(const float *stg, int lane, int g,
   }
 }
 
-template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED>
+template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF>
 __device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
                                             const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t (&zx)[4],
                                             float (&best)[4], int (&bi)[4]) {
@@ -886,17 +886,18 @@ __device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char 
   constexpr int CHB = RCH * ROWB;
   constexpr int NPC = CHB / 1024;
   const int rl = lane & 15, Q = lane >> 4;
-  // three chunk buffers: chunk c + 2 streams in while c feeds the MFMAs and c + 1 lands
+  // NBUF = 3: chunk c + 2 streams in while c feeds the MFMAs and c + 1 lands; NBUF = 2: c + 1
+  // streams in while c feeds them (less LDS per workgroup: room for other kernels on the CU)
   auto issue = [&](int c) {
     const char *g = gref + (int64_t)c * CHB + lane * 16;
-    char *l = ldsb + (c % 3) * CHB;
+    char *l = ldsb + (c % NBUF) * CHB;
     for (int q = w; q < NPC; q += NW)
       __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
   };
   constexpr int MINE_LO = NPC / NW;                  // pieces per wave: MINE_LO or MINE_LO + 1
   const int mine = (NPC - w + NW - 1) / NW;
   issue(0);
-  if (nch > 1) issue(1);
+  if (NBUF == 3 && nch > 1) issue(1);
   f32x4 pv[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g)
@@ -936,12 +937,12 @@ __device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char 
   for (int c = 0; c < nch; ++c) {
     // chunk c landed for this wave: only chunk c + 1's pieces may still be outstanding (loads
     // retire in order; hipcc does not count LDS-DMA before the barrier, see lay_sweep)
-    if (c + 1 >= nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NBUF == 2 || c + 1 >= nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if (mine > MINE_LO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO + 1) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO) : "memory");
     __syncthreads();  // every wave's pieces of c landed; everyone is past chunk c - 1
-    if (c + 2 < nch) issue(c + 2);
-    const char *buf = ldsb + (c % 3) * CHB;
+    if (c + NBUF - 1 < nch) issue(c + NBUF - 1);
+    const char *buf = ldsb + (c % NBUF) * CHB;
 #pragma unroll
     for (int rb = 0; rb < RCH; rb += 16) {
       f32x4 acc[4];
@@ -981,7 +982,7 @@ __device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char 
   }
 }
 
-template <class L, int NW>
+template <class L, int NW, int NBUF>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(const float *__restrict__ stack,
                                                                        int64_t P, const _Float16 *__restrict__ refh,
                                                                        int32_t R, int32_t Rpad,
@@ -1027,7 +1028,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(
   const int nch = Rpad / RCH;
   const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
   const bool keyed = !libneg && !__syncthreads_or((ng[0] | ng[1] | ng[2] | ng[3]) != 0);
-#define HRF_SWEEP16(Z, K) lay_sweep16<KT, ROWB, NW, L::NSEG, Z, K>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+#define HRF_SWEEP16(Z, K) \
+  lay_sweep16<KT, ROWB, NW, L::NSEG, Z, K, NBUF>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
   if (keyed) {
     if (zs) HRF_SWEEP16(true, true);
     else HRF_SWEEP16(false, true);
@@ -1307,12 +1309,22 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
     // community layout (R = 127, where it is 25 % faster).  HRF_CLASSIFY_MFMA16=0/1 forces one.
     static const int m16_env = getenv("HRF_CLASSIFY_MFMA16") ? atoi(getenv("HRF_CLASSIFY_MFMA16")) : -1;
     const int m16 = m16_env >= 0 ? m16_env : (lay == 1);
-    const size_t shm16 = std::max<size_t>((size_t)3 * RCH * rowb, sizeof(float) * 4 * 32 * C);
-#define HRF_LAY16(LAY)                                                                                         \
-  (void)hipFuncSetAttribute((const void *)classify_pixels_lay16_kernel<LAY, 4>,                                \
+    // chunk buffers of the 16x16x32 form (HRF_CLASSIFY_NBUF=2/3): two by default -- isolated
+    // the same, but 52 instead of 78 KB of LDS per workgroup leaves room on the CU for the
+    // segmentation kernels running beside it (+2 % end to end, interleaved A/B, 2 of 3 pairs)
+    static const int nbuf = getenv("HRF_CLASSIFY_NBUF") ? atoi(getenv("HRF_CLASSIFY_NBUF")) : 2;
+    const size_t shm16 = std::max<size_t>((size_t)(nbuf == 2 ? 2 : 3) * RCH * rowb, sizeof(float) * 4 * 32 * C);
+#define HRF_LAY16N(LAY, NB)                                                                                    \
+  (void)hipFuncSetAttribute((const void *)classify_pixels_lay16_kernel<LAY, 4, NB>,                            \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm16);                           \
-  classify_pixels_lay16_kernel<LAY, 4><<<(unsigned)hrf::cdiv(P, 256), 256, shm16, s>>>(                          \
+  classify_pixels_lay16_kernel<LAY, 4, NB><<<(unsigned)hrf::cdiv(P, 256), 256, shm16, s>>>(                      \
       stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
+#define HRF_LAY16(LAY)   \
+  if (nbuf == 2) {       \
+    HRF_LAY16N(LAY, 2);  \
+  } else {               \
+    HRF_LAY16N(LAY, 3);  \
+  }
     if (m16) {
       if (lay == 1) {
         HRF_LAY16(LayEcoli);
@@ -1322,6 +1334,7 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
       HRF_LAUNCHED();
       return HRF_OK;
     }
+#undef HRF_LAY16N
 #undef HRF_LAY16
     if (lay == 1) {
       if (nw == 8) {

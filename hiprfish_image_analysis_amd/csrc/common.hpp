@@ -91,7 +91,8 @@ int lp_table_3d(int patch, int ntheta, int nphi, int32_t *off /*[ndir][patch][3]
 // hrf_erosion_seeds with the component boxes already read back to the host (seeds.hip)
 hrf_status erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
                                  const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
-                                 hipStream_t s, int32_t *ovf_dev);
+                                 hipStream_t s, int32_t *ovf_dev, char *px_scratch);
+int64_t seed_px_scratch_bytes();  // px_scratch size for erosion_seeds_hostbox
 
 hrf_status kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32_t k1, int32_t k2, int32_t max_iter,
                                           int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1, uint8_t *top2,

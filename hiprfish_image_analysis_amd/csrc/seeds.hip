@@ -142,7 +142,7 @@ __device__ void box_cc(uint8_t *fl, int32_t *par, int32_t *sz, int bh, int bw, b
 }
 
 // flags: bit0 = in play (dist_lab != 0), bit1 = seed (dist_be), bit2 = erosion result
-// one component in LDS (box <= SEED_LDS_PX_MAX pixels)
+// one component in a scratch slice (box <= SEED_LDS_PX_MAX pixels)
 __device__ void seed_component_px(char *lds, const int32_t *__restrict__ labels, int64_t H, int64_t W,
                                   const int32_t *__restrict__ box, int comp, int32_t area_max, int32_t min_obj,
                                   uint8_t *__restrict__ be_out) {
@@ -199,16 +199,23 @@ __device__ void seed_component_px(char *lds, const int32_t *__restrict__ labels,
 }
 
 // the components the run kernel hands over (class 1, or over its run capacity), listed on the
-// device: a few workgroups walk the list, so no 160 KB-LDS grid is launched per component
-__global__ __launch_bounds__(1024) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
+// device: a few 256-thread workgroups walk the list, each with a 164 KB slice of global scratch.  Not LDS:
+// the kernel is launched for every tile but usually finds the list empty (no component of the
+// bench tiles reaches it), and a 160 KB-LDS workgroup cannot be dispatched until a whole CU's
+// LDS is free -- with the classifier's workgroups resident that wait was 0.2-1.6 ms of an
+// empty launch in the segmentation chain.  The rare real work pays L2 atomics instead.
+constexpr size_t SEED_SLICE = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
+constexpr int SEED_PX_WG = 16;
+__global__ __launch_bounds__(256) void erosion_seed_kernel(const int32_t *__restrict__ labels, int64_t H, int64_t W,
                                                            const int32_t *__restrict__ box,
                                                            const int32_t *__restrict__ list,
                                                            const int32_t *__restrict__ count, int32_t area_max,
-                                                           int32_t min_obj, uint8_t *__restrict__ be_out) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
+                                                           int32_t min_obj, char *__restrict__ scratch,
+                                                           uint8_t *__restrict__ be_out) {
   const int n = *count;
+  char *mem = scratch + (size_t)blockIdx.x * SEED_SLICE;
   for (int idx = blockIdx.x; idx < n; idx += gridDim.x) {
-    seed_component_px(lds, labels, H, W, box, list[idx], area_max, min_obj, be_out);
+    seed_component_px(mem, labels, H, W, box, list[idx], area_max, min_obj, be_out);
     __syncthreads();
   }
 }
@@ -556,7 +563,8 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   HRF_HIP(hipStreamSynchronize(s));
   int32_t *ovf = nullptr;
   HRF_HIP(hipMallocAsync((void **)&ovf, sizeof(int32_t), s));
-  hrf_status st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, ovf);
+  hrf_status st =
+      ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, ovf, nullptr);
   int32_t novf = 0;
   if (st == HRF_OK) {
     HRF_HIP(hipMemcpyAsync(&novf, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -564,18 +572,21 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   }
   HRF_HIP(hipFreeAsync(ovf, s));
   if (st == HRF_OK && novf > 0)  // a large-box component overflowed the run kernel: redo the classic way
-    st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, nullptr);
+    st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, nullptr,
+                                      nullptr);
   return st;
 }
 
 }  // extern "C"
+
+int64_t hrf::seed_px_scratch_bytes() { return (int64_t)SEED_PX_WG * (int64_t)SEED_SLICE; }
 
 // The same with the boxes already on the host (hb: (ncomp + 1) x 4, as hrf_label_boxes
 // writes them): the native E. coli driver reads them back at its component-count
 // synchronisation instead of a second one here.
 hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
                                       const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
-                                      hipStream_t s, int32_t *ovf_dev) {
+                                      hipStream_t s, int32_t *ovf_dev, char *px_scratch) {
   HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
   if (ovf_dev) HRF_HIP(hipMemsetAsync(ovf_dev, 0, sizeof(int32_t), s));
   if (ncomp == 0) return HRF_OK;
@@ -601,17 +612,29 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   // is copied from host memory, whose lifetime an asynchronous copy would outlive)
   int32_t *dlist = nullptr;
   const size_t nl = (size_t)ncomp + 3;
-  HRF_HIP(hipMallocAsync((void **)&dlist, sizeof(int32_t) * nl, s));
+  const int npx_wg = std::min(ncomp, SEED_PX_WG);
+  const size_t list_bytes = (sizeof(int32_t) * nl + 255) & ~(size_t)255;
+  // the pixel kernel's scratch: the caller's (the native driver's context holds one), else
+  // allocated with the list
+  HRF_HIP(hipMallocAsync((void **)&dlist, list_bytes + (px_scratch ? 0 : (size_t)npx_wg * SEED_SLICE), s));
+  if (!px_scratch) px_scratch = reinterpret_cast<char *>(dlist) + list_bytes;
   int32_t *dcount = dlist + ncomp + 1;  // [0] pixel-kernel list length, [1] large-box overflows
   HRF_HIP(hipMemsetAsync(dcount, 0, 2 * sizeof(int32_t), s));
-  const size_t shm_max = ((SEED_LDS_PX_MAX + 15) & ~15) + 8 * (size_t)SEED_LDS_PX_MAX;
-  HRF_HIP(hipFuncSetAttribute((const void *)erosion_seed_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)shm_max));
   erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, mode, area_max, min_obj, dlist,
                                                                  dcount, be_out);
   if (ovf_dev) HRF_HIP(hipMemcpyAsync(ovf_dev, dcount + 1, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-  erosion_seed_kernel<<<(unsigned)std::min(ncomp, 16), 1024, shm_max, s>>>(labels, H, W, box, dlist, dcount, area_max,
-                                                                          min_obj, be_out);
+  static const bool dbg = getenv("HRF_SEEDS_DEBUG") != nullptr;
+  if (dbg) {  // diagnostics: how many components the pixel kernel receives (synchronises)
+    int32_t hc[2] = {0, 0};
+    HRF_HIP(hipMemcpyAsync(hc, dcount, sizeof(hc), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+    int n1 = 0;
+    for (int c = 1; c <= ncomp; ++c) n1 += seed_class(hb, c, mode) == 1;
+    fprintf(stderr, "hrf_erosion_seeds: %d components, %d class 1, %d to the pixel kernel, %d large-box overflows\n",
+            ncomp, n1, hc[0], hc[1]);
+  }
+  erosion_seed_kernel<<<(unsigned)npx_wg, 256, 0, s>>>(labels, H, W, box, dlist, dcount, area_max, min_obj,
+                                                        px_scratch, be_out);
   HRF_LAUNCHED();
   hrf_status st = HRF_OK;
   if (br1 >= 0) {

@@ -29,6 +29,7 @@ struct hrf_seg_ctx {
   int32_t *hpin = nullptr;  // pinned host slots for counts read back at a later synchronisation
   void *km = nullptr;
   int64_t km_bytes = 0;
+  char *seed_px = nullptr;  // erosion seeding's pixel-kernel scratch
   // per-label scratch, grown on demand
   int64_t lab_cap = 0;
   int32_t *box = nullptr, *cnt = nullptr;
@@ -137,6 +138,7 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
   c->km_bytes = hrf_kmeans_sorted_workspace_bytes(c->n);
   if (c->km_bytes <= 0) return fail(HRF_EHIP);
   if ((r = dalloc((char **)&c->km, (size_t)c->km_bytes))) return fail(r);
+  if ((r = dalloc(&c->seed_px, (size_t)::hrf::seed_px_scratch_bytes()))) return fail(r);
   *out = c;
   return HRF_OK;
 }
@@ -160,6 +162,7 @@ hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *c) {
   if (c->hpin) hipHostFree(c->hpin);
   if (c->hbox) hipHostFree(c->hbox);
   hipFree(c->km);
+  hipFree(c->seed_px);
   hipFree(c->box);
   hipFree(c->cnt);
   hipFree(c->mom);
@@ -204,7 +207,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   // after them are redone with those components in the whole-image loop.
   for (int attempt = 0;; ++attempt) {
     HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s,
-                                         attempt == 0 ? c->dint + 8 : nullptr));
+                                         attempt == 0 ? c->dint + 8 : nullptr, c->seed_px));
     if (attempt == 0) HRF_HIP(hipMemcpyAsync(c->hpin + 2, c->dint + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
     HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
