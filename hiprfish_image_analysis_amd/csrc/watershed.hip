@@ -117,7 +117,6 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
                                                       int32_t *__restrict__ next_tile,
                                                       const int32_t *__restrict__ tile_work) {
   __shared__ double sl[WL * WL];
-  __shared__ double sf[WL * WL];
   __shared__ int32_t sh[WL * WL];
   __shared__ int32_t sd[WL * WL];
   __shared__ int32_t sb[WL * WL];
@@ -150,25 +149,30 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       sh[idx] = in.hop[g];
       sd[idx] = RELABEL ? 0 : in.dst[g];
       sb[idx] = in.lab[g];
-      sf[idx] = negate ? -f[g] : f[g];
       sm[idx] = (uint8_t)((inm ? 1 : 0) | ((inm && markers[g]) ? 2 : 0));
     } else {
       sl[idx] = __builtin_inf();
       sh[idx] = HOP_INF;
       sd[idx] = HOP_INF;
       sb[idx] = 0;
-      sf[idx] = 0.0;
       sm[idx] = 0;
     }
   }
   __syncthreads();
   // each thread owns 4 interior pixels: (row = tid/32 + 8k, col = tid%32)
+  // the owned pixels' own values stay in registers (only a pixel's own value is ever read:
+  // 9 KB less LDS per workgroup, room beside the classifier's workgroups on a CU)
   int own[4];
   int32_t par[4];
+  double fvk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     own[k] = ((tid >> 5) + 8 * k + 1) * WL + (tid & 31) + 1;
     par[k] = -1;
+    {
+      const int64_t gr = r0 + (own[k] / WL), gc = c0 + (own[k] % WL);
+      fvk[k] = (gr < H && gc < W) ? (negate ? -f[gr * W + gc] : f[gr * W + gc]) : 0.0;
+    }
     if (RELABEL) {
       const int64_t gr = r0 + (own[k] / WL), gc = c0 + (own[k] % WL);
       if (gr < H && gc < W) par[k] = ptr[gr * W + gc];
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
           }
         }
         if (bb) {
-          const double fv = sf[i];
+          const double fv = fvk[k];
           if (bl < fv) {  // entry of level fv
             nl[k] = fv;
             nh[k] = 0;
