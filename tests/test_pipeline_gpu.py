@@ -182,6 +182,11 @@ def test_native_segmentation_run_overflow(mods):
     for c in range(250, 480, 6):
         teeth[280:470, c:c + 3] = True
     teeth[280:284, 250:480] = True
+    # a second comb whose box fits the pixel kernel (110 x 120) but whose ~2200 runs do not fit
+    # the run kernel: handed over on the device (the context's scratch)
+    for c in range(40, 160, 6):
+        teeth[40:150, c:c + 3] = True
+    teeth[40:44, 40:160] = True
     st[teeth] = (3.0 * peak / st.shape[2]) * (1.0 + 0.05 * np.random.default_rng(5).random((int(teeth.sum()), 1)))
     dstack = torch.from_numpy(st).cuda()
     seg_n, mx_n = P.segment_ecoli(dstack)
