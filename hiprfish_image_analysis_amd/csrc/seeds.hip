@@ -6,13 +6,17 @@
 // None of these steps lets information cross an 8-connected component of the starting mask:
 // a pixel's cross neighbours are 8-adjacent (same component), 4-components and 8-components
 // of a subset stay inside the component, and each component's loop ends when it is empty.
-// So every component of `cell_sm` runs the loop independently: one workgroup per component
-// keeps the component's bounding box in LDS (1 flag byte + parent + size per pixel) and
-// iterates union-find / freeze / erode / sieve until it is empty, then writes its seed
-// pixels.  Components whose box exceeds the LDS budget (large clumps of touching cells) run
-// the same loop as whole-image passes over the crop that holds all of them, padded with one
-// background row/column wherever the crop edge is not the image edge (so the erosion's
-// border_value=True applies only at the true image border).
+// So every component of `cell_sm` runs the loop independently, to the end, in one workgroup:
+//  * erosion_seed_runs_kernel (one workgroup per component, 32 KB LDS): the box as bit planes,
+//    connected components over horizontal runs -- every component whose planes fit, large
+//    boxes included (SEED_BIG_RUNS);
+//  * erosion_seed_kernel: the components the run kernel hands over (its run arrays full, or
+//    planes that do not fit), 1 flag byte + parent + size per pixel of the box (<= 18176 px)
+//    in a global scratch slice per workgroup;
+//  * whole-image passes over a crop holding the rest (boxes above 18176 px whose planes do not
+//    fit, or every large box when a large-box component overflowed the run kernel and the
+//    caller redoes the stage), padded with one background row/column wherever the crop edge is
+//    not the image edge (so the erosion's border_value=True applies only at the true border).
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -22,9 +26,7 @@
 
 namespace {
 
-// 9 B/px of LDS: boxes up to 8192 px run two workgroups per CU (72 KB); boxes up to 18176 px
-// (a clump of a few touching cells) run in a second launch using the whole 160 KB
-constexpr int SEED_LDS_PX = 8192;
+// the pixel kernel's box capacity (9 B per pixel of scratch: the 160 KB it once took in LDS)
 constexpr int SEED_LDS_PX_MAX = 18176;
 
 constexpr int RS_T = 256;
