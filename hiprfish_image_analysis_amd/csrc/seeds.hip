@@ -19,6 +19,7 @@
 //    not the image edge (so the erosion's border_value=True applies only at the true border).
 #include <algorithm>
 #include <cstdlib>
+#include <map>
 #include <vector>
 
 #include "common.hpp"
@@ -563,19 +564,29 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   std::vector<int32_t> hb((size_t)(ncomp + 1) * 4);
   HRF_HIP(hipMemcpyAsync(hb.data(), box, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));
+  // the pixel kernel's scratch: one buffer per host thread and device, reused (this function
+  // synchronises before it returns, so the next call from the thread finds it free)
+  static thread_local std::map<int, char *> px_scratch;
+  int dev = 0;
+  HRF_HIP(hipGetDevice(&dev));
+  char *&pxs = px_scratch[dev];
+  if (!pxs) HRF_HIP(hipMalloc((void **)&pxs, (size_t)::hrf::seed_px_scratch_bytes()));
   int32_t *ovf = nullptr;
   HRF_HIP(hipMallocAsync((void **)&ovf, sizeof(int32_t), s));
   hrf_status st =
-      ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, ovf, nullptr);
+      ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, ovf, pxs);
   int32_t novf = 0;
   if (st == HRF_OK) {
     HRF_HIP(hipMemcpyAsync(&novf, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HRF_HIP(hipStreamSynchronize(s));
   }
   HRF_HIP(hipFreeAsync(ovf, s));
-  if (st == HRF_OK && novf > 0)  // a large-box component overflowed the run kernel: redo the classic way
+  // a large-box component overflowed the run kernel: redo the classic way
+  if (st == HRF_OK && novf > 0) {
     st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, nullptr,
-                                      nullptr);
+                                      pxs);
+    if (st == HRF_OK) HRF_HIP(hipStreamSynchronize(s));  // the scratch is free when this returns
+  }
   return st;
 }
 
