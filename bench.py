@@ -16,7 +16,10 @@ At N=1 the line also carries "extras": the other configurations of BASELINE.json
 same way (cfg3 with the f32-MFMA classifier and without the per-pixel GEMM; cfg2 synthetic-
 community tiles against the 127-barcode library with the NL-means roofline; cfg4 the biofilm
 volume chain from a 1024x1024x64x63 stack with the enhance3d roofline; the streaming kernels
-against HBM).  (for N > 1 launch with torch.distributed.run, one process per GPU)
+against HBM).  With --gpus N > 1 and no torch.distributed environment (WORLD_SIZE unset) bench.py
+starts torch.distributed.run itself -- N fresh worker processes, one per GPU, before anything
+here touches the GPU -- and exits with its status; launched by torch.distributed.run (the
+driver's form) it runs as one rank.
 """
 from __future__ import annotations
 
@@ -248,6 +251,28 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                          "steps": steps, "concurrent": T, "classifier_mode": 2,
                                          "note": "round 1's timed path (BENCH_r01.json 1044.5)"}
     del pre
+    # the headline path on bioformats-like samples (k/4095, as load_image returns 12-bit data):
+    # same timed work, plus the watershed's tie statistics of every tile (DESIGN.md "Watershed")
+    qtiles = [([(torch.round(l.double() * 4095.0) / 4095.0).float().contiguous() for l in t[0]], t[1])
+              for t in tiles]
+    torch.cuda.synchronize()
+    wstats = []
+
+    def qjob(t):
+        stack, cn = P.register_stack(t[0], want_cn=True)
+        r = P.process_tile(stack, lib_main, calibration=t[1], image_cn=cn)
+        wstats.append(K.seg_stats(stack.device, H, W))
+        return r
+    sec = _timed_tiles(qjob, qtiles, T, streams, pool, steps, 2)
+    del qtiles
+    cfg3["quantised_4095"] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
+                              "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
+                              "tiles_run": len(wstats),
+                              "watershed_passes_mean": round(float(np.mean([s["passes"] for s in wstats])), 2),
+                              "contested_px_per_tile_mean": round(float(np.mean([s["contests"] for s in wstats])), 2),
+                              "contested_px_per_tile_max": int(max(s["contests"] for s in wstats)),
+                              "resolution_rounds_max": int(max(s["rounds"] for s in wstats)),
+                              "equal_marker_decisions_total": int(sum(s["marker_ties"] for s in wstats))}
     out["cfg3"] = cfg3
     # cfg2: synthetic-community tiles
     b = S.MULTI_BOUNDS
@@ -294,6 +319,28 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_cmd(n, argv, port):
+    """the torch.distributed.run command one rank per GPU is started with (--gpus N > 1 without a
+    torch.distributed environment)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def _self_launch(n):
+    """run N ranks as child processes (never an exec of this process) and return their status"""
+    import subprocess
+    return subprocess.call(launch_cmd(n, sys.argv[1:], _free_port()), cwd=REPO)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -308,6 +355,8 @@ def main():
                     help="run the per-pixel classification after the segmentation on one stream")
     ap.add_argument("--dump-counts", default=None, help="rank 0 writes the all-reduced barcode counts (.npy)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
 
     import torch
     import torch.distributed as dist

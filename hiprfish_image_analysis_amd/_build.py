@@ -20,7 +20,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
           "-fvisibility=hidden", "-Wno-unused-result", "-I" + os.path.join(REPO, "include")]
-HEADERS = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.inc")) + \
+HEADERS = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.h")) + \
+    glob.glob(os.path.join(CSRC, "*.inc")) + \
     [os.path.join(REPO, "include", "hrf.h")]
 
 

@@ -27,7 +27,7 @@ _CT = {
     "int64_t": ctypes.c_int64, "int32_t": ctypes.c_int32, "double": ctypes.c_double,
     "float": ctypes.c_float, "uint32_t": ctypes.c_uint32, "uint64_t": ctypes.c_uint64, "int": ctypes.c_int,
     "const float *const *": ctypes.c_void_p, "double *const *": ctypes.c_void_p,
-    "hrf_seg_ctx *": ctypes.c_void_p, "hrf_seg_ctx * *": ctypes.c_void_p,
+    "hrf_seg_ctx *": ctypes.c_void_p, "hrf_seg_ctx * *": ctypes.c_void_p, "const hrf_seg_ctx *": ctypes.c_void_p,
 }
 
 

@@ -23,6 +23,7 @@
 #include <cmath>
 
 #include "common.hpp"
+#include "detmath.h"
 
 namespace {
 
@@ -84,7 +85,7 @@ __device__ double svc_kernel(const double *x, const double *y, const SvcModel &m
       const double d = x[i] - y[i];
       s += d * d;
     }
-    return exp(-m.gamma * s);
+    return hrf_det_exp(-m.gamma * s);
   }
   for (int i = 0; i < m.f; ++i) s += x[i] * y[i];
   if (m.kernel == 0) return s;
@@ -156,7 +157,7 @@ constexpr int PROB_SLOTS = PROB_KMAX / PROB_T;
 
 __device__ __forceinline__ double platt(double dec, double A, double B) {
   const double fApB = dec * A + B;
-  return fApB >= 0 ? exp(-fApB) / (1.0 + exp(-fApB)) : 1.0 / (1 + exp(fApB));
+  return fApB >= 0 ? hrf_det_exp(-fApB) / (1.0 + hrf_det_exp(-fApB)) : 1.0 / (1 + hrf_det_exp(fApB));
 }
 
 __global__ __launch_bounds__(PROB_T) void svc_proba_kernel(const double *__restrict__ x, int64_t ldx, SvcModel m,
@@ -386,7 +387,7 @@ __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *
   const double mean_all = *mean_dev;
   const double *di = dist + i * k;
   const int32_t *ii = idx + i * k;
-  const double target = log2(n_neighbors);
+  const double target = hrf_det_log(n_neighbors) * 1.4426950408889634;  /* log2 */
   float rho = 0.0f;
   int nnz = 0;
   for (int j = 0; j < k; ++j) nnz += di[j] > 0.0;
@@ -423,7 +424,7 @@ __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *
     double psum = 0.0;
     for (int j = 1; j < k; ++j) {
       const double dd = di[j] - (double)rho;
-      psum += dd > 0 ? exp(-(dd / mid)) : 1.0;
+      psum += dd > 0 ? hrf_det_exp(-(dd / mid)) : 1.0;
     }
     if (fabs(psum - target) < 1e-5) break;
     if (psum > target) {
@@ -450,7 +451,7 @@ __global__ void umap_init_kernel(const int32_t *__restrict__ idx, const double *
     float v = 0.0f;
     if (ii[j] >= 0) {
       const double dd = di[j] - (double)rho;
-      v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)exp(-(dd / (double)sigma));
+      v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)hrf_det_exp(-(dd / (double)sigma));
       w[n] = v;
       ord[n] = j;
       ++n;
@@ -548,8 +549,8 @@ __global__ void umap_refine_kernel(const int32_t *__restrict__ idx, const float 
       const double d2 = umap_rdist(cur, o, d);
       double gc = 0.0;
       if (d2 > 0.0) {
-        gc = -2.0 * a * b * pow(d2, bm1);
-        gc /= a * pow(d2, b) + 1.0;
+        gc = -2.0 * a * b * hrf_det_pow(d2, bm1);
+        gc /= a * hrf_det_pow(d2, b) + 1.0;
       }
       for (int c = 0; c < d; ++c) {
         const double g = umap_clip(gc * (double)(cur[c] - o[c]));
@@ -565,7 +566,7 @@ __global__ void umap_refine_kernel(const int32_t *__restrict__ idx, const float 
         double gn;
         if (dn > 0.0) {
           gn = 2.0 * gamma * b;
-          gn /= (0.001 + dn) * (a * pow(dn, b) + 1.0);
+          gn /= (0.001 + dn) * (a * hrf_det_pow(dn, b) + 1.0);
         } else if (kk == i) {
           continue;
         } else {

@@ -1,8 +1,8 @@
 // kmeans.hip -- 1-D KMeans thresholding (a8): sklearn's KMeans, k-means++ and all.
 //
 // Reference: sklearn KMeans(n_clusters=k, random_state=0).fit_predict(x.reshape(-1,1))
-// (ecoli measurement.py:73, :85; multispecies :125, :141) with the defaults of its era
-// (n_init=10).  Restated from sklearn 1.7.2 (KMeans.fit, _kmeans_plusplus,
+// (ecoli measurement.py:73, :85; multispecies :125, :141), n_init=10.  Restated from
+// sklearn 1.7.2 -- the sklearn importable here -- (KMeans.fit, _kmeans_plusplus,
 // _kmeans_single_lloyd, _relocate_empty_clusters_dense); the CPU restatement is
 // oracle/kmeans_sk.c, pinned to sklearn itself in tests/test_oracle_golden.py:
 //  * the random stream is numpy's RandomState(0) (MT19937, init_genrand) replayed on the host:
@@ -21,6 +21,10 @@
 // rint(x * 2^s) in int64 (prefix sums over the value-sorted array, plus 128-bit prefix sums of
 // their squares), so every decision is independent of reduction order and equal to the CPU
 // restatement's bit for bit.
+// Parity is pinned to sklearn 1.7.2 only.  The reference ran with the sklearn of its era
+// (0.20-0.22: first centre from randint, per-run int32 seeds, Elkan by default), whose random
+// streams differ; no fixture in the reference pins that, so parity with the reference-era
+// sklearn is unpinned (an ambiguous 1-D split could land differently).
 //
 // MI355X mapping.  The valid values are bucket sorted once (2^20 value buckets, a two-digit
 // counting sort without global atomics) and per-bucket prefix sums of q and q^2 are taken; a

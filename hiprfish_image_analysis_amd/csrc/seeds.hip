@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <map>
+#include <mutex>
 #include <vector>
 
 #include "common.hpp"
@@ -536,6 +537,44 @@ __global__ void box_kernel(const int32_t *__restrict__ lab, int64_t H, int64_t W
   }
 }
 
+// Pool of pixel-kernel scratch buffers for the standalone hrf_erosion_seeds (the native
+// drivers pass their context's).  A buffer is leased for one call; the lease's destructor
+// synchronises the call's stream and returns the buffer only if that succeeded (a stream in
+// error keeps its buffer out of circulation).  Pool size = the peak number of concurrent
+// calls per device; the buffers live for the process.
+struct PxScratchPool {
+  std::mutex mu;
+  std::map<int, std::vector<char *>> idle;
+};
+PxScratchPool &px_pool() {
+  static PxScratchPool *p = new PxScratchPool;  // never destroyed: outlives late callers
+  return *p;
+}
+struct PxScratchLease {
+  int dev;
+  hipStream_t s;
+  char *buf = nullptr;
+  PxScratchLease(int d, hipStream_t st) : dev(d), s(st) {}
+  hipError_t acquire() {
+    {
+      std::lock_guard<std::mutex> g(px_pool().mu);
+      auto &v = px_pool().idle[dev];
+      if (!v.empty()) {
+        buf = v.back();
+        v.pop_back();
+        return hipSuccess;
+      }
+    }
+    return hipMalloc((void **)&buf, (size_t)::hrf::seed_px_scratch_bytes());
+  }
+  ~PxScratchLease() {
+    if (!buf) return;
+    if (hipStreamSynchronize(s) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(px_pool().mu);
+    px_pool().idle[dev].push_back(buf);
+  }
+};
+
 }  // namespace
 
 extern "C" {
@@ -564,13 +603,14 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   std::vector<int32_t> hb((size_t)(ncomp + 1) * 4);
   HRF_HIP(hipMemcpyAsync(hb.data(), box, hb.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HRF_HIP(hipStreamSynchronize(s));
-  // the pixel kernel's scratch: one buffer per host thread and device, reused (this function
-  // synchronises before it returns, so the next call from the thread finds it free)
-  static thread_local std::map<int, char *> px_scratch;
+  // the pixel kernel's scratch: checked out of a per-device pool for this call and returned
+  // by the guard on every return path, after the stream has drained -- so no later call, from
+  // any thread or stream, can receive a buffer a kernel of this call may still touch
   int dev = 0;
   HRF_HIP(hipGetDevice(&dev));
-  char *&pxs = px_scratch[dev];
-  if (!pxs) HRF_HIP(hipMalloc((void **)&pxs, (size_t)::hrf::seed_px_scratch_bytes()));
+  PxScratchLease pxl(dev, s);
+  HRF_HIP(pxl.acquire());
+  char *pxs = pxl.buf;
   int32_t *ovf = nullptr;
   HRF_HIP(hipMallocAsync((void **)&ovf, sizeof(int32_t), s));
   hrf_status st =
@@ -585,8 +625,8 @@ hrf_status hrf_erosion_seeds(const int32_t *labels, int64_t H, int64_t W, int32_
   if (st == HRF_OK && novf > 0) {
     st = ::hrf::erosion_seeds_hostbox(labels, H, W, ncomp, box, hb.data(), area_max, min_obj, be_out, s, nullptr,
                                       pxs);
-    if (st == HRF_OK) HRF_HIP(hipStreamSynchronize(s));  // the scratch is free when this returns
   }
+  if (st == HRF_OK) HRF_HIP(hipStreamSynchronize(s));  // (the lease synchronises on error paths)
   return st;
 }
 

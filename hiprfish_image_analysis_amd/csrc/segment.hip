@@ -30,6 +30,9 @@ struct hrf_seg_ctx {
   void *km = nullptr;
   int64_t km_bytes = 0;
   char *seed_px = nullptr;  // erosion seeding's pixel-kernel scratch
+  // the last chain's watershed: passes, contested pixels, resolution rounds, decisions between
+  // equal-valued markers of different labels (hrf_watershed_ex ties_host) -- hrf_seg_ctx_stats
+  int32_t ws_stats[4] = {0, 0, 0, 0};
   // per-label scratch, grown on demand
   int64_t lab_cap = 0;
   int32_t *box = nullptr, *cnt = nullptr;
@@ -211,8 +214,8 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
     if (attempt == 0) HRF_HIP(hipMemcpyAsync(c->hpin + 2, c->dint + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
     HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
-    int32_t passes = 0;
-    HRF_TRY(hrf_watershed(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :113
+    HRF_TRY(hrf_watershed_ex(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, c->ws_stats,
+                             c->ws_stats + 1, s));  // :113
     if (attempt > 0 || c->hpin[2] == 0) break;
   }
   const int32_t nseeds = c->hpin[0];  // read back by the watershed's synchronisation
@@ -223,6 +226,12 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   HRF_TRY(hrf_region_props(c->mom, nseeds, c->props, s));
   HRF_TRY(hrf_shape_filter(lab3, H, W, c->props, nseeds, 15.0, 35.0, seg_out, s));   // :117-126
   *maxlab_host = nseeds;
+  return HRF_OK;
+}
+
+hrf_status hrf_seg_ctx_stats(const hrf_seg_ctx *c, int32_t *out) {
+  HRF_REQUIRE(c && out, "seg_ctx_stats: bad arguments");
+  for (int i = 0; i < 4; ++i) out[i] = c->ws_stats[i];
   return HRF_OK;
 }
 
@@ -272,8 +281,8 @@ hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t 
   HRF_TRY(hrf_mask_mul_f64(fin, bkg, n, final_bkg, s));                         // :150
   HRF_TRY(hrf_mask_labels(seeds, bkg, n, seeds_b, s));                          // :152
   HRF_TRY(hrf_and_u8(rough, bkg, n, a, s));                                     // :153
-  int32_t passes = 0;
-  HRF_TRY(hrf_watershed(final_bkg, 1, seeds_b, a, H, W, ws, c->ws_state, c->ws_flag, 100000, &passes, s));  // :154
+  HRF_TRY(hrf_watershed_ex(final_bkg, 1, seeds_b, a, H, W, ws, c->ws_state, c->ws_flag, 100000, c->ws_stats,
+                           c->ws_stats + 1, s));  // :154
   HRF_TRY(ensure_labels(c, nseeds, s));
   HRF_TRY(hrf_remove_small_objects_labels(ws, n, nseeds, 60, seeds, c->cnt, s));     // :155
   HRF_TRY(hrf_clear_border(seeds, H, W, lab3, c->parent, c->size, s));         // :156

@@ -460,12 +460,15 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   int32_t total = 0, rounds = 0;
   char *scratch = nullptr;
   int64_t scratch_bytes = 0;
+  // stream-ordered: a tile with contests must not stall the other tiles' streams (hipFree
+  // would synchronise the whole device)
   struct Scratch {
     char **p;
+    hipStream_t s;
     ~Scratch() {
-      if (*p) hipFree(*p);
+      if (*p) (void)hipFreeAsync(*p, s);
     }
-  } sguard{&scratch};
+  } sguard{&scratch, s};
   while (ncontest > 0) {
     total += ncontest;
     ++rounds;
@@ -477,10 +480,10 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       const int64_t stride = walker_bytes(cap, hcap, gcap);
       const int64_t nth = ntodo < threads ? ntodo : threads;
       if (nth * stride > scratch_bytes) {
-        if (scratch) HRF_HIP(hipFree(scratch));
+        if (scratch) HRF_HIP(hipFreeAsync(scratch, s));
         scratch = nullptr;
         scratch_bytes = 0;
-        HRF_HIP(hipMalloc((void **)&scratch, (size_t)(nth * stride)));
+        HRF_HIP(hipMallocAsync((void **)&scratch, (size_t)(nth * stride), s));
         scratch_bytes = nth * stride;
       }
       HRF_HIP(hipMemsetAsync(flag_ws + 3, 0, sizeof(int32_t), s));

@@ -312,7 +312,7 @@ HRF_HD inline bool ws_resolve_one(const WsGeom &g, int32_t x, int32_t *ptr, Walk
       }
       int32_t nt2 = 0;
       w.pb[nt2++] = wp;
-      for (int32_t qi = 0; qi < nt2; ++qi) {
+      for (int32_t qi = 0; qi < nt2 && !fail; ++qi) {
         const int32_t q = w.pb[qi];
         const int64_t r = q / g.W, c = q - r * g.W;
         const int32_t nb[4] = {r > 0 ? q - (int32_t)g.W : -1, c > 0 ? q - 1 : -1, c + 1 < g.W ? q + 1 : -1,
@@ -320,6 +320,10 @@ HRF_HD inline bool ws_resolve_one(const WsGeom &g, int32_t x, int32_t *ptr, Walk
         for (int j = 0; j < 4; ++j) {
           const int32_t y = nb[j];
           if (y < 0 || !w.contains(y, 0) || !w.insert(y, 1, &ovf)) continue;
+          if (nt2 >= cap) {  // the slot plus the whole component: cap + 1 entries at most
+            fail = true;
+            break;
+          }
           ptr[y] = q;
           w.pb[nt2++] = y;
         }

@@ -17,9 +17,21 @@ straight from the file with numpy, no JVM:
 
 Subblocks of the first scene at z = 0, t = 0, pyramid level 0 (stored size == size) are placed
 by their X / Y start (mosaic tiles stitched, later tiles over earlier ones in directory order)
-and C index.  Supported: uncompressed Gray8 / Gray16 / Gray32Float / Gray32 subblocks -- what
-ZEN 2.x writes for LSM 880 lambda-mode acquisitions.  JPEG-XR and zstd compressed subblocks
-(later ZEN versions) raise with the compression named: no decoder for them is in this image.
+and C index.  Supported: Gray8 / Gray16 / Gray32Float / Gray32 subblocks, uncompressed (what
+ZEN 2.x writes for LSM 880 lambda-mode acquisitions) or zstd-compressed (ZEN 3.x: "Zstd0" = a
+bare zstd frame, "Zstd1" = a small header whose chunk 1 flags the low/high byte split of 16-bit
+data, then the frame; decoded with the zstd codec pyarrow carries).  JPEG-XR subblocks raise with
+the compression named: no decoder for them is in this image.  A subblock must hold one plane
+(C, Z, T sizes 1 -- what ZEN writes for spectral acquisitions); anything else raises rather than
+returning part of it.
+
+The biofilm script's loaders (hiprfish_imaging_biofilm_analysis.py:55-120) are here too:
+`load_ztslice(path, z, t, series)`, the z-stacks `load_image_zstack_fixed_t(path, t)` ->
+(H, W, Z, C) (np.stack over z on axis 2, `load_image_tile` = t 0) and the z-window
+`load_image_zstack_fixed_t_memory_efficient`, and the OME sizes `get_{x,y,c,z,t}_range` /
+`get_image_count` from the directory.  A `series` selects a mosaic tile (M index) unstitched,
+as Bio-Formats' per-tile series do; series=None stitches the scene.
+
 Bio-Formats itself is absent here, so parity with load_image is unpinned; the layout follows
 the published ZISRAW specification and is exercised on files written to it (tests/test_czi.py).
 """
@@ -95,62 +107,202 @@ def read_directory(buf):
     return entries
 
 
+def _zstd(raw, nbytes):
+    try:
+        import pyarrow as pa
+    except ImportError as ex:  # pragma: no cover - pyarrow is in the image
+        raise CziError("zstd subblock but no zstd codec importable (%s)" % ex)
+    return pa.decompress(bytes(raw), decompressed_size=nbytes, codec="zstd", asbytes=True)
+
+
+def _decode(buf, off, size, compression, nbytes, itemsize):
+    """subblock payload -> nbytes of row-major little-endian samples"""
+    if compression == 0:
+        return buf, off
+    if compression == 5:      # Zstd0: one zstd frame
+        return _zstd(memoryview(buf)[off:off + size], nbytes), 0
+    if compression == 6:      # Zstd1: header (its own size in byte 0; chunk 1 = hi/lo flag)
+        hsize = buf[off]
+        if hsize < 1 or hsize > size:
+            raise CziError("Zstd1 header size %d" % hsize)
+        hilo = False
+        q = off + 1
+        while q < off + hsize:
+            chunk = buf[q]
+            if chunk != 1 or q + 1 >= off + hsize:
+                raise CziError("Zstd1 header chunk %d not understood" % chunk)
+            hilo = bool(buf[q + 1] & 1)
+            q += 2
+        data = _zstd(memoryview(buf)[off + hsize:off + size], nbytes)
+        if hilo and itemsize == 2:  # low bytes of every sample first, then the high bytes
+            lo = np.frombuffer(data, np.uint8, nbytes // 2)
+            hi = np.frombuffer(data, np.uint8, nbytes // 2, offset=nbytes // 2)
+            data = np.stack([lo, hi], axis=1).tobytes()
+        elif hilo:
+            raise CziError("Zstd1 low/high byte split on %d-byte samples" % itemsize)
+        return data, 0
+    raise CziError("subblock compression %s is not supported (no decoder in this build)"
+                   % COMPRESSION.get(compression, compression))
+
+
 def _subblock_pixels(buf, e):
     p = _segment(buf, e.file_position, "ZISRAWSUBBLOCK")
     meta_size, _att_size, data_size = struct.unpack_from("<iiq", buf, p)
     _, esize = _parse_entry(buf, p + 16)
     head = max(256, 16 + esize)
     data_off = p + head + meta_size
-    if e.compression != 0:
-        raise CziError("subblock compression %s is not supported (no decoder in this build)"
-                       % COMPRESSION.get(e.compression, e.compression))
+    for d in ("C", "Z", "T"):
+        if d in e.dims and (e.dims[d][1] != 1 or e.dims[d][2] != 1):
+            raise CziError("subblock with %s size %d: multi-plane subblocks are not supported"
+                           % (d, e.dims[d][1]))
     if e.pixel_type not in PIXEL_TYPES:
         raise CziError("pixel type %d is not a grey type this reader handles" % e.pixel_type)
     _, dt, _ = PIXEL_TYPES[e.pixel_type]
     ys, xs = e.dims["Y"][2], e.dims["X"][2]
     n = xs * ys
-    if data_size < n * np.dtype(dt).itemsize:
+    nbytes = n * np.dtype(dt).itemsize
+    src, off = _decode(buf, data_off, data_size, e.compression, nbytes, np.dtype(dt).itemsize)
+    if len(src) - off < nbytes or (e.compression == 0 and data_size < nbytes):
         raise CziError("subblock data %d bytes, %d x %d pixels expected" % (data_size, ys, xs))
-    return np.frombuffer(buf, dtype=dt, count=n, offset=data_off).reshape(ys, xs)
+    return np.frombuffer(src, dtype=dt, count=n, offset=off).reshape(ys, xs)
 
 
-def load_image(path, rescale=True, z=0, t=0):
-    """bioformats.load_image(path) for a CZI spectral acquisition: (H, W, C) float32 (rescaled
-    by the pixel type's maximum) or the raw sample type with rescale=False"""
+def _open(path):
     with open(path, "rb") as f:
-        buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+        return mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+
+
+def _close(buf):
     try:
-        entries = read_directory(buf)
-        sel = [e for e in entries if e.pyramid_type == 0 and e.start("Z") == z and e.start("T") == t
-               and e.dims["X"][1] == e.dims["X"][2] and e.dims["Y"][1] == e.dims["Y"][2]]
-        if not sel:
-            raise CziError("%s: no level-0 subblocks at z=%d, t=%d" % (path, z, t))
-        scene = min(e.start("S") for e in sel)
-        sel = [e for e in sel if e.start("S") == scene]
-        types = {e.pixel_type for e in sel}
-        if len(types) != 1:
-            raise CziError("%s: mixed pixel types %s" % (path, sorted(types)))
-        ptype = types.pop()
-        if ptype not in PIXEL_TYPES:
-            raise CziError("pixel type %d is not a grey type this reader handles" % ptype)
-        _, dt, scale = PIXEL_TYPES[ptype]
-        x0 = min(e.start("X") for e in sel)
-        y0 = min(e.start("Y") for e in sel)
-        W = max(e.start("X") + e.dims["X"][1] for e in sel) - x0
-        H = max(e.start("Y") + e.dims["Y"][1] for e in sel) - y0
-        c0 = min(e.start("C") for e in sel)
-        C = max(e.start("C") + (e.dims["C"][1] if "C" in e.dims else 1) for e in sel) - c0
-        out = np.zeros((H, W, C), dtype=dt)
-        for e in sel:
-            px = _subblock_pixels(buf, e)
-            ys, xs = e.start("Y") - y0, e.start("X") - x0
-            out[ys:ys + px.shape[0], xs:xs + px.shape[1], e.start("C") - c0] = px
-            del px
-    finally:
-        try:
-            buf.close()
-        except BufferError:      # a view survives an exception path; the map closes with it
-            pass
+        buf.close()
+    except BufferError:      # a view survives an exception path; the map closes with it
+        pass
+
+
+def _level0(entries):
+    return [e for e in entries if e.pyramid_type == 0
+            and e.dims["X"][1] == e.dims["X"][2] and e.dims["Y"][1] == e.dims["Y"][2]]
+
+
+def _plane(buf, entries, path, z, t, series):
+    sel = [e for e in _level0(entries) if e.start("Z") == z and e.start("T") == t]
+    if not sel:
+        raise CziError("%s: no level-0 subblocks at z=%d, t=%d" % (path, z, t))
+    scene = min(e.start("S") for e in sel)
+    sel = [e for e in sel if e.start("S") == scene]
+    if series is not None:
+        tiles = sorted({e.start("M") for e in sel})
+        if not 0 <= series < len(tiles):
+            raise CziError("%s: series %d of %d mosaic tiles" % (path, series, len(tiles)))
+        sel = [e for e in sel if e.start("M") == tiles[series]]
+    types = {e.pixel_type for e in sel}
+    if len(types) != 1:
+        raise CziError("%s: mixed pixel types %s" % (path, sorted(types)))
+    ptype = types.pop()
+    if ptype not in PIXEL_TYPES:
+        raise CziError("pixel type %d is not a grey type this reader handles" % ptype)
+    _, dt, scale = PIXEL_TYPES[ptype]
+    x0 = min(e.start("X") for e in sel)
+    y0 = min(e.start("Y") for e in sel)
+    W = max(e.start("X") + e.dims["X"][1] for e in sel) - x0
+    H = max(e.start("Y") + e.dims["Y"][1] for e in sel) - y0
+    c0 = min(e.start("C") for e in sel)
+    C = max(e.start("C") + (e.dims["C"][1] if "C" in e.dims else 1) for e in sel) - c0
+    out = np.zeros((H, W, C), dtype=dt)
+    for e in sel:
+        px = _subblock_pixels(buf, e)
+        ys, xs = e.start("Y") - y0, e.start("X") - x0
+        out[ys:ys + px.shape[0], xs:xs + px.shape[1], e.start("C") - c0] = px
+        del px
+    return out, scale
+
+
+def _rescaled(out, scale, rescale):
     if rescale:
         return (out.astype(np.float32) / np.float32(scale)) if scale != 1.0 else out.astype(np.float32)
     return out
+
+
+def load_image(path, rescale=True, z=0, t=0, series=None):
+    """bioformats.load_image(path, z=, t=, series=) for a CZI spectral acquisition: (H, W, C)
+    float32 (rescaled by the pixel type's maximum) or the raw sample type with rescale=False"""
+    buf = _open(path)
+    try:
+        out, scale = _plane(buf, read_directory(buf), path, z, t, series)
+    finally:
+        _close(buf)
+    return _rescaled(out, scale, rescale)
+
+
+def dims(path):
+    """{'X','Y','C','Z','T','M'} sizes of the first scene's level-0 plane set (the OME Pixels
+    sizes the biofilm script queries; M = mosaic tiles = Bio-Formats' series count per scene)"""
+    buf = _open(path)
+    try:
+        ent = _level0(read_directory(buf))
+    finally:
+        _close(buf)
+    if not ent:
+        raise CziError("%s: no level-0 subblocks" % path)
+    scene = min(e.start("S") for e in ent)
+    ent = [e for e in ent if e.start("S") == scene]
+    out = {}
+    for d in ("C", "Z", "T", "M"):
+        vals = {e.start(d) for e in ent}
+        out[d] = max(vals) - min(vals) + 1
+    out["X"] = max(e.start("X") + e.dims["X"][1] for e in ent) - min(e.start("X") for e in ent)
+    out["Y"] = max(e.start("Y") + e.dims["Y"][1] for e in ent) - min(e.start("Y") for e in ent)
+    return out
+
+
+def get_x_range(path):
+    return dims(path)["X"]
+
+
+def get_y_range(path):
+    return dims(path)["Y"]
+
+
+def get_c_range(path):
+    return dims(path)["C"]
+
+
+def get_z_range(path):
+    return dims(path)["Z"]
+
+
+def get_t_range(path):
+    return dims(path)["T"]
+
+
+def get_image_count(path):
+    return dims(path)["M"]
+
+
+def load_ztslice(path, z_index, t_index, series=None, rescale=True):
+    return load_image(path, rescale=rescale, z=z_index, t=t_index, series=series)
+
+
+def load_image_zstack_fixed_t_memory_efficient(path, t, z_min, z_max, series=None, rescale=True):
+    """(H, W, z_max - z_min, C): planes z_min..z_max-1 stacked on axis 2, the file mapped once"""
+    buf = _open(path)
+    try:
+        ent = read_directory(buf)
+        planes = []
+        scale = 1.0
+        for z in range(z_min, z_max):
+            a, scale = _plane(buf, ent, path, z, t, series)
+            planes.append(a)
+    finally:
+        _close(buf)
+    if not planes:
+        raise CziError("%s: empty z range [%d, %d)" % (path, z_min, z_max))
+    return _rescaled(np.stack(planes, axis=2), scale, rescale)
+
+
+def load_image_zstack_fixed_t(path, t, series=None, rescale=True):
+    return load_image_zstack_fixed_t_memory_efficient(path, t, 0, get_z_range(path), series, rescale)
+
+
+def load_image_tile(path, rescale=True):
+    return load_image_zstack_fixed_t(path, 0, rescale=rescale)

@@ -819,6 +819,16 @@ def _seg_ctx(dev, H, W):
     return h
 
 
+def seg_stats(device, H, W):
+    """the watershed of the last native chain run on the current stream's (H, W) context:
+    {passes, contests, rounds, marker_ties} (hrf_seg_ctx_stats; marker_ties = decisions between
+    equal-valued markers of different labels, DESIGN.md "Watershed")"""
+    import ctypes
+    out = (ctypes.c_int32 * 4)()
+    _lib.call("hrf_seg_ctx_stats", _seg_ctx(torch.device(device), H, W), ctypes.addressof(out))
+    return dict(zip(("passes", "contests", "rounds", "marker_ties"), list(out)))
+
+
 def segment_ecoli_native(stack, image_cn=None):
     """ecoli measurement.py:44-127 in one native call -> (segmentation int32, max label);
     with image_cn (log(sum + 1e-2), f64 H x W, e.g. from register_assemble(cn_mode=1)) the

@@ -291,6 +291,9 @@ HRF_API hrf_status hrf_watershed_ex(const double *image, int32_t negate, const i
 typedef struct hrf_seg_ctx hrf_seg_ctx;
 HRF_API hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out);
 HRF_API hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *ctx);
+/* the context's last chain, its watershed: out[4] = passes, contested pixels, resolution
+ * rounds, equal-valued-marker decisions (hrf_watershed_ex ties_host) */
+HRF_API hrf_status hrf_seg_ctx_stats(const hrf_seg_ctx *ctx, int32_t *out);
 /* ecoli measurement.py:44-127: seg_out (H*W int32, labels not re-sequenced), *maxlab_host */
 HRF_API hrf_status hrf_segment_ecoli(hrf_seg_ctx *ctx, const float *stack, int32_t C, int32_t *seg_out,
                                      int32_t *maxlab_host, hrf_stream_t stream);

@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include "../hiprfish_image_analysis_amd/csrc/detmath.h"
 
 static double svc_k(const double *x, const double *y, int f, int kernel, double gamma, double coef0, int degree) {
   double s = 0.0;
@@ -30,7 +31,7 @@ static double svc_k(const double *x, const double *y, int f, int kernel, double 
       const double d = x[i] - y[i];
       s += d * d;
     }
-    return exp(-gamma * s);
+    return hrf_det_exp(-gamma * s);
   }
   for (int i = 0; i < f; ++i) s += x[i] * y[i];
   if (kernel == 0) return s;
@@ -79,10 +80,35 @@ void oracle_svc_predict(const double *x, int64_t n, int64_t ldx, int f, const do
  * [1e-7, 1 - 1e-7], multiclass_probability (max(100, k) iterations, eps 0.005 / k) */
 static double sigmoid_predict(double dec, double A, double B) {
   const double fApB = dec * A + B;
-  if (fApB >= 0) return exp(-fApB) / (1.0 + exp(-fApB));
-  return 1.0 / (1 + exp(fApB));
+  if (fApB >= 0) return hrf_det_exp(-fApB) / (1.0 + hrf_det_exp(-fApB));
+  return 1.0 / (1 + hrf_det_exp(fApB));
 }
 
+/* multiclass_probability follows libsvm's svm.cpp (Wu, Lin and Weng's pairwise coupling, as
+ * sklearn vendors it), whose licence asks for this notice:
+ *
+ * Copyright (c) 2000-2019 Chih-Chung Chang and Chih-Jen Lin.  All rights reserved.
+ *
+ * Redistribution and use in source and binary forms, with or without modification, are
+ * permitted provided that the following conditions are met:
+ * 1. Redistributions of source code must retain the above copyright notice, this list of
+ *    conditions and the following disclaimer.
+ * 2. Redistributions in binary form must reproduce the above copyright notice, this list of
+ *    conditions and the following disclaimer in the documentation and/or other materials
+ *    provided with the distribution.
+ * 3. Neither name of copyright holders nor the names of its contributors may be used to
+ *    endorse or promote products derived from this software without specific prior written
+ *    permission.
+ *
+ * THIS SOFTWARE IS PROVIDED BY THE COPYRIGHT HOLDERS AND CONTRIBUTORS "AS IS" AND ANY EXPRESS
+ * OR IMPLIED WARRANTIES, INCLUDING, BUT NOT LIMITED TO, THE IMPLIED WARRANTIES OF
+ * MERCHANTABILITY AND FITNESS FOR A PARTICULAR PURPOSE ARE DISCLAIMED.  IN NO EVENT SHALL THE
+ * REGENTS OR CONTRIBUTORS BE LIABLE FOR ANY DIRECT, INDIRECT, INCIDENTAL, SPECIAL, EXEMPLARY,
+ * OR CONSEQUENTIAL DAMAGES (INCLUDING, BUT NOT LIMITED TO, PROCUREMENT OF SUBSTITUTE GOODS OR
+ * SERVICES; LOSS OF USE, DATA, OR PROFITS; OR BUSINESS INTERRUPTION) HOWEVER CAUSED AND ON ANY
+ * THEORY OF LIABILITY, WHETHER IN CONTRACT, STRICT LIABILITY, OR TORT (INCLUDING NEGLIGENCE OR
+ * OTHERWISE) ARISING IN ANY WAY OUT OF THE USE OF THIS SOFTWARE, EVEN IF ADVISED OF THE
+ * POSSIBILITY OF SUCH DAMAGE. */
 static void multiclass_probability(int k, double **r, double *p, double **Q, double *Qp) {
   int t, j, iter, max_iter = k > 100 ? k : 100;
   double pQp, eps = 0.005 / k;
@@ -232,7 +258,7 @@ void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k,
   double mean_all = 0.0;
   for (int64_t e = 0; e < nq * k; ++e) mean_all += dist[e];
   mean_all /= (double)(nq * k);
-  const double target = log2(n_neighbors);
+  const double target = hrf_det_log(n_neighbors) * 1.4426950408889634;  /* log2 */
   float *w = (float *)malloc(sizeof(float) * (size_t)k);
   int *ord = (int *)malloc(sizeof(int) * (size_t)k);
   for (int64_t i = 0; i < nq; ++i) {
@@ -273,7 +299,7 @@ void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k,
       double psum = 0.0;
       for (int j = 1; j < k; ++j) {
         const double dd = di[j] - (double)rho;
-        psum += dd > 0 ? exp(-(dd / mid)) : 1.0;
+        psum += dd > 0 ? hrf_det_exp(-(dd / mid)) : 1.0;
       }
       if (fabs(psum - target) < 1e-5) break;
       if (psum > target) {
@@ -298,7 +324,7 @@ void oracle_umap_init(const int32_t *idx, const double *dist, int64_t nq, int k,
       float v = 0.0f;
       if (ii[j] >= 0) {
         const double dd = di[j] - (double)rho;
-        v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)exp(-(dd / (double)sigma));
+        v = (dd <= 0.0 || sigma == 0.0f) ? 1.0f : (float)hrf_det_exp(-(dd / (double)sigma));
         w[n] = v;
         ord[n] = j;
         ++n;
@@ -396,8 +422,8 @@ void oracle_umap_refine(const int32_t *idx, const float *memb, int64_t nq, int k
         const double d2 = urdist(cur, o, d);
         double gc = 0.0;
         if (d2 > 0.0) {
-          gc = -2.0 * a * b * pow(d2, b - 1.0);
-          gc /= a * pow(d2, b) + 1.0;
+          gc = -2.0 * a * b * hrf_det_pow(d2, b - 1.0);
+          gc /= a * hrf_det_pow(d2, b) + 1.0;
         }
         for (int c = 0; c < d; ++c) {
           const double g = uclip(gc * (double)(cur[c] - o[c]));
@@ -413,7 +439,7 @@ void oracle_umap_refine(const int32_t *idx, const float *memb, int64_t nq, int k
           double gn;
           if (dn > 0.0) {
             gn = 2.0 * gamma * b;
-            gn /= (0.001 + dn) * (a * pow(dn, b) + 1.0);
+            gn /= (0.001 + dn) * (a * hrf_det_pow(dn, b) + 1.0);
           } else if (kk == i) {
             continue;
           } else {

@@ -19,7 +19,8 @@ _lib = None
 
 
 def build() -> str:
-    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c", "kmeans_sk.c", "backend.c")]
+    srcs = [os.path.join(_HERE, f) for f in ("hrf_oracle.c", "ws_order.c", "kmeans_sk.c", "backend.c",
+                                              "../hiprfish_image_analysis_amd/csrc/detmath.h")]
     if not os.path.exists(_LIB) or max(os.path.getmtime(s) for s in srcs) > os.path.getmtime(_LIB):
         subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
     return _LIB

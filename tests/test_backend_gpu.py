@@ -122,16 +122,14 @@ def test_umap_init_vs_oracle(orc, golden, lc):
     out, memb = K.umap_init_transform(torch.from_numpy(idx).cuda(), dev(dist), torch.from_numpy(emb).cuda(), 15, lc,
                                       want_memb=True)
     want, wmemb = orc.umap_init(idx, dist, emb, 15.0, lc, want_memb=True)
-    # float32 memberships: the device exp and glibc's may round one ulp apart
-    np.testing.assert_allclose(memb.cpu().numpy(), wmemb, rtol=2e-7, atol=0)
-    np.testing.assert_allclose(out.cpu().numpy(), want, rtol=1e-5, atol=1e-6)
-    assert (memb.cpu().numpy() == wmemb).mean() > 0.95
+    # exp written out in IEEE operations on both sides (csrc/detmath.h): bit-exact
+    assert np.array_equal(memb.cpu().numpy(), wmemb)
+    assert np.array_equal(out.cpu().numpy(), want)
 
 
 def test_umap_refine_vs_oracle(orc, golden):
-    """the layout refinement on the same float32 inputs: same per-cell streams, same schedule;
-    float32 state with f64 gradients (pow of the device libm vs glibc may differ by an ulp, which
-    the float32 store nearly always absorbs)"""
+    """the layout refinement on the same float32 inputs: same per-cell streams, same schedule,
+    float32 state with f64 gradients, pow from csrc/detmath.h on both sides: bit-exact"""
     g = golden("backend")
     idx, dist = orc.knn(g["knn7b_q"], g["knn7b_train"], 1, 15)
     rng = np.random.default_rng(12)
@@ -141,8 +139,7 @@ def test_umap_refine_vs_oracle(orc, golden):
         want = orc.umap_refine(idx, memb, init, emb, ne, 1.577, 0.8951, 1.0, 0.25, 5.0, seed=seed)
         got = K.umap_refine(torch.from_numpy(idx).cuda(), torch.from_numpy(memb).cuda(), torch.from_numpy(init).cuda(),
                             torch.from_numpy(emb).cuda(), ne, 1.577, 0.8951, 1.0, 0.25, 5.0, seed=seed).cpu().numpy()
-        assert (got == want).all(axis=1).mean() > 0.9
-        np.testing.assert_allclose(got, want, rtol=0, atol=1e-3)
+        assert np.array_equal(got, want)
 
 
 def _random_svc(rng, ncls, f, kernel="rbf"):
@@ -186,9 +183,9 @@ def test_features_and_classify_chain(orc):
     op = orc.svc_predict(e, svc.sv.cpu().numpy(), svc.coef.cpu().numpy(), svc.intercept.cpu().numpy(),
                          svc.start.cpu().numpy(), svc.kernel, svc.gamma, svc.coef0, svc.degree)
     got = cls.cpu().numpy()
-    # the embedding matches to ~1e-15; a cell whose SVC decision sits within that of 0 could
-    # flip -- require agreement everywhere else
-    assert (got == op).mean() > 0.995
+    # every stage in the same operation order with the same exp / pow: the embedding and the
+    # SVC decisions are bit-equal, so every cell's class is
+    assert np.array_equal(got, op)
 
 
 def test_features_multi_with_scaler(orc):

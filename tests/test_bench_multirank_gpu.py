@@ -1,6 +1,7 @@
 """bench.py's world > 1 path, run once on hardware: two ranks on the one leased GPU (gloo for the
-collectives -- HRF_DIST_BACKEND), launched by torch.distributed.run as the driver launches the
-8-GPU scaling run.  Every rank processes its own tile (registration + calibration +
+collectives -- HRF_DIST_BACKEND), started as `bench.py --gpus 2` (bench.py launches
+torch.distributed.run itself when WORLD_SIZE is unset; the driver's torchrun form runs the
+same rank code).  Every rank processes its own tile (registration + calibration +
 process_tile); the all-reduced per-barcode counts must equal one process's sum over the same
 two tiles (collect_measurement_results.py:92-98).  No scaling figure comes from this test."""
 import os
@@ -28,9 +29,9 @@ def _free_port():
 def test_bench_two_ranks_counts(tmp_path):
     out = tmp_path / "counts.npy"
     env = dict(os.environ, HRF_DIST_BACKEND="gloo", OMP_NUM_THREADS="4")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "0", "--concurrent", "1", "--tiles", "1", "--no-extras",
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0", "--concurrent", "1", "--tiles", "1", "--no-extras",
            "--no-cpu-baseline", "--dump-counts", str(out)]
     r = subprocess.run(cmd, env=env, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]

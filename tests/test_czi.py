@@ -53,11 +53,54 @@ def test_gray8_float_and_plane_selection(tmp_path):
     assert np.array_equal(got[:, :, 0], f) and np.array_equal(got[:, :, 1], f * 2)
 
 
+@pytest.mark.parametrize("compression,hilo", [(5, False), (6, False), (6, True)])
+def test_zstd_subblocks(tmp_path, compression, hilo):
+    """ZEN 3.x zstd subblocks: Zstd0 (bare frame) and Zstd1 (header; optional low/high byte
+    split of 16-bit samples)"""
+    rng = np.random.default_rng(4)
+    st = rng.integers(0, 4096, (33, 47, 5), dtype=np.uint16)
+    p = str(tmp_path / "zs.czi")
+    write_spectral(p, st, tiles=2, compression=compression, hilo=hilo)
+    assert np.array_equal(czi.load_image(p, rescale=False), st)
+    f = rng.random((6, 9)).astype(np.float32)
+    pf = str(tmp_path / "zf.czi")
+    write_czi(pf, [(f, {"C": 0})], compression=compression)
+    assert np.array_equal(czi.load_image(pf)[:, :, 0], f)
+
+
+def test_zstack_loaders_and_sizes(tmp_path):
+    """biofilm loaders (hiprfish_imaging_biofilm_analysis.py:55-120): (H, W, Z, C) z-stacks,
+    z windows, per-tile series and the OME sizes"""
+    rng = np.random.default_rng(5)
+    vol = rng.integers(0, 65536, (20, 30, 4, 6), dtype=np.uint16)
+    p = str(tmp_path / "v.czi")
+    write_spectral(p, vol, tiles=2)
+    d = czi.dims(p)
+    assert (d["X"], d["Y"], d["Z"], d["C"], d["T"], d["M"]) == (30, 20, 4, 6, 1, 2)
+    assert czi.get_z_range(p) == 4 and czi.get_c_range(p) == 6 and czi.get_image_count(p) == 2
+    got = czi.load_image_zstack_fixed_t(p, 0)
+    assert got.dtype == np.float32 and got.shape == (20, 30, 4, 6)
+    assert np.array_equal(got, vol.astype(np.float32) / np.float32(65535.0))
+    assert np.array_equal(czi.load_image_tile(p, rescale=False), vol)
+    assert np.array_equal(czi.load_image_zstack_fixed_t_memory_efficient(p, 0, 1, 3, rescale=False),
+                          vol[:, :, 1:3])
+    assert np.array_equal(czi.load_ztslice(p, 2, 0, rescale=False), vol[:, :, 2])
+    # series = one mosaic tile, unstitched
+    assert np.array_equal(czi.load_image(p, rescale=False, z=1, series=1), vol[:, 15:, 1])
+    with pytest.raises(czi.CziError, match="series"):
+        czi.load_image(p, series=2)
+
+
 def test_unsupported_raise(tmp_path):
     p = str(tmp_path / "z.czi")
-    write_czi(p, [(np.zeros((4, 4), np.uint16), {})], compression=5)
-    with pytest.raises(czi.CziError, match="Zstd0"):
+    write_czi(p, [(np.zeros((4, 4), np.uint16), {})], compression=4)
+    with pytest.raises(czi.CziError, match="JpegXr"):
         czi.load_image(p)
+    # a multi-channel subblock would be read as its first plane only: refused
+    pm = str(tmp_path / "mc.czi")
+    write_czi(pm, [(np.zeros((4, 4), np.uint16), {})], sizes={"C": 3})
+    with pytest.raises(czi.CziError, match="C size 3"):
+        czi.load_image(pm)
     bad = tmp_path / "bad.czi"
     bad.write_bytes(b"NOTACZI" + b"\0" * 100)
     with pytest.raises(czi.CziError):

@@ -82,3 +82,28 @@ def test_shard_covers_all_tiles():
     for world in (1, 2, 3, 8):
         got = sorted(t for r in range(world) for t in P.shard(20, r, world))
         assert got == list(range(20))
+
+
+def test_bench_self_launch(monkeypatch):
+    """`bench.py --gpus N` without a torch.distributed environment starts torch.distributed.run
+    with N ranks as a child process (no exec, nothing on the GPU first) and exits with its
+    status; the driver's own torchrun form (WORLD_SIZE set) does not re-launch."""
+    import sys as _sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    _sys.path.insert(0, repo)
+    import bench
+
+    cmd = bench.launch_cmd(8, ["--gpus", "8", "--steps", "5"], 12345)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    i = cmd.index("--nproc-per-node")
+    assert cmd[i + 1] == "8" and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"] and cmd[-5].endswith("bench.py")
+    calls = []
+    monkeypatch.setattr(bench, "_self_launch", lambda n: calls.append(n) or 3)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(_sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1"])
+    with pytest.raises(SystemExit) as ex:
+        bench.main()
+    assert ex.value.code == 3 and calls == [2]

@@ -68,8 +68,9 @@ def test_fullsize_community_tile(mods, orc):
     stack = quantised(stack, 4095)
     assert stack.shape == (2048, 2048, 63) and ref.shape[0] == 127
     lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), b, 7)
-    res = P.process_tile(stack, lib, per_pixel=False, measure=P.measure_multispecies, variant=2)
-    oseg, olabs, oavg, oavgn = OP.measure_multispecies(host(stack))
+    res = P.process_tile(stack, lib, per_pixel=True, measure=P.measure_multispecies, variant=2)
+    st = host(stack)
+    oseg, olabs, oavg, oavgn = OP.measure_multispecies(st)
     assert np.array_equal(host(res.meas.segmentation), oseg)
     assert np.array_equal(host(res.meas.labels), olabs) and len(olabs) > 500
     np.testing.assert_allclose(host(res.meas.avgint), oavg, rtol=1e-12)
@@ -77,3 +78,101 @@ def test_fullsize_community_tile(mods, orc):
     np.testing.assert_allclose(host(res.cell_dist), odist, rtol=1e-9, atol=1e-12)
     assert np.array_equal(host(res.cell_idx), oidx)
     assert np.array_equal(host(res.counts), orc.barcode_counts(oidx, 127))
+    # per pixel (cfg2's 2048x2048x63 against the 127-row library): exact argmin wherever the
+    # restatement separates best and runner-up
+    from test_kernels_gpu import check_pixel_argmin
+    rng = np.random.default_rng(3)
+    cells = np.nonzero(oseg.ravel() > 0)[0]
+    sel = np.concatenate([rng.choice(cells, 16384, replace=False), rng.choice(oseg.size, 4096, replace=False)])
+    x = st.reshape(oseg.size, -1)[sel].astype(np.float64)
+    check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
+                       ref.astype(np.float64), b, 0.5)
+
+
+@pytest.mark.parametrize("q", [None, 4095, 255])
+def test_fullsize_bench_workload(mods, orc, q):
+    """bench.py's exact timed workload on one tile at full size (2048x2048x95, R=1023): the five
+    misregistered per-laser acquisitions (bench.py's tile generation; continuous, or
+    bioformats-like k/4095 and k/255 samples) + the flat field -> channel-max projections, FFT
+    shifts on the device, registered assembly with the coverage mask and image_cn ->
+    segmentation -> flat-fielded per-cell spectra -> per-cell and per-pixel classification ->
+    counts, identification map.  Against the restatement of ecoli measurement.py:44-162 with
+    -c T (estimate_shifts, register_stacks, measure_ecoli(calibration)).  The watershed's
+    contest / equal-marker statistics of the tile are printed (DESIGN.md "Watershed")."""
+    P, S, OP = mods
+    import bench
+    from hiprfish_image_analysis_amd import kernels as K
+    from test_kernels_gpu import check_pixel_argmin
+    H = W = 2048
+    ref = S.reference_library(bench.NBIT, S.ECOLI_BOUNDS)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), S.ECOLI_BOUNDS, bench.NBIT)
+    seed = 20190101
+    lay = S.cell_layout(H, W, S.default_ncells(H, W), lib.R, seed)
+    truth, prof = S.render_truth(H, W, lay, with_profile=True)
+    stack = S.render_stack(truth, lay, ref, seed=seed, device="cuda", profile=prof)
+    lasers = S.laser_split(stack)
+    del stack
+    if q:
+        lasers = [quantised(l, q) for l in lasers]
+    cal = S.flat_field(H, W, device="cuda")
+    reg, cn = P.register_stack(lasers, want_cn=True)
+    res = P.process_tile(reg, lib, calibration=cal, per_pixel=True, image_cn=cn)
+    torch.cuda.synchronize()
+    stats = K.seg_stats(reg.device, H, W)
+    print("watershed stats q=%s: %s" % (q, stats))
+
+    hl = [host(l) for l in lasers]
+    shifts = OP.estimate_shifts(hl, "max", 15)
+    assert P.estimate_shifts(lasers) == shifts
+    oreg = OP.register_stacks(hl, shifts, True).astype(np.float32)
+    del hl
+    assert np.array_equal(host(reg), oreg)
+    np.testing.assert_allclose(host(cn), np.log(np.sum(oreg.astype(np.float64), axis=2) + 1e-2), rtol=4e-16, atol=0)
+    o = OP.process_tile(oreg, ref, S.ECOLI_BOUNDS, calibration=host(cal))
+    seg = host(res.meas.segmentation)
+    assert np.array_equal(seg, o["segmentation"])
+    assert len(o["labels"]) > 500
+    np.testing.assert_allclose(host(res.meas.avgint), o["avgint"], rtol=1e-12)
+    np.testing.assert_allclose(host(res.cell_dist), o["cell_dist"], rtol=1e-9, atol=1e-12)
+    assert np.array_equal(host(res.cell_idx), o["cell_idx"])
+    assert np.array_equal(host(res.counts), o["counts"])
+    assert np.array_equal(host(res.identification), orc.paint_ids(o["segmentation"], o["cell_idx"] + 1))
+    rng = np.random.default_rng(2)
+    cells = np.nonzero(seg.ravel() > 0)[0]
+    sel = np.concatenate([rng.choice(cells, 16384, replace=False), rng.choice(seg.size, 4096, replace=False)])
+    x = oreg.reshape(seg.size, -1)[sel].astype(np.float64)
+    check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
+                       ref.astype(np.float64), S.ECOLI_BOUNDS, 0.5)
+
+
+def _enhance_3d_threads(pad, nthreads=16, patch=11):
+    """oracle.enhance_3d over x slabs (each output voxel reads only its patch^3 neighbourhood, so
+    slabs with a patch - 1 halo are exact); the ctypes call releases the GIL, so threads run the
+    slabs in parallel"""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import oracle as O
+    X = pad.shape[0] - patch + 1
+    cuts = np.linspace(0, X, nthreads + 1).astype(int)
+    with ThreadPoolExecutor(nthreads) as ex:
+        parts = list(ex.map(lambda k: O.enhance_3d(pad[cuts[k]:cuts[k + 1] + patch - 1]), range(nthreads)))
+    return np.concatenate(parts, axis=0)
+
+
+def test_fullsize_volume_chain_full_xy():
+    """cfg4 at its own XY size: the biofilm volume chain (biofilm :808-817: channel sum, / max,
+    edge pad 5, line_profile_memory_efficient_v2 + post-chain) on a 1024x1024x6x63 volume -- the
+    full 1024x1024 plane of the benched 1024x1024x64x63 stack, 6 z planes -- bit-exact against
+    the restatement (the bench's 64 planes cost the single-threaded restatement ~11 minutes)."""
+    from hiprfish_image_analysis_amd import pipeline as P
+    X, Y, Z, C = 1024, 1024, 6, 63
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    vol = torch.rand((X, Y, Z, C), dtype=torch.float32, device="cuda", generator=g)
+    got = host(P.enhance_volume(vol))
+    s = np.sum(host(vol).astype(np.float64), axis=3)
+    del vol
+    pad = np.pad(s / np.max(s), 5, mode="edge")
+    want = _enhance_3d_threads(pad)
+    assert got.shape == want.shape == (X, Y, Z)
+    assert np.array_equal(got, want)

@@ -504,3 +504,50 @@ def test_label_boxes(K):
     box = host(K.label_boxes(dev(lab), 3))
     assert box[1].tolist() == [3, 5, 8, 19] and box[3].tolist() == [40, 50, 44, 57]
     assert box[2][2] < box[2][0]
+
+
+def test_erosion_seeds_two_threads_two_streams(K, S):
+    """the standalone hrf_erosion_seeds from two host threads on two streams at once: its
+    pixel-kernel scratch is leased per call from a pool (seeds.hip PxScratchLease), so calls in
+    flight never share it.  One mask hands a comb to the pixel kernel, the other overflows the
+    run kernel with a large-box comb (the stage is redone); each thread alternates them, and
+    every result equals the restatement."""
+    import threading
+
+    import pipeline as OP
+    H, W = 400, 420
+    lay = S.cell_layout(H, W, 70, 7, seed=3)
+    m1 = S.render_truth(H, W, lay) > 0
+    m1[160:270, 10:130] = False
+    m1[160, 10:130] = True
+    m1[161:270, 10:130:2] = True
+    m2 = np.zeros((420, 440), bool)
+    for k in range(12):
+        m2[10 + 14 * k:24 + 14 * k, 10 + 14 * k:24 + 14 * k] = True
+    m2[230:400, 200:410:4] = True
+    m2[230:233, 200:410] = True
+    masks = [m1, m2]
+    refs = [OP.erosion_seeds(m) for m in masks]
+    devm = [dev(m) for m in masks]
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(tid):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                for it in range(6):
+                    j = (tid + it) % 2
+                    got = K.erosion_seeds(devm[j])
+                    s.synchronize()
+                    if not np.array_equal(host(got).astype(bool), refs[j]):
+                        errors.append((tid, it, j))
+        except Exception as ex:  # noqa: BLE001
+            errors.append((tid, repr(ex)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
