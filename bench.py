@@ -48,7 +48,8 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak 
 F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
                2: ("classify_pixels_lay_kernel<LayEcoli>" if os.environ.get("HRF_CLASSIFY_MFMA16") == "0"
-                   else "classify_pixels_lay16_kernel<LayEcoli>")}
+                   else "classify_pixels_lay16_kernel<LayEcoli>" if os.environ.get("HRF_CLASSIFY_W16") == "0"
+                   else "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 3>")}
 # algorithmic work (DESIGN.md "Measurement"):
 NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixel, ~20 f64 ops each
 E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort

@@ -20,6 +20,7 @@
 // Per cell (reference semantics, gated by presence flags): f64, exact channel order of the
 // restatement, one workgroup per cell -- bit-identical to oracle_segcos.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -1060,6 +1061,302 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(
   }
 }
 
+// ---- round 3: the 16x16x32 sweep with a lane-per-pixel prologue and per-chunk argmax keys ----
+// Same table, products, scores and tie rules as classify_pixels_lay16_kernel; what changes is the
+// instruction count around the MFMAs (the lay16 kernel issues ~2.3 VALU per MFMA over its life,
+// which with two waves per SIMD leaves the matrix pipe idle ~40 % of the time):
+//  * prologue: in the B-operand layout a lane's columns 32t + 8Q + q belong to a segment that
+//    depends on the lane quarter Q, a runtime value, so build_b_lay16 selects among all NSEG
+//    segments for every value (~830 v_cndmask per wave).  Here the segment norms are taken by
+//    one lane per staged pixel walking its C channels -- every channel's segment a compile-time
+//    constant -- and the pixel is normalised in place in LDS; the B-operand lanes then only read
+//    and split into hi/lo fp16;
+//  * sweep: the argmax folds each block's 16 keys into a per-chunk key with v_max3 and compares
+//    with the running best once per chunk (the key's low 4 bits name the row within the chunk:
+//    4 * block + register, blocks of 16 rows, CR <= 64), instead of a compare-and-select per
+//    block;
+//  * NW waves per workgroup share CR-row chunks through NBUF LDS buffers (template parameters;
+//    the defaults are the measured best, DESIGN.md "Per-pixel classifier").
+template <class L>
+__host__ __device__ constexpr int lay_seg(int c) {
+  int s = 0;
+  for (int t = 1; t < L::NSEG; ++t) s += c >= L::b(t) ? 1 : 0;
+  return s;
+}
+
+// One staged 32-pixel group (row-major, stride C floats, at stg): lanes 0..31 (pixel = lane)
+// take the segment norms, flag all-zero segments (zx) and negative values (neg), and rewrite
+// the pixel normalised.  Same arithmetic as build_b_lay16 (f32 sums, v_rsq, f64 redo when a
+// sum underflows f32), summed in channel order.
+template <class L>
+__device__ __forceinline__ void norm_pixels_w16(float *stg, int lane, uint32_t &zx, uint32_t &neg) {
+  zx = 0;
+  neg = 0;
+  if (lane < 32) {
+    float *px = stg + lane * L::C;
+    float nn[L::NSEG];
+#pragma unroll
+    for (int s = 0; s < L::NSEG; ++s) nn[s] = 0.0f;
+    uint32_t sg = 0;
+#pragma unroll
+    for (int c = 0; c < L::C; ++c) {
+      const float x = px[c];
+      nn[lay_seg<L>(c)] = __builtin_fmaf(x, x, nn[lay_seg<L>(c)]);
+      sg |= __float_as_uint(x);
+    }
+    neg = sg >> 31;
+    float inv[L::NSEG];
+#pragma unroll
+    for (int s = 0; s < L::NSEG; ++s) {
+      inv[s] = rsqrtf(nn[s]);
+      if (!(nn[s] >= 1e-30f)) {  // zero, or an f32 underflow: decide from the bits, redo in f64
+        uint32_t nz = 0;
+        double td = 0.0;
+        for (int c = L::b(s); c < L::b(s + 1); ++c) {
+          const float x = px[c];
+          nz |= __float_as_uint(x) << 1;
+          td += (double)x * (double)x;
+        }
+        inv[s] = nz ? (float)(1.0 / sqrt(td)) : 0.0f;
+        zx |= (nz ? 0u : 1u) << s;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < L::C; ++c) px[c] = px[c] * inv[lay_seg<L>(c)];
+  }
+}
+
+// B operand of 16-pixel sub-group g of the normalised staged group: lane pixel (lane & 15) + 16g,
+// columns 32t + 8Q + q; column C is the validity-bias column (1), columns past it 0.
+template <class L, int KT>
+__device__ __forceinline__ void split_b_w16(const float *stg, int lane, int g, h8 (&bh)[KT], h8 (&bl)[KT]) {
+  const int jj = (lane & 15) + 16 * g, Q = lane >> 4;
+  const float *pc = stg + jj * L::C + 8 * Q;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    h8 vh, vl;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float x = pc[32 * t + q];  // past the row end: another pixel's value, replaced below
+      if (32 * t + 24 + q >= L::C) {  // only the last columns depend on Q
+        const int k = 32 * t + 8 * Q + q;
+        x = k < L::C ? x : (k == L::C ? 1.0f : 0.0f);
+      }
+      const _Float16 hv = (_Float16)x;
+      vh[q] = hv;
+      vl[q] = (_Float16)(x - (float)hv);
+    }
+    bh[t] = vh;
+    bl[t] = vl;
+  }
+}
+
+template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF, int CR, bool PIPE>
+__device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
+                                          const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t (&zx)[4],
+                                          float (&best)[4], int (&bi)[4]) {
+  constexpr int KP = 32 * KT;
+  constexpr int CHB = CR * ROWB;
+  constexpr int NPC = (CHB + 1023) / 1024;  // 1 KiB LDS-DMA pieces per chunk (the last may be partial)
+  constexpr int NB = CR / 16;               // 16-row blocks per chunk
+  static_assert(CR % 16 == 0 && NB <= 4, "chunk keys hold 4 * block + register in 4 bits");
+  const int rl = lane & 15, Q = lane >> 4;
+  auto issue = [&](int c) {
+    const char *g = gref + (int64_t)c * CHB + lane * 16;
+    char *l = ldsb + (c % NBUF) * CHB;
+    for (int q = w; q < NPC; q += NW)
+      if (CHB % 1024 == 0 || q * 1024 + lane * 16 < CHB)
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
+  };
+  // pieces this wave issues per chunk (the waitcnt below leaves chunk c + 1's outstanding)
+  const int mine = (NPC - w + NW - 1) / NW;
+  constexpr int MINE_LO = NPC / NW;
+  issue(0);
+  if (NBUF >= 3 && nch > 1) issue(1);
+  f32x4 pv[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pv[g][i] = -__builtin_inff();
+  int pr = 0;  // first row of the pending block
+  h8 bz[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bz[g][q] = (_Float16)((Q == 0 && q < NSEG && ((zx[g] >> q) & 1u)) ? 1.0f : 0.0f);
+  int key[4], ck[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) key[g] = ck[g] = INT32_MIN;
+  // fold the pending block into the chunk keys, groups [g0, g1); after the chunk's last block,
+  // the chunk key against the running best (strictly greater: earlier chunks win ties)
+  auto epi = [&](int g0, int g1) {
+    const int pb = (pr / 16) % NB;
+#pragma unroll
+    for (int g = g0; g < g1; ++g) {
+      if (KEYED) {
+        const int base = 15 - 4 * pb;
+        const int k0 = (__float_as_int(pv[g][0]) & -16) | (base - 0);
+        const int k1 = (__float_as_int(pv[g][1]) & -16) | (base - 1);
+        const int k2 = (__float_as_int(pv[g][2]) & -16) | (base - 2);
+        const int k3 = (__float_as_int(pv[g][3]) & -16) | (base - 3);
+        ck[g] = max(ck[g], max(k0, k1));
+        ck[g] = max(ck[g], max(k2, k3));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (pv[g][i] > best[g]) {
+            best[g] = pv[g][i];
+            bi[g] = pr + i;
+          }
+      }
+    }
+    if (KEYED && g1 == 4 && pb == NB - 1) {
+      const int cb = pr - 16 * pb;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (ck[g] > key[g]) {
+          key[g] = ck[g];
+          bi[g] = cb;
+        }
+        ck[g] = INT32_MIN;
+      }
+    }
+  };
+  for (int c = 0; c < nch; ++c) {
+    if (NBUF == 2 || c + 1 >= nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (mine > MINE_LO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO) : "memory");
+    if (NW > 1) __syncthreads();  // every wave's pieces of c landed; everyone is past chunk c - 1
+    if (c + NBUF - 1 < nch) issue(c + NBUF - 1);
+    const char *buf = ldsb + (c % NBUF) * CHB;
+#pragma unroll
+    for (int rb = 0; rb < CR; rb += 16) {
+      f32x4 acc[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char *row = buf + (rb + rl) * ROWB + 16 * Q;
+      h8 az;
+      if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + rl) * ROWB + 4 * KP);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
+        const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 64 * t);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
+        if (PIPE) epi((4 * t) / KT, (4 * (t + 1)) / KT);  // previous block, slice t
+      }
+      if (ZS) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz[g], acc[g], 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) pv[g] = acc[g];
+      pr = c * CR + rb;
+      if (!PIPE) epi(0, 4);  // this block at once (the other waves on the SIMD cover the MFMA latency)
+    }
+  }
+  if (PIPE) epi(0, 4);  // the last block (the end of the last chunk: finalises its key)
+  if (KEYED) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int code = 15 - (key[g] & 15);
+      bi[g] += 16 * (code >> 2) + (code & 3);
+      best[g] = __int_as_float(key[g] & -16);
+    }
+  }
+}
+
+template <class L, int NW, int NBUF, int CR, int OCC>
+__global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const float *__restrict__ stack,
+                                                                     int64_t P, const _Float16 *__restrict__ refh,
+                                                                     int32_t R, int32_t Rpad,
+                                                                     int32_t *__restrict__ best_idx,
+                                                                     float *__restrict__ best_dist) {
+  constexpr int KT = (L::C + 1 + 31) / 32;
+  constexpr int KP = 32 * KT;
+  constexpr int ROWB = 4 * KP + L::PADB;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
+  h8 bh[4][KT], bl[4][KT];
+  uint32_t zx[4], ng = 0;
+  float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
+  {
+    // both halves' loads in flight at once where the registers allow (two waves per SIMD);
+    // at three, the second half is loaded after the first is staged
+    constexpr int NV = OCC < 3 ? 2 : 1;
+    float4 v[NV][LDV];
+    load_group(stack, P, L::C, pbase, lane, v[0]);
+    if (NV == 2) load_group(stack, P, L::C, pbase + 32, lane, v[NV - 1]);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (NV == 1 && half == 1) load_group(stack, P, L::C, pbase + 32, lane, v[0]);
+#pragma unroll
+      for (int i = 0; i < LDV; ++i) {
+        const int e4 = lane + 64 * i;
+        if (e4 < 8 * L::C) reinterpret_cast<float4 *>(stg)[e4] = v[NV == 2 ? half : 0][i];
+      }
+      __syncthreads();
+      uint32_t zxp, ngp;
+      norm_pixels_w16<L>(stg, lane, zxp, ngp);
+      ng |= ngp;
+      __syncthreads();
+      split_b_w16<L, KT>(stg, lane, 0, bh[2 * half], bl[2 * half]);
+      split_b_w16<L, KT>(stg, lane, 1, bh[2 * half + 1], bl[2 * half + 1]);
+      zx[2 * half] = __shfl(zxp, lane & 15, 64);
+      zx[2 * half + 1] = __shfl(zxp, 16 + (lane & 15), 64);
+      __syncthreads();
+    }
+  }
+  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
+  float best[4];
+  int bi[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    best[g] = -__builtin_inff();
+    bi[g] = 0;
+  }
+  const char *gref = reinterpret_cast<const char *>(refh);
+  char *ldsb = reinterpret_cast<char *>(lds);
+  const int nch = Rpad / CR;
+  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
+  const bool keyed = !libneg && !__syncthreads_or(ng != 0);
+#define HRF_SWEEPW(Z, K) \
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+  if (keyed) {
+    if (zs) HRF_SWEEPW(true, true);
+    else HRF_SWEEPW(false, true);
+  } else {
+    if (zs) HRF_SWEEPW(true, false);
+    else HRF_SWEEPW(false, false);
+  }
+#undef HRF_SWEEPW
+  const int Q = lane >> 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float b = best[g];
+    int idx = bi[g] + 4 * Q;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ob = __shfl_xor(b, o, 64);
+      const int oi = __shfl_xor(idx, o, 64);
+      if (ob > b || (ob == b && oi < idx)) {
+        b = ob;
+        idx = oi;
+      }
+    }
+    const int64_t p = pbase + 16 * g + (lane & 15);
+    if (Q == 0 && p < P) {
+      best_idx[p] = idx;
+      best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
+    }
+  }
+}
+
 // mode-2 table: {hi[KP], lo[KP], pad 16 B} fp16 per row, KP = 16 * ceil((C + 1) / 16); column C
 // is the validity bias (0 real rows, -1024 padding rows); pad fp16 s (s < nseg) = 1 when the row's
 // segment s is all zero (the indicator k-step's A operand), fp16 6-7 of row 0 = the library's
@@ -1213,6 +1510,25 @@ int choose_ks(int K) {
   return -1;
 }
 
+template <class L, int NW, int NB, int CR, int OCC>
+hrf_status launch_w16_lay(const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad, int32_t *best_idx,
+                          float *best_dist, hipStream_t s) {
+  constexpr int KT = (L::C + 1 + 31) / 32;
+  const size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
+  HRF_REQUIRE(shm * OCC <= 160 * 1024 + 1024, "classify: w16 configuration exceeds the LDS");
+  (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+  classify_pixels_w16_kernel<L, NW, NB, CR, OCC><<<(unsigned)hrf::cdiv(P, 64 * NW), 64 * NW, shm, s>>>(
+      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist);
+  return HRF_OK;
+}
+template <int NW, int NB, int CR, int OCC>
+hrf_status launch_w16(int lay, const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad,
+                      int32_t *best_idx, float *best_dist, hipStream_t s) {
+  return lay == 1 ? launch_w16_lay<LayEcoli, NW, NB, CR, OCC>(stack, P, refx, R, rpad, best_idx, best_dist, s)
+                  : launch_w16_lay<LayMulti, NW, NB, CR, OCC>(stack, P, refx, R, rpad, best_idx, best_dist, s);
+}
+
 hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Bounds *bd) {
   HRF_REQUIRE(nseg >= 1 && nseg <= SMAX && bounds_host, "classify: 1..8 segments required");
   HRF_REQUIRE(bounds_host[0] == 0 && bounds_host[nseg] == C, "classify: segment bounds must span [0, C)");
@@ -1325,6 +1641,33 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
   } else {               \
     HRF_LAY16N(LAY, 3);  \
   }
+    // round-3 kernel (classify_pixels_w16_kernel), the default for the E. coli layout in its
+    // measured-best configuration (4 waves, 2 buffers of 64 rows, three workgroups per CU:
+    // 1.76 vs 1.83 ms isolated for the lay16 kernel on a 2048^2 tile, R = 1023);
+    // HRF_CLASSIFY_W16 = "NW,NBUF,CR[,OCC]" picks another configuration, "0" the lay16 kernel
+    static const int w16env = [] {
+      const char *e = getenv("HRF_CLASSIFY_W16");
+      if (!e || !*e) return -1;
+      int a = 0, b = 0, c = 0, o = 2;
+      if (sscanf(e, "%d,%d,%d,%d", &a, &b, &c, &o) < 3) return 0;
+      return o * 100000 + a * 10000 + b * 1000 + c;
+    }();
+    const int w16cfg = w16env >= 0 ? w16env : (lay == 1 && m16_env < 0 ? 342064 : 0);
+    if (m16 && w16cfg) {
+      hrf_status st = HRF_EINVAL;
+      switch (w16cfg) {
+        case 242064: st = launch_w16<4, 2, 64, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        case 243064: st = launch_w16<4, 3, 64, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        case 242032: st = launch_w16<4, 2, 32, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        case 342064: st = launch_w16<4, 2, 64, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        case 342032: st = launch_w16<4, 2, 32, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        case 343032: st = launch_w16<4, 3, 32, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
+        default: HRF_REQUIRE(false, "classify: HRF_CLASSIFY_W16 configuration not built");
+      }
+      if (st) return st;
+      HRF_LAUNCHED();
+      return HRF_OK;
+    }
     if (m16) {
       if (lay == 1) {
         HRF_LAY16(LayEcoli);

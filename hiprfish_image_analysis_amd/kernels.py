@@ -283,6 +283,39 @@ def register_translations_batch_dev(imgs, clamp=None):
     return out
 
 
+def xcorr_supported(n, H, W):
+    return int(_lib.lib().hrf_xcorr_workspace_bytes(n, H, W)) > 0
+
+
+def xcorr_shifts_dev(imgs, clamp=None):
+    """register_translations_dev(imgs[0], imgs[1:], clamp) from one (n, H, W) f64 tensor through
+    the hand-written FFT pipeline (xcorr.hip; power-of-two sizes) -> (n, 2) int32 device tensor"""
+    imgs = _dev(imgs, torch.float64, "imgs")
+    n, H, W = imgs.shape
+    nb = int(_lib.lib().hrf_xcorr_workspace_bytes(n, H, W))
+    if nb <= 0:
+        raise ValueError("xcorr_shifts: unsupported size %d x %d x %d" % (n, H, W))
+    work = torch.empty(nb, dtype=torch.uint8, device=imgs.device)
+    out = torch.empty((n, 2), dtype=torch.int32, device=imgs.device)
+    _lib.call("hrf_xcorr_shifts_dev", _ptr(imgs), n, H, W, _ptr(work), -1 if clamp is None else int(clamp), _ptr(out),
+              _stream())
+    return out
+
+
+def xcorr_surfaces(imgs):
+    """the cross-correlation surfaces of xcorr_shifts_dev: (n - 1, H, W) f64, H * W / 2 times
+    numpy.fft.ifft2(F(imgs[0]) * conj(F(imgs[t]))).real (tests)"""
+    imgs = _dev(imgs, torch.float64, "imgs")
+    n, H, W = imgs.shape
+    nb = int(_lib.lib().hrf_xcorr_workspace_bytes(n, H, W))
+    if nb <= 0:
+        raise ValueError("xcorr_surfaces: unsupported size %d x %d x %d" % (n, H, W))
+    work = torch.empty(nb, dtype=torch.uint8, device=imgs.device)
+    out = torch.empty((n - 1, H, W), dtype=torch.float64, device=imgs.device)
+    _lib.call("hrf_xcorr_surfaces_dev", _ptr(imgs), n, H, W, _ptr(work), _ptr(out), _stream())
+    return out
+
+
 def pad_edge_3d(a, width=5):
     """skimage.util.pad(a, width, mode='edge') of an (X, Y, Z) f64 volume (biofilm :810)"""
     a = _dev(a, torch.float64, "a")

@@ -46,6 +46,9 @@ NATIVE_SEG = os.environ.get("HRF_NATIVE_SEG", "1") != "0"
 # with four tiles in flight the batched transforms cost 1-7 % end to end against one transform
 # pair per target (4 of 4 interleaved pairs; DESIGN.md "Tried and not kept")
 BATCH_REGISTRATION = os.environ.get("HRF_BATCH_REG", "0") == "1"
+# power-of-two tiles: the registration cross-correlations through xcorr.hip (six launches for all
+# lasers) instead of hipFFT; HRF_XCORR=0 keeps hipFFT
+XCORR = os.environ.get("HRF_XCORR", "1") != "0"
 
 
 def segment_ecoli(stack: torch.Tensor, keep: dict | None = None, image_cn: torch.Tensor | None = None):
@@ -108,6 +111,8 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
     it on the device)."""
     if reduce == "max" and len(lasers) <= 8:
         proj = K.channel_max_multi(lasers, stacked=True)                 # one launch for all lasers
+        if device and len(lasers) >= 2 and XCORR and K.xcorr_supported(*proj.shape):
+            return K.xcorr_shifts_dev(proj, clamp)                      # hand-written FFT pipeline
         if device and len(lasers) >= 2 and BATCH_REGISTRATION:
             return K.register_translations_batch_dev(proj, clamp)       # batched FFTs
         proj = list(proj.unbind(0))

@@ -148,6 +148,22 @@ HRF_API hrf_status hrf_pad_edge3_f64(const double *a, int64_t X, int64_t Y, int6
 HRF_API hrf_status hrf_mask_mul_f64(const double *a, const uint8_t *mask, int64_t n, double *out,
                                     hrf_stream_t stream);
 
+/* ==== f1: registration shifts of a laser set, hand-written f64 FFT pipeline (xcorr.hip) ======
+ * register_translation(imgs[0], imgs[t]) for t = 1..nimg-1 (ecoli :45-57, multispecies :82-84)
+ * in six launches: rows, column four-step pass A, pass B fused with the conjugate product and its
+ * inverse, inverse pass A, inverse rows with the per-row first |cc| maximum, per-target shift.
+ * imgs: nimg x H x W f64 (reference first); H a power of two 16..4096, W 4..4096; nimg 2..16.
+ * work: hrf_xcorr_workspace_bytes(nimg, H, W) device bytes (-1: size unsupported -- use
+ * hrf_register_translations_batch_dev); shifts_dev: nimg x 2 int32, row 0 = (0, 0); clamp >= 0:
+ * |component| > clamp -> 0.  Stream-ordered, no synchronisation. */
+HRF_API int64_t hrf_xcorr_workspace_bytes(int32_t nimg, int64_t H, int64_t W);
+HRF_API hrf_status hrf_xcorr_shifts_dev(const double *imgs, int32_t nimg, int64_t H, int64_t W, void *work,
+                                        int32_t clamp, int32_t *shifts_dev, hrf_stream_t stream);
+/* the same pipeline writing the correlation surfaces instead of the shifts (tests): cc_out
+ * (nimg - 1) x H x W f64 = H * W / 2 * numpy.fft.ifft2(F(ref) conj(F(img_t))).real */
+HRF_API hrf_status hrf_xcorr_surfaces_dev(const double *imgs, int32_t nimg, int64_t H, int64_t W, void *work,
+                                          double *cc_out, hrf_stream_t stream);
+
 /* ==== f1: registration shift estimate (register.hip) ====================================
  * skimage.feature.register_translation(src, target)[0] (upsample_factor 1; ecoli :45-46,
  * multispecies :82-83): argmax |ifft(F(src) conj(F(target)))| wrapped to (-n/2, n/2] per
