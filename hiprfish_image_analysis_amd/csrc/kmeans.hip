@@ -412,10 +412,10 @@ __global__ __launch_bounds__(256) void km_scan_sum_kernel(const unsigned *__rest
   if (threadIdx.x == 0) bsum[blockIdx.x] = (unsigned)(sh[0] + sh[1] + sh[2] + sh[3]);
 }
 
-__global__ __launch_bounds__(1024) void km_scan_blocks_kernel(unsigned *__restrict__ bsum, int nb) {
-  __shared__ unsigned long long sh[16];
+__global__ __launch_bounds__(256) void km_scan_blocks_kernel(unsigned *__restrict__ bsum, int nb) {
+  __shared__ unsigned long long sh[4];
   unsigned long long carry = 0;
-  for (int b0 = 0; b0 < nb; b0 += 1024) {
+  for (int b0 = 0; b0 < nb; b0 += 256) {
     const int i = b0 + threadIdx.x;
     unsigned long long tot;
     const unsigned long long e = block_excl_scan_u64(i < nb ? bsum[i] : 0u, sh, &tot);
@@ -956,8 +956,12 @@ __global__ __launch_bounds__(PT) void km_pp_choose_kernel(KmState *st, Draws d, 
 }
 
 // ---- Lloyd on the sorted array ---------------------------------------------------------------
-constexpr int KS_T = 1024;           // threads of an iteration workgroup
-constexpr int KS_P = 4;              // probes per thread per round -> 4096-ary search
+// 256 threads: one wave per SIMD, so a run's workgroup fits in the registers one retiring
+// classifier workgroup frees (a 1024-thread workgroup needs four waves' worth on every SIMD of
+// one CU and, with the classifier resident everywhere, waited for its grid to drain: 2.2 ms
+// in-bench for a 21 us kernel)
+constexpr int KS_T = 256;            // threads of an iteration workgroup
+constexpr int KS_P = 16;             // probes per thread per round -> 4096-ary search
 static_assert(KS_T * KS_P == 4096, "index arithmetic below shifts by 12");
 
 // label of v: sklearn id of the first minimum of (v - c_j)^2 in sklearn order
@@ -1548,7 +1552,7 @@ __global__ void km_state_init_kernel(KmState *st) {
 hrf_status scan_u32(unsigned *a, int64_t n, unsigned *bsum, hipStream_t s) {
   const int nb = (int)((n + KSC_B - 1) / KSC_B);
   km_scan_sum_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
-  km_scan_blocks_kernel<<<1, 1024, 0, s>>>(bsum, nb);
+  km_scan_blocks_kernel<<<1, 256, 0, s>>>(bsum, nb);
   km_scan_apply_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
   HRF_LAUNCHED();
   return HRF_OK;
