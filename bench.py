@@ -46,10 +46,10 @@ NBIT = 10
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense FP32 matrix peak (mode 0)
 F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (modes 1, 2)
 F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
+# the timed path classifies from the registered tile's pixel table (pipeline.register_tile)
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
-               2: ("classify_pixels_lay_kernel<LayEcoli>" if os.environ.get("HRF_CLASSIFY_MFMA16") == "0"
-                   else "classify_pixels_lay16_kernel<LayEcoli>" if os.environ.get("HRF_CLASSIFY_W16") == "0"
-                   else "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 3>")}
+               2: "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3>"}
+REGTILE = os.environ.get("HRF_REGTILE", "1") != "0"   # A/B switch: 0 = register_stack + in-kernel operand build
 # algorithmic work (DESIGN.md "Measurement"):
 NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixel, ~20 f64 ops each
 E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort
@@ -233,8 +233,10 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
         if mode is not None:
             lib = P.Library(lib_main.spectra, lib_main.bounds, NBIT)
             lib._refx = K.classify_prepare(lib.spectra.to(torch.float32), lib.bounds, mode=mode)
-        def job(t, lib=lib, pp=pp):
-            stack, cn = P.register_stack(t[0], want_cn=True)
+        def job(t, lib=lib, pp=pp, mode=mode):
+            if mode is None:    # the headline path without the per-pixel GEMM
+                return P.process_tile(P.register_tile(t[0]), lib, calibration=t[1], per_pixel=False)
+            stack, cn = P.register_stack(t[0], want_cn=True)     # mode 0 reads the f32 stack
             return P.process_tile(stack, lib, calibration=t[1], per_pixel=pp, image_cn=cn)
         sec = _timed_tiles(job, tiles, T, streams, pool, steps, 2)
         cfg3[name] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
@@ -260,9 +262,9 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
     wstats = []
 
     def qjob(t):
-        stack, cn = P.register_stack(t[0], want_cn=True)
-        r = P.process_tile(stack, lib_main, calibration=t[1], image_cn=cn)
-        wstats.append(K.seg_stats(stack.device, H, W))
+        rt = P.register_tile(t[0])
+        r = P.process_tile(rt, lib_main, calibration=t[1])
+        wstats.append(K.seg_stats(rt.device, H, W))
         return r
     sec = _timed_tiles(qjob, qtiles, T, streams, pool, steps, 2)
     del qtiles
@@ -416,10 +418,15 @@ def main():
 
     def tile_job(j, tile, timed):
         with torch.cuda.stream(streams[j]):
-            stack, cn = P.register_stack(tile[0], want_cn=True)  # ecoli :45-72 (shifts stay on the device)
+            # ecoli :45-72: shifts on the device, one assembly pass writing image_cn and the
+            # classifier's pixel table (the registered stack is never materialised)
+            if REGTILE:
+                rt = P.register_tile(tile[0])
+                return P.process_tile(rt, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
+                                      pixel_events=ev if timed else None)
+            stack, cn = P.register_stack(tile[0], want_cn=True)  # HRF_REGTILE=0: the materialised stack
             return P.process_tile(stack, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
-                                  image_cn=cn,
-                                  pixel_events=ev if timed else None)
+                                  image_cn=cn, pixel_events=ev if timed else None)
 
     def worker(j, first, nsteps, timed):
         # worker j drives tiles first*T + j, (first+1)*T + j, ... on its own stream, with no
@@ -497,9 +504,9 @@ def main():
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         # the same kernel alone on the GPU (after the timed region): with the overlap the
         # timed-region duration includes the compute units it shares with the segmentation
-        stack0 = P.register_stack(tiles[0][0])
-        ms_iso = _event_ms(lambda: P.classify_pixels(stack0, lib), 3)
-        del stack0
+        rt0 = P.register_tile(tiles[0][0])
+        ms_iso = _event_ms(lambda: K.classify_pixels_table(rt0.pixtable, lib.refx(), lib.R), 3)
+        del rt0
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
         ach = flops / (ms * 1e-3) / 1e12
         mode = K.refx_mode(lib.refx(), C, bounds)

@@ -24,6 +24,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "pixtable.hpp"
 
 namespace {
 
@@ -480,18 +481,8 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
 // the sum equals adding the integer count after the products); its B operand is the pixel's
 // indicators.  95 -> 96 columns: 6 k-steps per 32-row block instead of 7, 19 MFMAs instead of
 // 18 in the zero-segment copy.
-struct LayEcoli {
-  static constexpr int C = 95, NSEG = 5;
-  static constexpr int PADB = 32;  // row pad bytes: 416-byte rows (see lay_sweep16's bank note)
-  __host__ __device__ static constexpr int b(int s) {
-    return s <= 0 ? 0 : s == 1 ? 32 : s == 2 ? 55 : s == 3 ? 75 : s == 4 ? 89 : 95;
-  }
-};
-struct LayMulti {
-  static constexpr int C = 63, NSEG = 4;
-  static constexpr int PADB = 16;
-  __host__ __device__ static constexpr int b(int s) { return s <= 0 ? 0 : s == 1 ? 23 : s == 2 ? 43 : s == 3 ? 57 : 63; }
-};
+using hrf_pix::LayEcoli;  // pixtable.hpp
+using hrf_pix::LayMulti;
 
 // segment of B-operand column k: 0..NSEG-1 for a channel, -1 for the bias column (k == C),
 // -2 for zero padding
@@ -1077,12 +1068,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(
 //    block;
 //  * NW waves per workgroup share CR-row chunks through NBUF LDS buffers (template parameters;
 //    the defaults are the measured best, DESIGN.md "Per-pixel classifier").
-template <class L>
-__host__ __device__ constexpr int lay_seg(int c) {
-  int s = 0;
-  for (int t = 1; t < L::NSEG; ++t) s += c >= L::b(t) ? 1 : 0;
-  return s;
-}
+using hrf_pix::lay_seg;
 
 // One staged 32-pixel group (row-major, stride C floats, at stg): lanes 0..31 (pixel = lane)
 // take the segment norms, flag all-zero segments (zx) and negative values (neg), and rewrite
@@ -1357,6 +1343,98 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
   }
 }
 
+// ---- the B operands from a pixel table (pixtable.hpp) ------------------------------------------
+// Standalone producer: 64 pixels per workgroup staged through LDS (coalesced float4 loads).
+template <class L>
+__global__ __launch_bounds__(256) void pixtable_prep_kernel(const float *__restrict__ stack, int64_t P,
+                                                            uint4 *__restrict__ table, uint8_t *__restrict__ flags) {
+  __shared__ __attribute__((aligned(16))) float tile[64 * L::C];
+  const int64_t p0 = (int64_t)blockIdx.x * 64;
+  const int np = (int)min((int64_t)64, P - p0);
+  const int nel = np * L::C;
+  const float *src = stack + p0 * L::C;
+  for (int e = threadIdx.x; e < (nel >> 2); e += 256)
+    reinterpret_cast<float4 *>(tile)[e] = reinterpret_cast<const float4 *>(src)[e];
+  for (int e = ((nel >> 2) << 2) + threadIdx.x; e < nel; e += 256) tile[e] = src[e];
+  __syncthreads();
+  hrf_pix::prep_tile<L>(tile, nullptr, np, p0, table, flags);
+}
+
+// classify_pixels_w16_kernel with the prologue replaced by direct loads of the prepared operands
+template <class L, int NW, int NBUF, int CR, int OCC>
+__global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(const uint4 *__restrict__ table,
+                                                                      const uint8_t *__restrict__ flags, int64_t P,
+                                                                      const _Float16 *__restrict__ refh, int32_t R,
+                                                                      int32_t Rpad, int32_t *__restrict__ best_idx,
+                                                                      float *__restrict__ best_dist) {
+  constexpr int KT = (L::C + 1 + 31) / 32;
+  constexpr int KP = 32 * KT;
+  constexpr int ROWB = 4 * KP + L::PADB;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
+  h8 bh[4][KT], bl[4][KT];
+  uint32_t zx[4], ng = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int64_t g16 = pbase / 16 + g;
+    const uint4 *e = table + g16 * (int64_t)(KT * 128) + lane;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const uint4 hv = e[t * 128], lv = e[t * 128 + 64];
+      bh[g][t] = *reinterpret_cast<const h8 *>(&hv);
+      bl[g][t] = *reinterpret_cast<const h8 *>(&lv);
+    }
+    const int64_t p = pbase + 16 * g + (lane & 15);
+    const uint32_t f = p < P ? flags[p] : 0x1fu;
+    zx[g] = f & 0x1fu;
+    ng |= f >> 7;
+  }
+  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
+  float best[4];
+  int bi[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    best[g] = -__builtin_inff();
+    bi[g] = 0;
+  }
+  const char *gref = reinterpret_cast<const char *>(refh);
+  char *ldsb = reinterpret_cast<char *>(lds);
+  const int nch = Rpad / CR;
+  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
+  const bool keyed = !libneg && !__syncthreads_or(ng != 0);
+#define HRF_SWEEPW(Z, K) \
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+  if (keyed) {
+    if (zs) HRF_SWEEPW(true, true);
+    else HRF_SWEEPW(false, true);
+  } else {
+    if (zs) HRF_SWEEPW(true, false);
+    else HRF_SWEEPW(false, false);
+  }
+#undef HRF_SWEEPW
+  const int Q = lane >> 4;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float b = best[g];
+    int idx = bi[g] + 4 * Q;
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ob = __shfl_xor(b, o, 64);
+      const int oi = __shfl_xor(idx, o, 64);
+      if (ob > b || (ob == b && oi < idx)) {
+        b = ob;
+        idx = oi;
+      }
+    }
+    const int64_t p = pbase + 16 * g + (lane & 15);
+    if (Q == 0 && p < P) {
+      best_idx[p] = idx;
+      best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
+    }
+  }
+}
+
 // mode-2 table: {hi[KP], lo[KP], pad 16 B} fp16 per row, KP = 16 * ceil((C + 1) / 16); column C
 // is the validity bias (0 real rows, -1024 padding rows); pad fp16 s (s < nseg) = 1 when the row's
 // segment s is all zero (the indicator k-step's A operand), fp16 6-7 of row 0 = the library's
@@ -1514,8 +1592,12 @@ template <class L, int NW, int NB, int CR, int OCC>
 hrf_status launch_w16_lay(const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad, int32_t *best_idx,
                           float *best_dist, hipStream_t s) {
   constexpr int KT = (L::C + 1 + 31) / 32;
-  const size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
+  size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
   HRF_REQUIRE(shm * OCC <= 160 * 1024 + 1024, "classify: w16 configuration exceeds the LDS");
+  // HRF_CLASSIFY_MAXWG = m: at most m workgroups per CU (the LDS request padded to 160 KB / m),
+  // leaving registers and LDS on every CU for the segmentation kernels running beside it
+  static const int maxwg = getenv("HRF_CLASSIFY_MAXWG") ? atoi(getenv("HRF_CLASSIFY_MAXWG")) : 0;
+  if (maxwg > 0 && maxwg < OCC) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
   (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   classify_pixels_w16_kernel<L, NW, NB, CR, OCC><<<(unsigned)hrf::cdiv(P, 64 * NW), 64 * NW, shm, s>>>(
@@ -1748,6 +1830,62 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
       HRF_REQUIRE(false, "classify_pixels: unsupported K");
   }
 #undef HRF_CP
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+int64_t hrf_pixtable_bytes(int64_t P, int32_t C, const int32_t *bounds_host, int32_t nseg) {
+  Bounds bd;
+  if (make_bounds(bounds_host, nseg, C, &bd) != HRF_OK) return -1;
+  const int lay = layout_id(bd, C);
+  if (lay == 0 || P < 0) return -1;
+  const int64_t groups = (P + 255) / 256 * 16;  // whole classifier workgroups
+  return groups * (lay == 1 ? hrf_pix::group_entries<LayEcoli>() : hrf_pix::group_entries<LayMulti>()) * 16;
+}
+
+hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                                void *table, uint8_t *flags, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  const int lay = layout_id(bd, C);
+  HRF_REQUIRE(lay != 0, "pixtable: the E. coli or multispecies channel layout only");
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(stack && table && flags, "pixtable: null buffer");
+  const unsigned g = (unsigned)hrf::cdiv(P, 64);
+  if (lay == 1)
+    pixtable_prep_kernel<LayEcoli><<<g, 256, 0, (hipStream_t)stream>>>(stack, P, (uint4 *)table, flags);
+  else
+    pixtable_prep_kernel<LayMulti><<<g, 256, 0, (hipStream_t)stream>>>(stack, P, (uint4 *)table, flags);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C, const void *refx,
+                                     int32_t R, const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                     float *best_dist, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, 2, &kp, &rpad)) return s;
+  const int lay = layout_id(bd, C);
+  HRF_REQUIRE(lay != 0, "classify_pixels_table: the E. coli or multispecies channel layout only");
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(table && flags && refx && best_idx && best_dist, "classify_pixels_table: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
+  auto go = [&](auto lay_tag) -> hrf_status {
+    using L = decltype(lay_tag);
+    constexpr int KT = (L::C + 1 + 31) / 32;
+    const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
+    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
+                                                                        (const _Float16 *)refx, R, rpad, best_idx,
+                                                                        best_dist);
+    return HRF_OK;
+  };
+  hrf_status st = lay == 1 ? go(LayEcoli{}) : go(LayMulti{});
+  if (st) return st;
   HRF_LAUNCHED();
   return HRF_OK;
 }

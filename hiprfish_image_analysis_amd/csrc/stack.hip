@@ -13,6 +13,8 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "pixtable.hpp"
+#include "wave.hpp"
 
 namespace {
 
@@ -218,7 +220,8 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 
 __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
-                                                             int cn_mode) {
+                                                             int cn_mode, uint4 *__restrict__ ptab,
+                                                             uint8_t *__restrict__ pflags) {
   constexpr int C = EcoliLasers<0>::C;
   __shared__ __attribute__((aligned(16))) float tile[AS_P * C];
   __shared__ uint8_t okp[AS_P];
@@ -239,9 +242,12 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
   lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
   lay_store<0, 5>(tile, tid, v);
   __syncthreads();
-  float *out = dst + (r * W + c0) * (int64_t)C;
-  const int n = np * C;
-  if (np == AS_P) {   // a full strip: 64 x 95 floats, 16-byte aligned (W multiple of 64)
+  float *out = dst ? dst + (r * W + c0) * (int64_t)C : nullptr;
+  const int n = dst ? np * C : 0;
+  if (!dst) {
+    // the registered stack is not materialised (the pixel table and image_cn are what the path
+    // reads; label sums read the lasers): no store
+  } else if (np == AS_P) {   // a full strip: 64 x 95 floats, 16-byte aligned (W multiple of 64)
     for (int vv = tid; vv < (n >> 2); vv += 256) {
       const int e = vv << 2;
       float4 x = reinterpret_cast<const float4 *>(tile)[vv];
@@ -280,6 +286,11 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
         cn_out[r * W + c0 + pi] = sv;
       }
     }
+  }
+  if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
+    __shared__ uint32_t fl[AS_P];
+    __syncthreads();
+    hrf_pix::prep_tile_ecoli(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl);
   }
 }
 
@@ -686,6 +697,122 @@ __global__ void calibrate_kernel(const float *__restrict__ stack, int64_t npix, 
   }
 }
 
+// a15 per-label spectra (label_sums_wave_kernel, stats.hip) read straight from the per-laser
+// acquisitions: lane = channel c (c, c + 64), its laser q(c) and local channel fixed per lane; a
+// foreground pixel's value is its laser's source pixel shifted by (dr_q, dc_q), 0 outside the
+// laser's frame or -- apply_mask -- outside any laser's frame (register_assemble's stack, which
+// then never has to exist).  CAL: a per-pixel flat field on channels [cal0, cal1).
+template <bool CAL>
+__global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+                                                                const int32_t *__restrict__ lab, int32_t maxlab,
+                                                                const float *__restrict__ cal, int cal0, int cal1,
+                                                                double *__restrict__ sums,
+                                                                unsigned long long *__restrict__ counts) {
+  constexpr int LB = 16;
+  __shared__ int sdr[LMAX], sdc[LMAX];
+  load_shifts(L, sdr, sdc);
+  const int C = L.c0[L.n];
+  const int64_t npix = H * W;
+  const int lane = hrf::lane_id();
+  const int64_t nchunks = (npix + 63) >> 6;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t ch = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int c0 = lane, c1 = lane + 64;
+  const bool v0 = c0 < C, v1 = c1 < C;
+  const bool k0 = CAL && c0 >= cal0 && c0 < cal1, k1 = CAL && c1 >= cal0 && c1 < cal1;
+  int q0 = 0, q1 = 0;
+#pragma unroll
+  for (int q = 1; q < LMAX; ++q) {
+    if (q < L.n && c0 >= L.c0[q]) q0 = q;
+    if (q < L.n && c1 >= L.c0[q]) q1 = q;
+  }
+  const int cl0 = L.c0[q0 + 1] - L.c0[q0], cl1 = L.c0[q1 + 1] - L.c0[q1];
+  const float *s0 = L.src[q0] + (c0 - L.c0[q0]), *s1 = L.src[q1] + (c1 - L.c0[q1]);
+  const int dr0 = sdr[q0], dc0 = sdc[q0], dr1 = sdr[q1], dc1 = sdc[q1];
+  auto load_label = [&](int64_t c) -> int32_t {
+    const int64_t p = (c << 6) + lane;
+    int32_t l = (c < nchunks && p < npix) ? __builtin_nontemporal_load(lab + p) : 0;
+    return (l < 0 || l > maxlab) ? 0 : l;
+  };
+  int32_t lnext = load_label(ch);
+  for (; ch < nchunks; ch += nwaves) {
+    const int32_t l = lnext;
+    lnext = load_label(ch + nwaves);
+    unsigned long long fg = __ballot(l != 0);
+    if (!fg) continue;
+    const int64_t p0 = ch << 6;
+    float pcal = 1.0f;
+    if (CAL) pcal = (p0 + lane < npix) ? cal[p0 + lane] : 1.0f;
+    // the chunk's pixels: lane = pixel for the coverage of the whole stack (apply_mask), a bit
+    // per pixel; the row of every pixel once (no 64-bit division per fetched pixel)
+    const int64_t pl = p0 + lane;
+    const int64_t rl = pl / W, cl = pl - rl * W;
+    bool okl = pl < npix;
+    if (apply_mask)
+      for (int q = 0; q < L.n; ++q) okl = okl && covered(rl, cl, H, W, sdr[q], sdc[q]);
+    const unsigned long long okmask = __ballot(okl);
+    int32_t run = 0;  // wave-uniform
+    unsigned long long n = 0;
+    double a0 = 0.0, a1 = 0.0;
+    while (fg) {
+      int idx[LB];
+      int nb = 0;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        idx[j] = fg ? __ffsll((long long)fg) - 1 : -1;
+        if (fg) {
+          fg &= fg - 1;
+          ++nb;
+        }
+      }
+      float x0[LB], x1[LB];
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        x0[j] = x1[j] = 0.0f;
+        if (j < nb) {
+          const int64_t r = __shfl(rl, idx[j], 64), c = __shfl(cl, idx[j], 64);
+          const bool ok = (okmask >> idx[j]) & 1ull;
+          if (ok && v0 && covered(r, c, H, W, dr0, dc0))
+            x0[j] = __builtin_nontemporal_load(s0 + ((r - dr0) * W + (c - dc0)) * cl0);
+          if (ok && v1 && covered(r, c, H, W, dr1, dc1))
+            x1[j] = __builtin_nontemporal_load(s1 + ((r - dr1) * W + (c - dc1)) * cl1);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        if (j < nb) {
+          const int32_t lj = __builtin_amdgcn_readlane(l, idx[j]);
+          if (lj != run) {
+            if (run) {
+              double *row = sums + (int64_t)run * C;
+              if (v0) atomicAdd(row + c0, a0);
+              if (v1) atomicAdd(row + c1, a1);
+              if (lane == 0) atomicAdd(counts + run, n);
+            }
+            run = lj;
+            a0 = a1 = 0.0;
+            n = 0;
+          }
+          ++n;
+          if (CAL) {
+            const double d = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                                 __builtin_bit_cast(int, pcal), idx[j]));
+            a0 += k0 ? (double)x0[j] / d : (double)x0[j];
+            a1 += k1 ? (double)x1[j] / d : (double)x1[j];
+          } else {
+            a0 += (double)x0[j];
+            a1 += (double)x1[j];
+          }
+        }
+      }
+    }
+    double *row = sums + (int64_t)run * C;
+    if (v0) atomicAdd(row + c0, a0);
+    if (v1) atomicAdd(row + c1, a1);
+    if (lane == 0) atomicAdd(counts + run, n);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -719,7 +846,8 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
     for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
     if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
-      assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode);
+      assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, nullptr,
+                                                                   nullptr);
       HRF_LAUNCHED();
       return HRF_OK;
     }
@@ -760,6 +888,68 @@ hrf_status hrf_register_assemble_cn_dev(const float *const *src_host, const int3
                                        stream))
     return r;
   return hrf_channel_sum(dst, H * W, C, nullptr, cn_mode, 0, cn_out, stream);
+}
+
+static hrf_status lasers_of(const float *const *src_host, const int32_t *channels_host, const int32_t *shifts_dev,
+                            int32_t nlaser, Lasers *L) {
+  HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && shifts_dev, "lasers: bad arguments");
+  *L = Lasers{};
+  L->n = nlaser;
+  L->dsh = shifts_dev;
+  for (int i = 0; i < nlaser; ++i) {
+    HRF_REQUIRE(channels_host[i] >= 1 && src_host[i], "lasers: laser %d empty", i);
+    L->src[i] = src_host[i];
+    L->c0[i + 1] = L->c0[i] + channels_host[i];
+  }
+  for (int i = nlaser + 1; i <= LMAX; ++i) L->c0[i] = L->c0[nlaser];
+  return HRF_OK;
+}
+
+hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const int32_t *channels_host,
+                                          const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                          int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode, void *table,
+                                          uint8_t *flags, hrf_stream_t stream) {
+  Lasers L;
+  if (hrf_status st = lasers_of(src_host, channels_host, shifts_dev, nlaser, &L)) return st;
+  bool ecoli = nlaser == 5;
+  for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
+  HRF_REQUIRE(ecoli && W % 16 == 0 && H <= 65535 && H >= 1 && W >= 16,
+              "register_assemble_pixtable: the five E. coli lasers and W a multiple of 16");
+  HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && table && flags, "register_assemble_pixtable: null output");
+  HRF_REQUIRE(!dst || ((uintptr_t)dst & 15) == 0, "register_assemble_pixtable: dst must be 16-byte aligned");
+  dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
+  assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode,
+                                                               (uint4 *)table, flags);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status hrf_label_sums_lasers(const float *const *src_host, const int32_t *channels_host, const int32_t *shifts_dev,
+                                 int32_t nlaser, int64_t H, int64_t W, int32_t apply_mask, const int32_t *labels,
+                                 int32_t maxlab, const float *cal, int32_t cal_c0, int32_t cal_c1, double *sums,
+                                 int64_t *counts, hrf_stream_t stream) {
+  Lasers L;
+  if (hrf_status st = lasers_of(src_host, channels_host, shifts_dev, nlaser, &L)) return st;
+  const int C = L.c0[nlaser];
+  HRF_REQUIRE(C <= 128 && maxlab >= 0 && H >= 0 && W >= 0, "label_sums_lasers: C must be <= 128");
+  HRF_REQUIRE(sums && counts, "label_sums_lasers: null output");
+  hipStream_t s = (hipStream_t)stream;
+  HRF_HIP(hipMemsetAsync(sums, 0, sizeof(double) * ((size_t)maxlab + 1) * C, s));
+  HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * ((size_t)maxlab + 1), s));
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(labels, "label_sums_lasers: null labels");
+  const int64_t nblk = hrf::cdiv(hrf::cdiv(H * W, 64), 4);
+  if (cal) {
+    const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<true>, 256, 0, nblk);
+    label_sums_lasers_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0, cal_c1, sums,
+                                                       (unsigned long long *)counts);
+  } else {
+    const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<false>, 256, 0, nblk);
+    label_sums_lasers_kernel<false><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, nullptr, 0, 0, sums,
+                                                        (unsigned long long *)counts);
+  }
+  HRF_LAUNCHED();
+  return HRF_OK;
 }
 
 hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,

@@ -616,6 +616,57 @@ def label_sums(stack, labels, maxlab, cal=None, cal_range=None):
     return sums, counts
 
 
+def _laser_args(lasers, shifts_dev):
+    import ctypes
+    srcs = [_dev(s, torch.float32, "laser stack") for s in lasers]
+    ch = _i32_host([s.shape[2] for s in srcs])
+    ptrs = (ctypes.c_void_p * len(srcs))(*[s.data_ptr() for s in srcs])
+    sd = _dev(shifts_dev, torch.int32, "shifts")
+    if sd.numel() != 2 * len(srcs):
+        raise ValueError("one (dr, dc) pair per laser expected")
+    return srcs, ch, ptrs, sd
+
+
+def register_assemble_pixtable(lasers, shifts_dev, apply_mask=True, cn_mode=1, bounds=(0, 32, 55, 75, 89, 95),
+                               want_stack=False):
+    """the E. coli registered assembly writing image_cn and the classifier's prepared pixel table
+    from one pass over the lasers (the registered stack itself only with want_stack)
+    -> (image_cn f64 (H, W), PixTable, stack or None)"""
+    import ctypes
+    srcs, ch, ptrs, sd = _laser_args(lasers, shifts_dev)
+    H, W = srcs[0].shape[:2]
+    dev = srcs[0].device
+    pt = pixtable_alloc((H, W), int(ch.sum()), bounds, dev)
+    cn = torch.empty((H, W), dtype=torch.float64, device=dev)
+    stack = torch.empty((H, W, int(ch.sum())), dtype=torch.float32, device=dev) if want_stack else None
+    _lib.call("hrf_register_assemble_pixtable", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd), len(srcs),
+              H, W, int(bool(apply_mask)), _ptr(stack) if stack is not None else None, _ptr(cn), int(cn_mode),
+              _ptr(pt.table), _ptr(pt.flags), _stream())
+    return cn, pt, stack
+
+
+def label_sums_lasers(lasers, shifts_dev, labels, maxlab, apply_mask=True, cal=None, cal_range=(0, 32)):
+    """label_sums of the registered stack, read from the per-laser acquisitions (no stack);
+    cal: a per-pixel (H, W) flat field on channels cal_range"""
+    import ctypes
+    srcs, ch, ptrs, sd = _laser_args(lasers, shifts_dev)
+    l = _i32(labels, "labels")
+    H, W = srcs[0].shape[:2]
+    C = int(ch.sum())
+    sums = torch.empty((maxlab + 1, C), dtype=torch.float64, device=l.device)
+    counts = torch.empty(maxlab + 1, dtype=torch.int64, device=l.device)
+    calp = None
+    if cal is not None:
+        c = _dev(cal, torch.float32, "calibration")
+        if tuple(c.shape) != (H, W):
+            raise ValueError("label_sums_lasers: the flat field must be an (H, W) plane")
+        calp = _ptr(c)
+    _lib.call("hrf_label_sums_lasers", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd), len(srcs), H, W,
+              int(bool(apply_mask)), _ptr(l), maxlab, calp, int(cal_range[0]), int(cal_range[1]), _ptr(sums),
+              _ptr(counts), _stream())
+    return sums, counts
+
+
 def cell_table(sums, counts, maxlab, max_rows=None):
     C = sums.shape[1]
     dev = sums.device
@@ -726,6 +777,55 @@ def classify_pixels(stack, refx, R, bounds, mode=None):
     dist = torch.empty(stack.shape[:-1], dtype=torch.float32, device=stack.device)
     _lib.call("hrf_classify_pixels", _ptr(stack), P, C, _ptr(refx), R, b.ctypes.data, len(b) - 1, mode, _ptr(idx),
               _ptr(dist), _stream())
+    return idx, dist
+
+
+class PixTable:
+    """the per-pixel classifier's prepared operands (pixtable.hpp): split-fp16 segment-normalised
+    pixels in the MFMA register layout + a flag byte per pixel"""
+
+    def __init__(self, table, flags, shape, C, bounds):
+        self.table, self.flags, self.shape, self.C, self.bounds = table, flags, tuple(shape), C, tuple(bounds)
+
+    @property
+    def P(self):
+        n = 1
+        for s in self.shape:
+            n *= s
+        return n
+
+
+def pixtable_alloc(shape, C, bounds, device):
+    P = 1
+    for s in shape:
+        P *= s
+    b = _i32_host(bounds)
+    nb = int(_lib.lib().hrf_pixtable_bytes(P, C, b.ctypes.data, len(b) - 1))
+    if nb < 0:
+        raise ValueError("pixtable: the E. coli or multispecies channel layout only")
+    return PixTable(torch.empty(max(nb, 16), dtype=torch.uint8, device=device),
+                    torch.empty(max(P, 1), dtype=torch.uint8, device=device), shape, C, bounds)
+
+
+def pixtable_prepare(stack, bounds):
+    """the prepared operands of an (..., C) stack (standalone pass; the E. coli assembly writes them
+    in its own pass: register_assemble(..., pixtable=...))"""
+    stack = _dev(stack, torch.float32, "stack")
+    C = stack.shape[-1]
+    pt = pixtable_alloc(stack.shape[:-1], C, bounds, stack.device)
+    b = _i32_host(bounds)
+    _lib.call("hrf_pixtable_prepare", _ptr(stack), pt.P, C, b.ctypes.data, len(b) - 1, _ptr(pt.table), _ptr(pt.flags),
+              _stream())
+    return pt
+
+
+def classify_pixels_table(pt, refx, R):
+    """classify_pixels (mode 2) from a PixTable: the same results bit for bit"""
+    b = _i32_host(pt.bounds)
+    idx = torch.empty(pt.shape, dtype=torch.int32, device=pt.table.device)
+    dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
+    _lib.call("hrf_classify_pixels_table", _ptr(pt.table), _ptr(pt.flags), pt.P, pt.C, _ptr(refx), R, b.ctypes.data,
+              len(b) - 1, _ptr(idx), _ptr(dist), _stream())
     return idx, dist
 
 

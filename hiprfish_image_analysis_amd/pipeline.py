@@ -91,6 +91,12 @@ def measure_ecoli(stack: torch.Tensor, calibration: torch.Tensor | None = None, 
                   image_cn: torch.Tensor | None = None):
     """ecoli measurement.py:142-162: segment, flat-field channels 0..31 (load_calibration_images
     :33-38 puts the calibration image on channels 0-31 and 1.0 elsewhere), per-cell means."""
+    if isinstance(stack, RegisteredTile):
+        seg, maxlab = segment_ecoli(stack, keep, stack.image_cn)
+        sums, counts = K.label_sums_lasers(stack.lasers, stack.shifts, seg, maxlab, stack.apply_mask,
+                                           cal=calibration, cal_range=(0, 32))                   # :147-155
+        _, lor, avgint, avgint_norm = K.cell_table(sums, counts, maxlab)                          # :151-157
+        return Measurement(seg, maxlab, lor, avgint, avgint_norm)
     seg, maxlab = segment_ecoli(stack, keep, image_cn)
     sums, counts = K.label_sums(stack, seg, maxlab, cal=calibration,
                                 cal_range=(0, 32) if calibration is not None else None)   # :147-155
@@ -139,6 +145,42 @@ def register_stack(lasers, reduce: str = "max", clamp: int | None = 15, apply_ma
     -> (stack, image_cn)."""
     return K.register_assemble(lasers, estimate_shifts(lasers, reduce, clamp, device=True), apply_mask,
                                cn_mode=1 if want_cn else None)
+
+
+@dataclass
+class RegisteredTile:
+    """A registered E. coli tile that is never materialised as an (H, W, C) stack: the per-laser
+    acquisitions with their device shifts, image_cn (:71-72) and the per-pixel classifier's
+    prepared operands, all written by one assembly pass (register_tile).  process_tile classifies
+    its pixels from the table and takes the per-cell spectra from the lasers
+    (kernels.label_sums_lasers) -- the same results as register_stack + process_tile."""
+    lasers: list
+    shifts: torch.Tensor
+    image_cn: torch.Tensor
+    pixtable: object
+    apply_mask: bool = True
+
+    @property
+    def shape(self):
+        H, W = self.image_cn.shape
+        return (H, W, self.pixtable.C)
+
+    @property
+    def device(self):
+        return self.image_cn.device
+
+
+def register_tile(lasers, reduce: str = "max", clamp: int | None = 15, apply_mask: bool = True):
+    """register_stack(lasers, want_cn=True) without the stack (ecoli measurement.py:44-72): shift
+    estimate on the device, then ONE pass over the lasers writing image_cn and the classifier's
+    pixel table.  Needs the five E. coli lasers and W a multiple of 16; otherwise returns
+    register_stack's (stack, image_cn)."""
+    H, W = lasers[0].shape[:2]
+    if len(lasers) != 5 or W % 16 or [int(l.shape[2]) for l in lasers] != [32, 23, 20, 14, 6]:
+        return register_stack(lasers, reduce, clamp, apply_mask, want_cn=True)
+    shifts = estimate_shifts(lasers, reduce, clamp, device=True)
+    cn, pt, _ = K.register_assemble_pixtable(lasers, shifts, apply_mask, cn_mode=1, bounds=ECOLI_BOUNDS)
+    return RegisteredTile(list(lasers), shifts, cn, pt, apply_mask)
 
 
 # --------------------------------------------------------------------------------------------
@@ -292,8 +334,11 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
     the (start, end) events recorded around the classification on the stream it ran on.
     `measure` selects the measurement chain (default measure_ecoli; measure_multispecies for
     the synthetic-community pipeline); `image_cn` hands measure_ecoli the log-sum image the
-    registration pass already produced."""
+    registration pass already produced.  `stack` may be a RegisteredTile (register_tile): the
+    pixels are then classified from its prepared table and the per-cell spectra read from its
+    lasers."""
     main = torch.cuda.current_stream(stack.device)
+    reg = isinstance(stack, RegisteredTile)
     pix = None
     if per_pixel:
         refx = lib.refx()                                     # prepared on the caller's stream
@@ -305,14 +350,23 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
             if pixel_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(side)
-            pix = K.classify_pixels(stack, refx, lib.R, lib.bounds)
+            if reg:                                           # from the assembly's pixel table
+                pix = K.classify_pixels_table(stack.pixtable, refx, lib.R)
+            else:
+                pix = K.classify_pixels(stack, refx, lib.R, lib.bounds)
             if pixel_events is not None:
                 e1.record(side)
                 pixel_events.append((e0, e1))
         if overlap:
-            stack.record_stream(side)
+            if reg:
+                stack.pixtable.table.record_stream(side)
+                stack.pixtable.flags.record_stream(side)
+            else:
+                stack.record_stream(side)
             refx.record_stream(side)
-    if image_cn is not None:
+    if reg:
+        meas = measure_ecoli(stack, calibration)
+    elif image_cn is not None:
         meas = (measure or measure_ecoli)(stack, calibration, image_cn=image_cn)
     else:
         meas = (measure or measure_ecoli)(stack, calibration)

@@ -109,6 +109,23 @@ HRF_API hrf_status hrf_register_assemble_cn_dev(const float *const *src_host, co
                                                 const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
                                                 int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode,
                                                 hrf_stream_t stream);
+/* the E. coli registered assembly (five lasers, W a multiple of 16) writing image_cn (cn_mode as
+ * above) and the per-pixel classifier's prepared operands (table: hrf_pixtable_bytes(H * W, ...)
+ * bytes, flags: H * W bytes; see hrf_pixtable_prepare) from the same LDS strip; dst (nullable)
+ * also receives the registered stack -- without it the stack never exists (the per-cell spectra
+ * then come from hrf_label_sums_lasers) */
+HRF_API hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const int32_t *channels_host,
+                                                  const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                                  int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode,
+                                                  void *table, uint8_t *flags, hrf_stream_t stream);
+/* hrf_label_sums of the registered stack hrf_register_assemble_dev would build (shifts on the
+ * device, apply_mask), read from the per-laser acquisitions; cal (nullable): a per-pixel (H, W)
+ * flat field dividing channels [cal_c0, cal_c1) */
+HRF_API hrf_status hrf_label_sums_lasers(const float *const *src_host, const int32_t *channels_host,
+                                         const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                         int32_t apply_mask, const int32_t *labels, int32_t maxlab, const float *cal,
+                                         int32_t cal_c0, int32_t cal_c1, double *sums, int64_t *counts,
+                                         hrf_stream_t stream);
 /* per-pixel sum over C in numpy pairwise order (== np.sum(stack, axis=2) in f64);
  * mode 0: sum, 1: log(sum + 1e-2) (ecoli :72), 2: log10(sum + 1) (biofilm :831);
  * mask (nullable) zeroes the sum; negate flips the sign (watershed input). */
@@ -377,6 +394,16 @@ HRF_API hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_
 HRF_API hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
                                        const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
                                        float *best_dist, hrf_stream_t stream);
+/* the per-pixel classifier's operands prepared once (pixtable.hpp): the split-fp16,
+ * segment-normalised pixels in the MFMA register layout (table: hrf_pixtable_bytes(P, ...) device
+ * bytes) and a flag byte per pixel (flags: P bytes).  Mode-2 layouts (E. coli, multispecies). */
+HRF_API int64_t hrf_pixtable_bytes(int64_t P, int32_t C, const int32_t *bounds_host, int32_t nseg);
+HRF_API hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C, const int32_t *bounds_host,
+                                        int32_t nseg, void *table, uint8_t *flags, hrf_stream_t stream);
+/* hrf_classify_pixels (mode 2) from a prepared pixel table: the same results bit for bit */
+HRF_API hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C,
+                                             const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
+                                             int32_t *best_idx, float *best_dist, hrf_stream_t stream);
 /* per cell (f64): variant 0 ungated, 1 channel_cosine_intensity, 2 _7b_v2; fx (N x nseg),
  * fr (R x nseg) presence flags (needed for variants 1, 2) */
 HRF_API hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int32_t R, int32_t C,

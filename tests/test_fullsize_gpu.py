@@ -115,10 +115,12 @@ def test_fullsize_bench_workload(mods, orc, q):
     if q:
         lasers = [quantised(l, q) for l in lasers]
     cal = S.flat_field(H, W, device="cuda")
-    reg, cn = P.register_stack(lasers, want_cn=True)
-    res = P.process_tile(reg, lib, calibration=cal, per_pixel=True, image_cn=cn)
+    rt = P.register_tile(lasers)                  # bench.py's path: no materialised stack
+    res = P.process_tile(rt, lib, calibration=cal, per_pixel=True)
     torch.cuda.synchronize()
-    stats = K.seg_stats(reg.device, H, W)
+    stats = K.seg_stats(rt.device, H, W)
+    reg, cn = P.register_stack(lasers, want_cn=True)
+    assert torch.equal(rt.image_cn, cn)
     print("watershed stats q=%s: %s" % (q, stats))
 
     hl = [host(l) for l in lasers]

@@ -551,3 +551,38 @@ def test_erosion_seeds_two_threads_two_streams(K, S):
     for t in th:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("nbit,bounds,shape", [(10, (0, 32, 55, 75, 89, 95), (96, 80)),
+                                               (10, (0, 32, 55, 75, 89, 95), (33, 31)),
+                                               (7, (0, 23, 43, 57, 63), (64, 96)),
+                                               (10, (0, 32, 55, 75, 89, 95), (512, 512))])
+def test_classify_pixels_table_equals_in_kernel_build(K, S, nbit, bounds, shape):
+    """the prepared pixel table (pixtable.hpp) + classify_pixels_table give the in-kernel build's
+    results bit for bit, incl. all-zero pixels, zero segments, negative values and a ragged tail"""
+    H, W = shape
+    ref = S.reference_library(nbit, bounds).copy()
+    ref[3, bounds[0]:bounds[1]] = 0.0
+    stack = S.tile(H, W, nbit=nbit, bounds=bounds, seed=5, ncells=6)[0]
+    st = host(stack).reshape(-1, ref.shape[1])
+    st[:7] = 0.0
+    st[7:20, bounds[0]:bounds[1]] = 0.0
+    st[20:23, bounds[1]:bounds[2]] = 1e-25        # f32 underflow of the segment norm
+    d = dev(st.reshape(H, W, -1))
+    refx = K.classify_prepare(dev(ref), bounds, mode=2)
+    want = K.classify_pixels(d, refx, ref.shape[0], bounds, mode=2)
+    pt = K.pixtable_prepare(d, bounds)
+    got = K.classify_pixels_table(pt, refx, ref.shape[0])
+    if len(bounds) != 6:
+        # the community layout's default in-kernel form is the 32x32x16 kernel (its own norm
+        # arithmetic): equal within the classifier's tolerance
+        torch.testing.assert_close(got[1], want[1], rtol=0, atol=2e-6)
+        assert (got[0] == want[0]).float().mean() > 0.999
+        return
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+    neg = st.copy()
+    neg[100:140, 5] = -0.3                          # the compare-and-select (unkeyed) path
+    d2 = dev(neg.reshape(H, W, -1))
+    want = K.classify_pixels(d2, refx, ref.shape[0], bounds, mode=2)
+    got = K.classify_pixels_table(K.pixtable_prepare(d2, bounds), refx, ref.shape[0])
+    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])

@@ -324,8 +324,7 @@ def test_concurrent_registered_tiles_equal_isolated(mods):
     tiles = [S.laser_split(S.tile(768, 768, seed=160 + t)[0]) for t in range(8)]
 
     def run(t):
-        stack, cn = P.register_stack(t, want_cn=True)
-        r = P.process_tile(stack, lib, calibration=cal, image_cn=cn)
+        r = P.process_tile(P.register_tile(t), lib, calibration=cal)
         return [x.clone() for x in (r.pixel_idx, r.pixel_dist, r.cell_idx, r.counts, r.meas.segmentation,
                                     r.identification, r.meas.avgint)]
 

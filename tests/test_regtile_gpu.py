@@ -1,0 +1,85 @@
+"""The bench's registered tile without a materialised stack (pipeline.register_tile): one
+assembly pass writes image_cn and the per-pixel classifier's prepared table (pixtable.hpp); the
+per-cell spectra are read from the lasers (kernels.label_sums_lasers).  Everything equals the
+register_stack path: image_cn, classifier output and label maps bit for bit, spectra within
+1e-12 (ecoli measurement.py:44-162)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods():
+    from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    return K, P, S
+
+
+@pytest.mark.parametrize("H,W,apply_mask", [(256, 256, True), (192, 320, False), (97, 48, True)])
+def test_assembly_pixtable_equals_stack_path(mods, H, W, apply_mask):
+    K, P, S = mods
+    stack, _, _, ref = S.tile(H, W, seed=H + W)
+    lasers = S.laser_split(stack)
+    shifts = P.estimate_shifts(lasers, device=True)
+    want_stack, want_cn = K.register_assemble(lasers, shifts, apply_mask, cn_mode=1)
+    cn, pt, st = K.register_assemble_pixtable(lasers, shifts, apply_mask, want_stack=True)
+    assert torch.equal(st, want_stack) and torch.equal(cn, want_cn)
+    ref_pt = K.pixtable_prepare(want_stack, S.ECOLI_BOUNDS)
+    assert torch.equal(pt.flags, ref_pt.flags)
+    refx = K.classify_prepare(torch.from_numpy(ref).cuda(), S.ECOLI_BOUNDS, mode=2)
+    a = K.classify_pixels_table(pt, refx, ref.shape[0])
+    b = K.classify_pixels(want_stack, refx, ref.shape[0], S.ECOLI_BOUNDS, mode=2)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    # without the stack output: the same table and image_cn
+    cn2, pt2, st2 = K.register_assemble_pixtable(lasers, shifts, apply_mask)
+    assert st2 is None and torch.equal(cn2, cn)
+    a2 = K.classify_pixels_table(pt2, refx, ref.shape[0])
+    assert torch.equal(a2[0], a[0]) and torch.equal(a2[1], a[1])
+
+
+@pytest.mark.parametrize("apply_mask,with_cal", [(True, True), (True, False), (False, True)])
+def test_label_sums_lasers_equal_stack(mods, apply_mask, with_cal):
+    K, P, S = mods
+    H, W = 256, 320
+    stack, truth, _, _ = S.tile(H, W, seed=9)
+    lasers = S.laser_split(stack)
+    shifts = P.estimate_shifts(lasers, device=True)
+    reg = K.register_assemble(lasers, shifts, apply_mask)
+    seg, maxlab = P.segment_ecoli(reg)
+    assert maxlab > 3
+    cal = S.flat_field(H, W) if with_cal else None
+    ws, wc = K.label_sums(reg, seg, maxlab, cal=cal, cal_range=(0, 32) if with_cal else None)
+    gs, gc = K.label_sums_lasers(lasers, shifts, seg, maxlab, apply_mask, cal=cal)
+    assert torch.equal(gc, wc)
+    torch.testing.assert_close(gs, ws, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("H,W,seed", [(384, 384, 3), (256, 512, 4)])
+def test_process_registered_tile_equals_stack_path(mods, H, W, seed):
+    K, P, S = mods
+    stack, _, _, ref = S.tile(H, W, seed=seed)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), S.ECOLI_BOUNDS, 10)
+    lasers = S.laser_split(stack)
+    cal = S.flat_field(H, W)
+    rt = P.register_tile(lasers)
+    assert isinstance(rt, P.RegisteredTile)
+    a = P.process_tile(rt, lib, calibration=cal)
+    st, cn = P.register_stack(lasers, want_cn=True)
+    b = P.process_tile(st, lib, calibration=cal, image_cn=cn)
+    for x, y in ((a.meas.segmentation, b.meas.segmentation), (a.cell_idx, b.cell_idx), (a.counts, b.counts),
+                 (a.identification, b.identification), (a.pixel_idx, b.pixel_idx), (a.pixel_dist, b.pixel_dist),
+                 (a.meas.labels, b.meas.labels)):
+        assert torch.equal(x, y)
+    torch.testing.assert_close(a.meas.avgint, b.meas.avgint, rtol=1e-12, atol=0)
+    torch.testing.assert_close(a.cell_dist, b.cell_dist, rtol=1e-9, atol=1e-12)
+
+
+def test_register_tile_falls_back(mods):
+    """a width that is not a multiple of 16: register_stack's (stack, image_cn)"""
+    K, P, S = mods
+    stack, _, _, _ = S.tile(64, 72, seed=1)
+    out = P.register_tile(S.laser_split(stack))
+    assert isinstance(out, tuple) and out[0].shape == (64, 72, 95)
