@@ -33,7 +33,7 @@ import numpy as np
 
 # Hardware queues per process (HIP's default, also exported on the GPU boxes, is 4).  Each tile
 # in flight uses two streams (its segmentation chain + the per-pixel classifier's side
-# stream); four tiles in flight need eight queues not to share them.  Set before the HIP
+# stream); six tiles in flight need twelve queues not to share them.  Set before the HIP
 # runtime initialises; HRF_HW_QUEUES overrides.  (DESIGN.md "Concurrency on one GPU")
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("HRF_HW_QUEUES", "16")
 
@@ -350,7 +350,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--tiles", type=int, default=0, help="distinct resident tiles per rank (default 2*concurrent)")
-    ap.add_argument("--concurrent", type=int, default=4, help="tiles processed concurrently per step per rank")
+    ap.add_argument("--concurrent", type=int, default=6,
+                    help="tiles processed concurrently per step per rank (DESIGN.md 'Concurrency on one GPU')")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-pixel", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the cfg2 / cfg3-variant / cfg4 measurements")

@@ -1,13 +1,21 @@
 #!/bin/bash
-# A/B of two bench argument sets, interleaved: bash tools/bench_ab_args.sh "<args A>" "<args B>" [reps]
+# Interleaved comparison of bench argument sets: bash tools/bench_ab_args.sh <reps> "<args A>" "<args B>" ...
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/ab_args.log
 : > $out
-A=$1; B=$2; reps=${3:-3}
+reps=$1; shift
 for rep in $(seq $reps); do
-  for a in "$A" "$B"; do
+  for a in "$@"; do
     r=$(timeout -k 10 240 python3 bench.py --no-cpu-baseline --no-extras --steps 40 --warmup 5 $a 2>/dev/null) || exit 1
     echo "[$a] $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("roofline", {}).get("kernel_ms"))')" >> $out
   done
 done
+python3 - "$out" <<'PY'
+import collections, sys, re
+d = collections.defaultdict(list)
+for line in open(sys.argv[1]):
+    m = re.match(r"\[(.*)\] (\S+)", line)
+    if m: d[m.group(1)].append(float(m.group(2)))
+for k, v in d.items(): print("%-40s mean %.1f  %s" % (k, sum(v) / len(v), v))
+PY
