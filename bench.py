@@ -50,6 +50,14 @@ F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
                2: "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3>"}
 REGTILE = os.environ.get("HRF_REGTILE", "1") != "0"   # A/B switch: 0 = register_stack + in-kernel operand build
+# HRF_LOOKAHEAD=1: each worker starts tile i+1 (registration + per-pixel classifier) before it
+# finishes tile i -- neutral with six tiles in flight (1046.7 vs 1048.5 Mpix/s, three interleaved
+# pairs), so off by default
+LOOKAHEAD = os.environ.get("HRF_LOOKAHEAD", "0") == "1"
+# one native call per tile (hrf_tile_ecoli: registration, both classifications, segmentation,
+# spectra, counts, identification map); HRF_TILE_NATIVE=0: the composed path (register_tile +
+# process_tile, ~15 foreign calls and a cell-count synchronisation per tile)
+NATIVE = os.environ.get("HRF_TILE_NATIVE", "1") != "0"
 # algorithmic work (DESIGN.md "Measurement"):
 NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixel, ~20 f64 ops each
 E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort
@@ -87,7 +95,7 @@ def _cpu_worker(seed, hs, npx, barrier, q):
     x = st.reshape(-1, C)[:npx].astype(np.float64)
     barrier.wait()
     t0 = time.perf_counter()
-    OP.process_tile(st, ref, S.ECOLI_BOUNDS)
+    OP.process_tile(st, ref, S.ECOLI_BOUNDS, variant=1)
     t1 = time.perf_counter()
     O.classify(x, ref.astype(np.float64), S.ECOLI_BOUNDS, 0)
     t2 = time.perf_counter()
@@ -116,7 +124,7 @@ def _cpu_baseline(ref, bounds):
     truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
     st = S.render_stack(truth, lay, ref, seed=99, device="cpu", profile=prof).numpy()
     t0 = time.perf_counter()
-    OP.process_tile(st, ref, bounds)
+    OP.process_tile(st, ref, bounds, variant=1)
     t_seg = (time.perf_counter() - t0) / (hs * hs)
     npx = 1 << 17
     x = st.reshape(-1, C)[:npx].astype(np.float64)
@@ -235,9 +243,11 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
             lib._refx = K.classify_prepare(lib.spectra.to(torch.float32), lib.bounds, mode=mode)
         def job(t, lib=lib, pp=pp, mode=mode):
             if mode is None:    # the headline path without the per-pixel GEMM
-                return P.process_tile(P.register_tile(t[0]), lib, calibration=t[1], per_pixel=False)
+                if NATIVE:
+                    return P.process_tile_native(t[0], lib, calibration=t[1], per_pixel=False, variant=1)
+                return P.process_tile(P.register_tile(t[0]), lib, calibration=t[1], per_pixel=False, variant=1)
             stack, cn = P.register_stack(t[0], want_cn=True)     # mode 0 reads the f32 stack
-            return P.process_tile(stack, lib, calibration=t[1], per_pixel=pp, image_cn=cn)
+            return P.process_tile(stack, lib, calibration=t[1], per_pixel=pp, image_cn=cn, variant=1)
         sec = _timed_tiles(job, tiles, T, streams, pool, steps, 2)
         cfg3[name] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
                       "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
@@ -248,7 +258,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
     # round-1-style synthetic stack)
     pre = [(P.register_stack(t[0], apply_mask=False),) for t in tiles]
     torch.cuda.synchronize()
-    sec = _timed_tiles(lambda t: P.process_tile(t[0], lib_main), pre, T, streams, pool, steps, 2)
+    sec = _timed_tiles(lambda t: P.process_tile(t[0], lib_main, variant=1), pre, T, streams, pool, steps, 2)
     cfg3["preassembled_uncalibrated"] = {"value": round(H * W * steps * T / sec / 1e6, 3),
                                          "unit": "Mpixel-spectra/s", "ms_per_step": round(sec / steps * 1e3, 3),
                                          "steps": steps, "concurrent": T, "classifier_mode": 2,
@@ -262,8 +272,12 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
     wstats = []
 
     def qjob(t):
+        if NATIVE:
+            r = P.process_tile_native(t[0], lib_main, calibration=t[1], variant=1)
+            wstats.append(K.tile_stats(t[0][0].device, H, W))
+            return r
         rt = P.register_tile(t[0])
-        r = P.process_tile(rt, lib_main, calibration=t[1])
+        r = P.process_tile(rt, lib_main, calibration=t[1], variant=1)
         wstats.append(K.seg_stats(rt.device, H, W))
         return r
     sec = _timed_tiles(qjob, qtiles, T, streams, pool, steps, 2)
@@ -385,6 +399,7 @@ def main():
     ref = S.reference_library(NBIT, bounds)
     lib = P.Library(torch.from_numpy(ref.astype(np.float64)).to(dev), bounds, NBIT)
     lib.refx()
+    lib.presence_flags()
     tiles = []
     if args.tiles <= 0:
         args.tiles = 2 * max(1, args.concurrent)
@@ -417,27 +432,49 @@ def main():
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(T)
 
-    def tile_job(j, tile, timed):
+    def tile_start(j, tile, timed):
         with torch.cuda.stream(streams[j]):
             # ecoli :45-72: shifts on the device, one assembly pass writing image_cn and the
             # classifier's pixel table (the registered stack is never materialised)
             if REGTILE:
-                rt = P.register_tile(tile[0])
-                return P.process_tile(rt, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
-                                      pixel_events=ev if timed else None)
-            stack, cn = P.register_stack(tile[0], want_cn=True)  # HRF_REGTILE=0: the materialised stack
-            return P.process_tile(stack, lib, calibration=tile[1], per_pixel=per_pixel, overlap=not args.no_overlap,
-                                  image_cn=cn, pixel_events=ev if timed else None)
+                st, cn = P.register_tile(tile[0]), None
+            else:
+                st, cn = P.register_stack(tile[0], want_cn=True)  # HRF_REGTILE=0: the materialised stack
+            p = P.start_tile(st, lib, per_pixel=per_pixel, overlap=not args.no_overlap,
+                             pixel_events=ev if timed else None)
+            return p, tile[1], cn
+
+    def tile_finish(j, started):
+        p, cal, cn = started
+        with torch.cuda.stream(streams[j]):
+            # per cell: the reference's gated channel_cosine_intensity (train_reference.py:223-386)
+            return P.finish_tile(p, calibration=cal, image_cn=cn, variant=1)
 
     def worker(j, first, nsteps, timed):
         # worker j drives tiles first*T + j, (first+1)*T + j, ... on its own stream, with no
         # barrier between steps: a tile's segmentation chain starts while the previous tile's
-        # classifier still runs, so the GPU never drains at a step boundary.  Counts are
-        # summed on the worker's stream (one all-reduce per job, after the join).
+        # classifier still runs, so the GPU never drains at a step boundary.  With LOOKAHEAD
+        # the worker registers tile i+1 and enqueues its per-pixel classifier before it runs
+        # tile i's segmentation chain (every tile is still registered, classified, segmented
+        # and counted inside the region it is timed in).  Counts are summed on the worker's
+        # stream (one all-reduce per job, after the join).
         acc = None
         res = None
-        for i in range(first, first + nsteps):
-            res = tile_job(j, tiles[(i * T + j) % len(tiles)], timed)
+        seq = [tiles[(i * T + j) % len(tiles)] for i in range(first, first + nsteps)]
+        nxt = tile_start(j, seq[0], timed) if (LOOKAHEAD and not NATIVE and seq) else None
+        for k, tile in enumerate(seq):
+            if NATIVE and REGTILE:
+                with torch.cuda.stream(streams[j]):
+                    res = P.process_tile_native(tile[0], lib, calibration=tile[1], per_pixel=per_pixel, variant=1,
+                                                overlap=not args.no_overlap, pixel_events=ev if timed else None)
+                    acc = res.counts.clone() if acc is None else acc.add_(res.counts)
+                continue
+            if LOOKAHEAD:
+                cur = nxt
+                nxt = tile_start(j, seq[k + 1], timed) if k + 1 < len(seq) else None
+            else:
+                cur = tile_start(j, tile, timed)
+            res = tile_finish(j, cur)
             with torch.cuda.stream(streams[j]):
                 acc = res.counts.clone() if acc is None else acc.add_(res.counts)
         return res, acc

@@ -28,6 +28,7 @@ _CT = {
     "float": ctypes.c_float, "uint32_t": ctypes.c_uint32, "uint64_t": ctypes.c_uint64, "int": ctypes.c_int,
     "const float *const *": ctypes.c_void_p, "double *const *": ctypes.c_void_p,
     "hrf_seg_ctx *": ctypes.c_void_p, "hrf_seg_ctx * *": ctypes.c_void_p, "const hrf_seg_ctx *": ctypes.c_void_p,
+    "hrf_tile_ctx *": ctypes.c_void_p, "hrf_tile_ctx * *": ctypes.c_void_p, "hrf_event_t": ctypes.c_void_p,
 }
 
 

@@ -1473,6 +1473,25 @@ __global__ __launch_bounds__(256) void ref_negflag_kernel(const float *__restric
   if (threadIdx.x == 0) *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(refh) + 4 * KP + 12) = (uint32_t)neg;
 }
 
+// presence flags of the gated metrics: out[n][s] = 1.0 when max over segment s of row n > thr (a NaN
+// in the segment makes the max NaN, and the comparison false), else 0.0
+__global__ __launch_bounds__(256) void segment_flags_kernel(const double *__restrict__ x, int64_t N, int32_t C,
+                                                            Bounds bd, double thr, double *__restrict__ out,
+                                                            const int32_t *__restrict__ n_dev) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n_dev) N = min(N, (int64_t)*n_dev);
+  if (i >= N * bd.nseg) return;
+  const int64_t n = i / bd.nseg;
+  const int sg = (int)(i - n * bd.nseg);
+  bool any = false, nan = false;
+  for (int c = bd.b[sg]; c < bd.b[sg + 1]; ++c) {
+    const double v = x[n * C + c];
+    any |= v > thr;
+    nan |= v != v;
+  }
+  out[i] = (any && !nan) ? 1.0 : 0.0;
+}
+
 // 1 = E. coli layout, 2 = synthetic-community layout, 0 = other
 template <class L>
 bool is_layout(const Bounds &bd, int C) {
@@ -1523,11 +1542,13 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *__res
                                                              Bounds bd, int32_t variant,
                                                              const double *__restrict__ fx,
                                                              const double *__restrict__ fr,
-                                                             int32_t *__restrict__ arg, double *__restrict__ dmin) {
+                                                             int32_t *__restrict__ arg, double *__restrict__ dmin,
+                                                             const int32_t *__restrict__ n_dev) {
   extern __shared__ double xs[];
   __shared__ double sbest[256];
   __shared__ int sidx[256];
   const int64_t i = blockIdx.x;
+  if (n_dev && i >= *n_dev) return;  // rows past the device-held count (hrf_tile_ecoli)
   const int tid = threadIdx.x;
   for (int c = tid; c < C; c += 256) xs[c] = X[i * C + c];
   __syncthreads();
@@ -1890,6 +1911,58 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
   return HRF_OK;
 }
 
+}  // extern "C"
+
+namespace hrf {
+
+// the per-cell tail of hrf_tile_ecoli: row counts held on the device (nrows_dev <= nmax), no host
+// synchronisation; refT = the library transposed to channel-major (transpose_f64)
+hrf_status transpose_f64(const double *a, int32_t R, int32_t C, double *t, hipStream_t s) {
+  transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(a, R, C, t);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status segment_flags_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, int32_t C,
+                              const int32_t *bounds_host, int32_t nseg, double thr, double *out, hipStream_t s) {
+  Bounds bd;
+  if (hrf_status st = make_bounds(bounds_host, nseg, C, &bd)) return st;
+  if (nmax == 0) return HRF_OK;
+  segment_flags_kernel<<<(unsigned)hrf::cdiv(nmax * nseg, 256), 256, 0, s>>>(x, nmax, C, bd, thr, out, nrows_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, const double *refT, int32_t R,
+                               int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
+                               const double *fr, int32_t *arg, double *dmin, hipStream_t s) {
+  Bounds bd;
+  if (hrf_status st = make_bounds(bounds_host, nseg, C, &bd)) return st;
+  HRF_REQUIRE(variant >= 0 && variant <= 2, "classify_cells: variant must be 0, 1 or 2");
+  HRF_REQUIRE(variant == 0 || (fx && fr), "classify_cells: gated variants need presence flags");
+  if (nmax == 0) return HRF_OK;
+  classify_cells_kernel<<<(unsigned)nmax, 256, sizeof(double) * C, s>>>(x, nmax, refT, R, C, bd, variant, fx, fr, arg,
+                                                                         dmin, nrows_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+}  // namespace hrf
+
+extern "C" {
+
+hrf_status hrf_segment_flags(const double *x, int64_t N, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                             double thr, double *out, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  if (N == 0) return HRF_OK;
+  HRF_REQUIRE(x && out, "segment_flags: null buffer");
+  segment_flags_kernel<<<(unsigned)hrf::cdiv(N * nseg, 256), 256, 0, (hipStream_t)stream>>>(x, N, C, bd, thr, out,
+                                                                                             nullptr);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
 hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int32_t R, int32_t C,
                               const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
                               const double *fr, int32_t *arg, double *dmin, hrf_stream_t stream) {
@@ -1905,7 +1978,7 @@ hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int
   transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, (hipStream_t)stream>>>(ref, R, C, refT);
   HRF_LAUNCHED();
   classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, (hipStream_t)stream>>>(x, N, refT, R, C, bd, variant,
-                                                                                       fx, fr, arg, dmin);
+                                                                                       fx, fr, arg, dmin, nullptr);
   HRF_LAUNCHED();
   HRF_HIP(hipFreeAsync(refT, (hipStream_t)stream));
   return HRF_OK;

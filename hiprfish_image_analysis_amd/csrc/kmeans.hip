@@ -42,7 +42,6 @@
 #include <unordered_map>
 #include <vector>
 
-#include <rocprim/device/device_select.hpp>
 
 #include "common.hpp"
 #include "wave.hpp"
@@ -443,6 +442,46 @@ __global__ __launch_bounds__(256) void km_scan_apply_kernel(unsigned *__restrict
       a[i0 + e] = (unsigned)acc;
       acc += v[e];
     }
+}
+
+// ---- order-preserving compaction of the valid samples (sklearn's sample order) ----
+// km_sel_count_kernel: valid samples per KSC_B block; km_scan_blocks_kernel turns the counts into
+// block offsets in place; km_sel_scatter_kernel writes each block's valid values in raster order
+// (16 consecutive samples per thread, a block scan of the per-thread counts) and the total.
+__global__ __launch_bounds__(256) void km_sel_count_kernel(const uint8_t *__restrict__ valid, long long n,
+                                                           unsigned *__restrict__ cnt) {
+  const long long i0 = (long long)blockIdx.x * KSC_B;
+  unsigned long long s = 0;
+  for (int e = threadIdx.x; e < KSC_B; e += 256)
+    if (i0 + e < n) s += valid[i0 + e] != 0;
+  s = hrf::wave_sum(s);
+  __shared__ unsigned long long sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (unsigned)(sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+__global__ __launch_bounds__(256) void km_sel_scatter_kernel(const double *__restrict__ x,
+                                                             const uint8_t *__restrict__ valid, long long n,
+                                                             const unsigned *__restrict__ boff,
+                                                             double *__restrict__ out,
+                                                             unsigned long long *__restrict__ nsel) {
+  __shared__ unsigned long long sh[4];
+  const long long i0 = (long long)blockIdx.x * KSC_B + threadIdx.x * 16;
+  unsigned m = 0;
+  unsigned long long loc = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool v = i0 + e < n && valid[i0 + e] != 0;
+    m |= (unsigned)v << e;
+    loc += v;
+  }
+  unsigned long long tot;
+  unsigned long long o = boff[blockIdx.x] + block_excl_scan_u64(loc, sh, &tot);
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    if ((m >> e) & 1u) out[o++] = x[i0 + e];
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *nsel = boff[blockIdx.x] + tot;
 }
 
 // ---- pass A: coarse digit over raster chunks ----
@@ -1459,12 +1498,9 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 int64_t nblocks(int64_t n) { return std::max<int64_t>(1, (n + PB - 1) / PB); }
 
+// the compaction's per-block offsets
 hrf_status sort_tmp_bytes(int64_t n, size_t *bytes) {
-  size_t d = 0;
-  const size_t m = (size_t)std::max<int64_t>(n, 1);
-  HRF_HIP(rocprim::select(nullptr, d, (const double *)nullptr, (const uint8_t *)nullptr, (double *)nullptr,
-                          (unsigned long long *)nullptr, m, (hipStream_t)0));
-  *bytes = d;
+  *bytes = sizeof(unsigned) * (size_t)((std::max<int64_t>(n, 1) + KSC_B - 1) / KSC_B);
   return HRF_OK;
 }
 
@@ -1589,8 +1625,12 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
       km_bucket_prefix_kernel<<<nch, PT, 0, s>>>(ws.xs, st, ws.geo, ws.cq, ws.cq2, ws.bq, ws.bq2);
       HRF_LAUNCHED();
       if (valid) {  // the valid samples in raster order (sklearn's sample order)
-        size_t tb = ws.tmp_bytes;
-        HRF_HIP(rocprim::select(ws.tmp, tb, x, valid, ws.xr, ws.nsel, (size_t)n, s));
+        const int nsb = (int)((n + KSC_B - 1) / KSC_B);
+        unsigned *boff = (unsigned *)ws.tmp;
+        km_sel_count_kernel<<<nsb, 256, 0, s>>>(valid, n, boff);
+        km_scan_blocks_kernel<<<1, 256, 0, s>>>(boff, nsb);
+        km_sel_scatter_kernel<<<nsb, 256, 0, s>>>(x, valid, n, boff, ws.xr, ws.nsel);
+        HRF_LAUNCHED();
       }
       km_tol_kernel<<<1, 1, 0, s>>>(st);
       km_count_le0_kernel<<<1, 1024, 0, s>>>(ws.xs, ws.off, ws.geo, st);

@@ -363,7 +363,8 @@ __global__ void props_kernel(const unsigned long long *__restrict__ mom, int32_t
 }
 
 __global__ void barcode_counts_kernel(const int32_t *__restrict__ bc, int64_t n, int32_t R,
-                                      unsigned long long *__restrict__ counts) {
+                                      unsigned long long *__restrict__ counts, const int32_t *__restrict__ n_dev) {
+  if (n_dev) n = min(n, (int64_t)*n_dev);
   const int64_t n_up = (n + 63) / 64 * 64;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t b = i < n ? bc[i] : -1;
@@ -373,10 +374,12 @@ __global__ void barcode_counts_kernel(const int32_t *__restrict__ bc, int64_t n,
 }
 
 __global__ void paint_kernel(const int32_t *__restrict__ lab, int64_t n, const int32_t *__restrict__ code,
-                             int32_t ncell, int32_t *__restrict__ out) {
+                             int32_t ncell, int32_t *__restrict__ out, const int32_t *__restrict__ ncell_dev,
+                             int32_t add) {
+  if (ncell_dev) ncell = min(ncell, *ncell_dev);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t l = lab[i];
-    out[i] = (l >= 1 && l <= ncell) ? code[l - 1] : 0;
+    out[i] = (l >= 1 && l <= ncell) ? code[l - 1] + add : 0;
   }
 }
 
@@ -507,7 +510,7 @@ hrf_status hrf_barcode_counts(const int32_t *bc, int64_t n, int32_t R, int64_t *
   HRF_REQUIRE(R >= 1 && counts, "barcode_counts: bad arguments");
   HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * R, s));
   if (n == 0) return HRF_OK;
-  barcode_counts_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(bc, n, R, (unsigned long long *)counts);
+  barcode_counts_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(bc, n, R, (unsigned long long *)counts, nullptr);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -516,9 +519,33 @@ hrf_status hrf_paint_ids(const int32_t *labels, int64_t n, const int32_t *code, 
                          hrf_stream_t stream) {
   if (n == 0) return HRF_OK;
   HRF_REQUIRE(labels && out && (code || ncell == 0), "paint_ids: null buffer");
-  paint_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(labels, n, code, ncell, out);
+  paint_kernel<<<hrf::stream_grid(n), 256, 0, (hipStream_t)stream>>>(labels, n, code, ncell, out, nullptr, 0);
   HRF_LAUNCHED();
   return HRF_OK;
 }
 
 }  // extern "C"
+
+namespace hrf {
+
+// hrf_barcode_counts / hrf_paint_ids with the cell count held on the device (hrf_tile_ecoli):
+// n_dev <= nmax rows; paint writes code[l - 1] + add
+hrf_status barcode_counts_devn(const int32_t *bc, int64_t nmax, const int32_t *n_dev, int32_t R, int64_t *counts,
+                               hipStream_t s) {
+  HRF_REQUIRE(R >= 1 && counts, "barcode_counts: bad arguments");
+  HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * R, s));
+  if (nmax == 0) return HRF_OK;
+  barcode_counts_kernel<<<hrf::stream_grid(nmax), 256, 0, s>>>(bc, nmax, R, (unsigned long long *)counts, n_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status paint_ids_devn(const int32_t *labels, int64_t n, const int32_t *code, int32_t nmax, const int32_t *ncell_dev,
+                          int32_t add, int32_t *out, hipStream_t s) {
+  if (n == 0) return HRF_OK;
+  paint_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, n, code, nmax, out, ncell_dev, add);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+}  // namespace hrf

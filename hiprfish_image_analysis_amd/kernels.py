@@ -829,6 +829,16 @@ def classify_pixels_table(pt, refx, R):
     return idx, dist
 
 
+def segment_flags(x, bounds, thr=0.1):
+    """(N, C) f64 -> (N, nseg) f64 presence flags: max over each segment > thr (NaN -> 0)"""
+    x = _dev(x, torch.float64, "x")
+    N, C = x.shape
+    b = _i32_host(bounds)
+    out = torch.empty((N, len(b) - 1), dtype=torch.float64, device=x.device)
+    _lib.call("hrf_segment_flags", _ptr(x), N, C, b.ctypes.data, len(b) - 1, float(thr), _ptr(out), _stream())
+    return out
+
+
 def classify_cells(x, ref, bounds, variant=0, fx=None, fr=None):
     x = _dev(x, torch.float64, "x")
     ref = _dev(ref, torch.float64, "ref")
@@ -950,6 +960,109 @@ def _seg_ctx(dev, H, W):
         _lib.call("hrf_seg_ctx_create", H, W, ctypes.addressof(h))
         _SEG_CTX[key] = h
     return h
+
+
+_TILE_CTX = {}
+
+
+def _tile_ctx(dev, H, W):
+    """one native tile context per (device, stream, tile size) (hrf_tile_ctx: its own segmentation
+    context, projections, registration workspace, image_cn, pixel table, per-label buffers)"""
+    import ctypes
+    key = (dev, _stream(), H, W)
+    h = _TILE_CTX.get(key)
+    if h is None:
+        h = ctypes.c_void_p()
+        _lib.call("hrf_tile_ctx_create", H, W, ctypes.addressof(h))
+        _TILE_CTX[key] = h
+    return h
+
+
+def tile_stats(device, H, W):
+    """seg_stats of the last native tile (tile_ecoli) run on the current stream's (H, W) context"""
+    import ctypes
+    seg = ctypes.c_void_p()
+    _lib.call("hrf_tile_ctx_seg", _tile_ctx(torch.device(device), H, W), ctypes.addressof(seg))
+    out = (ctypes.c_int32 * 4)()
+    _lib.call("hrf_seg_ctx_stats", seg, ctypes.addressof(out))
+    return dict(zip(("passes", "contests", "rounds", "marker_ties"), list(out)))
+
+
+_CELL_CAP = {}
+
+
+def tile_ecoli(lasers, cal, refx, lib, lib_flags, variant=1, flag_thr=0.1, per_pixel=True, side=None,
+               pix_events=None):
+    """one E. coli tile in one native call (hrf_tile_ecoli).  lasers: the five (H, W, C_l) f32
+    acquisitions; cal: (H, W) f32 flat field or None; refx: classify_prepare(library) (mode 2);
+    lib: (R, 95) f64 library; lib_flags: its presence flags (R, 5) f64 (gated variants).
+    -> dict of device tensors: seg, ident, counts, ncells (int32[1]), maxlab, and per-cell rows
+    (labels, avgint, avgint_norm, cell_idx, cell_dist; first ncells rows valid), pixel_idx /
+    pixel_dist.  side: the stream the per-pixel classifier runs on (default: the current one)."""
+    import ctypes
+    srcs = [_dev(l, torch.float32, "laser stack") for l in lasers]
+    if len(srcs) != 5 or [int(l.shape[2]) for l in srcs] != [32, 23, 20, 14, 6]:
+        raise ValueError("tile_ecoli: the five E. coli laser stacks (32, 23, 20, 14, 6 channels) expected")
+    H, W = srcs[0].shape[:2]
+    if any(tuple(l.shape[:2]) != (H, W) for l in srcs):
+        raise ValueError("tile_ecoli: the laser stacks must share H x W")
+    dev = srcs[0].device
+    lib = _dev(lib, torch.float64, "library")
+    R = lib.shape[0]
+    if lib.shape[1] != 95:
+        raise ValueError("tile_ecoli: a 95-channel library expected")
+    fl = _dev(lib_flags, torch.float64, "library flags") if lib_flags is not None else None
+    if variant and fl is None:
+        raise ValueError("tile_ecoli: the gated variants need the library's presence flags")
+    calp = None
+    if cal is not None:
+        c = _dev(cal, torch.float32, "calibration")
+        if tuple(c.shape) != (H, W):
+            raise ValueError("tile_ecoli: the flat field must be an (H, W) plane")
+        calp = _ptr(c)
+    ctx = _tile_ctx(dev, H, W)
+    ptrs = (ctypes.c_void_p * 5)(*[l.data_ptr() for l in srcs])
+    key = (dev, H, W)
+    cap = _CELL_CAP.get(key, 4096)
+    i32, f64 = torch.int32, torch.float64
+    seg = torch.empty((H, W), dtype=i32, device=dev)
+    ident = torch.empty((H, W), dtype=i32, device=dev)
+    counts = torch.empty(R, dtype=torch.int64, device=dev)
+    ncells = torch.empty(1, dtype=i32, device=dev)
+    pix_idx = torch.empty((H, W), dtype=i32, device=dev) if per_pixel else None
+    pix_dist = torch.empty((H, W), dtype=torch.float32, device=dev) if per_pixel else None
+
+    def rows(n):
+        return (torch.empty(n, dtype=i32, device=dev), torch.empty((n, 95), dtype=f64, device=dev),
+                torch.empty((n, 95), dtype=f64, device=dev), torch.empty(n, dtype=i32, device=dev),
+                torch.empty(n, dtype=f64, device=dev))
+    labs, avg, avgn, cidx, cdist = rows(cap)
+    mx = ctypes.c_int32(0)
+    e0 = e1 = None
+    if pix_events is not None and per_pixel:
+        st = side if side is not None else torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)        # creates the events (recorded again inside the call)
+        e1.record(st)
+        pix_events.append((e0, e1))
+    _lib.call("hrf_tile_ecoli", ctx, ctypes.cast(ptrs, ctypes.c_void_p), calp,
+              _ptr(refx) if per_pixel else None, _ptr(lib), _ptr(fl) if fl is not None else None, R, int(variant),
+              float(flag_thr), int(bool(per_pixel)), _ptr(seg), _ptr(pix_idx) if per_pixel else None,
+              _ptr(pix_dist) if per_pixel else None, cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx), _ptr(cdist),
+              _ptr(ident), _ptr(counts), _ptr(ncells), ctypes.addressof(mx), _stream(),
+              ctypes.c_void_p(side.cuda_stream) if side is not None else None,
+              ctypes.c_void_p(e0.cuda_event) if e0 is not None else None,
+              ctypes.c_void_p(e1.cuda_event) if e1 is not None else None)
+    maxlab = mx.value
+    if maxlab > cap:            # the per-cell part was left for buffers that hold every label
+        cap = 1 << max(12, (maxlab - 1).bit_length())
+        _CELL_CAP[key] = cap
+        labs, avg, avgn, cidx, cdist = rows(cap)
+        _lib.call("hrf_tile_ecoli_cells", ctx, _ptr(seg), _ptr(lib), _ptr(fl) if fl is not None else None, R,
+                  int(variant), float(flag_thr), cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx), _ptr(cdist),
+                  _ptr(ident), _ptr(counts), _ptr(ncells), _stream())
+    return dict(seg=seg, ident=ident, counts=counts, ncells=ncells, maxlab=maxlab, labels=labs, avgint=avg,
+                avgint_norm=avgn, cell_idx=cidx, cell_dist=cdist, pixel_idx=pix_idx, pixel_dist=pix_dist)
 
 
 def seg_stats(device, H, W):

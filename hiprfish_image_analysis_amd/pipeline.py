@@ -252,6 +252,7 @@ class Library:
     bounds: tuple
     nbit: int
     _refx: torch.Tensor | None = None
+    _flags: dict = field(default_factory=dict)
 
     @property
     def R(self):
@@ -263,14 +264,18 @@ class Library:
         return self._refx
 
     def presence_flags(self, thr: float = 0.1) -> torch.Tensor:
-        """per-segment presence of the library rows (max over the segment > thr)"""
-        return segment_flags(self.spectra, self.bounds, thr)
+        """per-segment presence of the library rows (max over the segment > thr), computed once
+        per threshold"""
+        f = self._flags.get(thr)
+        if f is None:
+            f = self._flags[thr] = segment_flags(self.spectra, self.bounds, thr)
+        return f
 
 
 def segment_flags(x: torch.Tensor, bounds, thr: float = 0.1) -> torch.Tensor:
-    # tiny (N x nseg) host-side bookkeeping of the gated metric's inputs
-    cols = [x[:, bounds[k]:bounds[k + 1]].amax(dim=1) > thr for k in range(len(bounds) - 1)]
-    return torch.stack(cols, 1).to(torch.float64).contiguous()
+    """the gated metrics' presence flags on the library path: max over each segment > thr
+    (hrf_segment_flags)"""
+    return K.segment_flags(x, bounds, thr)
 
 
 def classify_cells(avgint_norm: torch.Tensor, lib: Library, variant: int = 0, flag_thr: float = 0.1):
@@ -323,6 +328,18 @@ def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
     return s
 
 
+@dataclass
+class PendingTile:
+    """A tile whose per-pixel classification is enqueued (start_tile) and whose measurement is
+    not yet (finish_tile)."""
+    stack: object
+    lib: Library
+    main: torch.cuda.Stream
+    side: torch.cuda.Stream | None
+    pix: tuple | None
+    overlap: bool
+
+
 def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 0,
                  overlap: bool = True, pixel_events: list | None = None, measure=None, image_cn=None):
     """One tile of the hot path: measure (segment + per-cell spectra) + classify + count.
@@ -336,10 +353,21 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
     the synthetic-community pipeline); `image_cn` hands measure_ecoli the log-sum image the
     registration pass already produced.  `stack` may be a RegisteredTile (register_tile): the
     pixels are then classified from its prepared table and the per-cell spectra read from its
-    lasers."""
+    lasers.  process_tile = finish_tile(start_tile(...)); a caller driving a sequence of tiles
+    may start tile i+1 before finishing tile i, so that tile's classifier is queued while tile
+    i's segmentation chain runs."""
+    p = start_tile(stack, lib, per_pixel, overlap, pixel_events)
+    return finish_tile(p, calibration, variant, measure, image_cn)
+
+
+def start_tile(stack, lib: Library, per_pixel: bool = True, overlap: bool = True,
+               pixel_events: list | None = None) -> PendingTile:
+    """first half of process_tile: enqueue the per-pixel classification (side stream with
+    `overlap`, after everything the caller's stream holds so far, i.e. the stack / table)"""
     main = torch.cuda.current_stream(stack.device)
     reg = isinstance(stack, RegisteredTile)
     pix = None
+    side = None
     if per_pixel:
         refx = lib.refx()                                     # prepared on the caller's stream
         side = _side_stream(main) if overlap else main
@@ -364,6 +392,16 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
             else:
                 stack.record_stream(side)
             refx.record_stream(side)
+    return PendingTile(stack, lib, main, side, pix, overlap)
+
+
+def finish_tile(p: PendingTile, calibration=None, variant: int = 0, measure=None, image_cn=None) -> TileResult:
+    """second half of process_tile, on the stream start_tile was called on: measurement,
+    per-cell classification, counts, identification map, then the join with the per-pixel
+    classification"""
+    stack, lib, main, side, pix, overlap = p.stack, p.lib, p.main, p.side, p.pix, p.overlap
+    per_pixel = pix is not None
+    reg = isinstance(stack, RegisteredTile)
     if reg:
         meas = measure_ecoli(stack, calibration)
     elif image_cn is not None:
@@ -381,6 +419,55 @@ def process_tile(stack: torch.Tensor, lib: Library, calibration=None, per_pixel:
                 t.record_stream(main)
         res.pixel_idx, res.pixel_dist = pix
     return res
+
+
+class NativeTileResult:
+    """TileResult of process_tile_native: the per-cell rows are narrowed to the tile's cell count
+    on first access (one read of the device-held count); counts, the identification map and
+    the per-pixel outputs need no host round trip."""
+
+    def __init__(self, d):
+        self._d = d
+        self._n = None
+        self.counts = d["counts"]
+        self.identification = d["ident"]
+        self.pixel_idx = d["pixel_idx"]
+        self.pixel_dist = d["pixel_dist"]
+
+    @property
+    def ncells(self) -> int:
+        if self._n is None:
+            self._n = int(self._d["ncells"].item())
+        return self._n
+
+    @property
+    def cell_idx(self):
+        return self._d["cell_idx"][:self.ncells]
+
+    @property
+    def cell_dist(self):
+        return self._d["cell_dist"][:self.ncells]
+
+    @property
+    def meas(self) -> Measurement:
+        d, n = self._d, self.ncells
+        return Measurement(d["seg"], d["maxlab"], d["labels"][:n], d["avgint"][:n], d["avgint_norm"][:n])
+
+
+def process_tile_native(lasers, lib: Library, calibration=None, per_pixel: bool = True, variant: int = 1,
+                        overlap: bool = True, pixel_events: list | None = None) -> NativeTileResult:
+    """register_tile(lasers) + process_tile(..., variant) as ONE native call (hrf_tile_ecoli,
+    tile.hip): ecoli measurement.py:44-162 (-c T) + image_classification.py:43-71 + collect
+    :92-98, the per-pixel classifier on the side stream with `overlap`.  The same results as the
+    composed path bit for bit (tests/test_tile_gpu.py).  lasers: the five E. coli acquisitions
+    (H, W powers of two)."""
+    main = torch.cuda.current_stream(lasers[0].device)
+    side = _side_stream(main) if (per_pixel and overlap) else None
+    refx = lib.refx() if per_pixel else None
+    flags = lib.presence_flags() if variant else None
+    d = K.tile_ecoli(lasers, calibration, refx, lib.spectra, flags, variant=variant, per_pixel=per_pixel, side=side,
+                     pix_events=pixel_events)
+    return NativeTileResult(d)
 
 
 # --------------------------------------------------------------------------------------------

@@ -33,6 +33,7 @@ typedef int32_t hrf_status;
 #define HRF_ENOMEM 3   /* workspace too small */
 
 typedef void *hrf_stream_t;
+typedef void *hrf_event_t; /* hipEvent_t */
 
 #if defined(__GNUC__)
 #define HRF_API __attribute__((visibility("default")))
@@ -342,6 +343,39 @@ HRF_API hrf_status hrf_segment_multispecies(hrf_seg_ctx *ctx, const float *stack
                                             int32_t *seg_out, int32_t *nlab_host, double *image_sum_out,
                                             double *final_bkg_out, hrf_stream_t stream);
 
+/* ==== one E. coli tile in one call (tile.hip) ============================================
+ * ecoli measurement.py:44-162 (-c T) + image_classification.py:43-71 + collect :92-98:
+ * registration (channel-max projections, xcorr shifts, assembly writing image_cn and the pixel
+ * table), the per-pixel classifier on side_stream (nullable: the same stream; pix_start/pix_end,
+ * nullable, recorded around it there), the segmentation chain, flat-fielded label sums read from
+ * the lasers (cal: H x W f32 on channels 0-31, nullable), cell table, presence flags (variant 1/2:
+ * lib_flags R x 5 f64 = the library's), per-cell classification, counts (R int64), identification
+ * map.  Caller buffers: seg, ident (H*W int32), pixel_idx/pixel_dist (H*W, per_pixel only), the
+ * per-cell rows labels (cell_cap int32), avgint / avgint_norm (cell_cap x 95 f64), cell_idx
+ * (int32) / cell_dist (f64); ncells_dev (device int32) receives the row count, *maxlab_host the
+ * segmentation's maximum label.  When *maxlab_host > cell_cap the per-cell part is not run:
+ * call hrf_tile_ecoli_cells with buffers of at least *maxlab_host rows.  lasers_host: the five
+ * (H, W, 32/23/20/14/6) f32 acquisitions; H, W powers of two.  Stream-ordered after the
+ * segmentation's two synchronisations; side_stream is joined before return. */
+typedef struct hrf_tile_ctx hrf_tile_ctx;
+HRF_API hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out);
+HRF_API hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *ctx);
+/* the segmentation context the tile context runs (hrf_seg_ctx_stats of the last tile) */
+HRF_API hrf_status hrf_tile_ctx_seg(hrf_tile_ctx *ctx, hrf_seg_ctx **seg);
+HRF_API hrf_status hrf_tile_ecoli(hrf_tile_ctx *ctx, const float *const *lasers_host, const float *cal,
+                                  const void *refx, const double *lib, const double *lib_flags, int32_t R,
+                                  int32_t variant, double flag_thr, int32_t per_pixel, int32_t *seg,
+                                  int32_t *pixel_idx, float *pixel_dist, int32_t cell_cap, int32_t *labels,
+                                  double *avgint, double *avgint_norm, int32_t *cell_idx, double *cell_dist,
+                                  int32_t *ident, int64_t *counts, int32_t *ncells_dev, int32_t *maxlab_host,
+                                  hrf_stream_t stream, hrf_stream_t side_stream, hrf_event_t pix_start,
+                                  hrf_event_t pix_end);
+HRF_API hrf_status hrf_tile_ecoli_cells(hrf_tile_ctx *ctx, const int32_t *seg, const double *lib,
+                                        const double *lib_flags, int32_t R, int32_t variant, double flag_thr,
+                                        int32_t cell_cap, int32_t *labels, double *avgint, double *avgint_norm,
+                                        int32_t *cell_idx, double *cell_dist, int32_t *ident, int64_t *counts,
+                                        int32_t *ncells_dev, hrf_stream_t stream);
+
 /* ==== a14-a16, a20, a21, a23: per-label reductions (stats.hip) ==========================
  * regionprops(seg, intensity_image=stack[:,:,k]).mean_intensity for all k in ONE pass
  * (ecoli :151-155, multispecies :167-171): sums[(maxlab+1)*C] f64, counts[maxlab+1];
@@ -404,6 +438,10 @@ HRF_API hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C
 HRF_API hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C,
                                              const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
                                              int32_t *best_idx, float *best_dist, hrf_stream_t stream);
+/* presence flags of the gated variants on the library path (no classifier bundle): out (N x nseg)
+ * f64, 1.0 where max(x[n, bounds[s]:bounds[s+1]]) > thr, else 0.0 (a NaN in the segment: 0.0) */
+HRF_API hrf_status hrf_segment_flags(const double *x, int64_t N, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                                     double thr, double *out, hrf_stream_t stream);
 /* per cell (f64): variant 0 ungated, 1 channel_cosine_intensity, 2 _7b_v2; fx (N x nseg),
  * fr (R x nseg) presence flags (needed for variants 1, 2) */
 HRF_API hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int32_t R, int32_t C,

@@ -91,9 +91,9 @@ def classify_cells(avgint_norm, library, bounds, variant=0, flag_thr=0.1):
     return O.classify(avgint_norm, library.astype(np.float64), bounds, variant, fx, fr)
 
 
-def process_tile(stack, library, bounds, calibration=None):
+def process_tile(stack, library, bounds, calibration=None, variant=0):
     seg, labs, avgint, avgint_norm = measure_ecoli(stack, calibration)
-    idx, dist = classify_cells(avgint_norm, library, bounds)
+    idx, dist = classify_cells(avgint_norm, library, bounds, variant)
     counts = O.barcode_counts(idx, library.shape[0])
     return dict(segmentation=seg, labels=labs, avgint=avgint, avgint_norm=avgint_norm, cell_idx=idx,
                 cell_dist=dist, counts=counts)

@@ -116,7 +116,7 @@ def test_fullsize_bench_workload(mods, orc, q):
         lasers = [quantised(l, q) for l in lasers]
     cal = S.flat_field(H, W, device="cuda")
     rt = P.register_tile(lasers)                  # bench.py's path: no materialised stack
-    res = P.process_tile(rt, lib, calibration=cal, per_pixel=True)
+    res = P.process_tile(rt, lib, calibration=cal, per_pixel=True, variant=1)   # bench.py's per-cell metric
     torch.cuda.synchronize()
     stats = K.seg_stats(rt.device, H, W)
     reg, cn = P.register_stack(lasers, want_cn=True)
@@ -130,7 +130,7 @@ def test_fullsize_bench_workload(mods, orc, q):
     del hl
     assert np.array_equal(host(reg), oreg)
     np.testing.assert_allclose(host(cn), np.log(np.sum(oreg.astype(np.float64), axis=2) + 1e-2), rtol=4e-16, atol=0)
-    o = OP.process_tile(oreg, ref, S.ECOLI_BOUNDS, calibration=host(cal))
+    o = OP.process_tile(oreg, ref, S.ECOLI_BOUNDS, calibration=host(cal), variant=1)
     seg = host(res.meas.segmentation)
     assert np.array_equal(seg, o["segmentation"])
     assert len(o["labels"]) > 500

@@ -408,6 +408,21 @@ def test_classify_cells_bitexact(K, orc, S, variant):
     ra, rd = orc.classify(x, ref, bounds, variant, fx if variant else None, fr if variant else None)
     assert np.array_equal(host(a), ra)
     assert np.array_equal(host(d), rd)
+    # the presence flags the library path computes on the device (hrf_segment_flags)
+    assert np.array_equal(host(K.segment_flags(dev(x), bounds, 0.1)), fx)
+    assert np.array_equal(host(K.segment_flags(dev(ref), bounds, 0.1)), fr)
+
+
+def test_segment_flags_edges(K):
+    """max over a segment > thr; a value equal to thr is not present; a NaN in the segment gives 0
+    (torch/numpy max propagate it and the comparison is false); an empty row set is fine"""
+    bounds = (0, 2, 5)
+    x = np.array([[0.1, 0.0, 0.2, 0.0, 0.0],
+                  [0.3, np.nan, 0.0, 0.0, 0.1],
+                  [0.0, 0.0, 0.0, 0.5, np.nan]])
+    want = np.array([[0.0, 1.0], [0.0, 0.0], [0.0, 0.0]])
+    assert np.array_equal(host(K.segment_flags(dev(x), bounds, 0.1)), want)
+    assert host(K.segment_flags(dev(np.zeros((0, 5))), bounds, 0.1)).shape == (0, 2)
 
 
 # ---- a22 adjacency -----------------------------------------------------------------------

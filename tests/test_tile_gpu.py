@@ -1,0 +1,147 @@
+"""One E. coli tile as one native call (hrf_tile_ecoli, tile.hip) against the composed path
+(pipeline.register_tile + process_tile), which the full-size tests check against the CPU
+restatement: label map, per-cell labels, barcodes, counts, identification map and per-pixel
+barcodes and distances bit for bit; per-cell spectra and distances within 1e-12 / 1e-9 (f64
+atomics in the label sums).  Reference: ecoli
+measurement.py:44-162 (-c T), image_classification.py:43-71, collect_measurement_results.py:92-98.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mods():
+    from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
+    return K, P, S
+
+
+def _lib(P, S):
+    ref = S.reference_library(10, S.ECOLI_BOUNDS)
+    return P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), S.ECOLI_BOUNDS, 10)
+
+
+def _lasers(S, H, W, seed, q=None):
+    lib_ref = S.reference_library(10, S.ECOLI_BOUNDS)
+    lay = S.cell_layout(H, W, S.default_ncells(H, W), lib_ref.shape[0], seed)
+    truth, prof = S.render_truth(H, W, lay, with_profile=True)
+    stack = S.render_stack(truth, lay, lib_ref, seed=seed, device="cuda", profile=prof)
+    lasers = S.laser_split(stack)
+    if q:
+        lasers = [(torch.round(l.double() * q) / q).float().contiguous() for l in lasers]
+    return lasers
+
+
+def _same(a, b):
+    return torch.equal(a, b)
+
+
+def _check(nat, ref, per_pixel=True):
+    """integer outputs bit for bit; the spectra within 1e-12 (label sums accumulate with f64
+    atomics, so their last bits depend on the order the flushes land in -- the tolerance every
+    label-sums test uses) and the per-cell distances with them"""
+    assert _same(nat.meas.segmentation, ref.meas.segmentation)
+    assert nat.meas.maxlab == ref.meas.maxlab
+    assert _same(nat.meas.labels, ref.meas.labels)
+    np.testing.assert_allclose(nat.meas.avgint.cpu().numpy(), ref.meas.avgint.cpu().numpy(), rtol=1e-12, atol=0)
+    np.testing.assert_allclose(nat.meas.avgint_norm.cpu().numpy(), ref.meas.avgint_norm.cpu().numpy(), rtol=1e-12,
+                               atol=0)
+    assert _same(nat.cell_idx, ref.cell_idx)
+    np.testing.assert_allclose(nat.cell_dist.cpu().numpy(), ref.cell_dist.cpu().numpy(), rtol=1e-9, atol=1e-12)
+    assert _same(nat.counts, ref.counts)
+    assert _same(nat.identification, ref.identification)
+    if per_pixel:
+        assert _same(nat.pixel_idx, ref.pixel_idx)
+        assert _same(nat.pixel_dist, ref.pixel_dist)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("calibrated", [False, True])
+def test_tile_native_equals_composed(mods, variant, calibrated):
+    K, P, S = mods
+    H = W = 512
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190107)
+    cal = S.flat_field(H, W, device="cuda") if calibrated else None
+    nat = P.process_tile_native(lasers, lib, calibration=cal, variant=variant)
+    ref = P.process_tile(P.register_tile(lasers), lib, calibration=cal, per_pixel=True, variant=variant)
+    torch.cuda.synchronize()
+    assert nat.ncells > 20
+    _check(nat, ref)
+
+
+def test_tile_native_no_overlap_no_pixels(mods):
+    K, P, S = mods
+    H = W = 256
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190108, q=4095)
+    cal = S.flat_field(H, W, device="cuda")
+    ref = P.process_tile(P.register_tile(lasers), lib, calibration=cal, per_pixel=True, variant=1)
+    a = P.process_tile_native(lasers, lib, calibration=cal, variant=1, overlap=False)
+    _check(a, ref)
+    b = P.process_tile_native(lasers, lib, calibration=cal, variant=1, per_pixel=False)
+    _check(b, ref, per_pixel=False)
+    assert b.pixel_idx is None
+
+
+def test_tile_native_cell_capacity_retry(mods):
+    """more labels than the per-cell buffers hold: the tail runs again through
+    hrf_tile_ecoli_cells with buffers sized for every label"""
+    K, P, S = mods
+    H = W = 512
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190109)
+    cal = S.flat_field(H, W, device="cuda")
+    key = (lasers[0].device, H, W)
+    K._CELL_CAP[key] = 8
+    try:
+        nat = P.process_tile_native(lasers, lib, calibration=cal, variant=1)
+        assert K._CELL_CAP[key] >= nat.meas.maxlab > 8
+    finally:
+        K._CELL_CAP.pop(key, None)
+    ref = P.process_tile(P.register_tile(lasers), lib, calibration=cal, per_pixel=True, variant=1)
+    _check(nat, ref)
+
+
+def test_tile_native_concurrent_streams(mods):
+    """two host threads, each with its own stream (and so its own tile context and side stream),
+    as bench.py drives them: equal to the isolated results"""
+    K, P, S = mods
+    H = W = 512
+    lib = _lib(P, S)
+    lib.refx()
+    lib.presence_flags()
+    tiles = [_lasers(S, H, W, 20190110 + i) for i in range(2)]
+    cal = S.flat_field(H, W, device="cuda")
+    want = [P.process_tile_native(t, lib, calibration=cal) for t in tiles]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in tiles]
+    got = [None, None]
+
+    def run(j):
+        with torch.cuda.stream(streams[j]):
+            for _ in range(3):
+                got[j] = P.process_tile_native(tiles[j], lib, calibration=cal)
+            streams[j].synchronize()
+    th = [threading.Thread(target=run, args=(j,)) for j in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    torch.cuda.synchronize()
+    for g, w in zip(got, want):
+        _check(g, w)
+
+
+def test_tile_native_rejects_bad_input(mods):
+    K, P, S = mods
+    lib = _lib(P, S)
+    lasers = _lasers(S, 256, 256, 20190111)
+    with pytest.raises(ValueError):
+        P.process_tile_native(lasers[:4], lib)
+    with pytest.raises(ValueError):
+        K.tile_ecoli(lasers, None, None, lib.spectra, None, variant=1, per_pixel=False)

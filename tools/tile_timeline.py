@@ -42,6 +42,6 @@ for i in range(4):
     torch.cuda.synchronize()
     torch.zeros(1, device="cuda").fill_(1.0)
     torch.cuda.synchronize()
-    stack, cn = P.register_stack(lasers, want_cn=True)
-    P.process_tile(stack, lib, calibration=cal, image_cn=cn, overlap=False)
+    rt = P.register_tile(lasers)                 # bench.py's path (pixel table, no stack)
+    P.process_tile(rt, lib, calibration=cal, overlap=False)
     torch.cuda.synchronize()
