@@ -1602,6 +1602,156 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *__res
   }
 }
 
+// library prep for the blocked kernel: refT = channel-major library (t[c * R + r]) and ny[r * S + s]
+// = the segment's sum of squares in channel order (seg_dist's ny, bit for bit)
+__global__ void cells_lib_prep_kernel(const double *__restrict__ a, int32_t R, int32_t C, Bounds bd,
+                                      double *__restrict__ t, double *__restrict__ ny) {
+  const int64_t n = (int64_t)R * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / C, c = e - r * C;
+    t[c * R + r] = a[e];
+  }
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)R * bd.nseg;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / bd.nseg;
+    const int sg = (int)(e - r * bd.nseg);
+    double v = 0;
+    for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+      const double y = a[r * C + i];
+      v += y * y;
+    }
+    ny[e] = v;
+  }
+}
+
+// classify_cells_kernel for CB cells per workgroup: each library value read from L2 feeds CB
+// cells, and only the dot products run per (cell, row) -- the segment norms are taken once, the
+// cells' in the workgroup (nx) and the library's by cells_lib_prep_kernel (ny), in seg_dist's
+// channel order, so every distance equals classify_cells_kernel's bit for bit.  Rows are visited
+// in increasing order per thread and ties go to the smaller row, as there.
+template <int CB, int NT>
+__global__ __launch_bounds__(NT) void classify_cells_blk_kernel(const double *__restrict__ X, int64_t N,
+                                                                 const double *__restrict__ refT,
+                                                                 const double *__restrict__ ny, int32_t R, int32_t C,
+                                                                 Bounds bd, int32_t variant,
+                                                                 const double *__restrict__ fx,
+                                                                 const double *__restrict__ fr,
+                                                                 int32_t *__restrict__ arg, double *__restrict__ dmin,
+                                                                 const int32_t *__restrict__ n_dev) {
+  extern __shared__ double xs[];  // CB x C
+  __shared__ double snx[CB][SMAX];
+  __shared__ double sfx[CB][SMAX];
+  __shared__ double sbest[NT];
+  __shared__ int sidx[NT];
+  const int tid = threadIdx.x;
+  const int S = bd.nseg;
+  const int64_t nmax = n_dev ? min(N, (int64_t)*n_dev) : N;
+  const int64_t n0 = (int64_t)blockIdx.x * CB;
+  if (n0 >= nmax) return;
+  const int nc = (int)min((int64_t)CB, nmax - n0);
+  for (int e = tid; e < CB * C; e += NT) {
+    const int j = e / C;
+    xs[e] = j < nc ? X[(n0 + j) * C + (e - j * C)] : 0.0;
+  }
+  __syncthreads();
+  if (tid < CB * S) {
+    const int j = tid / S, sg = tid - j * S;
+    double v = 0;
+    for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+      const double x = xs[j * C + i];
+      v += x * x;
+    }
+    snx[j][sg] = v;
+    sfx[j][sg] = (variant && j < nc) ? fx[(n0 + j) * S + sg] : 0.0;
+  }
+  __syncthreads();
+  double best[CB];
+  int bi[CB];
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    best[j] = __builtin_inf();
+    bi[j] = 0x7fffffff;
+  }
+  for (int r = tid; r < R; r += NT) {
+    double sd[CB][SMAX];
+    for (int sg = 0; sg < S; ++sg) {
+      double d[CB];
+#pragma unroll
+      for (int j = 0; j < CB; ++j) d[j] = 0;
+      // the segment's library values in batches of 8 independent loads (the L2 latency of one
+      // load per iteration otherwise serialises the walk), accumulated in channel order
+      const int lo = bd.b[sg], hi = bd.b[sg + 1];
+      for (int i0 = lo; i0 < hi; i0 += 8) {
+        double yv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) yv[u] = i0 + u < hi ? refT[(int64_t)(i0 + u) * R + r] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (i0 + u < hi)
+#pragma unroll
+            for (int j = 0; j < CB; ++j) d[j] += xs[j * C + i0 + u] * yv[u];
+      }
+      const double yy = ny[(int64_t)r * S + sg];
+#pragma unroll
+      for (int j = 0; j < CB; ++j) {
+        const double xx = snx[j][sg];
+        sd[j][sg] = (xx == 0.0 && yy == 0.0) ? 0.0 : ((xx == 0.0 || yy == 0.0) ? 1.0 : 1.0 - d[j] / sqrt(xx * yy));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      double dist;
+      if (variant == 0) {
+        double sum = 0;
+        for (int k = 0; k < S; ++k) sum += sd[j][k];
+        dist = sum / S;
+      } else {
+        double chk = 0;
+        for (int k = 0; k < S; ++k) chk += fabs(sfx[j][k] - fr[(int64_t)r * S + k]);
+        if (chk < 0.01) {
+          double sum = 0;
+          for (int k = 0; k < S; ++k) sum += sfx[j][k] == 0 ? 0.0 : sd[j][k];
+          dist = variant == 1 ? sum / S : 0.5 * sum / S;
+        } else if (variant == 2) {
+          dist = 1.0;
+        } else {
+          double sum = 0;
+          for (int k = 0; k < S; ++k) sum += sd[j][k];
+          dist = sum / S;
+        }
+      }
+      if (dist < best[j]) {
+        best[j] = dist;
+        bi[j] = r;
+      }
+    }
+  }
+  for (int j = 0; j < nc; ++j) {
+    sbest[tid] = best[j];
+    sidx[tid] = bi[j];
+    __syncthreads();
+    for (int o = NT / 2; o > 0; o >>= 1) {
+      if (tid < o) {
+        const double b2 = sbest[tid + o];
+        const int i2 = sidx[tid + o];
+        if (b2 < sbest[tid] || (b2 == sbest[tid] && i2 < sidx[tid])) {
+          sbest[tid] = b2;
+          sidx[tid] = i2;
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      arg[n0 + j] = sidx[0] == 0x7fffffff ? 0 : sidx[0];
+      dmin[n0 + j] = sbest[0];
+    }
+    __syncthreads();
+  }
+}
+
+constexpr int CELLS_CB = 4;    // cells per workgroup of the blocked kernel
+constexpr int CELLS_NT = 1024; // threads (library rows in flight) per workgroup
+
 int choose_ks(int K) {
   static const int ks[] = {8, 16, 18, 24, 32, 34, 40, 50, 56, 64};
   for (int v : ks)
@@ -1917,8 +2067,11 @@ namespace hrf {
 
 // the per-cell tail of hrf_tile_ecoli: row counts held on the device (nrows_dev <= nmax), no host
 // synchronisation; refT = the library transposed to channel-major (transpose_f64)
-hrf_status transpose_f64(const double *a, int32_t R, int32_t C, double *t, hipStream_t s) {
-  transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(a, R, C, t);
+hrf_status cells_lib_prep(const double *a, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg, double *t,
+                          double *ny, hipStream_t s) {
+  Bounds bd;
+  if (hrf_status st = make_bounds(bounds_host, nseg, C, &bd)) return st;
+  cells_lib_prep_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(a, R, C, bd, t, ny);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -1933,16 +2086,18 @@ hrf_status segment_flags_devn(const double *x, int64_t nmax, const int32_t *nrow
   return HRF_OK;
 }
 
-hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, const double *refT, int32_t R,
-                               int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
-                               const double *fr, int32_t *arg, double *dmin, hipStream_t s) {
+hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, const double *refT,
+                               const double *ny, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                               int32_t variant, const double *fx, const double *fr, int32_t *arg, double *dmin,
+                               hipStream_t s) {
   Bounds bd;
   if (hrf_status st = make_bounds(bounds_host, nseg, C, &bd)) return st;
   HRF_REQUIRE(variant >= 0 && variant <= 2, "classify_cells: variant must be 0, 1 or 2");
   HRF_REQUIRE(variant == 0 || (fx && fr), "classify_cells: gated variants need presence flags");
   if (nmax == 0) return HRF_OK;
-  classify_cells_kernel<<<(unsigned)nmax, 256, sizeof(double) * C, s>>>(x, nmax, refT, R, C, bd, variant, fx, fr, arg,
-                                                                         dmin, nrows_dev);
+  classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(nmax, CELLS_CB), CELLS_NT,
+                                                  sizeof(double) * CELLS_CB * C, s>>>(
+      x, nmax, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nrows_dev);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -1973,14 +2128,23 @@ hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int
   HRF_REQUIRE(R >= 1 && C >= 1, "classify_cells: bad sizes");
   if (N == 0) return HRF_OK;
   HRF_REQUIRE(x && ref && arg && dmin, "classify_cells: null buffer");
+  hipStream_t s = (hipStream_t)stream;
   double *refT = nullptr;
-  HRF_HIP(hipMallocAsync((void **)&refT, sizeof(double) * (size_t)R * C, (hipStream_t)stream));
-  transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, (hipStream_t)stream>>>(ref, R, C, refT);
+  HRF_HIP(hipMallocAsync((void **)&refT, sizeof(double) * (size_t)R * (C + bd.nseg), s));
+  double *ny = refT + (size_t)R * C;
+  static const bool per_cell = getenv("HRF_CELLS_PERCELL") != nullptr;  // A/B: one workgroup per cell
+  if (per_cell) {
+    transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(ref, R, C, refT);
+    classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, s>>>(x, N, refT, R, C, bd, variant, fx, fr, arg,
+                                                                       dmin, nullptr);
+  } else {
+    cells_lib_prep_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(ref, R, C, bd, refT, ny);
+    classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(N, CELLS_CB), CELLS_NT,
+                                                    sizeof(double) * CELLS_CB * C, s>>>(
+        x, N, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nullptr);
+  }
   HRF_LAUNCHED();
-  classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, (hipStream_t)stream>>>(x, N, refT, R, C, bd, variant,
-                                                                                       fx, fr, arg, dmin, nullptr);
-  HRF_LAUNCHED();
-  HRF_HIP(hipFreeAsync(refT, (hipStream_t)stream));
+  HRF_HIP(hipFreeAsync(refT, s));
   return HRF_OK;
 }
 

@@ -99,12 +99,14 @@ hrf_status kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32_t k1
                                           void *work, int64_t work_bytes, hipStream_t s, int32_t *err_pinned);
 
 // the per-cell tail with device-held row counts (classify.hip, stats.hip; used by tile.hip)
-hrf_status transpose_f64(const double *a, int32_t R, int32_t C, double *t, hipStream_t s);
+hrf_status cells_lib_prep(const double *a, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg, double *t,
+                          double *ny, hipStream_t s);
 hrf_status segment_flags_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, int32_t C,
                               const int32_t *bounds_host, int32_t nseg, double thr, double *out, hipStream_t s);
-hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, const double *refT, int32_t R,
-                               int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t variant, const double *fx,
-                               const double *fr, int32_t *arg, double *dmin, hipStream_t s);
+hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nrows_dev, const double *refT,
+                               const double *ny, int32_t R, int32_t C, const int32_t *bounds_host, int32_t nseg,
+                               int32_t variant, const double *fx, const double *fr, int32_t *arg, double *dmin,
+                               hipStream_t s);
 hrf_status barcode_counts_devn(const int32_t *bc, int64_t nmax, const int32_t *n_dev, int32_t R, int64_t *counts,
                                hipStream_t s);
 hrf_status paint_ids_devn(const int32_t *labels, int64_t n, const int32_t *code, int32_t nmax, const int32_t *ncell_dev,

@@ -55,7 +55,7 @@ struct hrf_tile_ctx {
   int32_t *rol = nullptr;
   double *fx = nullptr;         // cell presence flags (cap x NL)
   int32_t *nrows = nullptr;     // device row count
-  double *refT = nullptr;       // library, channel-major
+  double *refT = nullptr;       // library, channel-major, then its segment norms (R x 5)
   int64_t refT_cap = 0;
   hipEvent_t ev_reg = nullptr, ev_pix = nullptr;
   int32_t maxlab = 0;           // the last tile's, for hrf_tile_ecoli_cells
@@ -95,16 +95,17 @@ hrf_status tile_cells(hrf_tile_ctx *t, const int32_t *seg, const double *lib, co
   HRF_REQUIRE(variant == 0 || lib_flags, "tile_ecoli: the gated variants need the library's presence flags");
   HRF_TRY(hrf_cell_table(t->sums, t->counts, maxlab, C, maxlab, t->rol, labels, avgint, avgint_norm, ncells_dev, s));
   if (variant) HRF_TRY(hrf::segment_flags_devn(avgint_norm, maxlab, ncells_dev, C, BOUNDS, NL, flag_thr, t->fx, s));
-  if ((int64_t)R * C > t->refT_cap) {
+  if ((int64_t)R * (C + NL) > t->refT_cap) {
     HRF_HIP(hipStreamSynchronize(s));
     hipFree(t->refT);
     t->refT = nullptr;
     t->refT_cap = 0;
-    HRF_TRY(dalloc(&t->refT, (size_t)R * C));
-    t->refT_cap = (int64_t)R * C;
+    HRF_TRY(dalloc(&t->refT, (size_t)R * (C + NL)));
+    t->refT_cap = (int64_t)R * (C + NL);
   }
-  HRF_TRY(hrf::transpose_f64(lib, R, C, t->refT, s));
-  HRF_TRY(hrf::classify_cells_devn(avgint_norm, maxlab, ncells_dev, t->refT, R, C, BOUNDS, NL, variant,
+  double *ny = t->refT + (size_t)R * C;
+  HRF_TRY(hrf::cells_lib_prep(lib, R, C, BOUNDS, NL, t->refT, ny, s));
+  HRF_TRY(hrf::classify_cells_devn(avgint_norm, maxlab, ncells_dev, t->refT, ny, R, C, BOUNDS, NL, variant,
                                    variant ? t->fx : nullptr, variant ? lib_flags : nullptr, cell_idx, cell_dist, s));
   HRF_TRY(hrf::barcode_counts_devn(cell_idx, maxlab, ncells_dev, R, counts, s));              // collect :92-98
   HRF_TRY(hrf::paint_ids_devn(seg, t->H * t->W, cell_idx, maxlab, ncells_dev, 1, ident, s));   // :65-71

@@ -36,3 +36,11 @@ print("label_sums_lasers (cal)    %.4f ms" % ev(lambda: K.label_sums_lasers(lase
 pt = K.register_assemble_pixtable(lasers, shifts, True)[1]
 print("classify w16 (stack)       %.4f ms" % ev(lambda: K.classify_pixels(reg, refx, lib.R, lib.bounds)))
 print("classify w16t (table)      %.4f ms" % ev(lambda: K.classify_pixels_table(pt, refx, lib.R)))
+print("channel_max_multi          %.4f ms" % ev(lambda: K.channel_max_multi(lasers, stacked=True)))
+proj = K.channel_max_multi(lasers, stacked=True)
+print("xcorr shifts               %.4f ms" % ev(lambda: K.xcorr_shifts_dev(proj, 15)))
+cells = P.process_tile(pt and P.register_tile(lasers), lib, calibration=cal, per_pixel=False, variant=1)
+xn = cells.meas.avgint_norm
+fr = lib.presence_flags()
+fx = K.segment_flags(xn, lib.bounds)
+print("classify_cells (%d cells)  %.4f ms" % (xn.shape[0], ev(lambda: K.classify_cells(xn, lib.spectra, lib.bounds, 1, fx, fr))))
