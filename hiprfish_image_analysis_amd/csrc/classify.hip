@@ -2047,7 +2047,10 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
   auto go = [&](auto lay_tag) -> hrf_status {
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
-    const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
+    size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
+    // HRF_CLASSIFY_MAXWG = m < 3: at most m workgroups per CU (as launch_w16_lay)
+    static const int maxwg = getenv("HRF_CLASSIFY_MAXWG") ? atoi(getenv("HRF_CLASSIFY_MAXWG")) : 0;
+    if (maxwg > 0 && maxwg < 3) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
     (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,

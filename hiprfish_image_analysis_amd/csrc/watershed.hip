@@ -30,6 +30,7 @@
 // One departure from skimage remains, reported in ties_host[2]: when two competing strings
 // are equal down to markers of the same value, skimage's choice depends on where its binary
 // heap happens to hold the two age-0 items; here the marker with the smaller raster index wins.
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -106,6 +107,10 @@ __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_
 // neighbours can swap stale labels forever.  RELABEL = true: keys are final; a pixel with a resolved
 // parent copies its label, any other takes the least non-zero label of its candidates (0 =
 // not yet reached, so labels flow out of the markers again after a reset).
+// The pass walks the tiles persistently: a resident grid of workgroups takes tiles t = blockIdx.x,
+// + gridDim.x, ... (ntx x nty tiles), so a pass costs a resident grid's dispatches instead of one
+// per tile -- most tiles are skipped after the first passes, and under the concurrent classifier
+// every dispatch waits for a CU's LDS.
 template <bool RELABEL>
 __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__ f, int negate,
                                                       const int32_t *__restrict__ markers,
@@ -115,29 +120,31 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
                                                       const int32_t *__restrict__ prev_tile,
                                                       int32_t *__restrict__ cur_tile,
                                                       int32_t *__restrict__ next_tile,
-                                                      const int32_t *__restrict__ tile_work) {
+                                                      const int32_t *__restrict__ tile_work, int ntx, int nty) {
   __shared__ double sl[WL * WL];
   __shared__ int32_t sh[WL * WL];
   __shared__ int32_t sd[WL * WL];
   __shared__ int32_t sb[WL * WL];
   __shared__ uint8_t sm[WL * WL];
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.y * WT - 1, c0 = (int64_t)blockIdx.x * WT - 1;
+  for (int tile = blockIdx.x; tile < ntx * nty; tile += gridDim.x) {
+  const int bx = tile % ntx, by = tile / ntx;
+  const int64_t r0 = (int64_t)by * WT - 1, c0 = (int64_t)bx * WT - 1;
   // Tile flags rotate through three generations: this pass reads prev, sets cur, and clears
   // next for the following pass (last read as prev by the pass before this one, which has
   // finished), so no memset is needed between passes.
-  if (tid == 0) next_tile[blockIdx.y * gridDim.x + blockIdx.x] = 0;
-  if (!tile_work[blockIdx.y * gridDim.x + blockIdx.x]) return;  // nothing relaxable: state fixed
+  if (tid == 0) next_tile[tile] = 0;
+  if (!tile_work[tile]) continue;  // nothing relaxable: state fixed
   // A tile whose 3x3 tile neighbourhood did not change in the previous pass is skipped: its
   // own state did not change either, so both ping-pong buffers already hold it.
   if (prev_tile) {
     int act = 0;
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
-        const int ty = (int)blockIdx.y + dy, tx = (int)blockIdx.x + dx;
-        if (ty >= 0 && ty < (int)gridDim.y && tx >= 0 && tx < (int)gridDim.x) act |= prev_tile[ty * gridDim.x + tx];
+        const int ty = by + dy, tx = bx + dx;
+        if (ty >= 0 && ty < nty && tx >= 0 && tx < ntx) act |= prev_tile[ty * ntx + tx];
       }
-    if (!act) return;
+    if (!act) continue;
   }
   for (int idx = tid; idx < WL * WL; idx += 256) {
     const int lr = idx / WL, lc = idx - lr * WL;
@@ -282,7 +289,8 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   }
   if (__syncthreads_or(any_change) && tid == 0) {
     *changed = 1;
-    cur_tile[blockIdx.y * gridDim.x + blockIdx.x] = 1;
+    cur_tile[tile] = 1;
+  }
   }
 }
 
@@ -409,6 +417,15 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 8, s));
   int passes = 0;
   static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
+  // persistent pass grids (HRF_WS_TILEGRID=1: one workgroup per tile, as before)
+  static const bool tilegrid = getenv("HRF_WS_TILEGRID") != nullptr;
+  static const int gcap = getenv("HRF_WS_GRID") ? atoi(getenv("HRF_WS_GRID")) : 0;
+  unsigned pgrid_t = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
+  unsigned pgrid_f = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
+  if (gcap > 0) {
+    pgrid_t = std::min<unsigned>(pgrid_t, (unsigned)gcap);
+    pgrid_f = std::min<unsigned>(pgrid_f, (unsigned)gcap);
+  }
 
   // Passes run in batches with one host read per batch (change flag + contest count): the
   // first batch of 8 covers the typical tile (~7 passes) with a single synchronisation, later
@@ -424,11 +441,11 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
         int32_t *next = tf + ((local + 1) % 3) * ntiles;
         int32_t *chg = flag_ws + (k == batch - 1 ? 0 : 1);
         if (relabel)
-          ws_pass_kernel<true><<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev, cur,
-                                                    next, B.tw);
+          ws_pass_kernel<true><<<pgrid_t, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
+                                                       cur, next, B.tw, (int)grid.x, (int)grid.y);
         else
-          ws_pass_kernel<false><<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev, cur,
-                                                     next, B.tw);
+          ws_pass_kernel<false><<<pgrid_f, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
+                                                        cur, next, B.tw, (int)grid.x, (int)grid.y);
         WsState t = a;
         a = b;
         b = t;
