@@ -419,13 +419,8 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
   // persistent pass grids (HRF_WS_TILEGRID=1: one workgroup per tile, as before)
   static const bool tilegrid = getenv("HRF_WS_TILEGRID") != nullptr;
-  static const int gcap = getenv("HRF_WS_GRID") ? atoi(getenv("HRF_WS_GRID")) : 0;
-  unsigned pgrid_t = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
-  unsigned pgrid_f = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
-  if (gcap > 0) {
-    pgrid_t = std::min<unsigned>(pgrid_t, (unsigned)gcap);
-    pgrid_f = std::min<unsigned>(pgrid_f, (unsigned)gcap);
-  }
+  const unsigned pgrid_t = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
+  const unsigned pgrid_f = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
 
   // Passes run in batches with one host read per batch (change flag + contest count): the
   // first batch of 8 covers the typical tile (~7 passes) with a single synchronisation, later
