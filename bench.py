@@ -63,6 +63,14 @@ NL_OPS_PER_PIXEL = 264 * 20    # skimage fast NL-means: 264 shift pairs per pixe
 E3_OPS_PER_VOXEL = 72 * 24 + 73 + 450 + 10   # 72 profiles of 11 taps (min/max/norm), mean, percentile sort
 
 
+def _progress(msg):
+    """a progress line on stderr (long runs keep writing; stdout carries only the JSON line)"""
+    print("[bench %.0fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def _cpu_info():
     model = None
     try:
@@ -123,6 +131,7 @@ def _cpu_baseline(ref, bounds):
     lay = S.cell_layout(hs, hs, S.default_ncells(hs, hs), ref.shape[0], seed=99)
     truth, prof = S.render_truth(hs, hs, lay, with_profile=True)
     st = S.render_stack(truth, lay, ref, seed=99, device="cpu", profile=prof).numpy()
+    _progress("cpu baseline: one process on a 2048x2048 tile")
     t0 = time.perf_counter()
     OP.process_tile(st, ref, bounds, variant=1)
     t_seg = (time.perf_counter() - t0) / (hs * hs)
@@ -136,10 +145,14 @@ def _cpu_baseline(ref, bounds):
     nw = max(1, min(nproc or 1, 16))
     ctx = mp.get_context("spawn")          # fresh interpreters: no GPU state crosses
     barrier, q = ctx.Barrier(nw), ctx.Queue()
+    _progress("cpu baseline: %d concurrent processes" % nw)
     procs = [ctx.Process(target=_cpu_worker, args=(1000 + i, 1024, 1 << 14, barrier, q)) for i in range(nw)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=600) for _ in procs]
+    res = []
+    for i in range(len(procs)):
+        res.append(q.get(timeout=600))
+        _progress("cpu baseline: %d of %d processes done" % (i + 1, len(procs)))
     for p in procs:
         p.join(timeout=60)
     agg = round(sum(1e-6 / (a + b) for a, b in res), 4)
@@ -224,6 +237,35 @@ def _hbm_kernels(dev):
     return out
 
 
+def _watershed_ties(dev, n=512):
+    """The watershed's tie path on an adversarial n x n image: a plateau-heavy integer image (4
+    levels in 4x4 blocks, multi-pixel markers with distinct values per label, 10 % of pixels outside
+    the mask) forces contests that the resolver decides exactly; the same markers on a continuous
+    image have none.  Mean time of hrf_watershed_ex (HIP events) and the tie statistics of each.
+    (The bench tiles -- continuous, k/4095, k/255 -- have no contest; see the quantised lines.)"""
+    import torch
+
+    from hiprfish_image_analysis_amd import kernels as K
+    rng = np.random.default_rng(7)
+    f = np.kron(rng.integers(0, 4, (n // 4, n // 4)), np.ones((4, 4))).astype(np.float64)
+    markers = np.zeros((n, n), np.int32)
+    for lab in range(1, n * n // 300 + 1):
+        r, c = rng.integers(1, n - 1), rng.integers(1, n - 1)
+        markers[r - 1:r + 2, c - 1:c + 2] = lab
+    f = f + 1e-3 * markers
+    mask = rng.random((n, n)) < 0.9
+    mk, mm = torch.from_numpy(markers).to(dev), torch.from_numpy(mask).to(dev)
+    out = {"size": [n, n]}
+    for name, img in (("plateaus", f), ("continuous", f + rng.random((n, n)))):
+        x = torch.from_numpy(img).to(dev)
+        ties = []
+        K.watershed(x, mk, mm, ties=ties)
+        ms = _event_ms(lambda: K.watershed(x, mk, mm), 3)
+        out[name] = {"ms": round(ms, 3), "contested_px": int(ties[0]), "resolution_rounds": int(ties[1]),
+                     "equal_marker_decisions": int(ties[2])}
+    return out
+
+
 def _extras(dev, T, streams, pool, tiles, lib_main):
     """BASELINE.json configs 3 (the other classifier settings), 2 and 4 on this GPU (inputs
     resident, synthetic data)."""
@@ -264,33 +306,38 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                          "steps": steps, "concurrent": T, "classifier_mode": 2,
                                          "note": "round 1's timed path (BENCH_r01.json 1044.5)"}
     del pre
-    # the headline path on bioformats-like samples (k/4095, as load_image returns 12-bit data):
-    # same timed work, plus the watershed's tie statistics of every tile (DESIGN.md "Watershed")
-    qtiles = [([(torch.round(l.double() * 4095.0) / 4095.0).float().contiguous() for l in t[0]], t[1])
-              for t in tiles]
-    torch.cuda.synchronize()
-    wstats = []
+    # the headline path on bioformats-like samples (k/4095, as load_image returns 12-bit data, and
+    # k/255 for 8-bit data): same timed work, plus the watershed's tie statistics of every tile
+    # (DESIGN.md "Watershed")
+    for q in (4095, 255):
+      qtiles = [([(torch.round(l.double() * float(q)) / float(q)).float().contiguous() for l in t[0]], t[1])
+                for t in tiles]
+      torch.cuda.synchronize()
+      wstats = []
 
-    def qjob(t):
-        if NATIVE:
-            r = P.process_tile_native(t[0], lib_main, calibration=t[1], variant=1)
-            wstats.append(K.tile_stats(t[0][0].device, H, W))
-            return r
-        rt = P.register_tile(t[0])
-        r = P.process_tile(rt, lib_main, calibration=t[1], variant=1)
-        wstats.append(K.seg_stats(rt.device, H, W))
-        return r
-    sec = _timed_tiles(qjob, qtiles, T, streams, pool, steps, 2)
-    del qtiles
-    cfg3["quantised_4095"] = {"value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
-                              "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T,
-                              "tiles_run": len(wstats),
-                              "watershed_passes_mean": round(float(np.mean([s["passes"] for s in wstats])), 2),
-                              "contested_px_per_tile_mean": round(float(np.mean([s["contests"] for s in wstats])), 2),
-                              "contested_px_per_tile_max": int(max(s["contests"] for s in wstats)),
-                              "resolution_rounds_max": int(max(s["rounds"] for s in wstats)),
-                              "equal_marker_decisions_total": int(sum(s["marker_ties"] for s in wstats))}
+      def qjob(t, wstats=wstats):
+          if NATIVE:
+              r = P.process_tile_native(t[0], lib_main, calibration=t[1], variant=1)
+              wstats.append(K.tile_stats(t[0][0].device, H, W))
+              return r
+          rt = P.register_tile(t[0])
+          r = P.process_tile(rt, lib_main, calibration=t[1], variant=1)
+          wstats.append(K.seg_stats(rt.device, H, W))
+          return r
+      sec = _timed_tiles(qjob, qtiles, T, streams, pool, steps, 2)
+      del qtiles
+      cfg3["quantised_%d" % q] = {
+          "value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
+          "ms_per_step": round(sec / steps * 1e3, 3), "steps": steps, "concurrent": T, "tiles_run": len(wstats),
+          "watershed_passes_mean": round(float(np.mean([s["passes"] for s in wstats])), 2),
+          "contested_px_per_tile_mean": round(float(np.mean([s["contests"] for s in wstats])), 2),
+          "contested_px_per_tile_max": int(max(s["contests"] for s in wstats)),
+          "resolution_rounds_max": int(max(s["rounds"] for s in wstats)),
+          "equal_marker_decisions_total": int(sum(s["marker_ties"] for s in wstats))}
+    _progress("extras: quantised lines done")
+    cfg3["watershed_tie_path"] = _watershed_ties(dev)
     out["cfg3"] = cfg3
+    _progress("extras: cfg3 variants done")
     # cfg2: synthetic-community tiles
     b = S.MULTI_BOUNDS
     ref = S.reference_library(7, b)
@@ -312,6 +359,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                 "algorithmic_ops_per_pixel": NL_OPS_PER_PIXEL, "achieved": round(ach, 3),
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s", "frac": round(ach / F64_VALU_PEAK_TOPS, 4)}}
     del ctiles, s, norm
+    _progress("extras: cfg2 done")
     # cfg4: the biofilm volume chain from a 1024x1024x64x63 stack
     X, Y, Z, CV = 1024, 1024, 64, 63
     g = torch.Generator(device=dev)
@@ -332,6 +380,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                 "algorithmic_ops_per_voxel": E3_OPS_PER_VOXEL, "achieved": round(ach3, 3),
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s",
                                 "frac": round(ach3 / F64_VALU_PEAK_TOPS, 4)}}
+    _progress("extras: cfg4 done")
     out["hbm_kernels"] = _hbm_kernels(dev)
     return out
 
@@ -491,6 +540,8 @@ def main():
             counts = counts + a
         return outs[-1][0], counts
 
+    if rank == 0:
+        _progress("%d tiles resident; warm-up" % len(tiles))
     run(0, args.warmup, False)
     if world > 1:
         dist.barrier()
@@ -519,6 +570,8 @@ def main():
 
     pixels = H * W * args.steps * world * T
     value = pixels / elapsed / 1e6
+    if rank == 0:
+        _progress("timed region: %.1f Mpixel-spectra/s" % value)
     out = {
         "metric": "Mpixel-spectra/s (segment+classify) on 2048²×95 vs 1023 refs; 1/2/4/8 GPU",
         "value": round(value, 3), "unit": "Mpixel-spectra/s", "n_gpus": world, "steps": args.steps,

@@ -55,7 +55,8 @@ def test_bench_two_ranks_counts(tmp_path):
         lay = S.cell_layout(bench.H, bench.W, S.default_ncells(bench.H, bench.W), lib.R, seed)
         truth, prof = S.render_truth(bench.H, bench.W, lay, with_profile=True)
         stack = S.render_stack(truth, lay, ref, seed=seed, profile=prof)
-        res = P.process_tile(P.register_stack(S.laser_split(stack)), lib, calibration=cal)
+        # bench.py's per-cell metric: the gated channel_cosine_intensity (variant 1)
+        res = P.process_tile(P.register_stack(S.laser_split(stack)), lib, calibration=cal, variant=1)
         c = res.counts.cpu().numpy()
         want = c if want is None else want + c
     assert got.sum() > 1000
