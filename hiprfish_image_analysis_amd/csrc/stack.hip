@@ -218,6 +218,9 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
   if constexpr (q + 1 < NL) lay_store<q + 1, NL>(tile, tid, v + U);
 }
 
+// Strips t = blockIdx.x, + gridDim.x, ... (row t / nsx, columns (t % nsx) * 64 ..): launched on a
+// resident grid (round 3), a 2048^2 tile is ~1.5 k workgroup dispatches instead of 65 k -- under
+// the concurrent classifier every dispatch waits for a CU slot.  Per strip unchanged.
 __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
@@ -226,10 +229,13 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
   __shared__ __attribute__((aligned(16))) float tile[AS_P * C];
   __shared__ uint8_t okp[AS_P];
   __shared__ int sdr[LMAX], sdc[LMAX];
+  __shared__ uint32_t fl[AS_P];
   load_shifts(L, sdr, sdc);
   const int tid = threadIdx.x;
-  const int64_t r = blockIdx.y;
-  const int64_t c0 = (int64_t)blockIdx.x * AS_P;
+  const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
+  for (int64_t t = blockIdx.x; t < nstrip; t += gridDim.x) {
+  const int64_t r = t / nsx;
+  const int64_t c0 = (t - r * nsx) * AS_P;
   const int np = (int)min((int64_t)AS_P, W - c0);
   if (tid < AS_P) {
     bool ok = tid < np;
@@ -288,10 +294,18 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
     }
   }
   if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
-    __shared__ uint32_t fl[AS_P];
     __syncthreads();
     hrf_pix::prep_tile_ecoli(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl);
   }
+  __syncthreads();  // the next strip rewrites tile, okp and fl
+  }
+}
+
+// workgroups of the E. coli assembly: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one per strip)
+unsigned assemble_grid(int64_t W, int64_t H) {
+  const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
+  static const bool per_strip = getenv("HRF_ASSEMBLE_STRIPGRID") != nullptr;
+  return per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel, 256, 0, nstrip);
 }
 
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
@@ -846,7 +860,8 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
     for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
     if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
-      assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, nullptr,
+      assemble_ecoli_kernel<<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
+                                                                                 cn_mode, nullptr,
                                                                    nullptr);
       HRF_LAUNCHED();
       return HRF_OK;
@@ -917,9 +932,8 @@ hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const in
               "register_assemble_pixtable: the five E. coli lasers and W a multiple of 16");
   HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && table && flags, "register_assemble_pixtable: null output");
   HRF_REQUIRE(!dst || ((uintptr_t)dst & 15) == 0, "register_assemble_pixtable: dst must be 16-byte aligned");
-  dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
-  assemble_ecoli_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out, cn_mode,
-                                                               (uint4 *)table, flags);
+  assemble_ecoli_kernel<<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
+                                                                               cn_mode, (uint4 *)table, flags);
   HRF_LAUNCHED();
   return HRF_OK;
 }
