@@ -28,6 +28,8 @@
 #include <tuple>
 #include <vector>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace {
@@ -138,12 +140,16 @@ __device__ __forceinline__ void lds_fft(double2 *buf, const double2 *__restrict_
 }
 
 // 1. forward rows: image img, row y -> spec[(img * H + y) * P + k], k <= M = W / 2 (P = M + 1)
+// The row and column passes walk their rows / tiles on a resident grid (round 3: ~1-2 k workgroup
+// dispatches per pass instead of ~10 k; under the concurrent classifier each dispatch waits for a
+// CU slot).  nrows = all (img, y) rows of the pass.
 template <int LGM>
 __global__ __launch_bounds__(XT) void xc_row_fwd_kernel(const double *__restrict__ imgs, int64_t H,
-                                                        double2 *__restrict__ spec, const double2 *__restrict__ twW) {
+                                                        double2 *__restrict__ spec, const double2 *__restrict__ twW,
+                                                        int64_t nrows) {
   constexpr int M = 1 << LGM, P = M + 1;
   __shared__ double2 buf[M];
-  const int64_t row = blockIdx.x;  // img * H + y
+  for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {  // img * H + y
   const double2 *src = reinterpret_cast<const double2 *>(imgs + row * 2 * M);
   for (int n = threadIdx.x; n < M; n += XT) buf[n] = src[n];
   __syncthreads();
@@ -155,6 +161,8 @@ __global__ __launch_bounds__(XT) void xc_row_fwd_kernel(const double *__restrict
     const double2 d = make_double2(0.5 * (zk.x - zc.x), 0.5 * (zk.y - zc.y));
     const double2 od = make_double2(d.y, -d.x);  // -i d
     dst[k] = cadd(e, cmul(twW[k], od));
+  }
+  __syncthreads();
   }
 }
 
@@ -182,12 +190,14 @@ constexpr int lg2c(int n) { return n <= 1 ? 0 : 1 + lg2c(n / 2); }
 // tile blockIdx.x; rows n2 + H2 * i, i < H1
 template <int LGH1, int LGH2, bool INV>
 __global__ __launch_bounds__(XT) void xc_col_a_kernel(double2 *__restrict__ spec, int img0, int P,
-                                                      const double2 *__restrict__ twH) {
+                                                      const double2 *__restrict__ twH, int ta, int nimgs) {
   constexpr int H1 = 1 << LGH1, H2 = 1 << LGH2;
   constexpr int64_t H = (int64_t)H1 * H2;
   __shared__ double2 buf[H1 * TCA];
-  const int n2 = blockIdx.y, c0 = blockIdx.x * TCA;
-  double2 *img = spec + (int64_t)(img0 + blockIdx.z) * H * P;
+  for (int64_t job = blockIdx.x; job < (int64_t)ta * H2 * nimgs; job += gridDim.x) {  // (img, n2, tile)
+  const int tx = (int)(job % ta), n2 = (int)((job / ta) % H2), iz = (int)(job / ((int64_t)ta * H2));
+  const int c0 = tx * TCA;
+  double2 *img = spec + (int64_t)(img0 + iz) * H * P;
   tile_load<TCA>(img, P, n2, H2, H1, c0, buf);
   __syncthreads();
   if (INV) {  // conj twiddle on element k1, then the inverse DFT over k1
@@ -200,6 +210,8 @@ __global__ __launch_bounds__(XT) void xc_col_a_kernel(double2 *__restrict__ spec
     __syncthreads();
   }
   tile_store<TCA>(img, P, n2, H2, H1, c0, buf);
+  __syncthreads();
+  }
 }
 
 // 3. column pass B + product + inverse pass B: k1 = blockIdx.y, tile blockIdx.x; rows H2 k1 + n2
@@ -241,13 +253,14 @@ struct RowBest {
 template <int LGM>
 __global__ __launch_bounds__(XT) void xc_row_inv_kernel(const double2 *__restrict__ spec, int64_t H,
                                                         const double2 *__restrict__ twW, RowBest *__restrict__ rowbest,
-                                                        double *__restrict__ cc_out) {
+                                                        double *__restrict__ cc_out, int64_t nrows) {
   constexpr int M = 1 << LGM, P = M + 1;
   __shared__ double2 buf[M];
   __shared__ double rv[XT / 64];
   __shared__ int rc[XT / 64];
-  const int t = 1 + blockIdx.y;
-  const int64_t y = blockIdx.x;
+  for (int64_t job = blockIdx.x; job < nrows; job += gridDim.x) {  // (target - 1) * H + y
+  const int64_t ti = job / H, y = job - ti * H;
+  const int t = 1 + (int)ti;
   const double2 *X = spec + ((int64_t)t * H + y) * P;
   for (int k = threadIdx.x; k < M; k += XT) {
     const double2 xk = X[k], xc = conj2(X[M - k]);
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(XT) void xc_row_inv_kernel(const double2 *__restric
   __syncthreads();
   lds_fft<LGM, 0, true>(buf, twW, 2);
   if (cc_out) {  // the correlation surface itself (tests): H * W / 2 times numpy.fft.ifft2
-    double2 *o = reinterpret_cast<double2 *>(cc_out + ((int64_t)blockIdx.y * H + y) * 2 * M);
+    double2 *o = reinterpret_cast<double2 *>(cc_out + (ti * H + y) * 2 * M);
     for (int n = threadIdx.x; n < M; n += XT) o[n] = buf[n];
   }
   double bv = -1.0;
@@ -296,7 +309,9 @@ __global__ __launch_bounds__(XT) void xc_row_inv_kernel(const double2 *__restric
         bv = rv[q];
         bc = rc[q];
       }
-    rowbest[(int64_t)blockIdx.y * H + y] = RowBest{bv, bc, 0};
+    rowbest[ti * H + y] = RowBest{bv, bc, 0};
+  }
+  __syncthreads();
   }
 }
 
@@ -346,6 +361,13 @@ __global__ __launch_bounds__(XT) void xc_shifts_kernel(const RowBest *__restrict
     shift[2 * (1 + blockIdx.x) + 1] = (int32_t)c;
     if (blockIdx.x == 0) shift[0] = shift[1] = 0;
   }
+}
+
+// a resident grid for the walking passes (HRF_XCORR_FULLGRID=1: one workgroup per job, as before)
+template <class Kern>
+unsigned xgrid(Kern k, int64_t njobs) {
+  static const bool full = getenv("HRF_XCORR_FULLGRID") != nullptr;
+  return full ? (unsigned)njobs : hrf::resident_grid(k, XT, 0, njobs);
 }
 
 int ilog2(int64_t n) {
@@ -413,7 +435,7 @@ static hrf_status xcorr_run(const double *imgs, int32_t nimg, int64_t H, int64_t
   switch (lgM) {
 #define HRF_XR(L)                                                                                        \
   case L:                                                                                                \
-    xc_row_fwd_kernel<L><<<(unsigned)(nimg * H), XT, 0, s>>>(imgs, H, spec, twW);                         \
+    xc_row_fwd_kernel<L><<<xgrid(xc_row_fwd_kernel<L>, nimg * H), XT, 0, s>>>(imgs, H, spec, twW, nimg * H); \
     break;
     HRF_XR(1) HRF_XR(2) HRF_XR(3) HRF_XR(4) HRF_XR(5) HRF_XR(6) HRF_XR(7) HRF_XR(8) HRF_XR(9) HRF_XR(10) HRF_XR(11)
 #undef HRF_XR
@@ -423,9 +445,11 @@ static hrf_status xcorr_run(const double *imgs, int32_t nimg, int64_t H, int64_t
 #define HRF_XC(LH)                                                                                        \
   case LH: {                                                                                              \
     constexpr int L1 = LH / 2, L2 = LH - LH / 2;                                                          \
-    xc_col_a_kernel<L1, L2, false><<<dim3(ta, 1u << L2, (unsigned)nimg), XT, 0, s>>>(spec, 0, P, twH);    \
+    xc_col_a_kernel<L1, L2, false><<<xgrid(xc_col_a_kernel<L1, L2, false>, (int64_t)ta * (1 << L2) * nimg), XT, 0, \
+                                     s>>>(spec, 0, P, twH, (int)ta, nimg);                                  \
     xc_col_b_kernel<L1, L2><<<dim3(tb, 1u << L1), XT, 0, s>>>(spec, nimg, P, twH);                        \
-    xc_col_a_kernel<L1, L2, true><<<dim3(ta, 1u << L2, (unsigned)(nimg - 1)), XT, 0, s>>>(spec, 1, P, twH); \
+    xc_col_a_kernel<L1, L2, true><<<xgrid(xc_col_a_kernel<L1, L2, true>, (int64_t)ta * (1 << L2) * (nimg - 1)),   \
+                                    XT, 0, s>>>(spec, 1, P, twH, (int)ta, nimg - 1);                       \
     break;                                                                                                \
   }
     HRF_XC(4) HRF_XC(5) HRF_XC(6) HRF_XC(7) HRF_XC(8) HRF_XC(9) HRF_XC(10) HRF_XC(11) HRF_XC(12)
@@ -434,7 +458,8 @@ static hrf_status xcorr_run(const double *imgs, int32_t nimg, int64_t H, int64_t
   switch (lgM) {
 #define HRF_XI(L)                                                                                           \
   case L:                                                                                                   \
-    xc_row_inv_kernel<L><<<dim3((unsigned)H, (unsigned)(nimg - 1)), XT, 0, s>>>(spec, H, twW, rowbest, cc_out); \
+    xc_row_inv_kernel<L><<<xgrid(xc_row_inv_kernel<L>, (nimg - 1) * H), XT, 0, s>>>(spec, H, twW, rowbest, cc_out, \
+                                                                                (nimg - 1) * H);           \
     break;
     HRF_XI(1) HRF_XI(2) HRF_XI(3) HRF_XI(4) HRF_XI(5) HRF_XI(6) HRF_XI(7) HRF_XI(8) HRF_XI(9) HRF_XI(10) HRF_XI(11)
 #undef HRF_XI
