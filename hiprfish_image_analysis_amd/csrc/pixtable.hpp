@@ -119,6 +119,12 @@ __device__ __forceinline__ void prep_tile(float *tile, const uint8_t *ok, int np
 // a segment group, lane = pixel: segments 0 | 1 | 2 | 3 + 4, at most 32 channels per wave instead
 // of 95 per lane): the assembly kernel calls this on its strip.  Same arithmetic per segment (the
 // segments' sums are independent), so the table is bit-identical to prep_tile's.
+// workgroup barrier ordering LDS only (s_barrier after the LDS counter drains): unlike
+// __syncthreads it does not wait for the wave's global loads, so loads issued before it stay in
+// flight across it (the E. coli assembly prefetches its next strip that way)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool LDSB = false>
 __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, int np, int64_t p0,
                                                 uint4 *__restrict__ table, uint8_t *__restrict__ flags,
                                                 uint32_t *fl /* LDS, 64 words */) {
@@ -126,7 +132,8 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
   constexpr int C = L::C, KT = lay_kt<L>();
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   if (tid < 64) fl[tid] = 0;
-  __syncthreads();
+  if (LDSB) lds_barrier();
+  else __syncthreads();
   auto seg = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (lane >= np) return;
@@ -165,7 +172,8 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
     seg(std::integral_constant<int, 3>{});
     seg(std::integral_constant<int, 4>{});
   }
-  __syncthreads();
+  if (LDSB) lds_barrier();
+  else __syncthreads();
   if (tid < np) flags[p0 + tid] = (uint8_t)fl[tid];
   const int ne = (np + 15) / 16 * KT * 2 * 64;
   for (int e = tid; e < ne; e += 256) {

@@ -221,6 +221,9 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 // Strips t = blockIdx.x, + gridDim.x, ... (row t / nsx, columns (t % nsx) * 64 ..): launched on a
 // resident grid (round 3), a 2048^2 tile is ~1.5 k workgroup dispatches instead of 65 k -- under
 // the concurrent classifier every dispatch waits for a CU slot.  Per strip unchanged.
+// PF: the next strip's loads are issued right after this strip is staged in LDS and stay in flight
+// through its image_cn and pixel-table phases (barriers there order LDS only, lds_barrier).
+template <bool PF>
 __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
@@ -233,6 +236,9 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
   load_shifts(L, sdr, sdc);
   const int tid = threadIdx.x;
   const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
+  constexpr int UT = 8 + 6 + 5 + 4 + 2;
+  float v[UT];
+  if (PF && (int64_t)blockIdx.x < nstrip) lay_load<0, 5>(L, sdr, sdc, blockIdx.x / nsx, (blockIdx.x % nsx) * AS_P, H, W, tid, v);
   for (int64_t t = blockIdx.x; t < nstrip; t += gridDim.x) {
   const int64_t r = t / nsx;
   const int64_t c0 = (t - r * nsx) * AS_P;
@@ -243,11 +249,15 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
       for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, sdr[q], sdc[q]);
     okp[tid] = (uint8_t)ok;
   }
-  constexpr int UT = 8 + 6 + 5 + 4 + 2;
-  float v[UT];
-  lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
+  if (!PF) lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
   lay_store<0, 5>(tile, tid, v);
-  __syncthreads();
+  if (PF) {
+    hrf_pix::lds_barrier();
+    const int64_t tn = t + gridDim.x;  // the next strip's loads: in flight until its lay_store
+    if (tn < nstrip) lay_load<0, 5>(L, sdr, sdc, tn / nsx, (tn % nsx) * AS_P, H, W, tid, v);
+  } else {
+    __syncthreads();
+  }
   float *out = dst ? dst + (r * W + c0) * (int64_t)C : nullptr;
   const int n = dst ? np * C : 0;
   if (!dst) {
@@ -294,10 +304,12 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
     }
   }
   if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
-    __syncthreads();
-    hrf_pix::prep_tile_ecoli(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl);
+    if (PF) hrf_pix::lds_barrier();
+    else __syncthreads();
+    hrf_pix::prep_tile_ecoli<PF>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl);
   }
-  __syncthreads();  // the next strip rewrites tile, okp and fl
+  if (PF) hrf_pix::lds_barrier();  // the next strip rewrites tile, okp and fl
+  else __syncthreads();
   }
 }
 
@@ -305,7 +317,13 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
 unsigned assemble_grid(int64_t W, int64_t H) {
   const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
   static const bool per_strip = getenv("HRF_ASSEMBLE_STRIPGRID") != nullptr;
-  return per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel, 256, 0, nstrip);
+  return per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel<true>, 256, 0, nstrip);
+}
+
+// HRF_ASSEMBLE_PF=0: no prefetch of the next strip (A/B)
+bool assemble_pf() {
+  static const bool pf = !(getenv("HRF_ASSEMBLE_PF") && atoi(getenv("HRF_ASSEMBLE_PF")) == 0);
+  return pf;
 }
 
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
@@ -860,7 +878,12 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
     for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
     if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
-      assemble_ecoli_kernel<<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
+      if (assemble_pf())
+        assemble_ecoli_kernel<true><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
+                                                                                 cn_mode, nullptr,
+                                                                   nullptr);
+      else
+        assemble_ecoli_kernel<false><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
                                                                                  cn_mode, nullptr,
                                                                    nullptr);
       HRF_LAUNCHED();
@@ -932,8 +955,14 @@ hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const in
               "register_assemble_pixtable: the five E. coli lasers and W a multiple of 16");
   HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && table && flags, "register_assemble_pixtable: null output");
   HRF_REQUIRE(!dst || ((uintptr_t)dst & 15) == 0, "register_assemble_pixtable: dst must be 16-byte aligned");
-  assemble_ecoli_kernel<<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
-                                                                               cn_mode, (uint4 *)table, flags);
+  if (assemble_pf())
+    assemble_ecoli_kernel<true><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst,
+                                                                                     cn_out, cn_mode, (uint4 *)table,
+                                                                                     flags);
+  else
+    assemble_ecoli_kernel<false><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst,
+                                                                                      cn_out, cn_mode, (uint4 *)table,
+                                                                                      flags);
   HRF_LAUNCHED();
   return HRF_OK;
 }
