@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over the isolated classifier (tools/time_classify.py, R = 1023), one counter
 # group per rocprofv3 run (gfx950 slot limits: 8 SQ, 4 TCC -- FETCH_SIZE 3, WRITE_SIZE 2).
-# usage: bash tools/gpu_pmc.sh <tag> [mode]
+# usage: bash tools/gpu_pmc.sh <tag> [mode]   (mode "t": the pixel-table kernel the bench times)
 set -o pipefail
 export TMPDIR=/tmp
 tag=${1:-dev}

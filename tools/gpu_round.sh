@@ -11,4 +11,4 @@ tail -1 $o/pytest_gpu.txt
 timeout -k 10 600 python -u bench.py > $o/bench.json 2> $o/bench.err || { echo "bench failed"; tail -30 $o/bench.err; exit 1; }
 cut -c1-300 $o/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof -o run -- python3 bench.py --steps 30 --warmup 5 --no-extras --no-cpu-baseline > $o/prof_bench.json 2> $o/prof.err || { echo "profile failed"; exit 1; }
-bash tools/gpu_pmc.sh $tag 2 || { echo "pmc failed"; exit 1; }
+bash tools/gpu_pmc.sh $tag t || { echo "pmc failed"; exit 1; }
