@@ -91,7 +91,8 @@ def test_fullsize_community_tile(mods, orc):
 
 @pytest.mark.parametrize("q", [None, 4095, 255])
 def test_fullsize_bench_workload(mods, orc, q):
-    """bench.py's exact timed workload on one tile at full size (2048x2048x95, R=1023): the five
+    """bench.py's exact timed workload on one tile at full size (2048x2048x95, R=1023), through the
+    native tile call the bench times (and equal to the composed path): the five
     misregistered per-laser acquisitions (bench.py's tile generation; continuous, or
     bioformats-like k/4095 and k/255 samples) + the flat field -> channel-max projections, FFT
     shifts on the device, registered assembly with the coverage mask and image_cn ->
@@ -115,13 +116,22 @@ def test_fullsize_bench_workload(mods, orc, q):
     if q:
         lasers = [quantised(l, q) for l in lasers]
     cal = S.flat_field(H, W, device="cuda")
-    rt = P.register_tile(lasers)                  # bench.py's path: no materialised stack
-    res = P.process_tile(rt, lib, calibration=cal, per_pixel=True, variant=1)   # bench.py's per-cell metric
+    # bench.py's path: one native call per tile (hrf_tile_ecoli), gated per-cell metric
+    res = P.process_tile_native(lasers, lib, calibration=cal, per_pixel=True, variant=1)
     torch.cuda.synchronize()
-    stats = K.seg_stats(rt.device, H, W)
+    stats = K.tile_stats(lasers[0].device, H, W)
+    print("watershed stats q=%s: %s" % (q, stats))
+    # the composed path (register_tile without a stack + process_tile) gives the same tile
+    rt = P.register_tile(lasers)
+    comp = P.process_tile(rt, lib, calibration=cal, per_pixel=True, variant=1)
+    for x, y in ((res.meas.segmentation, comp.meas.segmentation), (res.cell_idx, comp.cell_idx),
+                 (res.counts, comp.counts), (res.identification, comp.identification),
+                 (res.pixel_idx, comp.pixel_idx), (res.pixel_dist, comp.pixel_dist)):
+        assert torch.equal(x, y)
+    del comp
     reg, cn = P.register_stack(lasers, want_cn=True)
     assert torch.equal(rt.image_cn, cn)
-    print("watershed stats q=%s: %s" % (q, stats))
+    del rt
 
     hl = [host(l) for l in lasers]
     shifts = OP.estimate_shifts(hl, "max", 15)
