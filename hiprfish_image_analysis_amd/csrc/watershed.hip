@@ -111,7 +111,7 @@ __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_
 // + gridDim.x, ... (ntx x nty tiles), so a pass costs a resident grid's dispatches instead of one
 // per tile -- most tiles are skipped after the first passes, and under the concurrent classifier
 // every dispatch waits for a CU's LDS.
-template <bool RELABEL>
+template <bool RELABEL, bool JACOBI = false>
 __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__ f, int negate,
                                                       const int32_t *__restrict__ markers,
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
@@ -166,15 +166,16 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
     }
   }
   __syncthreads();
-  // each thread owns 4 interior pixels: (row = tid/32 + 8k, col = tid%32)
-  // the owned pixels' own values stay in registers (only a pixel's own value is ever read:
-  // 9 KB less LDS per workgroup, room beside the classifier's workgroups on a CU)
+  // each thread owns 4 interior pixels: Jacobi (row = tid/32 + 8k, col = tid%32); red-black
+  // (row = 4 (tid/32) + k, col = tid%32), so a thread's pixels alternate in colour with k.
+  // The owned pixels' own values stay in registers (only a pixel's own value is ever read:
+  // 9 KB less LDS per workgroup, room beside the classifier's workgroups on a CU).
   int own[4];
   int32_t par[4];
   double fvk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    own[k] = ((tid >> 5) + 8 * k + 1) * WL + (tid & 31) + 1;
+    own[k] = (JACOBI ? ((tid >> 5) + 8 * k + 1) : (4 * (tid >> 5) + k + 1)) * WL + (tid & 31) + 1;
     par[k] = -1;
     {
       const int64_t gr = r0 + (own[k] / WL), gc = c0 + (own[k] % WL);
@@ -185,89 +186,115 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
       if (gr < H && gc < W) par[k] = ptr[gr * W + gc];
     }
   }
-  bool any_change = false;
-  for (int it = 0; it < 4 * WT * WT; ++it) {
-    double nl[4];
-    int32_t nh[4], nd[4], nb[4];
-    bool ch = false;
+  // the new state of pixel i from its neighbours' current state; true if it changes
+  auto relax = [&](int i, double fv, int32_t parent, double &nl, int32_t &nh, int32_t &nd, int32_t &nb) -> bool {
+    nl = sl[i];
+    nh = sh[i];
+    nd = sd[i];
+    nb = sb[i];
+    if ((sm[i] & 3) != 1) return false;  // outside mask or a marker
+    const int nbr[4] = {i - WL, i - 1, i + 1, i + WL};
+    if (!RELABEL) {
+      // first-popped neighbour = least (lambda, h) among labelled in-mask neighbours
+      double bl = __builtin_inf();
+      int32_t bh = HOP_INF, bd = HOP_INF, bb = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int i = own[k];
-      nl[k] = sl[i];
-      nh[k] = sh[i];
-      nd[k] = sd[i];
-      nb[k] = sb[i];
-      if ((sm[i] & 3) != 1) continue;  // outside mask or a marker
-      const int nbr[4] = {i - WL, i - 1, i + 1, i + WL};
-      if (!RELABEL) {
-        // first-popped neighbour = least (lambda, h) among labelled in-mask neighbours
-        double bl = __builtin_inf();
-        int32_t bh = HOP_INF, bd = HOP_INF, bb = 0;
+      for (int d = 0; d < 4; ++d) {
+        const int j = nbr[d];
+        const int32_t bj = sb[j];
+        if (!bj || !(sm[j] & 1)) continue;
+        if (better(sl[j], sh[j], sd[j], bj, bl, bh, bd, bb)) {
+          bl = sl[j];
+          bh = sh[j];
+          bd = sd[j];
+          bb = bj;
+        }
+      }
+      if (bb) {
+        if (bl < fv) {  // entry of level fv
+          nl = fv;
+          nh = 0;
+          nd = 0;
+        } else if (bl == fv) {  // plateau pixel: next FIFO layer
+          nl = bl;
+          nh = bh + 1;
+          nd = 0;
+        } else {  // basin pixel: filled in the slot that reached it
+          nl = bl;
+          nh = bh;
+          nd = bd + 1;
+        }
+        nb = bb;
+      }
+      return (nb != sb[i]) || (nl != sl[i]) || (nh != sh[i]) || (nd != sd[i]);
+    }
+    int32_t lb = 0;
+    if (parent >= 0) {
+      const int64_t pr = parent / W - r0, pc = parent % W - c0;
+      lb = (pr >= 0 && pr < WL && pc >= 0 && pc < WL) ? sb[pr * WL + pc] : in.lab[parent];
+    } else {
+      double bl = __builtin_inf();
+      int32_t bh = HOP_INF;
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          const int j = nbr[d];
-          const int32_t bj = sb[j];
-          if (!bj || !(sm[j] & 1)) continue;
-          if (better(sl[j], sh[j], sd[j], bj, bl, bh, bd, bb)) {
-            bl = sl[j];
-            bh = sh[j];
-            bd = sd[j];
-            bb = bj;
-          }
+      for (int d = 0; d < 4; ++d) {
+        const int j = nbr[d];
+        if (!(sm[j] & 1) || sl[j] == __builtin_inf()) continue;
+        const int32_t bj = sb[j];
+        if (sl[j] < bl || (sl[j] == bl && sh[j] < bh)) {
+          bl = sl[j];
+          bh = sh[j];
+          lb = bj;
+        } else if (sl[j] == bl && sh[j] == bh && bj && (!lb || bj < lb)) {
+          lb = bj;
         }
-        if (bb) {
-          const double fv = fvk[k];
-          if (bl < fv) {  // entry of level fv
-            nl[k] = fv;
-            nh[k] = 0;
-            nd[k] = 0;
-          } else if (bl == fv) {  // plateau pixel: next FIFO layer
-            nl[k] = bl;
-            nh[k] = bh + 1;
-            nd[k] = 0;
-          } else {  // basin pixel: filled in the slot that reached it
-            nl[k] = bl;
-            nh[k] = bh;
-            nd[k] = bd + 1;
-          }
-          nb[k] = bb;
-        }
-        ch |= (nb[k] != sb[i]) || (nl[k] != sl[i]) || (nh[k] != sh[i]) || (nd[k] != sd[i]);
-      } else {
-        int32_t lb = 0;
-        if (par[k] >= 0) {
-          const int64_t pr = par[k] / W - r0, pc = par[k] % W - c0;
-          lb = (pr >= 0 && pr < WL && pc >= 0 && pc < WL) ? sb[pr * WL + pc] : in.lab[par[k]];
-        } else {
-          double bl = __builtin_inf();
-          int32_t bh = HOP_INF;
-#pragma unroll
-          for (int d = 0; d < 4; ++d) {
-            const int j = nbr[d];
-            if (!(sm[j] & 1) || sl[j] == __builtin_inf()) continue;
-            const int32_t bj = sb[j];
-            if (sl[j] < bl || (sl[j] == bl && sh[j] < bh)) {
-              bl = sl[j];
-              bh = sh[j];
-              lb = bj;
-            } else if (sl[j] == bl && sh[j] == bh && bj && (!lb || bj < lb)) {
-              lb = bj;
-            }
-          }
-        }
-        nb[k] = lb;
-        ch |= nb[k] != sb[i];
       }
     }
-    __syncthreads();
+    nb = lb;
+    return nb != sb[i];
+  };
+  auto store = [&](int i, double nl, int32_t nh, int32_t nd, int32_t nb) {
+    if (!RELABEL) {
+      sl[i] = nl;
+      sh[i] = nh;
+      sd[i] = nd;
+    }
+    sb[i] = nb;
+  };
+  bool any_change = false;
+  for (int it = 0; it < 4 * WT * WT; ++it) {
+    bool ch = false;
+    if (JACOBI) {
+      double nl[4];
+      int32_t nh[4], nd[4], nb[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!RELABEL) {
-        sl[own[k]] = nl[k];
-        sh[own[k]] = nh[k];
-        sd[own[k]] = nd[k];
+      for (int k = 0; k < 4; ++k) ch |= relax(own[k], fvk[k], par[k], nl[k], nh[k], nd[k], nb[k]);
+      __syncthreads();  // every read of the old state is done before the writes
+#pragma unroll
+      for (int k = 0; k < 4; ++k) store(own[k], nl[k], nh[k], nd[k], nb[k]);
+    } else {
+      // Red-black (checkerboard) relaxation: a pixel's four neighbours have the other colour, so
+      // one colour's pixels update in place from the other's current state (no two neighbours
+      // ever update together, nothing is staged) and a label travels two pixels per iteration.
+      // The update is monotone, so it reaches the Jacobi form's least fixpoint
+      // (HRF_WS_JACOBI=1 keeps that form).  Colour of pixel k: (k + tid) & 1; every lane updates
+      // two pixels per colour.
+#pragma unroll
+      for (int colour = 0; colour < 2; ++colour) {
+        const bool odd = (colour ^ (tid & 1)) != 0;  // this lane's pixels of the colour: k = odd, odd + 2
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int i = odd ? own[2 * j + 1] : own[2 * j];
+          const double fv = odd ? fvk[2 * j + 1] : fvk[2 * j];
+          const int32_t pa = odd ? par[2 * j + 1] : par[2 * j];
+          double nl;
+          int32_t nh, nd, nb;
+          if (relax(i, fv, pa, nl, nh, nd, nb)) {
+            store(i, nl, nh, nd, nb);
+            ch = true;
+          }
+        }
+        if (colour == 0) __syncthreads();  // red written before black reads it
       }
-      sb[own[k]] = nb[k];
     }
     any_change |= ch;
     if (!__syncthreads_or(ch)) break;
@@ -419,6 +446,7 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
   // persistent pass grids (HRF_WS_TILEGRID=1: one workgroup per tile, as before)
   static const bool tilegrid = getenv("HRF_WS_TILEGRID") != nullptr;
+  static const bool jacobi = getenv("HRF_WS_JACOBI") != nullptr;  // A/B: the Jacobi relaxation
   const unsigned pgrid_t = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
   const unsigned pgrid_f = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
 
@@ -435,9 +463,15 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
         const int32_t *prev = local == 0 ? B.tm : tf + ((local + 2) % 3) * ntiles;
         int32_t *next = tf + ((local + 1) % 3) * ntiles;
         int32_t *chg = flag_ws + (k == batch - 1 ? 0 : 1);
-        if (relabel)
+        if (relabel && jacobi)
+          ws_pass_kernel<true, true><<<pgrid_t, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg,
+                                                             prev, cur, next, B.tw, (int)grid.x, (int)grid.y);
+        else if (relabel)
           ws_pass_kernel<true><<<pgrid_t, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
                                                        cur, next, B.tw, (int)grid.x, (int)grid.y);
+        else if (jacobi)
+          ws_pass_kernel<false, true><<<pgrid_f, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg,
+                                                              prev, cur, next, B.tw, (int)grid.x, (int)grid.y);
         else
           ws_pass_kernel<false><<<pgrid_f, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
                                                         cur, next, B.tw, (int)grid.x, (int)grid.y);
