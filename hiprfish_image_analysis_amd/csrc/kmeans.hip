@@ -939,9 +939,15 @@ __global__ __launch_bounds__(PT) void km_pp_corr_kernel(const double *__restrict
       any |= rg[q][0] < c1 && rg[q][1] > c0;
     }
     if (!any) continue;
+    // the closest potentials of the run, in fixed point once for all its trials (the f64 -> u64
+    // conversion is a multi-instruction sequence on gfx950)
     double dc[PB / PT];
+    unsigned long long dcq[PB / PT];
 #pragma unroll
-    for (int e = 0; e < PB / PT; ++e) dc[e] = closest_sq(v[e], cen[r], c);
+    for (int e = 0; e < PB / PT; ++e) {
+      dc[e] = closest_sq(v[e], cen[r], c);
+      dcq[e] = (unsigned long long)(dc[e] * scaleS);
+    }
     for (int t = 0; t < d.nt; ++t) {
       const int q = r * NTMAX + t;
       const long long a = rg[q][0], b = rg[q][1];
@@ -952,8 +958,7 @@ __global__ __launch_bounds__(PT) void km_pp_corr_kernel(const double *__restrict
       for (int e = 0; e < PB / PT; ++e) {
         const long long i = c0 + (long long)e * PT + threadIdx.x;
         const double dt = (v[e] - cv) * (v[e] - cv);
-        if (i >= a && i < b && i < c1 && dt < dc[e])
-          s += (unsigned long long)(dc[e] * scaleS) - (unsigned long long)(dt * scaleS);
+        if (i >= a && i < b && i < c1 && dt < dc[e]) s += dcq[e] - (unsigned long long)(dt * scaleS);
       }
       const U128 w = wave_sum128(P(s));
       if ((threadIdx.x & 63) == 0 && (w.lo | w.hi)) {
