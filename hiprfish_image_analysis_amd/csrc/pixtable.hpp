@@ -124,16 +124,17 @@ __device__ __forceinline__ void prep_tile(float *tile, const uint8_t *ok, int np
 // flight across it (the E. coli assembly prefetches its next strip that way)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Caller contract: fl[0..63] is zero and the tile is staged (both ordered by a barrier before
+// the call); the f64 channel sums the caller left in cns[0..np) (nullable) are turned into
+// image_cn by wave 2 (log(s + 1e-2), cn_mode 1, or log10(s + 1), cn_mode 2) beside its segment.
 template <bool LDSB = false>
 __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, int np, int64_t p0,
                                                 uint4 *__restrict__ table, uint8_t *__restrict__ flags,
-                                                uint32_t *fl /* LDS, 64 words */) {
+                                                uint32_t *fl /* LDS, 64 words, zero */, const double *cns,
+                                                int cn_mode, double *__restrict__ cn_out) {
   using L = LayEcoli;
   constexpr int C = L::C, KT = lay_kt<L>();
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  if (tid < 64) fl[tid] = 0;
-  if (LDSB) lds_barrier();
-  else __syncthreads();
   auto seg = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (lane >= np) return;
@@ -141,7 +142,7 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
     const bool use = !ok || ok[lane];
     float nn = 0.0f;
     uint32_t sg = 0;
-#pragma unroll
+#pragma unroll 4
     for (int c = L::b(s); c < L::b(s + 1); ++c) {
       const float x = use ? px[c] : 0.0f;
       nn = __builtin_fmaf(x, x, nn);
@@ -160,40 +161,52 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
       inv = nz ? (float)(1.0 / sqrt(td)) : 0.0f;
       zx = nz ? 0u : (1u << s);
     }
-#pragma unroll
+#pragma unroll 4
     for (int c = L::b(s); c < L::b(s + 1); ++c) px[c] = use ? px[c] * inv : 0.0f;
     const uint32_t f = zx | ((sg >> 31) << 7);
     if (f) atomicOr(&fl[lane], f);
   };
   if (w == 0) seg(std::integral_constant<int, 0>{});
   else if (w == 1) seg(std::integral_constant<int, 1>{});
-  else if (w == 2) seg(std::integral_constant<int, 2>{});
-  else {
+  else if (w == 2) {
+    seg(std::integral_constant<int, 2>{});
+    if (cns && lane < np) {
+      double sv = 0.0 + cns[lane];
+      if (cn_mode == 1) sv = log(sv + 1e-2);
+      else if (cn_mode == 2) sv = log10(sv + 1.0);
+      cn_out[p0 + lane] = sv;
+    }
+  } else {
     seg(std::integral_constant<int, 3>{});
     seg(std::integral_constant<int, 4>{});
   }
   if (LDSB) lds_barrier();
   else __syncthreads();
   if (tid < np) flags[p0 + tid] = (uint8_t)fl[tid];
-  const int ne = (np + 15) / 16 * KT * 2 * 64;
+  // one item = one (group, k-block, lane): its 8 values once, the hi and the lo entry from them
+  const int ne = (np + 15) / 16 * KT * 64;
+#pragma unroll 1
   for (int e = tid; e < ne; e += 256) {
-    const int ln = e & 63, hl = (e >> 6) & 1, gt = e >> 7;
+    const int ln = e & 63, gt = e >> 6;
     const int g = gt / KT, t = gt - g * KT;
     const int i = 16 * g + (ln & 15), Q = ln >> 4;
     const float *pc = tile + (i < np ? i : 0) * C;
     union {
       _Float16 h[8];
       uint4 u;
-    } o;
+    } hi, lo;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int k = 32 * t + 8 * Q + q;
       float x = k < C ? pc[k] : (k == C ? 1.0f : 0.0f);
       if (i >= np) x = 0.0f;
       const _Float16 hv = (_Float16)x;
-      o.h[q] = hl ? (_Float16)(x - (float)hv) : hv;
+      hi.h[q] = hv;
+      lo.h[q] = (_Float16)(x - (float)hv);
     }
-    table[(p0 / 16 + g) * (int64_t)(KT * 2 * 64) + t * 128 + hl * 64 + ln] = o.u;
+    uint4 *dst = table + (p0 / 16 + g) * (int64_t)(KT * 2 * 64) + t * 128 + ln;
+    dst[0] = hi.u;
+    dst[64] = lo.u;
   }
 }
 

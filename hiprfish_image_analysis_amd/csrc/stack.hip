@@ -193,12 +193,20 @@ __device__ __forceinline__ void lay_load(const Lasers &L, const int *sdr, const 
   const bool row_ok = r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0);
   const int64_t cmin = dc > 0 ? dc : 0, cmax = W + (dc < 0 ? dc : 0);
   const float *src = L.src[q] + ((r - dr) * W + (c0 - dc)) * (int64_t)cl;
+  if (row_ok && c0 >= cmin && c0 + AS_P <= cmax && c0 + AS_P <= W) {  // the whole strip in range
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int e = tid + 256 * u;
-    const int pp = e / cl;
-    const int64_t c = c0 + pp;
-    v[u] = (e < AS_P * cl && row_ok && c >= cmin && c < cmax && c < W) ? src[e] : 0.0f;
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + 256 * u;
+      v[u] = ((AS_P * cl) % 256 == 0 || u + 1 < U || e < AS_P * cl) ? src[e] : 0.0f;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + 256 * u;
+      const int pp = e / cl;
+      const int64_t c = c0 + pp;
+      v[u] = (e < AS_P * cl && row_ok && c >= cmin && c < cmax && c < W) ? src[e] : 0.0f;
+    }
   }
   if constexpr (q + 1 < NL) lay_load<q + 1, NL>(L, sdr, sdc, r, c0, H, W, tid, v + U);
 }
@@ -223,8 +231,8 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 // the concurrent classifier every dispatch waits for a CU slot.  Per strip unchanged.
 // PF: the next strip's loads are issued right after this strip is staged in LDS and stay in flight
 // through its image_cn and pixel-table phases (barriers there order LDS only, lds_barrier).
-template <bool PF>
-__global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+template <bool PF, int WPE = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
                                                              uint8_t *__restrict__ pflags) {
@@ -233,6 +241,7 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
   __shared__ uint8_t okp[AS_P];
   __shared__ int sdr[LMAX], sdc[LMAX];
   __shared__ uint32_t fl[AS_P];
+  __shared__ double cns[AS_P];  // the strip's channel sums, to prep_tile_ecoli (pixel-table mode)
   load_shifts(L, sdr, sdc);
   const int tid = threadIdx.x;
   const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
@@ -248,9 +257,19 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
     if (apply_mask)
       for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, sdr[q], sdc[q]);
     okp[tid] = (uint8_t)ok;
+    fl[tid] = 0;
   }
-  if (!PF) lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
-  lay_store<0, 5>(tile, tid, v);
+  if (PF) {
+    lay_store<0, 5>(tile, tid, v);
+  } else if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
+    lay_load<0, 2>(L, sdr, sdc, r, c0, H, W, tid, v);
+    lay_store<0, 2>(tile, tid, v);
+    lay_load<2, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
+    lay_store<2, 5>(tile, tid, v);
+  } else {
+    lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
+    lay_store<0, 5>(tile, tid, v);
+  }
   if (PF) {
     hrf_pix::lds_barrier();
     const int64_t tn = t + gridDim.x;  // the next strip's loads: in flight until its lay_store
@@ -287,7 +306,7 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
       const float *a = tile + (pi < np ? pi : 0) * C;
       const bool ok = pi < np && (!apply_mask || okp[pi]);
       double rr = ok ? (double)a[j] : 0.0;
-#pragma unroll
+#pragma unroll 2
       for (int i = 8; i < main_n; i += 8) rr += ok ? (double)a[i + j] : 0.0;
       rr = rr + __shfl_xor(rr, 1, 64);
       rr = rr + __shfl_xor(rr, 2, 64);
@@ -296,34 +315,55 @@ __global__ __launch_bounds__(256) void assemble_ecoli_kernel(Lasers L, int64_t H
       if (j == 0)
         for (int i = main_n; i < C; ++i) res += ok ? (double)a[i] : 0.0;
       if (j == 0 && pi < np) {
-        double sv = 0.0 + res;
-        if (cn_mode == 1) sv = log(sv + 1e-2);
-        else if (cn_mode == 2) sv = log10(sv + 1.0);
-        cn_out[r * W + c0 + pi] = sv;
+        if (ptab) {  // the log is taken once per pixel in prep_tile_ecoli
+          cns[pi] = res;
+        } else {
+          double sv = 0.0 + res;
+          if (cn_mode == 1) sv = log(sv + 1e-2);
+          else if (cn_mode == 2) sv = log10(sv + 1.0);
+          cn_out[r * W + c0 + pi] = sv;
+        }
       }
     }
   }
   if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
     if (PF) hrf_pix::lds_barrier();
     else __syncthreads();
-    hrf_pix::prep_tile_ecoli<PF>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl);
+    hrf_pix::prep_tile_ecoli<PF>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl,
+                                 cn_out ? cns : nullptr, cn_mode, cn_out);
   }
   if (PF) hrf_pix::lds_barrier();  // the next strip rewrites tile, okp and fl
   else __syncthreads();
   }
 }
 
-// workgroups of the E. coli assembly: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one per strip)
-unsigned assemble_grid(int64_t W, int64_t H) {
+// E. coli assembly launch: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one workgroup per strip);
+// HRF_ASSEMBLE_PF=0: no prefetch of the next strip; HRF_ASSEMBLE_WPE=3: the kernel built for
+// three workgroups per CU (A/B switches)
+template <bool PF, int WPE>
+void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
+                       uint4 *table, uint8_t *flags, hipStream_t s) {
   const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
   static const bool per_strip = getenv("HRF_ASSEMBLE_STRIPGRID") != nullptr;
-  return per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel<true>, 256, 0, nstrip);
+  const unsigned grid =
+      per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel<PF, WPE>, 256, 0, nstrip);
+  assemble_ecoli_kernel<PF, WPE><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
 }
 
-// HRF_ASSEMBLE_PF=0: no prefetch of the next strip (A/B)
-bool assemble_pf() {
+void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
+                     uint4 *table, uint8_t *flags, hipStream_t s) {
   static const bool pf = !(getenv("HRF_ASSEMBLE_PF") && atoi(getenv("HRF_ASSEMBLE_PF")) == 0);
-  return pf;
+  static const int wpe = getenv("HRF_ASSEMBLE_WPE") ? atoi(getenv("HRF_ASSEMBLE_WPE")) : 2;
+  if (wpe == 4) {
+    if (pf) launch_assemble_t<true, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+    else launch_assemble_t<false, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  } else if (wpe == 3) {
+    if (pf) launch_assemble_t<true, 3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+    else launch_assemble_t<false, 3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  } else {
+    if (pf) launch_assemble_t<true, 2>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+    else launch_assemble_t<false, 2>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  }
 }
 
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
@@ -878,14 +918,7 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
     for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
     if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
-      if (assemble_pf())
-        assemble_ecoli_kernel<true><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
-                                                                                 cn_mode, nullptr,
-                                                                   nullptr);
-      else
-        assemble_ecoli_kernel<false><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst, cn_out,
-                                                                                 cn_mode, nullptr,
-                                                                   nullptr);
+      launch_assemble(L, H, W, apply_mask, dst, cn_out, cn_mode, nullptr, nullptr, (hipStream_t)stream);
       HRF_LAUNCHED();
       return HRF_OK;
     }
@@ -955,14 +988,7 @@ hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const in
               "register_assemble_pixtable: the five E. coli lasers and W a multiple of 16");
   HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && table && flags, "register_assemble_pixtable: null output");
   HRF_REQUIRE(!dst || ((uintptr_t)dst & 15) == 0, "register_assemble_pixtable: dst must be 16-byte aligned");
-  if (assemble_pf())
-    assemble_ecoli_kernel<true><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst,
-                                                                                     cn_out, cn_mode, (uint4 *)table,
-                                                                                     flags);
-  else
-    assemble_ecoli_kernel<false><<<assemble_grid(W, H), 256, 0, (hipStream_t)stream>>>(L, H, W, apply_mask, dst,
-                                                                                      cn_out, cn_mode, (uint4 *)table,
-                                                                                      flags);
+  launch_assemble(L, H, W, apply_mask, dst, cn_out, cn_mode, (uint4 *)table, flags, (hipStream_t)stream);
   HRF_LAUNCHED();
   return HRF_OK;
 }
