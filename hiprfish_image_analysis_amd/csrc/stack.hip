@@ -337,9 +337,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-// E. coli assembly launch: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one workgroup per strip);
-// HRF_ASSEMBLE_PF=0: no prefetch of the next strip; HRF_ASSEMBLE_WPE=3: the kernel built for
-// three workgroups per CU (A/B switches)
+// E. coli assembly launch: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one workgroup per strip)
+// of the kernel built for three workgroups per CU (165 VGPRs, no spills).  Interleaved on one box:
+// 1035 vs 991 Mpix/s end to end against the 2-per-CU build (197 VGPRs), isolated 1.03 vs 1.38 ms;
+// with the next strip prefetched (HRF_ASSEMBLE_PF=1) 1035 either way; 4 per CU
+// (HRF_ASSEMBLE_WPE=4) spills and loses (985).
 template <bool PF, int WPE>
 void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                        uint4 *table, uint8_t *flags, hipStream_t s) {
@@ -352,8 +354,8 @@ void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, fl
 
 void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                      uint4 *table, uint8_t *flags, hipStream_t s) {
-  static const bool pf = !(getenv("HRF_ASSEMBLE_PF") && atoi(getenv("HRF_ASSEMBLE_PF")) == 0);
-  static const int wpe = getenv("HRF_ASSEMBLE_WPE") ? atoi(getenv("HRF_ASSEMBLE_WPE")) : 2;
+  static const bool pf = getenv("HRF_ASSEMBLE_PF") && atoi(getenv("HRF_ASSEMBLE_PF")) == 1;
+  static const int wpe = getenv("HRF_ASSEMBLE_WPE") ? atoi(getenv("HRF_ASSEMBLE_WPE")) : 3;
   if (wpe == 4) {
     if (pf) launch_assemble_t<true, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
     else launch_assemble_t<false, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
