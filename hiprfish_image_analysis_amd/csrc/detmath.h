@@ -17,8 +17,10 @@
 
 #ifdef __HIPCC__
 #define HRF_DM_FN static inline __host__ __device__
+#define HRF_DM_TAB static constexpr
 #else
 #define HRF_DM_FN static inline
+#define HRF_DM_TAB static const
 #endif
 
 HRF_DM_FN double hrf_det_exp(double x) {
@@ -74,6 +76,175 @@ HRF_DM_FN double hrf_det_log(double x) {
   const double lm = fma(2.0 * s * z, p, 2.0 * s); /* 2s + 2s z p */
   const double de = (double)e;
   return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, lm));
+}
+
+/* ---- correctly rounded log / log10 -------------------------------------------------------
+ * image_cn = log(sum + 1e-2) (ecoli measurement.py:72) feeds the KMeans thresholds and the
+ * watershed priorities, so a last-ulp difference can move a pixel between clusters or reorder a
+ * watershed contest.  numpy's own log is not a fixed function: its AVX-512 path (SVML) and glibc
+ * differ in the last ulp on ~3e-4 of inputs, and neither is correctly rounded everywhere.  libhrf
+ * and the oracle therefore both use the correctly rounded logarithm, computed in double-double
+ * (relative error < 2^-100) from IEEE +, -, *, /, fma only, then rounded once: the two sides are
+ * bit-identical by construction, and equal to the exact log rounded to nearest except for inputs
+ * within 2^-100 of a rounding midpoint (none in the checks: tests/test_oracle_golden.py compares
+ * against Python's decimal ln at 50 digits).
+ *
+ * x = m 2^e, m in [0.75, 1.5); c = k/128 the nearest multiple of 1/128 (exact, k in 96..192);
+ * log m = log c + 2 atanh(s), s = (m - c) / (m + c), |s| < 2^-8.5; the series' s, s^3/3, s^5/5
+ * in double-double, s^7/7 .. s^13/13 in double; log c and ln 2 from double-double tables. */
+HRF_DM_FN void hrf_dd_two_sum(double a, double b, double *s, double *e) {
+  const double t = a + b, bb = t - a;
+  *e = (a - (t - bb)) + (b - bb);
+  *s = t;
+}
+HRF_DM_FN void hrf_dd_fast(double a, double b, double *s, double *e) { /* |a| >= |b| or a == 0 */
+  const double t = a + b;
+  *e = b - (t - a);
+  *s = t;
+}
+HRF_DM_FN void hrf_dd_add(double ah, double al, double bh, double bl, double *rh, double *rl) {
+  double s, e, t, f;
+  hrf_dd_two_sum(ah, bh, &s, &e);
+  hrf_dd_two_sum(al, bl, &t, &f);
+  e += t;
+  hrf_dd_fast(s, e, &s, &e);
+  e += f;
+  hrf_dd_fast(s, e, rh, rl);
+}
+HRF_DM_FN void hrf_dd_mul(double ah, double al, double bh, double bl, double *rh, double *rl) {
+  const double p = ah * bh;
+  double e = fma(ah, bh, -p);
+  e += ah * bl + al * bh;
+  hrf_dd_fast(p, e, rh, rl);
+}
+
+/* BEGIN LOGTAB (gen_logtab.py) */
+HRF_DM_TAB double hrf_logtab_hi[97] = {
+  -0.2876820724517809, -0.27731928541623435, -0.26706278524904525, -0.2569104137850272,
+  -0.24686007793152578, -0.2369097470783577, -0.22705745063534608, -0.2173012756899814,
+  -0.2076393647782445, -0.1980699137620938, -0.18859116980755003, -0.179201429457711,
+  -0.16989903679539747, -0.16068238169047347, -0.15154989812720093, -0.14250006260728304,
+  -0.13353139262452263, -0.1246424452072766, -0.1158318155251217, -0.1070981355563671,
+  -0.09844007281325252, -0.08985632912186105, -0.0813456394539524, -0.07290677080808779,
+  -0.06453852113757118, -0.05623971832287608, -0.048009219186360606, -0.039845908547199674,
+  -0.0317486983145803, -0.023716526617316044, -0.015748356968139168, -0.007843177461025893,
+  0.0, 0.007782140442054949, 0.015504186535965254, 0.02316705928153438,
+  0.030771658666753687, 0.0383188643021366, 0.0458095360312942, 0.053244514518812285,
+  0.06062462181643484, 0.06795066190850775, 0.07522342123758753, 0.08244366921107459,
+  0.08961215868968714, 0.09672962645855111, 0.10379679368164356, 0.11081436634029011,
+  0.11778303565638346, 0.12470347850095724, 0.13157635778871926, 0.13840232285911913,
+  0.1451820098444979, 0.15191604202584197, 0.15860503017663857, 0.16524957289530717,
+  0.17185025692665923, 0.1784076574728183, 0.184922338494012, 0.19139485299962947,
+  0.19782574332991987, 0.2042155414286909, 0.21056476910734964, 0.21687393830061436,
+  0.22314355131420976, 0.22937410106484582, 0.2355660713127669, 0.24171993688714516,
+  0.24783616390458127, 0.25391520998096345, 0.25995752443692605, 0.26596354849713794,
+  0.27193371548364176, 0.2778684510034563, 0.2837681731306446, 0.28963329258304266,
+  0.2954642128938359, 0.3012613305781618, 0.3070250352949119, 0.3127557100038969,
+  0.3184537311185346, 0.324119468654212, 0.329753286372468, 0.3353555419211378,
+  0.3409265869705932, 0.34646676734620857, 0.3519764231571782, 0.3574558889218038,
+  0.3629054936893685, 0.3683255611587076, 0.37371640979358406, 0.37907835293496944,
+  0.38441169891033206, 0.3897167511400252, 0.394993808240869, 0.4002431641270127,
+  0.4054651081081644,
+};
+HRF_DM_TAB double hrf_logtab_lo[97] = {
+  -2.607160616442564e-17, 7.44528405583513e-18, 7.32891532732017e-18, -2.502843296152504e-17,
+  -1.361743371748368e-17, -1.9682402978398164e-18, -9.551415762738488e-18, -1.6168452453763015e-18,
+  -1.2053243216686129e-17, -3.742843482461439e-18, 7.432164219196925e-18, 1.0785017454858423e-17,
+  4.868008764439071e-19, 3.650183553047837e-18, -5.1669593684615594e-18, 9.926388234225749e-18,
+  3.664457663660085e-18, 5.808912678940971e-18, -4.338484369808096e-18, 1.73705104015906e-18,
+  4.439009633675136e-18, 6.273760163689594e-19, -5.07707635593117e-18, 6.306860257532778e-18,
+  6.470486661692933e-18, 3.2835149805605613e-18, -1.4390903347292205e-18, 3.129547680315208e-18,
+  -3.0382263084680858e-18, 1.5774243488668215e-18, -1.0021578630528974e-18, -2.764708154124904e-19,
+  0.0, -1.2819179123343845e-20, -3.278321022892429e-19, -1.1769544932063305e-18,
+  1.0431732029005968e-18, -2.357996157351286e-18, 1.902959866474257e-18, -1.665575816973663e-18,
+  2.6424025938726934e-18, -1.2802141240611733e-18, -5.930604196293241e-18, 5.700437773813987e-18,
+  -5.4268129336647135e-18, -5.597397486289965e-19, 5.47772415726659e-18, 1.183748342825649e-18,
+  -1.1971685747593677e-18, -4.6522609636496624e-18, 1.1123000879729588e-17, 4.447777301357527e-18,
+  8.242418783022475e-18, 6.4838631244022194e-18, 1.1257003872182592e-17, -1.0094935622322628e-17,
+  -6.0224538210113705e-18, -1.2432553788701131e-17, 3.0236614153574064e-18, -1.2129496905792884e-17,
+  1.2821194372980142e-17, 2.7338281018722773e-18, -4.249405314729895e-18, 4.551026193234283e-18,
+  -9.091270597324799e-18, 9.927671823978025e-18, -2.3943371495187355e-18, 8.900990022166643e-18,
+  -1.2432209578702523e-17, -8.048097394424201e-18, 2.069806938978935e-17, 5.3393802761314314e-18,
+  7.83319637697442e-19, -9.16018294909263e-19, -2.032665581126656e-17, 2.0535953219858174e-17,
+  -2.16461086040599e-17, -9.048511144048564e-18, -1.2319916200101964e-17, -1.451808353098951e-17,
+  2.7114779367326236e-17, -7.958214381893813e-18, 2.122020616196946e-18, 1.834564437059473e-17,
+  1.7467136443544747e-17, 1.028583585496265e-17, -1.2953893030191963e-17, -2.5136910072413547e-17,
+  -2.1492361455310972e-17, 2.690672380132659e-17, 2.1836211281198184e-17, 1.587939415338447e-17,
+  -1.612149700764673e-17, 2.734172667856699e-17, -1.5113724418336168e-17, -1.1349239205188711e-17,
+  -2.8811380259626426e-18,
+};
+#define HRF_DD_LN2_HI 0.6931471805599453
+#define HRF_DD_LN2_LO 2.3190468138462996e-17
+#define HRF_DD_THIRD_HI 0.3333333333333333
+#define HRF_DD_THIRD_LO 1.850371707708594e-17
+#define HRF_DD_FIFTH_HI 0.2
+#define HRF_DD_FIFTH_LO -1.1102230246251566e-17
+#define HRF_DD_INVLN10_HI 0.4342944819032518
+#define HRF_DD_INVLN10_LO 1.098319650216765e-17
+/* END LOGTAB */
+
+/* log(x) as a normalised double-double (x > 0 finite) */
+HRF_DM_FN void hrf_dd_log(double x, double *rh, double *rl) {
+  int e = 0;
+  double m = frexp(x, &e); /* [0.5, 1) */
+  if (m < 0.75) {
+    m = m * 2.0;
+    e -= 1;
+  }
+  const int k = (int)rint(m * 128.0);
+  const double c = (double)k * 0.0078125;
+  const double d = m - c; /* exact */
+  double uh, ul;
+  hrf_dd_two_sum(m, c, &uh, &ul);
+  /* s = d / (uh + ul): the remainder of a correctly rounded quotient is exact under fma */
+  const double q1 = d / uh;
+  const double r = fma(-q1, uh, d) - q1 * ul;
+  double sh, sl;
+  hrf_dd_fast(q1, r / uh, &sh, &sl);
+  double zh, zl, s3h, s3l, s5h, s5l, t3h, t3l, t5h, t5l;
+  hrf_dd_mul(sh, sl, sh, sl, &zh, &zl);
+  hrf_dd_mul(sh, sl, zh, zl, &s3h, &s3l);
+  hrf_dd_mul(s3h, s3l, zh, zl, &s5h, &s5l);
+  hrf_dd_mul(s3h, s3l, HRF_DD_THIRD_HI, HRF_DD_THIRD_LO, &t3h, &t3l);
+  hrf_dd_mul(s5h, s5l, HRF_DD_FIFTH_HI, HRF_DD_FIFTH_LO, &t5h, &t5l);
+  double p = fma(zh, 1.0 / 13.0, 1.0 / 11.0);
+  p = fma(zh, p, 1.0 / 9.0);
+  p = fma(zh, p, 1.0 / 7.0);
+  const double tail = s5h * zh * p;
+  double ah, al;
+  hrf_dd_add(t5h, t5l, tail, 0.0, &ah, &al);
+  hrf_dd_add(t3h, t3l, ah, al, &ah, &al);
+  hrf_dd_add(sh, sl, ah, al, &ah, &al);
+  ah *= 2.0;
+  al *= 2.0;
+  /* e ln2 + log c */
+  const double de = (double)e;
+  const double eh = de * HRF_DD_LN2_HI;
+  double el = fma(de, HRF_DD_LN2_HI, -eh);
+  el = fma(de, HRF_DD_LN2_LO, el);
+  double bh, bl;
+  hrf_dd_fast(eh, el, &bh, &bl);
+  hrf_dd_add(bh, bl, hrf_logtab_hi[k - 96], hrf_logtab_lo[k - 96], &bh, &bl);
+  hrf_dd_add(bh, bl, ah, al, rh, rl);
+}
+
+HRF_DM_FN double hrf_cr_log(double x) {
+  if (x != x || x < 0.0) return NAN;
+  if (x == 0.0) return -INFINITY;
+  if (x == INFINITY) return x;
+  double h, l;
+  hrf_dd_log(x, &h, &l);
+  return h + l;
+}
+
+HRF_DM_FN double hrf_cr_log10(double x) {
+  if (x != x || x < 0.0) return NAN;
+  if (x == 0.0) return -INFINITY;
+  if (x == INFINITY) return x;
+  double h, l;
+  hrf_dd_log(x, &h, &l);
+  hrf_dd_mul(h, l, HRF_DD_INVLN10_HI, HRF_DD_INVLN10_LO, &h, &l);
+  return h + l;
 }
 
 /* x >= 0 (umap's squared distances): x^y */

@@ -16,6 +16,8 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "detmath.h"
+
 namespace hrf_pix {
 
 struct LayEcoli {
@@ -172,8 +174,8 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
     seg(std::integral_constant<int, 2>{});
     if (cns && lane < np) {
       double sv = 0.0 + cns[lane];
-      if (cn_mode == 1) sv = log(sv + 1e-2);
-      else if (cn_mode == 2) sv = log10(sv + 1.0);
+      if (cn_mode == 1) sv = hrf_cr_log(sv + 1e-2);
+      else if (cn_mode == 2) sv = hrf_cr_log10(sv + 1.0);
       cn_out[p0 + lane] = sv;
     }
   } else {

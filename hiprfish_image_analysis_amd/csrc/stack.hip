@@ -15,6 +15,7 @@
 #include "common.hpp"
 #include "pixtable.hpp"
 #include "wave.hpp"
+#include "detmath.h"
 
 namespace {
 
@@ -165,8 +166,8 @@ __global__ __launch_bounds__(256) void assemble_lds_kernel(Lasers L, int64_t H, 
       }
       if (j == 0 && pi < np) {
         double sv = 0.0 + res;
-        if (cn_mode == 1) sv = log(sv + 1e-2);
-        else if (cn_mode == 2) sv = log10(sv + 1.0);
+        if (cn_mode == 1) sv = hrf_cr_log(sv + 1e-2);
+        else if (cn_mode == 2) sv = hrf_cr_log10(sv + 1.0);
         cn_out[r * W + c0 + pi] = sv;
       }
     }
@@ -311,8 +312,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           cns[pi] = res;
         } else {
           double sv = 0.0 + res;
-          if (cn_mode == 1) sv = log(sv + 1e-2);
-          else if (cn_mode == 2) sv = log10(sv + 1.0);
+          if (cn_mode == 1) sv = hrf_cr_log(sv + 1e-2);
+          else if (cn_mode == 2) sv = hrf_cr_log10(sv + 1.0);
           cn_out[r * W + c0 + pi] = sv;
         }
       }
@@ -397,8 +398,8 @@ __global__ void channel_sum_kernel(const float *__restrict__ stack, int64_t npix
                                    const uint8_t *__restrict__ mask, int mode, int negate, double *__restrict__ out) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
     double s = (mask && !mask[p]) ? 0.0 : 0.0 + pw_sum(stack + p * C, C);
-    if (mode == 1) s = log(s + 1e-2);
-    else if (mode == 2) s = log10(s + 1.0);
+    if (mode == 1) s = hrf_cr_log(s + 1e-2);
+    else if (mode == 2) s = hrf_cr_log10(s + 1.0);
     out[p] = negate ? -s : s;
   }
 }
@@ -501,8 +502,8 @@ __global__ __launch_bounds__(256) void channel_sum_lds_kernel(const float *__res
       if (j == 0 && pi < np) {
         const int64_t p = p0 + pi;
         double sv = (mask && !mask[p]) ? 0.0 : 0.0 + res;
-        if (mode == 1) sv = log(sv + 1e-2);
-        else if (mode == 2) sv = log10(sv + 1.0);
+        if (mode == 1) sv = hrf_cr_log(sv + 1e-2);
+        else if (mode == 2) sv = hrf_cr_log10(sv + 1.0);
         out[p] = negate ? -sv : sv;
       }
     }

@@ -526,9 +526,10 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       const int64_t stride = walker_bytes(cap, hcap, gcap);
       const int64_t nth = ntodo < threads ? ntodo : threads;
       if (nth * stride > scratch_bytes) {
-        if (scratch) HRF_HIP(hipFreeAsync(scratch, s));
-        scratch = nullptr;
+        const hipError_t fe = scratch ? hipFreeAsync(scratch, s) : hipSuccess;
+        scratch = nullptr;  // before the status check: the guard must not free it again
         scratch_bytes = 0;
+        HRF_HIP(fe);
         HRF_HIP(hipMallocAsync((void **)&scratch, (size_t)(nth * stride), s));
         scratch_bytes = nth * stride;
       }

@@ -819,8 +819,23 @@ def pixtable_prepare(stack, bounds):
     return pt
 
 
+def check_refx_table(refx, R, C, bounds, where):
+    """the pixel-table classifier (w16t) reads a mode-2 table of Rpad rows of the mode-2 pitch; a
+    mode-0/1 table (f32, or rows of another width) would be read as split-fp16 rows, past its end"""
+    if not isinstance(refx, torch.Tensor) or not refx.is_cuda:
+        raise ValueError("%s: the prepared library must be a device tensor" % where)
+    if 2 not in classify_modes(bounds) or refx_mode(refx, C, bounds) != 2:
+        raise ValueError("%s: a mode-2 prepared library (classify_prepare(..., mode=2)) is required" % where)
+    _, rpad = classify_geometry(C, len(bounds) - 1, R, 2)
+    need = rpad * classify_table_row_bytes(C, bounds, 2)
+    if refx.numel() * refx.element_size() < need or not refx.is_contiguous():
+        raise ValueError("%s: prepared library holds %d bytes, %d rows of the mode-2 pitch need %d"
+                         % (where, refx.numel() * refx.element_size(), rpad, need))
+
+
 def classify_pixels_table(pt, refx, R):
     """classify_pixels (mode 2) from a PixTable: the same results bit for bit"""
+    check_refx_table(refx, R, pt.C, pt.bounds, "classify_pixels_table")
     b = _i32_host(pt.bounds)
     idx = torch.empty(pt.shape, dtype=torch.int32, device=pt.table.device)
     dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
@@ -946,45 +961,96 @@ def erosion_seeds(cell_sm, area_max=600, min_obj=10):
 
 
 # ---- native segmentation drivers (segment.hip) ------------------------------------------------
-_SEG_CTX = {}
+class _CtxCache:
+    """Native contexts (hrf_seg_ctx / hrf_tile_ctx) keyed by (device, stream handle, H, W), at most
+    `cap` alive (HRF_CTX_CACHE, default 8; a 2048^2 tile context holds ~2 GB of HBM).  The least
+    recently used idle one beyond the cap is destroyed once the event recorded behind its last call
+    has completed -- an event outlives the stream it was recorded on, so a caller that makes a
+    stream per image and drops it does not leak the context (the reference runs one process per
+    FOV, ecoli Snakefile:67-82; a long-lived driver must not grow).  Thread-safe: a context in use
+    by a call on another host thread is never evicted."""
+
+    def __init__(self, create, destroy):
+        import threading
+        from collections import OrderedDict
+        self._create, self._destroy = create, destroy
+        self._d = OrderedDict()       # key -> [handle, last-use event or None, calls in flight]
+        self._lock = threading.Lock()
+        self.cap = max(1, int(os.environ.get("HRF_CTX_CACHE", "8")))
+
+    def use(self, dev, H, W):
+        """context manager: the (device, current stream, H, W) context for one native call"""
+        import contextlib
+        import ctypes
+        key = (torch.device(dev), _stream(), H, W)
+
+        @contextlib.contextmanager
+        def cm():
+            evict = []
+            with self._lock:
+                ent = self._d.get(key)
+                if ent is None:
+                    h = ctypes.c_void_p()
+                    _lib.call(self._create, H, W, ctypes.addressof(h))
+                    ent = self._d[key] = [h, None, 0]
+                else:
+                    self._d.move_to_end(key)
+                ent[2] += 1
+                over = len(self._d) - self.cap
+                for k in list(self._d):
+                    if over <= 0:
+                        break
+                    if self._d[k][2] == 0:
+                        evict.append(self._d.pop(k))
+                        over -= 1
+            for e in evict:
+                self._free(e)
+            try:
+                yield ent[0]
+            finally:
+                with self._lock:
+                    if ent[1] is None:
+                        ent[1] = torch.cuda.Event()
+                    ent[1].record(torch.cuda.current_stream())
+                    ent[2] -= 1
+        return cm()
+
+    def _free(self, ent):
+        h, ev, _ = ent
+        if ev is not None:
+            ev.synchronize()
+        _lib.call(self._destroy, h)
+
+    def clear(self):
+        """destroy every idle context (after its last queued use)"""
+        with self._lock:
+            idle = [k for k, e in self._d.items() if e[2] == 0]
+            ents = [self._d.pop(k) for k in idle]
+        for e in ents:
+            self._free(e)
+
+    def __len__(self):
+        return len(self._d)
 
 
-def _seg_ctx(dev, H, W):
-    """one driver context per (device, stream, tile size): concurrent tiles on different streams
-    never share buffers"""
-    import ctypes
-    key = (dev, _stream(), H, W)
-    h = _SEG_CTX.get(key)
-    if h is None:
-        h = ctypes.c_void_p()
-        _lib.call("hrf_seg_ctx_create", H, W, ctypes.addressof(h))
-        _SEG_CTX[key] = h
-    return h
+_SEG_CTX = _CtxCache("hrf_seg_ctx_create", "hrf_seg_ctx_destroy")
+_TILE_CTX = _CtxCache("hrf_tile_ctx_create", "hrf_tile_ctx_destroy")
 
 
-_TILE_CTX = {}
-
-
-def _tile_ctx(dev, H, W):
-    """one native tile context per (device, stream, tile size) (hrf_tile_ctx: its own segmentation
-    context, projections, registration workspace, image_cn, pixel table, per-label buffers)"""
-    import ctypes
-    key = (dev, _stream(), H, W)
-    h = _TILE_CTX.get(key)
-    if h is None:
-        h = ctypes.c_void_p()
-        _lib.call("hrf_tile_ctx_create", H, W, ctypes.addressof(h))
-        _TILE_CTX[key] = h
-    return h
+def release_contexts():
+    """destroy the cached native segmentation and tile contexts (each after its last queued call)"""
+    _SEG_CTX.clear()
+    _TILE_CTX.clear()
 
 
 def tile_stats(device, H, W):
     """seg_stats of the last native tile (tile_ecoli) run on the current stream's (H, W) context"""
     import ctypes
     seg = ctypes.c_void_p()
-    _lib.call("hrf_tile_ctx_seg", _tile_ctx(torch.device(device), H, W), ctypes.addressof(seg))
     out = (ctypes.c_int32 * 4)()
-    _lib.call("hrf_seg_ctx_stats", seg, ctypes.addressof(out))
+    with _TILE_CTX.use(device, H, W) as ctx:
+        _lib.call("hrf_tile_ctx_seg", ctx, ctypes.addressof(seg))
+        _lib.call("hrf_seg_ctx_stats", seg, ctypes.addressof(out))
     return dict(zip(("passes", "contests", "rounds", "marker_ties"), list(out)))
 
 
@@ -1014,13 +1080,14 @@ def tile_ecoli(lasers, cal, refx, lib, lib_flags, variant=1, flag_thr=0.1, per_p
     fl = _dev(lib_flags, torch.float64, "library flags") if lib_flags is not None else None
     if variant and fl is None:
         raise ValueError("tile_ecoli: the gated variants need the library's presence flags")
+    if per_pixel:
+        check_refx_table(refx, R, 95, REFERENCE_LAYOUTS[0], "tile_ecoli")
     calp = None
     if cal is not None:
         c = _dev(cal, torch.float32, "calibration")
         if tuple(c.shape) != (H, W):
             raise ValueError("tile_ecoli: the flat field must be an (H, W) plane")
         calp = _ptr(c)
-    ctx = _tile_ctx(dev, H, W)
     ptrs = (ctypes.c_void_p * 5)(*[l.data_ptr() for l in srcs])
     key = (dev, H, W)
     cap = _CELL_CAP.get(key, 4096)
@@ -1045,22 +1112,24 @@ def tile_ecoli(lasers, cal, refx, lib, lib_flags, variant=1, flag_thr=0.1, per_p
         e0.record(st)        # creates the events (recorded again inside the call)
         e1.record(st)
         pix_events.append((e0, e1))
-    _lib.call("hrf_tile_ecoli", ctx, ctypes.cast(ptrs, ctypes.c_void_p), calp,
-              _ptr(refx) if per_pixel else None, _ptr(lib), _ptr(fl) if fl is not None else None, R, int(variant),
-              float(flag_thr), int(bool(per_pixel)), _ptr(seg), _ptr(pix_idx) if per_pixel else None,
-              _ptr(pix_dist) if per_pixel else None, cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx), _ptr(cdist),
-              _ptr(ident), _ptr(counts), _ptr(ncells), ctypes.addressof(mx), _stream(),
-              ctypes.c_void_p(side.cuda_stream) if side is not None else None,
-              ctypes.c_void_p(e0.cuda_event) if e0 is not None else None,
-              ctypes.c_void_p(e1.cuda_event) if e1 is not None else None)
+    with _TILE_CTX.use(dev, H, W) as ctx:
+        _lib.call("hrf_tile_ecoli", ctx, ctypes.cast(ptrs, ctypes.c_void_p), calp, _ptr(refx) if per_pixel else None,
+                  _ptr(lib), _ptr(fl) if fl is not None else None, R, int(variant), float(flag_thr),
+                  int(bool(per_pixel)), _ptr(seg), _ptr(pix_idx) if per_pixel else None,
+                  _ptr(pix_dist) if per_pixel else None, cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx),
+                  _ptr(cdist), _ptr(ident), _ptr(counts), _ptr(ncells), ctypes.addressof(mx), _stream(),
+                  ctypes.c_void_p(side.cuda_stream) if side is not None else None,
+                  ctypes.c_void_p(e0.cuda_event) if e0 is not None else None,
+                  ctypes.c_void_p(e1.cuda_event) if e1 is not None else None)
     maxlab = mx.value
     if maxlab > cap:            # the per-cell part was left for buffers that hold every label
         cap = 1 << max(12, (maxlab - 1).bit_length())
         _CELL_CAP[key] = cap
         labs, avg, avgn, cidx, cdist = rows(cap)
-        _lib.call("hrf_tile_ecoli_cells", ctx, _ptr(seg), _ptr(lib), _ptr(fl) if fl is not None else None, R,
-                  int(variant), float(flag_thr), cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx), _ptr(cdist),
-                  _ptr(ident), _ptr(counts), _ptr(ncells), _stream())
+        with _TILE_CTX.use(dev, H, W) as ctx:
+            _lib.call("hrf_tile_ecoli_cells", ctx, _ptr(seg), _ptr(lib), _ptr(fl) if fl is not None else None, R,
+                      int(variant), float(flag_thr), cap, _ptr(labs), _ptr(avg), _ptr(avgn), _ptr(cidx),
+                      _ptr(cdist), _ptr(ident), _ptr(counts), _ptr(ncells), _stream())
     return dict(seg=seg, ident=ident, counts=counts, ncells=ncells, maxlab=maxlab, labels=labs, avgint=avg,
                 avgint_norm=avgn, cell_idx=cidx, cell_dist=cdist, pixel_idx=pix_idx, pixel_dist=pix_dist)
 
@@ -1071,7 +1140,8 @@ def seg_stats(device, H, W):
     equal-valued markers of different labels, DESIGN.md "Watershed")"""
     import ctypes
     out = (ctypes.c_int32 * 4)()
-    _lib.call("hrf_seg_ctx_stats", _seg_ctx(torch.device(device), H, W), ctypes.addressof(out))
+    with _SEG_CTX.use(device, H, W) as ctx:
+        _lib.call("hrf_seg_ctx_stats", ctx, ctypes.addressof(out))
     return dict(zip(("passes", "contests", "rounds", "marker_ties"), list(out)))
 
 
@@ -1085,14 +1155,14 @@ def segment_ecoli_native(stack, image_cn=None):
         cn = _dev(image_cn, torch.float64, "image_cn")
         H, W = cn.shape
         seg = torch.empty((H, W), dtype=torch.int32, device=cn.device)
-        _lib.call("hrf_segment_ecoli_cn", _seg_ctx(cn.device, H, W), _ptr(cn), _ptr(seg), ctypes.addressof(mx),
-                  _stream())
+        with _SEG_CTX.use(cn.device, H, W) as ctx:
+            _lib.call("hrf_segment_ecoli_cn", ctx, _ptr(cn), _ptr(seg), ctypes.addressof(mx), _stream())
         return seg, mx.value
     stack = _dev(stack, torch.float32, "stack")
     H, W, C = stack.shape
     seg = torch.empty((H, W), dtype=torch.int32, device=stack.device)
-    _lib.call("hrf_segment_ecoli", _seg_ctx(stack.device, H, W), _ptr(stack), C, _ptr(seg), ctypes.addressof(mx),
-              _stream())
+    with _SEG_CTX.use(stack.device, H, W) as ctx:
+        _lib.call("hrf_segment_ecoli", ctx, _ptr(stack), C, _ptr(seg), ctypes.addressof(mx), _stream())
     return seg, mx.value
 
 
@@ -1110,8 +1180,9 @@ def segment_multispecies_native(stack, cal=None):
     s = torch.empty((H, W), dtype=torch.float64, device=stack.device)
     fb = torch.empty((H, W), dtype=torch.float64, device=stack.device)
     n = ctypes.c_int32(0)
-    _lib.call("hrf_segment_multispecies", _seg_ctx(stack.device, H, W), _ptr(stack), C, calp, sp, sc, c0, c1,
-              _ptr(seg), ctypes.addressof(n), _ptr(s), _ptr(fb), _stream())
+    with _SEG_CTX.use(stack.device, H, W) as ctx:
+        _lib.call("hrf_segment_multispecies", ctx, _ptr(stack), C, calp, sp, sc, c0, c1, _ptr(seg),
+                  ctypes.addressof(n), _ptr(s), _ptr(fb), _stream())
     return seg, n.value, s, fb
 
 

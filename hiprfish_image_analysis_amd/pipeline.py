@@ -252,6 +252,7 @@ class Library:
     bounds: tuple
     nbit: int
     _refx: torch.Tensor | None = None
+    _refx2: torch.Tensor | None = None
     _flags: dict = field(default_factory=dict)
 
     @property
@@ -262,6 +263,16 @@ class Library:
         if self._refx is None:
             self._refx = K.classify_prepare(self.spectra.to(torch.float32), self.bounds)
         return self._refx
+
+    def refx_table(self):
+        """the mode-2 table the pixel-table classifier (register_tile, process_tile_native) reads,
+        whatever mode refx() was prepared in"""
+        r = self.refx()
+        if K.refx_mode(r, self.spectra.shape[1], self.bounds) == 2:
+            return r
+        if self._refx2 is None:
+            self._refx2 = K.classify_prepare(self.spectra.to(torch.float32), self.bounds, mode=2)
+        return self._refx2
 
     def presence_flags(self, thr: float = 0.1) -> torch.Tensor:
         """per-segment presence of the library rows (max over the segment > thr), computed once
@@ -369,7 +380,7 @@ def start_tile(stack, lib: Library, per_pixel: bool = True, overlap: bool = True
     pix = None
     side = None
     if per_pixel:
-        refx = lib.refx()                                     # prepared on the caller's stream
+        refx = lib.refx_table() if reg else lib.refx()        # prepared on the caller's stream
         side = _side_stream(main) if overlap else main
         if overlap:
             side.wait_stream(main)                            # stack (and refx) ready
@@ -463,7 +474,7 @@ def process_tile_native(lasers, lib: Library, calibration=None, per_pixel: bool 
     (H, W powers of two)."""
     main = torch.cuda.current_stream(lasers[0].device)
     side = _side_stream(main) if (per_pixel and overlap) else None
-    refx = lib.refx() if per_pixel else None
+    refx = lib.refx_table() if per_pixel else None
     flags = lib.presence_flags() if variant else None
     d = K.tile_ecoli(lasers, calibration, refx, lib.spectra, flags, variant=variant, per_pixel=per_pixel, side=side,
                      pix_events=pixel_events)

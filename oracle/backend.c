@@ -458,3 +458,10 @@ void oracle_umap_refine(const int32_t *idx, const float *memb, int64_t nq, int k
   free(eps);
   free(tl);
 }
+
+/* correctly rounded log / log10 (detmath.h hrf_cr_log*, the functions libhrf's image_cn uses):
+ * image_cn = log(sum + 1e-2) (ecoli measurement.py:72), log10(sum + 1) (biofilm :831).
+ * mode 0: log, 1: log10 */
+__attribute__((visibility("default"))) void oracle_cr_log(const double *x, int64_t n, int mode, double *out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = mode ? hrf_cr_log10(x[i]) : hrf_cr_log(x[i]);
+}

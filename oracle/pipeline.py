@@ -37,7 +37,8 @@ def erosion_seeds(cell_sm, area_max=600, min_obj=10):
 def segment_ecoli(stack, keep=None, image_cn=None):
     """ecoli measurement.py:44-127 on the registered (H, W, C) stack"""
     if image_cn is None:
-        image_cn = np.log(np.sum(stack.astype(np.float64), axis=2) + 1e-2)         # :71-72
+        # :71-72 np.log(...), correctly rounded (numpy's own log varies by CPU in the last ulp)
+        image_cn = O.cr_log(np.sum(stack.astype(np.float64), axis=2) + 1e-2)
     l2, _, _ = O.kmeans_sk(image_cn, 2)                                           # :73
     i0, i1 = (image_cn[l2 == j].mean() if (l2 == j).any() else np.nan for j in (0, 1))
     rough_mask = (l2 == 1) if i0 < i1 else (l2 == 0)                              # :74-84

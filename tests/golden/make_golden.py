@@ -15,6 +15,9 @@ box except the .npz data it writes.  Reference code is executed, never copied:
   @numba.njit decorator dropped (numba is absent), run as plain Python.
 * CC labelling against scipy.ndimage.label (raster-first numbering, the semantics skimage.label
   shares), and the partition sklearn 1.7.2 KMeans(random_state=0, n_init=10) finds on 1-D data.
+* the binary morphology skimage 0.14 wraps (scipy.ndimage binary_erosion / dilation /
+  fill_holes, label + bincount sieves) and the erosion-seed loop composed from them
+  (`make_golden.py morphology` -> morphology.npz).
 
 Usage: python tests/golden/make_golden.py   (writes tests/golden/*.npz)
 """
@@ -331,8 +334,116 @@ def main_backend():
     print("backend.npz written")
 
 
+CROSS = np.array([[0, 1, 0], [1, 1, 1], [0, 1, 0]], bool)
+SQUARE = np.ones((3, 3), bool)
+
+
+def _rso_bool(m, min_size, conn):
+    """skimage.morphology.remove_small_objects(bool image, min_size, connectivity) (0.14-era source):
+    ndi.label with generate_binary_structure(2, conn), bincount of the labels, components with
+    size < min_size set to False"""
+    from scipy import ndimage as ndi
+    ccs, _ = ndi.label(m, CROSS if conn == 1 else SQUARE)
+    sizes = np.bincount(ccs.ravel())
+    out = m.copy()
+    out[sizes[ccs] < min_size] = False
+    return out
+
+
+def _seeds_scipy(cell_sm):
+    """ecoli measurement.py:97-112 composed from scipy.ndimage primitives: skimage's label
+    (8-connected), regionprops areas (bincount), binary_erosion (cross, border_value=True),
+    remove_small_objects(., 10) (4-connected), then label(rso(label(dist_be), 10)).  The loop is
+    capped as libhrf's (4 (H + W) + 8 rounds; the fixtures never reach the cap)."""
+    from scipy import ndimage as ndi
+    H, W = cell_sm.shape
+    lab, _ = ndi.label(cell_sm, SQUARE)
+    be = np.zeros(cell_sm.shape, bool)
+    rounds = 0
+    while lab.max() > 0:
+        assert rounds < 4 * (H + W) + 8
+        rounds += 1
+        sizes = np.bincount(lab.ravel())
+        small = (lab > 0) & (sizes[lab] < 600)
+        be |= small
+        lab[small] = 0
+        er = ndi.binary_erosion(lab > 0, CROSS, border_value=1)
+        lab, _ = ndi.label(_rso_bool(er, 10, 1), SQUARE)
+    lb, _ = ndi.label(be, SQUARE)
+    sizes = np.bincount(lb.ravel())
+    lb[sizes[lb] < 10] = 0
+    seeds, n = ndi.label(lb > 0, SQUARE)
+    return be, seeds.astype(np.int32), rounds
+
+
+def main_morphology():
+    """morphology.npz: the a9 / a11 / a13 primitives on E. coli-like masks, computed by
+    scipy.ndimage (the functions skimage 0.14's binary morphology wraps): binary_erosion with
+    the cross and border_value=1 (skimage.morphology.binary_erosion), binary_dilation,
+    skimage's binary_opening = dilation(erosion), remove_small_objects / remove_small_holes as
+    ndi.label + a bincount sieve, binary_fill_holes, and the erosion-seed loop of ecoli :97-112.
+    Masks: the interior / cell_sm / rough masks of synthetic 256^2 E. coli tiles (plain and
+    12-bit quantised; the oracle pipeline only makes the INPUTS), thresholded smooth noise with
+    holes on ragged shapes, and degenerate cases."""
+    import torch
+    from scipy import ndimage as ndi
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, REPO)
+    import pipeline as OP
+    from hiprfish_image_analysis_amd import synthetic as S
+    rng = np.random.default_rng(20190401)
+    masks = {}
+    for name, seed, q in [("ecoli_a", 301, None), ("ecoli_q", 302, 4095)]:
+        st = S.tile(256, 256, seed=seed, device="cpu")[0]
+        if q:
+            st = (torch.round(st.double() * q) / q).float()
+        keep = {}
+        OP.segment_ecoli(st.numpy(), keep=keep)
+        masks[name + "_interior"] = keep["interior"]
+        masks[name + "_cellsm"] = keep["cell_sm"]
+        masks[name + "_rough"] = keep["rough_mask"]
+    for name, shape, thr in [("blob_a", (96, 112), 0.55), ("blob_b", (61, 47), 0.5), ("blob_c", (128, 128), 0.6)]:
+        f = ndi.gaussian_filter(rng.random(shape), 2.0)
+        masks[name] = f > np.quantile(f, thr)
+    edge = np.zeros((20, 24), bool)
+    edge[:, :3] = True
+    edge[5:9, 10:15] = True
+    edge[6, 12] = False
+    masks["edge"] = edge
+    masks["empty"] = np.zeros((9, 13), bool)
+    masks["full"] = np.ones((7, 5), bool)
+    one = np.zeros((8, 8), bool)
+    one[3, 4] = True
+    masks["one"] = one
+    out = {}
+    for name, m in masks.items():
+        m = np.ascontiguousarray(m, bool)
+        ero = ndi.binary_erosion(m, CROSS, border_value=1)
+        out["m_" + name] = m
+        out["ero_" + name] = ero
+        out["dil_" + name] = ndi.binary_dilation(m, CROSS)
+        out["open_" + name] = ndi.binary_dilation(ero, CROSS)
+        out["rso50c1_" + name] = _rso_bool(m, 50, 1)
+        out["rso10c1_" + name] = _rso_bool(m, 10, 1)
+        out["rso10c2_" + name] = _rso_bool(m, 10, 2)
+        out["rsh64_" + name] = ~_rso_bool(~m, 64, 1)
+        out["fill_" + name] = ndi.binary_fill_holes(m)
+        # ecoli :95-96 cell_sm = rso(opening(rsh(interior)), 50)
+        out["cellsm_" + name] = _rso_bool(ndi.binary_dilation(ndi.binary_erosion(~_rso_bool(~m, 64, 1), CROSS,
+                                                                                     border_value=1), CROSS), 50, 1)
+    for name in ("ecoli_a_cellsm", "ecoli_q_cellsm", "blob_a", "blob_c", "edge", "one", "empty"):
+        be, seeds, rounds = _seeds_scipy(out["m_" + name])
+        out["be_" + name] = be
+        out["seeds_" + name] = seeds
+        print("seeds", name, "rounds", rounds, "n", int(seeds.max()))
+    np.savez_compressed(os.path.join(HERE, "morphology.npz"), **out)
+    print("morphology.npz written")
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["v3"]:
+    if sys.argv[1:] == ["morphology"]:
+        main_morphology()
+    elif sys.argv[1:] == ["v3"]:
         main_v3()
     elif sys.argv[1:] == ["kmeans_images"]:
         main_kmeans_images()

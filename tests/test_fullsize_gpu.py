@@ -139,7 +139,14 @@ def test_fullsize_bench_workload(mods, orc, q):
     oreg = OP.register_stacks(hl, shifts, True).astype(np.float32)
     del hl
     assert np.array_equal(host(reg), oreg)
-    np.testing.assert_allclose(host(cn), np.log(np.sum(oreg.astype(np.float64), axis=2) + 1e-2), rtol=4e-16, atol=0)
+    # image_cn bit for bit: the correctly rounded log of numpy's pairwise channel sum; numpy's own
+    # log differs from it in the last ulp on a few pixels (reported)
+    ssum = np.sum(oreg.astype(np.float64), axis=2) + 1e-2
+    want_cn = orc.cr_log(ssum)
+    assert np.array_equal(host(cn), want_cn)
+    print("image_cn pixels where np.log differs from the correctly rounded log: %d of %d"
+          % (int((np.log(ssum) != want_cn).sum()), ssum.size))
+    del ssum, want_cn
     o = OP.process_tile(oreg, ref, S.ECOLI_BOUNDS, calibration=host(cal), variant=1)
     seg = host(res.meas.segmentation)
     assert np.array_equal(seg, o["segmentation"])

@@ -49,6 +49,40 @@ def test_label_golden(K, golden):
     assert np.array_equal(host(l4), g["l4"]) and n4 == g["l4"].max()
 
 
+# ---- a9 / a11 / a13 against scipy.ndimage (tests/golden/make_golden.py morphology) ----------
+def test_morphology_matches_scipy_fixtures(K, golden):
+    """the device morphology on the scipy-generated fixtures: binary_erosion(cross, border 1),
+    binary_dilation, skimage's opening, remove_small_objects (4- and 8-connected),
+    remove_small_holes, binary_fill_holes, ecoli :95-96's cell_sm chain"""
+    g = golden("morphology")
+    names = sorted(k[2:] for k in g.files if k.startswith("m_"))
+    for n in names:
+        m = dev(g["m_" + n].astype(np.uint8))
+        b = lambda t: host(t).astype(bool)   # noqa: E731
+        assert np.array_equal(b(K.binary_erosion(m, 1)), g["ero_" + n]), n
+        assert np.array_equal(b(K.binary_dilation(m)), g["dil_" + n]), n
+        assert np.array_equal(b(K.binary_opening(m)), g["open_" + n]), n
+        assert np.array_equal(b(K.remove_small_objects(m, 50, conn=1)), g["rso50c1_" + n]), n
+        assert np.array_equal(b(K.remove_small_objects(m, 10, conn=1)), g["rso10c1_" + n]), n
+        assert np.array_equal(b(K.remove_small_objects(m, 10, conn=2)), g["rso10c2_" + n]), n
+        assert np.array_equal(b(K.remove_small_holes(m, 64, 1)), g["rsh64_" + n]), n
+        assert np.array_equal(b(K.fill_holes(m)), g["fill_" + n]), n
+        cs = K.remove_small_objects(K.binary_opening(K.remove_small_holes(m, 64, 1)), 50, conn=1)
+        assert np.array_equal(b(cs), g["cellsm_" + n]), n
+
+
+def test_erosion_seeds_match_scipy_fixtures(K, golden):
+    """ecoli :97-112 on the device (per-component seeding kernel + the label sieve) equals the
+    loop composed from scipy.ndimage"""
+    g = golden("morphology")
+    for n in sorted(k[3:] for k in g.files if k.startswith("be_")):
+        m = dev(g["m_" + n].astype(np.uint8))
+        be = K.erosion_seeds(m)
+        assert np.array_equal(host(be).astype(bool), g["be_" + n]), n
+        seeds, ns = K.label(K.remove_small_objects(be, 10, conn=2), conn=2)
+        assert np.array_equal(host(seeds), g["seeds_" + n]) and ns == g["seeds_" + n].max(), n
+
+
 @pytest.mark.parametrize("shape", SHAPES)
 @pytest.mark.parametrize("conn", [1, 2])
 def test_label_vs_oracle(K, orc, shape, conn):
@@ -460,8 +494,13 @@ def test_register_assemble_and_channel_sum(K):
     assert np.array_equal(out, refst)
     s0 = host(K.channel_sum(dev(out), mode=0))
     assert np.array_equal(s0, np.sum(refst.astype(np.float64), axis=2))
+    # image_cn (ecoli :72) and the biofilm log10 (:831): the correctly rounded log bit for bit
+    import oracle as O
     s1 = host(K.channel_sum(dev(out), mode=1))
-    np.testing.assert_allclose(s1, np.log(np.sum(refst.astype(np.float64), axis=2) + 1e-2), rtol=4e-16, atol=0)
+    assert np.array_equal(s1, O.cr_log(np.sum(refst.astype(np.float64), axis=2) + 1e-2))
+    np.testing.assert_allclose(s1, np.log(np.sum(refst.astype(np.float64), axis=2) + 1e-2), rtol=3e-16, atol=0)
+    s10 = host(K.channel_sum(dev(out), mode=2))
+    assert np.array_equal(s10, O.cr_log10(np.sum(refst.astype(np.float64), axis=2) + 1.0))
     m = rng.random((H, W)) > 0.5
     s2 = host(K.channel_sum(dev(out), mask=dev(m), mode=0, negate=True))
     assert np.array_equal(s2, -np.sum(refst.astype(np.float64) * m[:, :, None], axis=2))

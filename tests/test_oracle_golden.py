@@ -219,3 +219,68 @@ def test_kmeans_matches_sklearn_random(orc, block):
         lab, cen, info = orc.kmeans_sk(x, k)
         sk = KMeans(n_clusters=k, random_state=0, n_init=10).fit(x.reshape(-1, 1))
         assert np.array_equal(lab, sk.labels_), (block, t, n, k)
+
+
+# ---- a9 / a11 / a13 morphology pinned to scipy.ndimage (make_golden.py morphology) -----------
+def _morph_names(g):
+    return sorted(k[2:] for k in g.files if k.startswith("m_"))
+
+
+def test_morphology_primitives_match_scipy(orc, golden):
+    """skimage 0.14's binary morphology is scipy.ndimage underneath: binary_erosion(cross,
+    border_value=True) (ecoli :107, :122), binary_dilation, binary_opening = dilation(erosion)
+    (:95, multispecies :136), remove_small_objects / remove_small_holes as ndi.label + bincount
+    sieves (:95-96, :108, :111), binary_fill_holes (multispecies :138-139)"""
+    g = golden("morphology")
+    names = _morph_names(g)
+    assert len(names) >= 10
+    for n in names:
+        m = g["m_" + n]
+        assert np.array_equal(orc.erode(m, 1), g["ero_" + n]), n
+        assert np.array_equal(orc.dilate(m), g["dil_" + n]), n
+        assert np.array_equal(orc.opening(m), g["open_" + n]), n
+        assert np.array_equal(orc.remove_small_objects_mask(m, 50, 1), g["rso50c1_" + n]), n
+        assert np.array_equal(orc.remove_small_objects_mask(m, 10, 1), g["rso10c1_" + n]), n
+        assert np.array_equal(orc.remove_small_objects_mask(m, 10, 2), g["rso10c2_" + n]), n
+        assert np.array_equal(orc.remove_small_holes(m, 64, 1), g["rsh64_" + n]), n
+        assert np.array_equal(orc.fill_holes(m), g["fill_" + n]), n
+        cs = orc.remove_small_objects_mask(orc.opening(orc.remove_small_holes(m, 64, 1)), 50, 1)
+        assert np.array_equal(cs, g["cellsm_" + n]), n
+
+
+def test_erosion_seed_loop_matches_scipy(orc, golden):
+    """ecoli :97-112 (freeze < 600 px, erode, sieve < 10 px, repeat; then
+    label(rso(label(dist_be), 10))) composed from scipy.ndimage equals the restatement"""
+    import pipeline as OP
+    g = golden("morphology")
+    seen = 0
+    for n in _morph_names(g):
+        if "be_" + n not in g.files:
+            continue
+        be = OP.erosion_seeds(g["m_" + n])
+        assert np.array_equal(be, g["be_" + n]), n
+        seeds, _ = orc.label(orc.remove_small_objects_mask(be, 10, 2).astype(np.int32), 2)
+        assert np.array_equal(seeds, g["seeds_" + n]), n
+        seen += int(g["seeds_" + n].max())
+    assert seen > 80
+
+
+def test_cr_log_is_correctly_rounded(orc):
+    """detmath.h hrf_cr_log / hrf_cr_log10 (image_cn, ecoli :72; biofilm :831) against Python's
+    decimal ln / log10 at 50 digits, on the image_cn range, near 1, at the table knots, across
+    the exponent range and on subnormals"""
+    import decimal
+    decimal.getcontext().prec = 50
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(0.01, 96.0, 6000), np.exp(rng.uniform(-744, 709, 2000)),
+                        1 + rng.uniform(-1e-3, 1e-3, 1000), 1 + rng.uniform(-1e-13, 1e-13, 300),
+                        np.arange(96, 193) / 128.0, np.nextafter(np.arange(96, 193) / 128.0, 0),
+                        2.0 ** np.arange(-1074, 1024, 11.0), [5e-324, 2.2e-308, 1.7976931348623157e308, 1.0,
+                                                             0.01, 10.0, 100.0, 1e-2 + 1.0]])
+    got = orc.cr_log(x)
+    want = np.array([float(decimal.Decimal(v).ln()) for v in x])
+    assert np.array_equal(got, want)
+    got10 = orc.cr_log10(x)
+    want10 = np.array([float(decimal.Decimal(v).log10()) for v in x])
+    assert np.array_equal(got10, want10)
+    assert orc.cr_log(np.array([0.0]))[0] == -np.inf and np.isnan(orc.cr_log(np.array([-1.0]))[0])

@@ -145,3 +145,98 @@ def test_tile_native_rejects_bad_input(mods):
         P.process_tile_native(lasers[:4], lib)
     with pytest.raises(ValueError):
         K.tile_ecoli(lasers, None, None, lib.spectra, None, variant=1, per_pixel=False)
+
+
+def test_tile_native_six_streams_fullsize(mods):
+    """the bench's schedule at the bench's size: six host threads, six high-priority streams (each
+    with its own tile context and classifier side stream), 2048^2 tiles, every tile twice --
+    equal to the same tiles run one at a time (bench.py main, DESIGN.md 'Concurrency on one GPU')"""
+    K, P, S = mods
+    H = W = 2048
+    T = 6
+    lib = _lib(P, S)
+    lib.refx_table()
+    lib.presence_flags()
+    tiles = [_lasers(S, H, W, 20190301 + i) for i in range(T)]
+    cal = S.flat_field(H, W, device="cuda")
+    want = [P.process_tile_native(t, lib, calibration=cal, variant=1) for t in tiles]
+    torch.cuda.synchronize()
+    prio = torch.cuda.Stream.priority_range()[1]
+    streams = [torch.cuda.Stream(priority=prio) for _ in range(T)]
+    got = [None] * T
+    errs = []
+
+    def run(j):
+        try:
+            with torch.cuda.stream(streams[j]):
+                for _ in range(2):
+                    got[j] = P.process_tile_native(tiles[j], lib, calibration=cal, variant=1)
+                streams[j].synchronize()
+        except Exception as e:       # surfaced below
+            errs.append(e)
+    th = [threading.Thread(target=run, args=(j,)) for j in range(T)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for g, w in zip(got, want):
+        assert g.ncells > 300
+        _check(g, w)
+
+
+def test_tile_context_cache_bounded(mods):
+    """a caller that makes a fresh stream per tile: the contexts stay within the cache's cap and
+    device memory does not grow with the number of streams"""
+    K, P, S = mods
+    H = W = 512
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190112)
+    cal = S.flat_field(H, W, device="cuda")
+    want = P.process_tile_native(lasers, lib, calibration=cal, variant=1)
+    torch.cuda.synchronize()
+    cn = P.register_tile(lasers).image_cn
+    K.release_contexts()
+    cap = K._TILE_CTX.cap
+
+    def one():
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            r = P.process_tile_native(lasers, lib, calibration=cal, variant=1)
+            K.segment_ecoli_native(None, image_cn=cn)
+        s.synchronize()
+        return r
+    for _ in range(cap):
+        one()
+    torch.cuda.synchronize()
+    free_full = torch.cuda.mem_get_info()[0]
+    for _ in range(20):
+        r = one()
+        assert len(K._TILE_CTX) <= cap and len(K._SEG_CTX) <= cap
+    torch.cuda.synchronize()
+    grown = free_full - torch.cuda.mem_get_info()[0]
+    assert grown < 64 << 20, "device memory grew by %d bytes over 20 fresh streams" % grown
+    _check(r, want)
+    K.release_contexts()
+    assert len(K._TILE_CTX) == 0 and len(K._SEG_CTX) == 0
+
+
+def test_pixel_table_needs_mode2_table(mods):
+    """the pixel-table classifier refuses a mode-0/1 prepared library (it would read it as split-fp16
+    rows of another pitch); the Library hands it a mode-2 table whatever refx() holds"""
+    K, P, S = mods
+    H = W = 256
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190113)
+    rt = P.register_tile(lasers)
+    for mode in (0, 1):
+        bad = K.classify_prepare(lib.spectra.to(torch.float32), lib.bounds, mode=mode)
+        with pytest.raises(ValueError):
+            K.classify_pixels_table(rt.pixtable, bad, lib.R)
+        with pytest.raises(ValueError):
+            K.tile_ecoli(lasers, None, bad, lib.spectra, lib.presence_flags(), variant=1)
+    want = P.process_tile_native(lasers, lib, variant=1)
+    lib1 = _lib(P, S)
+    lib1._refx = K.classify_prepare(lib1.spectra.to(torch.float32), lib1.bounds, mode=1)
+    got = P.process_tile_native(lasers, lib1, variant=1)
+    torch.cuda.synchronize()
+    _check(got, want)
