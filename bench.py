@@ -48,7 +48,8 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak 
 F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
 # the timed path classifies from the registered tile's pixel table (pipeline.register_tile)
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
-               2: "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3>"}
+               2: "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 3>",
+               "t": "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3>"}
 REGTILE = os.environ.get("HRF_REGTILE", "1") != "0"   # A/B switch: 0 = register_stack + in-kernel operand build
 # HRF_LOOKAHEAD=1: each worker starts tile i+1 (registration + per-pixel classifier) before it
 # finishes tile i -- neutral with six tiles in flight (1046.7 vs 1048.5 Mpix/s, three interleaved
@@ -204,36 +205,63 @@ def _event_ms(fn, n=5):
     return a.elapsed_time(b) / n
 
 
-def _hbm_kernels(dev):
-    """The streaming (HBM-bound) kernels of the path on one resident cfg3 tile, isolated:
-    algorithmic bytes per launch / mean launch time (HIP events) against the 8 TB/s peak."""
+# The streaming kernels of the timed path (hrf_tile_ecoli, tile.hip) and the kernel symbols
+# rocprofv3 lists them under -- the hbm_kernels rows and tools/time_kernels.py path's PMC passes
+HBM_KERNELS = {"channel_max_multi": "channel_max_multi_pf_kernel",
+               "assemble_pixtable": "assemble_ecoli_kernel<false, 3>",
+               "label_sums_lasers_cal": "label_sums_lasers_kernel<true>"}
+
+
+def path_kernel_rows(lasers, cal, lib):
+    """(name -> (launch, algorithmic bytes)) for the streaming kernels the timed tile runs, on one
+    resident cfg3 tile: the five per-laser channel-max projections (ecoli :45-50: the lasers read,
+    five f64 planes written), the registered assembly writing image_cn and the classifier's pixel
+    table (:51-72), and the flat-fielded per-cell sums read straight from the lasers (:147-155:
+    the label map, and for every labelled pixel its 95 channels + the flat-field value)."""
+    import torch
+
+    from hiprfish_image_analysis_amd import _lib
     from hiprfish_image_analysis_amd import kernels as K
     from hiprfish_image_analysis_amd import pipeline as P
-    from hiprfish_image_analysis_amd import synthetic as S
-    stack, _, _, _ = S.tile(H, W, seed=20190301, device=dev)
-    seg, maxlab = P.segment_ecoli(stack)
+    HW = H * W
+    shifts = P.estimate_shifts(lasers, device=True)
+    res = P.process_tile_native(lasers, lib, calibration=cal, per_pixel=False, variant=1)
+    seg, maxlab = res.meas.segmentation, res.meas.maxlab
     fg = int(K.count_nonzero(seg))
-    lasers = S.laser_split(stack)
-    rows = {
-        # bytes: stack read + f64 image written
-        "channel_sum": (lambda: K.channel_sum(stack, mode=1), H * W * (4 * C + 8)),
-        # bytes: per-laser stacks read + assembled stack written
-        "register_assemble": (lambda: K.register_assemble(lasers, S.LASER_SHIFTS, apply_mask=True), H * W * 8 * C),
-        # bytes: label map read + the spectra of labelled pixels read (background is skipped)
-        "label_sums": (lambda: K.label_sums(stack, seg, maxlab), H * W * 4 + fg * 4 * C),
-    }
+    b = np.array(P.ECOLI_BOUNDS, np.int32)
+    tb = int(_lib.lib().hrf_pixtable_bytes(HW, C, b.ctypes.data, len(b) - 1))
+    torch.cuda.synchronize()
+    return {
+        "channel_max_multi": (lambda: K.channel_max_multi(lasers, stacked=True), HW * (4 * C + 5 * 8)),
+        "assemble_pixtable": (lambda: K.register_assemble_pixtable(lasers, shifts, True, cn_mode=1),
+                              HW * 4 * C + tb + HW // 16 + HW * 8),
+        "label_sums_lasers_cal": (lambda: K.label_sums_lasers(lasers, shifts, seg, maxlab, True, cal=cal,
+                                                              cal_range=(0, 32)),
+                                  HW * 4 + fg * (4 * C + 4)),
+    }, {"foreground_px": fg, "labels": maxlab, "pixtable_bytes": tb}
+
+
+def _hbm_kernels(lasers, cal, lib):
+    """The timed path's streaming (HBM-bound) kernels isolated on one resident cfg3 tile:
+    algorithmic bytes per launch / mean launch time (HIP events) against the 8 TB/s peak, with the
+    HBM traffic of the same launches from the committed PMC passes (profiles/hbm_kernels_pmc.json,
+    tools/gpu_pmc_hbm.sh)."""
+    rows, info = path_kernel_rows(lasers, cal, lib)
     pmc = {}
-    try:   # HBM bytes per launch from the committed PMC passes (profiles/hbm_kernels_pmc.json)
-        pmc = json.load(open(os.path.join(REPO, "profiles", "hbm_kernels_pmc.json")))["kernels"]
+    try:
+        pmc = json.load(open(os.path.join(REPO, "profiles", "hbm_kernels_pmc.json")))
     except Exception:
         pmc = {}
     out = {}
     for name, (fn, nbytes) in rows.items():
         ms = _event_ms(fn, 10)
         gbs = nbytes / (ms * 1e-3) / 1e9
-        out[name] = {"ms": round(ms, 4), "algorithmic_bytes": nbytes, "achieved_GBps": round(gbs, 1),
-                     "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4),
-                     "traffic": pmc.get(name, {}).get("hbm_bytes_per_launch")}
+        rec = pmc.get("kernels", {}).get(name, {})
+        out[name] = {"kernel": HBM_KERNELS[name], "ms": round(ms, 4), "algorithmic_bytes": nbytes,
+                     "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4),
+                     "traffic": rec.get("hbm_bytes_per_launch"),
+                     "traffic_ratio": rec.get("traffic_ratio"), "pmc_round": pmc.get("round")}
+    out["tile"] = info
     return out
 
 
@@ -381,7 +409,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s",
                                 "frac": round(ach3 / F64_VALU_PEAK_TOPS, 4)}}
     _progress("extras: cfg4 done")
-    out["hbm_kernels"] = _hbm_kernels(dev)
+    out["hbm_kernels"] = _hbm_kernels(tiles[0][0], tiles[0][1], lib_main)
     return out
 
 
@@ -592,45 +620,61 @@ def main():
         out["config"]["dist_backend"] = backend
     if per_pixel and ev:
         from hiprfish_image_analysis_amd import kernels as K
-        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-        # the same kernel alone on the GPU (after the timed region): with the overlap the
-        # timed-region duration includes the compute units it shares with the segmentation
-        rt0 = P.register_tile(tiles[0][0])
-        ms_iso = _event_ms(lambda: K.classify_pixels_table(rt0.pixtable, lib.refx(), lib.R), 3)
-        del rt0
+        ms_in = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        # The classifier's own efficiency: the same launch alone on its stream after the timed
+        # region (HIP events, mean of 5).  Inside the timed region the launch shares the CUs with
+        # five other tiles' chains at higher priority, so its event time there (ms_in) is overlap,
+        # not kernel work: reported as a note, with the aggregate over the driver's step time.
+        if REGTILE:
+            rt0 = P.register_tile(tiles[0][0])
+            refx = lib.refx_table()
+            ms_iso = _event_ms(lambda: K.classify_pixels_table(rt0.pixtable, refx, lib.R), 5)
+            del rt0
+            mode = 2
+        else:
+            st0, _ = P.register_stack(tiles[0][0], want_cn=True)
+            refx = lib.refx()
+            mode = K.refx_mode(refx, C, bounds)
+            ms_iso = _event_ms(lambda: K.classify_pixels(st0, refx, lib.R, bounds), 5)
+            del st0
+        kname = KERNEL_NAME["t" if REGTILE else mode]
         flops = 2.0 * H * W * lib.R * C            # algorithmic: 2*R*C per pixel
-        ach = flops / (ms * 1e-3) / 1e12
-        mode = K.refx_mode(lib.refx(), C, bounds)
         kp, rpad = K.classify_geometry(C, len(bounds) - 1, lib.R, mode)
         peak = F16_MFMA_PEAK_TFLOPS if mode else F32_MFMA_PEAK_TFLOPS
+        ach = flops / (ms_iso * 1e-3) / 1e12
         # MFMA flops the hardware executes: padded K x padded R, x3 products in split-fp16 modes
-        executed = 2.0 * H * W * rpad * kp * (3 if mode else 1) / (ms * 1e-3) / 1e12
-        traffic = None
+        executed = 2.0 * H * W * rpad * kp * (3 if mode else 1) / (ms_iso * 1e-3) / 1e12
+        agg = flops * T * world / (elapsed / args.steps) / 1e12 / world   # per GPU
+        traffic, pmc_rec = None, {}
         pmc = os.path.join(REPO, "profiles", "classify_pixels_pmc.json")
         if os.path.exists(pmc):
             try:
-                rec = json.load(open(pmc))
+                pmc_rec = json.load(open(pmc))
                 # only a PMC record of the kernel this run used counts
-                if KERNEL_NAME[mode].split("<")[0] in rec.get("kernel", ""):
-                    traffic = rec.get("hbm_bytes_per_launch")
+                if kname.split("<")[0] in pmc_rec.get("kernel", ""):
+                    traffic = pmc_rec.get("hbm_bytes_per_launch")
+                else:
+                    pmc_rec = {}
             except Exception:
-                traffic = None
-        out["roofline"] = {"bound": "mfma",
-                           "kernel": KERNEL_NAME[mode],
-                           "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                           "frac": round(ach / peak, 4), "traffic": traffic, "kernel_ms": round(ms, 4),
-                           "mfma_dtype": ("f16 (split hi/lo, 3 MFMA per f32 product; v_mfma_f32_%s_f16)" %
-                                          ("32x32x16" if "lay_kernel" in KERNEL_NAME[mode] else "16x16x32")
-                                          if mode else "f32"),
-                           "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4),
-                           "overlapped_with_segmentation": not args.no_overlap,
-                           "isolated_kernel_ms": round(ms_iso, 4),
-                           "isolated_achieved": round(flops / (ms_iso * 1e-3) / 1e12, 2),
-                           "isolated_frac": round(flops / (ms_iso * 1e-3) / 1e12 / peak, 4),
-                           "note": ("kernel_ms: mean launch time on the classifier's side stream inside the timed "
-                                    "region, where %d tiles are in flight and the segmentation streams run at higher "
-                                    "priority (the classifier yields to them); isolated_*: the same launch alone "
-                                    "after the timed region" % T)}
+                pmc_rec = {}
+        out["roofline"] = {
+            "bound": "mfma", "kernel": kname,
+            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "traffic": traffic, "kernel_ms": round(ms_iso, 4),
+            "launch": "isolated: one 2048x2048 tile's launch alone on its stream after the timed region, HIP "
+                      "events, mean of 5; algorithmic 2*R*C flop per pixel = %.4f TFLOP per launch" % (flops / 1e12),
+            "mfma_dtype": ("f16 (split hi/lo, 3 MFMA per f32 product; v_mfma_f32_16x16x32_f16)" if mode
+                           else "f32"),
+            "executed_mfma_tflops": round(executed, 1), "executed_frac": round(executed / peak, 4),
+            "pmc": {k: pmc_rec[k] for k in ("round", "mfma_busy_frac", "sq_busy_cycles_per_grbm", "sclk_mhz_mean",
+                                            "avg_duration_us_kernel_trace") if k in pmc_rec} or None,
+            "aggregate": {"achieved": round(agg, 2), "frac": round(agg / peak, 4),
+                          "note": "classifier flops of the %d tiles per step / the step time (ms_per_step): the "
+                                  "classifier's share of the whole-job rate, per GPU" % T},
+            "in_timed_region": {"kernel_ms": round(ms_in, 4), "frac": round(flops / (ms_in * 1e-3) / 1e12 / peak, 4),
+                                "note": "mean launch time on the classifier's side stream inside the timed region "
+                                        "(HIP events), where %d tiles are in flight and the segmentation streams run "
+                                        "at higher priority: overlap, not kernel work" % T}}
     if world == 1 and not args.no_extras:
         out["extras"] = _extras(dev, T, streams, pool, tiles, lib)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

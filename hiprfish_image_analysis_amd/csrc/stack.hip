@@ -811,7 +811,11 @@ __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_
     if (!fg) continue;
     const int64_t p0 = ch << 6;
     float pcal = 1.0f;
-    if (CAL) pcal = (p0 + lane < npix) ? cal[p0 + lane] : 1.0f;
+    double prc = 1.0;  // lane = pixel: one division per 64 pixels, 1 / flat field
+    if (CAL) {
+      pcal = (p0 + lane < npix) ? cal[p0 + lane] : 1.0f;
+      prc = 1.0 / (double)pcal;
+    }
     // the chunk's pixels: lane = pixel for the coverage of the whole stack (apply_mask), a bit
     // per pixel; the row of every pixel once (no 64-bit division per fetched pixel)
     const int64_t pl = p0 + lane;
@@ -864,10 +868,21 @@ __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_
           }
           ++n;
           if (CAL) {
-            const double d = (double)__builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                                 __builtin_bit_cast(int, pcal), idx[j]));
-            a0 += k0 ? (double)x0[j] / d : (double)x0[j];
-            a1 += k1 ? (double)x1[j] / d : (double)x1[j];
+            // x / d bit for bit through the pixel's reciprocal (detmath.h hrf_div_rcp: x and d
+            // are float32 values); d zero or not finite keeps the division
+            const float df = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pcal), idx[j]));
+            const double d = (double)df;
+            const unsigned long long rb = __builtin_bit_cast(unsigned long long, prc);
+            const double r = __builtin_bit_cast(
+                double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(rb >> 32), idx[j]) << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rb, idx[j]));
+            if (df != 0.0f && __builtin_isfinite(df)) {
+              a0 += k0 ? hrf_div_rcp((double)x0[j], d, r) : (double)x0[j];
+              a1 += k1 ? hrf_div_rcp((double)x1[j], d, r) : (double)x1[j];
+            } else {
+              a0 += k0 ? (double)x0[j] / d : (double)x0[j];
+              a1 += k1 ? (double)x1[j] / d : (double)x1[j];
+            }
           } else {
             a0 += (double)x0[j];
             a1 += (double)x1[j];

@@ -7,6 +7,7 @@ Each function cites the reference lines it stands in for.
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from dataclasses import dataclass, field
 
 import torch
@@ -325,17 +326,23 @@ class TileResult:
     pixel_dist: torch.Tensor | None = None
 
 
-_SIDE_STREAMS: dict = {}
+_SIDE_STREAMS: "OrderedDict" = OrderedDict()
 SIDE_PRIORITY = 0   # stream priority of the classifier side streams (torch convention: lower = higher)
+SIDE_STREAMS_MAX = 64
 
 
 def _side_stream(main: torch.cuda.Stream) -> torch.cuda.Stream:
     """the side stream paired with `main` (one per caller stream, so concurrent tiles on
-    different streams do not serialise on a shared one)"""
+    different streams do not serialise on a shared one); the least recently used beyond
+    SIDE_STREAMS_MAX are dropped (work queued on them is held by the events their callers joined)"""
     key = (main.device, main.cuda_stream, SIDE_PRIORITY)
     s = _SIDE_STREAMS.get(key)
     if s is None:
         s = _SIDE_STREAMS[key] = torch.cuda.Stream(device=main.device, priority=SIDE_PRIORITY)
+        while len(_SIDE_STREAMS) > SIDE_STREAMS_MAX:
+            _SIDE_STREAMS.popitem(last=False)
+    else:
+        _SIDE_STREAMS.move_to_end(key)
     return s
 
 

@@ -465,3 +465,35 @@ void oracle_umap_refine(const int32_t *idx, const float *memb, int64_t nq, int k
 __attribute__((visibility("default"))) void oracle_cr_log(const double *x, int64_t n, int mode, double *out) {
   for (int64_t i = 0; i < n; ++i) out[i] = mode ? hrf_cr_log10(x[i]) : hrf_cr_log(x[i]);
 }
+
+/* hrf_div_rcp (detmath.h) against the IEEE division on n float32 pairs: random bit patterns
+ * (finite, d nonzero), plus directed significands (all ones, 1 + ulp, powers of two) -> the
+ * number of pairs whose results differ (tests/test_oracle_golden.py). */
+__attribute__((visibility("default"))) int64_t oracle_div_rcp_check(uint64_t seed, int64_t n) {
+  uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
+  int64_t bad = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t w[2];
+    for (int k = 0; k < 2; ++k) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      w[k] = (uint32_t)(s >> 11);
+    }
+    const int mode = (int)(i & 7);
+    if (mode == 1) w[1] |= 0x007FFFFFu;                  /* d significand all ones */
+    if (mode == 2) w[1] = (w[1] & 0xFF800000u) | 1u;     /* d = 2^e (1 + ulp) */
+    if (mode == 3) w[0] |= 0x007FFFFFu;
+    if (mode == 4) w[1] &= 0xFF800000u;                  /* d a power of two */
+    if (mode == 5) w[1] = (w[1] & 0x807FFFFFu) | 0x3F000000u;   /* d in [0.5, 1) (flat fields) */
+    if (mode == 6) w[0] = (w[0] & 0x007FFFFFu) | 0x3E000000u;   /* x in [0.125, 0.25) */
+    float xf, df;
+    memcpy(&xf, &w[0], 4);
+    memcpy(&df, &w[1], 4);
+    if (!isfinite(xf) || !isfinite(df) || df == 0.0f) continue;
+    const double x = xf, d = df, r = 1.0 / d;
+    const double a = x / d, b = hrf_div_rcp(x, d, r);
+    if (memcmp(&a, &b, 8) != 0) ++bad;
+  }
+  return bad;
+}

@@ -284,3 +284,13 @@ def test_cr_log_is_correctly_rounded(orc):
     want10 = np.array([float(decimal.Decimal(v).log10()) for v in x])
     assert np.array_equal(got10, want10)
     assert orc.cr_log(np.array([0.0]))[0] == -np.inf and np.isnan(orc.cr_log(np.array([-1.0]))[0])
+
+
+def test_flat_field_division_through_reciprocal(orc):
+    """detmath.h hrf_div_rcp (the lasers label sums' flat-field division, ecoli :41 image /
+    calibration_norm, with both operands float32 values): equal to the IEEE quotient on 2e7
+    random and directed float pairs"""
+    import ctypes
+    f = orc.lib().oracle_div_rcp_check
+    f.restype = ctypes.c_int64
+    assert f(ctypes.c_uint64(7), ctypes.c_int64(20_000_000)) == 0

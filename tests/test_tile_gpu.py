@@ -205,15 +205,19 @@ def test_tile_context_cache_bounded(mods):
             K.segment_ecoli_native(None, image_cn=cn)
         s.synchronize()
         return r
+    def free_bytes():
+        # torch's caching allocator keeps freed blocks per stream (a fresh stream cannot reuse
+        # another's): released before reading what the device has left
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        return torch.cuda.mem_get_info()[0]
     for _ in range(cap):
         one()
-    torch.cuda.synchronize()
-    free_full = torch.cuda.mem_get_info()[0]
+    free_full = free_bytes()
     for _ in range(20):
         r = one()
         assert len(K._TILE_CTX) <= cap and len(K._SEG_CTX) <= cap
-    torch.cuda.synchronize()
-    grown = free_full - torch.cuda.mem_get_info()[0]
+    grown = free_full - free_bytes()
     assert grown < 64 << 20, "device memory grew by %d bytes over 20 fresh streams" % grown
     _check(r, want)
     K.release_contexts()

@@ -1,6 +1,6 @@
 """Time individual libhrf kernels on resident 2048x2048 inputs (HIP events, mean of 5).
 
-python tools/time_kernels.py [nlmeans] [classify] [stream]
+python tools/time_kernels.py [nlmeans] [classify] [stream] [path] [pathcal]
 """
 import sys
 
@@ -44,6 +44,40 @@ def main():
                 ms = timed(lambda: K.classify_pixels(stack, refx, R, bounds, mode))
                 tf = 2.0 * H * W * R * C / ms / 1e9
                 print("classify C=%d R=%d mode %d: %.3f ms  %.1f TF/s algorithmic" % (C, R, mode, ms, tf))
+
+    if "path" in what or "pathcal" in what:
+        # the timed path's streaming kernels (bench.py path_kernel_rows) on one bench tile;
+        # "pathcal": label_sums_lasers over a map with every pixel labelled (16x16 blocks), whose
+        # algorithmic read is known exactly -- the FETCH_SIZE calibration of its 4-byte lane reads
+        sys.path.insert(0, ".")
+        import numpy as np
+        import bench as B
+        from hiprfish_image_analysis_amd import pipeline as P
+        ref = S.reference_library(B.NBIT, S.ECOLI_BOUNDS)
+        lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), S.ECOLI_BOUNDS, B.NBIT)
+        seed = 20190101
+        lay = S.cell_layout(H, W, S.default_ncells(H, W), lib.R, seed)
+        truth, prof = S.render_truth(H, W, lay, with_profile=True)
+        stack = S.render_stack(truth, lay, ref, seed=seed, device="cuda", profile=prof)
+        lasers = S.laser_split(stack)
+        del stack
+        cal = S.flat_field(H, W, device="cuda")
+        rows, info = B.path_kernel_rows(lasers, cal, lib)
+        if "path" in what:
+            for name, (fn, nb) in rows.items():
+                ms = timed(fn, 10)
+                print("%s: %.4f ms  %.0f GB/s algorithmic (%.3f of 8 TB/s), %d bytes" % (name, ms, nb / ms / 1e6,
+                                                                                       nb / ms / 8e9, nb))
+            print(info)
+        else:
+            rr = torch.arange(H, device="cuda", dtype=torch.int32)[:, None] // 16
+            cc = torch.arange(W, device="cuda", dtype=torch.int32)[None, :] // 16
+            dense = (1 + rr * (W // 16) + cc).contiguous()
+            shifts = P.estimate_shifts(lasers, device=True)
+            ms = timed(lambda: K.label_sums_lasers(lasers, shifts, dense, int(dense.max()), True, cal=cal,
+                                                   cal_range=(0, 32)), 10)
+            nbd = H * W * (4 + 4 * 95 + 4)
+            print("label_sums_lasers dense calibration map: %.4f ms, %d algorithmic read bytes" % (ms, nbd))
 
     if "stream" in what:
         from hiprfish_image_analysis_amd import pipeline as P
