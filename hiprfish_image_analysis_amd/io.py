@@ -1,8 +1,10 @@
 """File surface of the reference stages (inputs and the CSV/npy/png outputs they write).
 
-CZI input needs bioformats + a JVM (ecoli measurement.py:15-16,31,145), which this build does
-not ship.  A stage given `{stem}.czi` reads the (H, W, C_l) array from
-`{stem}.npy` next to it instead; everything written keeps the reference's names and formats.
+CZI input: the reference reads it through bioformats + a JVM (ecoli measurement.py:15-16,31,145);
+here `czi.py` reads the ZISRAW file natively (uncompressed, Zstd and JPEG-XR grey subblocks as
+czi.py documents).  When only an array is at hand, a stage given `{stem}.czi` reads the
+(H, W, C_l) array from `{stem}.npy` next to it instead; everything written keeps the reference's
+names and formats.
 """
 from __future__ import annotations
 

@@ -173,12 +173,17 @@ def _cal_layout(cal, H, W, C, cal_range=None):
                      % (tuple(c.shape), H, W, C))
 
 
-def channel_sum(stack, mask=None, mode=0, negate=False, cal=None, cal_range=None):
+def channel_sum(stack, mask=None, mode=0, negate=False, cal=None, cal_range=None, out=None):
     """np.sum(stack, axis=2) (f64, numpy pairwise order); mode 1 -> log(s+1e-2), 2 -> log10(s+1);
-    cal: np.sum(stack / cal, axis=2) (multispecies measurement.py:104-105)"""
+    cal: np.sum(stack / cal, axis=2) (multispecies measurement.py:104-105); out: a contiguous
+    (H, W) f64 tensor to write into"""
     stack = _dev(stack, torch.float32, "stack")
     H, W, C = stack.shape
-    out = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    if out is None:
+        out = torch.empty((H, W), dtype=torch.float64, device=stack.device)
+    elif out.dtype != torch.float64 or tuple(out.shape) != (H, W) or not out.is_contiguous() \
+            or out.device != stack.device:
+        raise ValueError("channel_sum: out must be a contiguous (%d, %d) f64 tensor on the stack's device" % (H, W))
     if cal is not None:
         if mask is not None or negate:
             raise ValueError("channel_sum: calibration with mask/negate is not supported")

@@ -116,6 +116,7 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
     -> [(0, 0), (dr_1, dc_1), ...] ready for kernels.register_assemble; with `device` an
     (nlaser, 2) int32 device tensor instead (no host synchronisation; register_assemble reads
     it on the device)."""
+    H, W = lasers[0].shape[:2]
     if reduce == "max" and len(lasers) <= 8:
         proj = K.channel_max_multi(lasers, stacked=True)                 # one launch for all lasers
         if device and len(lasers) >= 2 and XCORR and K.xcorr_supported(*proj.shape):
@@ -123,6 +124,11 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
         if device and len(lasers) >= 2 and BATCH_REGISTRATION:
             return K.register_translations_batch_dev(proj, clamp)       # batched FFTs
         proj = list(proj.unbind(0))
+    elif reduce == "sum" and device and len(lasers) >= 2 and XCORR and K.xcorr_supported(len(lasers), H, W):
+        proj = torch.empty((len(lasers), H, W), dtype=torch.float64, device=lasers[0].device)
+        for i, s in enumerate(lasers):
+            K.channel_sum(s, out=proj[i])                               # numpy's pairwise order
+        return K.xcorr_shifts_dev(proj, clamp)
     else:
         proj = [K.channel_max(s) if reduce == "max" else K.channel_sum(s) for s in lasers]
     if device:
@@ -146,6 +152,17 @@ def register_stack(lasers, reduce: str = "max", clamp: int | None = 15, apply_ma
     -> (stack, image_cn)."""
     return K.register_assemble(lasers, estimate_shifts(lasers, reduce, clamp, device=True), apply_mask,
                                cn_mode=1 if want_cn else None)
+
+
+def register_multispecies(lasers, shifts=None):
+    """multispecies measurement.py:79-102: the four acquisitions (488, 514, 561, 633) registered on
+    their channel sums -- skimage register_translation(sum_0, sum_i), no clamp (:82-84) -- and
+    concatenated with zeros outside each shifted frame and NO coverage-mask multiply (:85-102;
+    the mask is built but never applied).  shifts: (n, 2) device tensor or host pairs to use
+    instead of the estimate.  -> (H, W, C) f32 registered stack (one stream, no synchronisation)"""
+    if shifts is None:
+        shifts = estimate_shifts(lasers, reduce="sum", clamp=None, device=True)
+    return K.register_assemble(lasers, shifts, apply_mask=False)
 
 
 @dataclass

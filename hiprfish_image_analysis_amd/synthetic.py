@@ -153,3 +153,15 @@ def flat_field(H: int, W: int, device="cuda"):
     y = torch.linspace(-1.0, 1.0, H, device=device)[:, None]
     x = torch.linspace(-1.0, 1.0, W, device=device)[None, :]
     return (1.0 - 0.3 * (0.6 * y * y + 0.4 * x * x)).to(torch.float32).contiguous()
+
+
+COMMUNITY_SHIFTS = ((0, 0), (3, -2), (-1, 4), (2, 1))   # 488, 514, 561, 633 (multispecies :79-84)
+
+
+def calibration_stack(H: int, W: int, C: int, device="cuda"):
+    """A (H, W, C) f32 calibration array for the community stage (multispecies :103-104 divides the
+    registered stack by the loaded calibration image with numpy broadcasting): the flat field
+    times a smooth per-channel gain in [0.8, 1.2]."""
+    import torch
+    g = 1.0 + 0.2 * torch.sin(torch.arange(C, device=device, dtype=torch.float32) * 0.37)
+    return (flat_field(H, W, device)[:, :, None] * g[None, None, :]).to(torch.float32).contiguous()

@@ -195,3 +195,74 @@ def test_fullsize_volume_chain_full_xy():
     want = _enhance_3d_threads(pad)
     assert got.shape == want.shape == (X, Y, Z)
     assert np.array_equal(got, want)
+
+
+def test_fullsize_volume_chain_64_planes():
+    """cfg4 at the benched size: the device chain on the whole 1024x1024x64x63 volume bench.py
+    times (same generator, same seed), compared with the restatement on three z slabs -- both
+    boundaries and the middle -- each computed from the globally normalised, edge-padded array
+    with its patch - 1 halo (an output voxel reads only its 11^3 neighbourhood, so a slab is exact)."""
+    from hiprfish_image_analysis_amd import pipeline as P
+    X, Y, Z, C = 1024, 1024, 64, 63
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    vol = torch.rand((X, Y, Z, C), dtype=torch.float32, device="cuda", generator=g)
+    got = P.enhance_volume(vol)
+    # numpy's channel sum in f64, streamed over x (the f64 copy of the whole volume is 34 GB)
+    s = np.concatenate([np.sum(host(vol[x0:x0 + 64]).astype(np.float64), axis=3) for x0 in range(0, X, 64)], axis=0)
+    del vol
+    pad = np.pad(s / np.max(s), 5, mode="edge")
+    del s
+    for z0 in (0, 29, 58):
+        want = _enhance_3d_threads(pad[:, :, z0:z0 + 6 + 10])
+        part = host(got[:, :, z0:z0 + 6])
+        assert part.shape == want.shape == (X, Y, 6)
+        assert np.array_equal(part, want), z0
+
+
+def test_fullsize_community_registered_calibrated(mods, orc):
+    """cfg2 as the reference runs it (multispecies generate_2d_segmentation :78-159 +
+    measure_biofilm_images_no_reference :161-174): four misregistered 2048x2048 acquisitions
+    (23 / 20 / 14 / 6 channels, bioformats-like k/4095 samples) registered on their channel sums
+    with no clamp and no coverage-mask multiply (:82-102), divided by a (H, W, C) calibration
+    array (:103-104), then the whole segmentation + per-cell chain; against oracle/pipeline.py
+    (estimate_shifts 'sum', register_stacks without the mask, measure_multispecies with the
+    calibration).  Also the _registered.npy array (:166) bit for bit."""
+    P, S, OP = mods
+    from hiprfish_image_analysis_amd import kernels as K
+    b = P.MULTI_BOUNDS
+    H = W = 2048
+    stack, _, _, ref = S.tile(H, W, nbit=7, bounds=b, seed=20190205)
+    stack = quantised(stack, 4095)
+    lasers = S.laser_split(stack, b, S.COMMUNITY_SHIFTS)
+    del stack
+    cal = S.calibration_stack(H, W, 63)
+    lib = P.Library(torch.from_numpy(ref.astype(np.float64)).cuda(), b, 7)
+    shifts_dev = P.estimate_shifts(lasers, reduce="sum", clamp=None, device=True)
+    reg = P.register_multispecies(lasers, shifts_dev)
+    res = P.process_tile(reg, lib, calibration=cal, per_pixel=True, measure=P.measure_multispecies, variant=2)
+    torch.cuda.synchronize()
+    hl = [host(l) for l in lasers]
+    shifts = OP.estimate_shifts(hl, "sum", None)
+    assert [tuple(int(v) for v in r) for r in host(shifts_dev)] == shifts
+    assert shifts[1:] == [tuple(s) for s in S.COMMUNITY_SHIFTS[1:]]
+    oreg = OP.register_stacks(hl, shifts, False).astype(np.float32)
+    del hl
+    assert np.array_equal(host(reg), oreg)
+    hcal = host(cal)
+    assert np.array_equal(host(K.calibrate(reg, cal)), oreg.astype(np.float64) / hcal.astype(np.float64))   # :166
+    oseg, olabs, oavg, oavgn = OP.measure_multispecies(oreg, calibration=hcal)
+    assert np.array_equal(host(res.meas.segmentation), oseg)
+    assert np.array_equal(host(res.meas.labels), olabs) and len(olabs) > 500
+    np.testing.assert_allclose(host(res.meas.avgint), oavg, rtol=1e-12)
+    oidx, odist = OP.classify_cells(oavgn, ref, b, variant=2)
+    np.testing.assert_allclose(host(res.cell_dist), odist, rtol=1e-9, atol=1e-12)
+    assert np.array_equal(host(res.cell_idx), oidx)
+    assert np.array_equal(host(res.counts), orc.barcode_counts(oidx, 127))
+    from test_kernels_gpu import check_pixel_argmin
+    rng = np.random.default_rng(4)
+    cells = np.nonzero(oseg.ravel() > 0)[0]
+    sel = np.concatenate([rng.choice(cells, 8192, replace=False), rng.choice(oseg.size, 2048, replace=False)])
+    x = oreg.reshape(oseg.size, -1)[sel].astype(np.float64)
+    check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
+                       ref.astype(np.float64), b, 0.5)
