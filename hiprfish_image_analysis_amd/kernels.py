@@ -982,6 +982,7 @@ class _CtxCache:
         self._d = OrderedDict()       # key -> [handle, last-use event or None, calls in flight]
         self._lock = threading.Lock()
         self.cap = max(1, int(os.environ.get("HRF_CTX_CACHE", "8")))
+        self.created = 0              # contexts made so far (tests: churn under the cap)
 
     def use(self, dev, H, W):
         """context manager: the (device, current stream, H, W) context for one native call"""
@@ -998,6 +999,7 @@ class _CtxCache:
                     h = ctypes.c_void_p()
                     _lib.call(self._create, H, W, ctypes.addressof(h))
                     ent = self._d[key] = [h, None, 0]
+                    self.created += 1
                 else:
                     self._d.move_to_end(key)
                 ent[2] += 1
