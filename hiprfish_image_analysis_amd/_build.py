@@ -43,6 +43,31 @@ def _compile(src):
     return obj, False
 
 
+JXR_INC = os.environ.get("HRF_JXR_INCLUDE", "/opt/conda/include/jxrlib")
+JXR_LIB = os.environ.get("HRF_JXR_LIBDIR", "/opt/conda/lib")
+JXR_SO = os.path.join(PKG, "libhrfjxr.so")
+
+
+def build_jxr(verbose: bool = True):
+    """libhrfjxr.so: the host-side JPEG-XR shim (csrc/jxr.c) over jxrlib, when the image carries
+    jxrlib's headers and libraries (czi.py decodes JPEG-XR subblocks through it)"""
+    src = os.path.join(CSRC, "jxr.c")
+    if not (os.path.isdir(JXR_INC) and os.path.exists(os.path.join(JXR_LIB, "libjxrglue.so"))):
+        if verbose:
+            print("jxrlib not found (%s, %s): libhrfjxr.so not built" % (JXR_INC, JXR_LIB))
+        return None
+    if _newer(src, JXR_SO):
+        cmd = ["gcc", "-O2", "-fPIC", "-shared", "-fvisibility=hidden", "-D__ANSI__", "-DDISABLE_PERF_MEASUREMENT",
+               "-Wno-endif-labels", "-I" + JXR_INC, src, "-o", JXR_SO, "-L" + JXR_LIB, "-ljxrglue", "-ljpegxr",
+               "-Wl,-rpath," + JXR_LIB]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("jxr shim build failed:\n%s" % r.stderr[-4000:])
+        if verbose:
+            print("built", JXR_SO)
+    return JXR_SO
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     os.makedirs(OBJ, exist_ok=True)
     gen = os.path.join(CSRC, "gen_tables.py")
@@ -64,6 +89,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
             raise RuntimeError("link failed:\n%s" % r.stderr[-4000:])
         if verbose:
             print("built", LIB)
+    build_jxr(verbose)
     return LIB
 
 

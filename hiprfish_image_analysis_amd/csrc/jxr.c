@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include "JXRGlue.h"
+#include "../../include/hrf_jxr.h"
 
 #define EXPORT __attribute__((visibility("default")))
 

@@ -20,8 +20,11 @@ by their X / Y start (mosaic tiles stitched, later tiles over earlier ones in di
 and C index.  Supported: Gray8 / Gray16 / Gray32Float / Gray32 subblocks, uncompressed (what
 ZEN 2.x writes for LSM 880 lambda-mode acquisitions) or zstd-compressed (ZEN 3.x: "Zstd0" = a
 bare zstd frame, "Zstd1" = a small header whose chunk 1 flags the low/high byte split of 16-bit
-data, then the frame; decoded with the zstd codec pyarrow carries).  JPEG-XR subblocks raise with
-the compression named: no decoder for them is in this image.  A subblock must hold one plane
+data, then the frame; decoded with the zstd codec pyarrow carries) or JPEG-XR-compressed ("JpegXr",
+compression 4: each subblock a JPEG XR file, lossless or lossy, decoded by jxrlib -- Microsoft's
+reference implementation of ITU-T T.832, present in this image -- through the in-tree shim
+csrc/jxr.c, libhrfjxr.so; the decoded size and grey pixel format must match the directory
+entry).  A subblock must hold one plane
 (C, Z, T sizes 1 -- what ZEN writes for spectral acquisitions); anything else raises rather than
 returning part of it.
 
@@ -141,8 +144,51 @@ def _decode(buf, off, size, compression, nbytes, itemsize):
         elif hilo:
             raise CziError("Zstd1 low/high byte split on %d-byte samples" % itemsize)
         return data, 0
+    if compression == 4:
+        raise CziError("JpegXrFile subblock reached the byte decoder")   # decoded in _subblock_pixels
     raise CziError("subblock compression %s is not supported (no decoder in this build)"
                    % COMPRESSION.get(compression, compression))
+
+
+_JXR = None
+
+
+def _jxr_lib():
+    """libhrfjxr.so (built by _build.build_jxr next to libhrf.so)"""
+    global _JXR
+    if _JXR is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhrfjxr.so")
+        if not os.path.exists(path):
+            raise CziError("JpegXrFile subblock but libhrfjxr.so is not built (jxrlib absent at build time)")
+        lib = ctypes.CDLL(path)
+        lib.hrf_jxr_info.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]
+        lib.hrf_jxr_decode.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
+        _JXR = lib
+    return _JXR
+
+
+def _jpegxr(raw, ys, xs, dt):
+    """one JPEG XR subblock -> (ys, xs) array of dt (the directory's pixel type)"""
+    import ctypes
+    lib = _jxr_lib()
+    data = bytes(raw)
+    w, h, b = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    r = lib.hrf_jxr_info(data, len(data), ctypes.addressof(w), ctypes.addressof(h), ctypes.addressof(b))
+    if r == -100:
+        raise CziError("JPEG-XR subblock with a pixel format that is not grey 8/16-bit or 32-bit float")
+    if r != 0:
+        raise CziError("JPEG-XR subblock: decoder error %d" % r)
+    if (h.value, w.value) != (ys, xs) or b.value != np.dtype(dt).itemsize:
+        raise CziError("JPEG-XR subblock of %d x %d x %d bytes, the directory says %d x %d x %d"
+                       % (h.value, w.value, b.value, ys, xs, np.dtype(dt).itemsize))
+    out = np.empty((ys, xs), dtype=dt)
+    r = lib.hrf_jxr_decode(data, len(data), out.ctypes.data, xs * np.dtype(dt).itemsize)
+    if r != 0:
+        raise CziError("JPEG-XR subblock: decoder error %d" % r)
+    return out
 
 
 def _subblock_pixels(buf, e):
@@ -161,6 +207,8 @@ def _subblock_pixels(buf, e):
     ys, xs = e.dims["Y"][2], e.dims["X"][2]
     n = xs * ys
     nbytes = n * np.dtype(dt).itemsize
+    if e.compression == 4:
+        return _jpegxr(memoryview(buf)[data_off:data_off + data_size], ys, xs, dt)
     src, off = _decode(buf, data_off, data_size, e.compression, nbytes, np.dtype(dt).itemsize)
     if len(src) - off < nbytes or (e.compression == 0 and data_size < nbytes):
         raise CziError("subblock data %d bytes, %d x %d pixels expected" % (data_size, ys, xs))

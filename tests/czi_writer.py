@@ -22,10 +22,73 @@ def _entry(pixel_type, pos, compression, dims, pyramid=0):
     return out
 
 
-def _compress(data, compression, itemsize, hilo):
+JXR_ENC = "/opt/conda/bin/JxrEncApp"     # jxrlib's encoder (the image's conda tree)
+JXR_DEC = "/opt/conda/bin/JxrDecApp"
+
+
+def write_tiff(path, a):
+    """a minimal baseline TIFF (one strip, uncompressed, BlackIsZero) of a grey uint8 / uint16
+    image: JxrEncApp's input format"""
+    H, W = a.shape
+    data = np.ascontiguousarray(a).astype(a.dtype.newbyteorder("<")).tobytes()
+    tags = [(256, 4, W), (257, 4, H), (258, 3, a.dtype.itemsize * 8), (259, 3, 1), (262, 3, 1), (273, 4, 0),
+            (277, 3, 1), (278, 4, H), (279, 4, len(data)), (284, 3, 1)]
+    data_off = 8 + 2 + 12 * len(tags) + 4
+    out = bytearray(b"II*\x00" + struct.pack("<IH", 8, len(tags)))
+    for tag, typ, val in tags:
+        val = data_off if tag == 273 else val
+        out += struct.pack("<HHIHH", tag, typ, 1, val, 0) if typ == 3 else struct.pack("<HHII", tag, typ, 1, val)
+    out += struct.pack("<I", 0) + data
+    with open(path, "wb") as f:
+        f.write(bytes(out))
+
+
+def read_tiff(path, dtype):
+    """the strip of a one-strip grey TIFF written by JxrDecApp (tag 273 / 279)"""
+    b = open(path, "rb").read()
+    assert b[:4] == b"II*\x00"
+    off = struct.unpack_from("<I", b, 4)[0]
+    n = struct.unpack_from("<H", b, off)[0]
+    vals = {}
+    for i in range(n):
+        tag, typ, cnt, v = struct.unpack_from("<HHII", b, off + 2 + 12 * i)
+        vals[tag] = v & 0xFFFF if typ == 3 else v
+    W, H = vals[256], vals[257]
+    return np.frombuffer(b, dtype=np.dtype(dtype).newbyteorder("<"), count=W * H, offset=vals[273]).reshape(H, W)
+
+
+def jxr_encode(a, quality="1"):
+    """JPEG XR file of a grey uint8 / uint16 plane by jxrlib's JxrEncApp (-q 1: lossless)"""
+    import os
+    import subprocess
+    import tempfile
+    fmt = {np.dtype(np.uint8): "2", np.dtype(np.uint16): "3"}[a.dtype]
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.tif"), os.path.join(d, "out.jxr")
+        write_tiff(src, a)
+        subprocess.run([JXR_ENC, "-i", src, "-o", dst, "-c", fmt, "-q", str(quality)], check=True,
+                       capture_output=True)
+        return open(dst, "rb").read()
+
+
+def jxr_decode_app(codestream, dtype):
+    """the same codestream decoded by jxrlib's own JxrDecApp (to a TIFF)"""
+    import os
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        src, dst = os.path.join(d, "in.jxr"), os.path.join(d, "out.tif")
+        open(src, "wb").write(codestream)
+        subprocess.run([JXR_DEC, "-i", src, "-o", dst], check=True, capture_output=True)
+        return read_tiff(dst, dtype).copy()
+
+
+def _compress(data, compression, itemsize, hilo, plane=None, jxr_quality=None):
     import pyarrow as pa
 
-    if compression in (0, 4):      # 4: marked JPEG-XR, payload left raw (the reader must refuse it)
+    if compression == 4 and jxr_quality is not None:     # JPEG XR file per subblock (jxrlib)
+        return jxr_encode(plane, jxr_quality)
+    if compression in (0, 4):      # 4 without a quality: marked JPEG-XR, payload left raw (corrupt)
         return data
     if compression == 6 and hilo and itemsize == 2:   # Zstd1 low/high byte split
         a = np.frombuffer(data, np.uint8).reshape(-1, 2)
@@ -38,7 +101,7 @@ def _compress(data, compression, itemsize, hilo):
     raise ValueError(compression)
 
 
-def write_czi(path, blocks, compression=0, hilo=False, sizes=None):
+def write_czi(path, blocks, compression=0, hilo=False, sizes=None, jxr_quality=None):
     """blocks: list of (array (ys, xs) of uint8/uint16/float32, {dim: start}); dims X, Y
     from the array shape, C/Z/T/S/M from the dict (default 0); compression 5/6 = Zstd0/Zstd1
     (pyarrow's zstd); sizes: {dim: size} written for C/Z/T instead of 1 (malformed files)"""
@@ -57,7 +120,8 @@ def write_czi(path, blocks, compression=0, hilo=False, sizes=None):
         pt = ptype[arr.dtype]
         e = _entry(pt, pos, compression, dims, where.get("pyramid", 0))
         meta = b"<METADATA><Tags><AcquisitionTime>2018-08-18</AcquisitionTime></Tags></METADATA>"
-        data = _compress(arr.astype(arr.dtype.newbyteorder("<")).tobytes(), compression, arr.dtype.itemsize, hilo)
+        data = _compress(arr.astype(arr.dtype.newbyteorder("<")).tobytes(), compression, arr.dtype.itemsize, hilo,
+                         arr, jxr_quality)
         head = struct.pack("<iiq", len(meta), 0, len(data)) + e
         head += b"\0" * (max(256, len(head)) - len(head))
         seg = _seg("ZISRAWSUBBLOCK", head + meta + data)
@@ -75,7 +139,7 @@ def write_czi(path, blocks, compression=0, hilo=False, sizes=None):
         f.write(SEG.pack(b"ZISRAWFILE".ljust(16, b"\0"), 512, 512) + fh + body + directory + metadata)
 
 
-def write_spectral(path, stack_u16, tiles=1, compression=0, hilo=False):
+def write_spectral(path, stack_u16, tiles=1, compression=0, hilo=False, jxr_quality=None):
     """(H, W, C) or (H, W, Z, C) uint16 -> one subblock per channel (and z plane; per mosaic
     tile along x when tiles > 1)"""
     if stack_u16.ndim == 3:
@@ -88,4 +152,4 @@ def write_spectral(path, stack_u16, tiles=1, compression=0, hilo=False):
             for c in range(C):
                 blocks.append((stack_u16[:, xs[t]:xs[t + 1], z, c],
                                {"X": 100 + xs[t], "Y": 50, "C": c, "M": t, "Z": z}))
-    write_czi(path, blocks, compression, hilo)
+    write_czi(path, blocks, compression, hilo, jxr_quality=jxr_quality)

@@ -57,3 +57,16 @@ def test_bad_arguments_raise_value_error():
     t = np.zeros(4, np.int32)
     with pytest.raises(ValueError):
         _lib.call("hrf_lp_table_2d", 0, 9, t.ctypes.data)
+
+
+def test_jxr_shim_exports_declared_symbols():
+    """libhrfjxr.so (the CZI reader's JPEG-XR decoder, include/hrf_jxr.h) exports what it declares"""
+    import re
+    so = os.path.join(os.path.dirname(_lib.LIB_PATH), "libhrfjxr.so")
+    if not os.path.exists(so):
+        pytest.skip("jxrlib absent at build time: libhrfjxr.so not built")
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(_lib.LIB_PATH)), "include", "hrf_jxr.h")).read()
+    decl = re.findall(r"^int (hrf_\w+)\(", hdr, re.M)
+    assert decl == ["hrf_jxr_info", "hrf_jxr_decode"]
+    L = ctypes.CDLL(so)
+    assert all(hasattr(L, n) for n in decl)

@@ -91,11 +91,49 @@ def test_zstack_loaders_and_sizes(tmp_path):
         czi.load_image(p, series=2)
 
 
+JXR = os.path.exists("/opt/conda/bin/JxrEncApp")
+
+
+@pytest.mark.skipif(not JXR, reason="jxrlib's encoder is not in this image")
+@pytest.mark.parametrize("dtype,tiles", [(np.uint16, 1), (np.uint16, 2), (np.uint8, 1)])
+def test_jpegxr_subblocks_lossless(tmp_path, dtype, tiles):
+    """JPEG-XR subblocks (ZEN's 'JpegXrFile', compression 4), each a JPEG XR file written by
+    jxrlib's own encoder (JxrEncApp, lossless): load_image equals the uncompressed read of the
+    same planes, rescale included (ecoli measurement.py:145 bioformats.load_image)"""
+    rng = np.random.default_rng(6)
+    hi = 4096 if dtype == np.uint16 else 256
+    st = rng.integers(0, hi, (29, 46, 4), dtype=dtype)
+    pu, pj = str(tmp_path / "u.czi"), str(tmp_path / "j.czi")
+    write_spectral(pu, st, tiles=tiles)
+    write_spectral(pj, st, tiles=tiles, compression=4, jxr_quality=1)
+    got = czi.load_image(pj)
+    assert np.array_equal(got, czi.load_image(pu))
+    assert np.array_equal(czi.load_image(pj, rescale=False), st)
+
+
+@pytest.mark.skipif(not JXR, reason="jxrlib's encoder is not in this image")
+def test_jpegxr_lossy_equals_reference_decoder(tmp_path):
+    """lossy JPEG-XR subblocks: every plane equals jxrlib's own decoder application (JxrDecApp)
+    on the same codestream, and is close to the source"""
+    from czi_writer import jxr_decode_app, jxr_encode
+    rng = np.random.default_rng(7)
+    yy, xx = np.mgrid[0:40, 0:52]
+    st = np.stack([(2000 + 1500 * np.sin(yy / 5.0 + c) * np.cos(xx / 7.0) + rng.integers(0, 50, yy.shape))
+                   for c in range(3)], -1).astype(np.uint16)
+    p = str(tmp_path / "lossy.czi")
+    write_spectral(p, st, compression=4, jxr_quality=0.8)
+    got = czi.load_image(p, rescale=False)
+    for c in range(3):
+        ref = jxr_decode_app(jxr_encode(st[:, :, c], 0.8), np.uint16)
+        assert np.array_equal(got[:, :, c], ref)
+    assert 0 < np.abs(got.astype(np.int64) - st).max() < 400
+
+
 def test_unsupported_raise(tmp_path):
     p = str(tmp_path / "z.czi")
     write_czi(p, [(np.zeros((4, 4), np.uint16), {})], compression=4)
-    with pytest.raises(czi.CziError, match="JpegXr"):
-        czi.load_image(p)
+    with pytest.raises(czi.CziError, match="JPEG-XR|JpegXr"):
+        czi.load_image(p)            # a corrupt (raw) JPEG-XR payload
     # a multi-channel subblock would be read as its first plane only: refused
     pm = str(tmp_path / "mc.czi")
     write_czi(pm, [(np.zeros((4, 4), np.uint16), {})], sizes={"C": 3})
