@@ -1360,40 +1360,18 @@ __global__ __launch_bounds__(256) void pixtable_prep_kernel(const float *__restr
   hrf_pix::prep_tile<L>(tile, nullptr, np, p0, table, flags);
 }
 
-// (score, row) as one unsigned key whose order is the sweep's: larger score first, then the smaller
-// row (the sweeps keep the first row on ties).  -0.0 is taken as +0.0, as the float compare does.
-__device__ __forceinline__ unsigned long long score_key(float b, int idx) {
-  uint32_t u = __float_as_uint(b == 0.0f ? 0.0f : b);
-  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  return ((unsigned long long)u << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
-}
-__device__ __forceinline__ void score_unkey(unsigned long long k, float *b, int *idx) {
-  uint32_t u = (uint32_t)(k >> 32);
-  u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
-  *b = __uint_as_float(u);
-  *idx = (int)(0xFFFFFFFFu - (uint32_t)k);
-}
-
 // classify_pixels_w16_kernel with the prologue replaced by direct loads of the prepared operands
 template <class L, int NW, int NBUF, int CR, int OCC>
 __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(const uint4 *__restrict__ table,
                                                                       const uint8_t *__restrict__ flags, int64_t P,
                                                                       const _Float16 *__restrict__ refh, int32_t R,
                                                                       int32_t Rpad, int32_t *__restrict__ best_idx,
-                                                                      float *__restrict__ best_dist,
-                                                                      unsigned long long *__restrict__ keys) {
+                                                                      float *__restrict__ best_dist) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   constexpr int KP = 32 * KT;
   constexpr int ROWB = 4 * KP + L::PADB;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // library split (gridDim.y > 1): this workgroup sweeps chunks [c0, c1) of the library and
-  // merges its per-pixel best into keys[] (score order, then the smaller row) by atomicMax; a
-  // workgroup's lifetime is 1 / gridDim.y of the whole sweep, so the chain kernels sharing the
-  // CUs wait that much less for a slot (DESIGN.md "Library split")
-  const int nchall = Rpad / CR;
-  const int c0 = (int)((int64_t)nchall * blockIdx.y / gridDim.y);
-  const int c1 = (int)((int64_t)nchall * (blockIdx.y + 1) / gridDim.y);
   const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
   h8 bh[4][KT], bl[4][KT];
   uint32_t zx[4], ng = 0;
@@ -1420,9 +1398,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     best[g] = -__builtin_inff();
     bi[g] = 0;
   }
-  const char *gref = reinterpret_cast<const char *>(refh) + (int64_t)c0 * CR * ROWB;
+  const char *gref = reinterpret_cast<const char *>(refh);
   char *ldsb = reinterpret_cast<char *>(lds);
-  const int nch = c1 - c0;
+  const int nch = Rpad / CR;
   const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
   const bool keyed = !libneg && !__syncthreads_or(ng != 0);
 #define HRF_SWEEPW(Z, K) \
@@ -1435,8 +1413,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     else HRF_SWEEPW(false, false);
   }
 #undef HRF_SWEEPW
-#pragma unroll
-  for (int g = 0; g < 4; ++g) bi[g] += c0 * CR;
   const int Q = lane >> 4;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -1453,29 +1429,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     }
     const int64_t p = pbase + 16 * g + (lane & 15);
     if (Q == 0 && p < P) {
-      if (gridDim.y > 1) {
-        atomicMax(keys + p, score_key(b, idx));
-      } else {
-        best_idx[p] = idx;
-        best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
-      }
+      best_idx[p] = idx;
+      best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
     }
-  }
-}
-
-// the split sweep's merged keys -> (row, distance) per pixel, as the unsplit kernel writes them;
-// the keys are cleared for the next launch
-template <int NSEG>
-__global__ void score_keys_finish_kernel(unsigned long long *__restrict__ keys, int64_t P, int32_t *__restrict__ best_idx,
-                                         float *__restrict__ best_dist) {
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x) {
-    const unsigned long long k = keys[p];
-    keys[p] = 0ull;
-    float b;
-    int idx;
-    score_unkey(k, &b, &idx);
-    best_idx[p] = idx;
-    best_dist[p] = ((float)NSEG - b) / (float)NSEG;
   }
 }
 
@@ -2075,23 +2031,19 @@ hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C, const 
   return HRF_OK;
 }
 
-hrf_status hrf_classify_pixels_table_split(const void *table, const uint8_t *flags, int64_t P, int32_t C,
-                                           const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
-                                           int32_t nsplit, void *keys, int32_t *best_idx, float *best_dist,
-                                           hrf_stream_t stream) {
+hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C, const void *refx,
+                                     int32_t R, const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                     float *best_dist, hrf_stream_t stream) {
   Bounds bd;
   if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
   int32_t kp = 0, rpad = 0;
   if (hrf_status s = hrf_classify_geometry(C, nseg, R, 2, &kp, &rpad)) return s;
   const int lay = layout_id(bd, C);
   HRF_REQUIRE(lay != 0, "classify_pixels_table: the E. coli or multispecies channel layout only");
-  HRF_REQUIRE(nsplit >= 1 && nsplit <= 16 && (nsplit == 1 || keys), "classify_pixels_table: nsplit 1..16 (keys for > 1)");
   if (P == 0) return HRF_OK;
   HRF_REQUIRE(table && flags && refx && best_idx && best_dist, "classify_pixels_table: null buffer");
   hipStream_t s = (hipStream_t)stream;
-  const int nch = rpad / 64;
-  if (nsplit > nch) nsplit = nch;
-  const dim3 grid((unsigned)hrf::cdiv(P, 256), (unsigned)nsplit);
+  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
   auto go = [&](auto lay_tag) -> hrf_status {
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
@@ -2101,25 +2053,15 @@ hrf_status hrf_classify_pixels_table_split(const void *table, const uint8_t *fla
     if (maxwg > 0 && maxwg < 3) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
     (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>(
-        (const uint4 *)table, flags, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist,
-        (unsigned long long *)keys);
-    if (nsplit > 1)
-      score_keys_finish_kernel<L::NSEG><<<hrf::stream_grid(P), 256, 0, s>>>((unsigned long long *)keys, P, best_idx,
-                                                                          best_dist);
+    classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
+                                                                        (const _Float16 *)refx, R, rpad, best_idx,
+                                                                        best_dist);
     return HRF_OK;
   };
   hrf_status st = lay == 1 ? go(LayEcoli{}) : go(LayMulti{});
   if (st) return st;
   HRF_LAUNCHED();
   return HRF_OK;
-}
-
-hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C, const void *refx,
-                                     int32_t R, const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
-                                     float *best_dist, hrf_stream_t stream) {
-  return hrf_classify_pixels_table_split(table, flags, P, C, refx, R, bounds_host, nseg, 1, nullptr, best_idx,
-                                         best_dist, stream);
 }
 
 }  // extern "C"

@@ -16,7 +16,6 @@
 // The calls are the library's own entry points (or their device-count twins), in pipeline.py's
 // order, so the results equal the composed path bit for bit (tests/test_tile_gpu.py).
 #include <algorithm>
-#include <cstdlib>
 
 #include "common.hpp"
 
@@ -49,7 +48,6 @@ struct hrf_tile_ctx {
   double *cn = nullptr;         // image_cn
   void *table = nullptr;        // pixel table
   uint8_t *flags = nullptr;
-  void *keys = nullptr;         // per-pixel merge keys of the split library sweep (zero between tiles)
   // per-label buffers, grown on demand (capacity cap labels + 1)
   int64_t cap = 0;
   double *sums = nullptr;
@@ -137,12 +135,8 @@ hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out) {
   if ((r = hrf_seg_ctx_create(H, W, &t->seg))) return fail(r);
   if ((r = dalloc(&t->proj, NL * n)) || (r = dalloc((char **)&t->xwork, (size_t)xb)) ||
       (r = dalloc(&t->shifts, 2 * NL)) || (r = dalloc(&t->cn, n)) || (r = dalloc((char **)&t->table, (size_t)tb)) ||
-      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)) || (r = dalloc((uint64_t **)&t->keys, n)))
+      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)))
     return fail(r);
-  if (hipMemset(t->keys, 0, sizeof(uint64_t) * n) != hipSuccess) {  // once: each split sweep leaves them zero
-    ::hrf::set_error("tile_ctx: key buffer initialisation failed");
-    return fail(HRF_EHIP);
-  }
   if (hipEventCreateWithFlags(&t->ev_reg, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&t->ev_pix, hipEventDisableTiming) != hipSuccess) {
     ::hrf::set_error("tile_ctx: event creation failed");
@@ -161,7 +155,6 @@ hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *t) {
   hipFree(t->cn);
   hipFree(t->table);
   hipFree(t->flags);
-  hipFree(t->keys);
   hipFree(t->nrows);
   hipFree(t->sums);
   hipFree(t->counts);
@@ -207,10 +200,7 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
       HRF_HIP(hipStreamWaitEvent(side, t->ev_reg, 0));
     }
     if (pix_start) HRF_HIP(hipEventRecord((hipEvent_t)pix_start, side));
-    // HRF_CLASSIFY_SPLIT = s: the library sweep as s workgroups per pixel block
-    static const int nsplit = getenv("HRF_CLASSIFY_SPLIT") ? atoi(getenv("HRF_CLASSIFY_SPLIT")) : 1;
-    HRF_TRY(hrf_classify_pixels_table_split(t->table, t->flags, n, C, refx, R, BOUNDS, NL, nsplit < 1 ? 1 : nsplit,
-                                            t->keys, pixel_idx, pixel_dist, side));
+    HRF_TRY(hrf_classify_pixels_table(t->table, t->flags, n, C, refx, R, BOUNDS, NL, pixel_idx, pixel_dist, side));
     if (pix_end) HRF_HIP(hipEventRecord((hipEvent_t)pix_end, side));
     if (side != s) HRF_HIP(hipEventRecord(t->ev_pix, side));
   }

@@ -838,16 +838,14 @@ def check_refx_table(refx, R, C, bounds, where):
                          % (where, refx.numel() * refx.element_size(), rpad, need))
 
 
-def classify_pixels_table(pt, refx, R, nsplit=1):
-    """classify_pixels (mode 2) from a PixTable: the same results bit for bit; nsplit > 1 splits
-    the library sweep over that many workgroups per pixel block (hrf_classify_pixels_table_split)"""
+def classify_pixels_table(pt, refx, R):
+    """classify_pixels (mode 2) from a PixTable: the same results bit for bit"""
     check_refx_table(refx, R, pt.C, pt.bounds, "classify_pixels_table")
     b = _i32_host(pt.bounds)
     idx = torch.empty(pt.shape, dtype=torch.int32, device=pt.table.device)
     dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
-    keys = torch.zeros(max(pt.P, 1), dtype=torch.int64, device=pt.table.device) if nsplit > 1 else None
-    _lib.call("hrf_classify_pixels_table_split", _ptr(pt.table), _ptr(pt.flags), pt.P, pt.C, _ptr(refx), R,
-              b.ctypes.data, len(b) - 1, int(nsplit), _ptr(keys), _ptr(idx), _ptr(dist), _stream())
+    _lib.call("hrf_classify_pixels_table", _ptr(pt.table), _ptr(pt.flags), pt.P, pt.C, _ptr(refx), R, b.ctypes.data,
+              len(b) - 1, _ptr(idx), _ptr(dist), _stream())
     return idx, dist
 
 

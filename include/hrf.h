@@ -438,14 +438,6 @@ HRF_API hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C
 HRF_API hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C,
                                              const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
                                              int32_t *best_idx, float *best_dist, hrf_stream_t stream);
-/* the same with the library sweep split over nsplit workgroups per pixel block (each sweeps
- * 1/nsplit of the rows; shorter workgroup lifetimes for the kernels sharing the CUs): keys = P
- * zeroed uint64 (the per-pixel merge; zeroed again on return, so a context allocates them once),
- * results bit for bit those of hrf_classify_pixels_table */
-HRF_API hrf_status hrf_classify_pixels_table_split(const void *table, const uint8_t *flags, int64_t P, int32_t C,
-                                                   const void *refx, int32_t R, const int32_t *bounds_host,
-                                                   int32_t nseg, int32_t nsplit, void *keys, int32_t *best_idx,
-                                                   float *best_dist, hrf_stream_t stream);
 /* presence flags of the gated variants on the library path (no classifier bundle): out (N x nseg)
  * f64, 1.0 where max(x[n, bounds[s]:bounds[s+1]]) > thr, else 0.0 (a NaN in the segment: 0.0) */
 HRF_API hrf_status hrf_segment_flags(const double *x, int64_t N, int32_t C, const int32_t *bounds_host, int32_t nseg,

@@ -83,29 +83,3 @@ def test_register_tile_falls_back(mods):
     stack, _, _, _ = S.tile(64, 72, seed=1)
     out = P.register_tile(S.laser_split(stack))
     assert isinstance(out, tuple) and out[0].shape == (64, 72, 95)
-
-
-@pytest.mark.parametrize("bounds,nbit,dup", [("ecoli", 10, False), ("ecoli", 10, True), ("multi", 7, True)])
-def test_split_library_sweep_bit_exact(mods, bounds, nbit, dup):
-    """hrf_classify_pixels_table_split: the library sweep as 2, 3 or 4 workgroups per pixel block
-    merged by atomicMax on (score, row) keys gives the unsplit kernel's rows and distances bit for
-    bit -- with duplicated library rows in different parts (exact ties: the smaller row wins, as
-    the unsplit sweep keeps the first), all-zero segments and negative samples"""
-    K, P, S = mods
-    b = S.ECOLI_BOUNDS if bounds == "ecoli" else S.MULTI_BOUNDS
-    stack, _, _, ref = S.tile(192, 256, nbit=nbit, bounds=b, seed=31)
-    if dup:
-        ref = ref.copy()
-        half = ref.shape[0] // 2
-        ref[half + 1:half + 40] = ref[1:40]          # row i and row half + i identical
-    st = stack.clone()
-    st[:4, :, b[1]:b[2]] = 0.0                       # an all-zero segment
-    st[4:6, :8, 0] = -0.01                           # negative samples (the unkeyed sweep)
-    pt = K.pixtable_prepare(st, b)
-    refx = K.classify_prepare(torch.from_numpy(ref).cuda(), b, mode=2)
-    want = K.classify_pixels_table(pt, refx, ref.shape[0])
-    for ns in (2, 3, 4):
-        got = K.classify_pixels_table(pt, refx, ref.shape[0], nsplit=ns)
-        assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]), ns
-    if dup:
-        assert int((want[0] > half).sum()) < want[0].numel()   # the duplicated rows are in play
