@@ -330,92 +330,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-__device__ float g_zero_src[4];  // zero-initialised: the source of every sample outside a laser's frame
-
-// The pixel-table assembly with the strips streamed by LDS-DMA (round 4): a strip's 64 x 95 tile is
-// 95 global_load_lds_dword instructions (64 lanes each: tile positions k*64 .. k*64 + 63, lane =
-// one (pixel, channel) of the pixel-major tile, read from its laser's shifted source -- or from
-// g_zero_src outside the laser's frame), issued by the four waves for strip t + gridDim.x into the
-// second LDS buffer while strip t is summed, normalised and written as the pixel table.  No
-// registers hold the prefetch (the register-held prefetch, HRF_ASSEMBLE_PF, spilled), and phase
-// barriers order LDS only (lds_barrier), so the next strip's loads stay in flight through them.
-// Two 24 KB tiles + per-strip bytes: three workgroups per CU.  Bit-identical outputs (same tile,
-// same phases as assemble_ecoli_kernel).
-__global__ __launch_bounds__(256) void assemble_ecoli_dma_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
-                                                                 double *__restrict__ cn_out, int cn_mode,
-                                                                 uint4 *__restrict__ ptab, uint8_t *__restrict__ pflags) {
-  constexpr int C = EcoliLasers<0>::C;
-  constexpr int NI = (AS_P * C + 63) / 64;  // 95 DMA instructions per strip
-  __shared__ __attribute__((aligned(16))) float tile[2][AS_P * C];
-  __shared__ uint8_t okp[2][AS_P];
-  __shared__ uint32_t fl[2][AS_P];
-  __shared__ double cns[AS_P];
-  __shared__ int sdr[LMAX], sdc[LMAX];
-  load_shifts(L, sdr, sdc);
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
-  auto issue = [&](int64_t t, int b) {
-    const int64_t r = t / nsx, c0 = (t - r * nsx) * AS_P;
-    const int np = (int)min((int64_t)AS_P, W - c0);
-    if (tid < AS_P) {  // coverage of every laser (apply_mask) and the flag accumulators of strip t
-      bool ok = tid < np;
-      if (apply_mask)
-        for (int q = 0; q < L.n; ++q) ok = ok && covered(r, c0 + tid, H, W, sdr[q], sdc[q]);
-      okp[b][tid] = (uint8_t)ok;
-      fl[b][tid] = 0;
-    }
-    for (int k = w; k < NI; k += 4) {
-      const int pos = k * 64 + lane;
-      const int i = pos / C, c = pos - i * C;
-      const int q = c < 32 ? 0 : c < 55 ? 1 : c < 75 ? 2 : c < 89 ? 3 : 4;
-      const int off = q == 0 ? 0 : q == 1 ? 32 : q == 2 ? 55 : q == 3 ? 75 : 89;
-      const int cl = q == 0 ? 32 : q == 1 ? 23 : q == 2 ? 20 : q == 3 ? 14 : 6;
-      const int dr = sdr[q], dc = sdc[q];
-      const int64_t cc = c0 + i;
-      const bool valid = pos < AS_P * C && i < np && covered(r, cc, H, W, dr, dc);
-      const float *src = valid ? L.src[q] + ((r - dr) * W + (cc - dc)) * (int64_t)cl + (c - off) : g_zero_src;
-      __builtin_amdgcn_global_load_lds((glb_void_t *)src, (lds_void_t *)(&tile[b][k * 64]), 4, 0, 0);
-    }
-  };
-  int b = 0;
-  if ((int64_t)blockIdx.x < nstrip) issue(blockIdx.x, 0);
-  for (int64_t t = blockIdx.x; t < nstrip; t += gridDim.x, b ^= 1) {
-    // strip t landed in tile[b] (every wave's pieces: vmcnt, then the barrier), and everyone is past
-    // strip t - 1, whose buffer the next issue reuses
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + gridDim.x < nstrip) issue(t + gridDim.x, b ^ 1);
-    const int64_t r = t / nsx, c0 = (t - r * nsx) * AS_P;
-    const int np = (int)min((int64_t)AS_P, W - c0);
-    const float *tb = tile[b];
-    {  // image_cn's channel sums in numpy's pairwise order (as assemble_ecoli_kernel)
-      const int j = tid & 7;
-      constexpr int main_n = C - (C % 8);
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int pi = half * 32 + (tid >> 3);
-        const float *a = tb + (pi < np ? pi : 0) * C;
-        const bool ok = pi < np && (!apply_mask || okp[b][pi]);
-        double rr = ok ? (double)a[j] : 0.0;
-#pragma unroll 2
-        for (int i = 8; i < main_n; i += 8) rr += ok ? (double)a[i + j] : 0.0;
-        rr = rr + __shfl_xor(rr, 1, 64);
-        rr = rr + __shfl_xor(rr, 2, 64);
-        rr = rr + __shfl_xor(rr, 4, 64);
-        double res = rr;
-        if (j == 0)
-          for (int i = main_n; i < C; ++i) res += ok ? (double)a[i] : 0.0;
-        if (j == 0 && pi < np) cns[pi] = res;
-      }
-    }
-    hrf_pix::lds_barrier();
-    hrf_pix::prep_tile_ecoli<true>(tile[b], apply_mask ? okp[b] : nullptr, np, r * W + c0, ptab, pflags, fl[b], cns,
-                                   cn_mode, cn_out);
-  }
-}
-
 // E. coli assembly launch: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one workgroup per strip)
 // of the kernel built for three workgroups per CU (165 VGPRs, no spills).  Interleaved on one box:
 // 1035 vs 991 Mpix/s end to end against the 2-per-CU build (197 VGPRs), isolated 1.03 vs 1.38 ms;
@@ -433,15 +347,6 @@ void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, fl
 
 void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                      uint4 *table, uint8_t *flags, hipStream_t s) {
-  // the pixel table without the stack: the LDS-DMA streamed kernel (HRF_ASSEMBLE_DMA=0: the
-  // register-staged one)
-  static const char *edma = getenv("HRF_ASSEMBLE_DMA");
-  if (table && !dst && cn_out && !(edma && atoi(edma) == 0)) {
-    const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
-    const unsigned grid = hrf::resident_grid(assemble_ecoli_dma_kernel, 256, 0, nstrip);
-    assemble_ecoli_dma_kernel<<<grid, 256, 0, s>>>(L, H, W, apply_mask, cn_out, cn_mode, table, flags);
-    return;
-  }
   // the stack-writing form (no table) runs the 4-per-CU build: 0.650 vs 0.687 ms (2 per CU, prefetch)
   static const char *epf = getenv("HRF_ASSEMBLE_PF"), *ewpe = getenv("HRF_ASSEMBLE_WPE");
   const bool pf = epf && atoi(epf) == 1;
