@@ -2051,6 +2051,10 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
     // HRF_CLASSIFY_MAXWG = m < 3: at most m workgroups per CU (as launch_w16_lay)
     static const int maxwg = getenv("HRF_CLASSIFY_MAXWG") ? atoi(getenv("HRF_CLASSIFY_MAXWG")) : 0;
     if (maxwg > 0 && maxwg < 3) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
+    // HRF_CLASSIFY_SHM = bytes: the LDS request raised to that (e.g. 56 KB: two workgroups per CU
+    // and 48 KB of LDS and a third of the VGPRs left for the chain kernels on the same CU)
+    static const long shm_env = getenv("HRF_CLASSIFY_SHM") ? atol(getenv("HRF_CLASSIFY_SHM")) : 0;
+    if (shm_env > 0) shm = std::max<size_t>(shm, (size_t)shm_env);
     (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,

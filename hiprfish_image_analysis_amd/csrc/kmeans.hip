@@ -925,6 +925,15 @@ __global__ __launch_bounds__(PT) void km_pp_corr_kernel(const double *__restrict
   __syncthreads();
   const int64_t nv = (int64_t)st->nvalid;
   const long long c0 = (long long)blockIdx.x * PB, c1 = c0 + PB < nv ? c0 + PB : nv;
+  // a chunk no trial's cell reaches: zero parts, and none of its values is read
+  bool reach = false;
+  for (int q = 0; q < d.nrun * NTMAX; ++q)
+    reach |= q % NTMAX < d.nt && rg[q][0] < c1 && rg[q][1] > c0;
+  if (!reach) {
+    for (int p = threadIdx.x; p < d.nrun * NTMAX; p += PT)
+      if (p % NTMAX < d.nt) part2[(int64_t)p * nch + blockIdx.x] = U128{0ull, 0ull};
+    return;
+  }
   const double scaleS = ldexp(1.0, st->S);
   double v[PB / PT];
 #pragma unroll
