@@ -43,7 +43,8 @@ struct hrf_tile_ctx {
   int64_t H = 0, W = 0;
   hrf_seg_ctx *seg = nullptr;
   double *proj = nullptr;       // NL x H x W channel-max projections
-  void *xwork = nullptr;        // xcorr workspace
+  void *xwork = nullptr;        // xcorr workspace (power-of-two tiles) or the hipFFT one (others)
+  bool pow2 = true;
   int32_t *shifts = nullptr;    // NL x 2
   double *cn = nullptr;         // image_cn
   void *table = nullptr;        // pixel table
@@ -119,13 +120,17 @@ extern "C" {
 hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out) {
   HRF_REQUIRE(out && H >= 1 && W >= 16 && W % 16 == 0 && H * W < ((int64_t)1 << 31),
               "tile_ctx: bad size (W a multiple of 16)");
-  const int64_t xb = hrf_xcorr_workspace_bytes(NL, H, W);
-  HRF_REQUIRE(xb > 0, "tile_ctx: the registration FFT needs power-of-two H and W");
+  // power-of-two tiles: the hand-written FFT pipeline (xcorr.hip); other sizes: hipFFT per target
+  // (register.hip), the same shifts (tests/test_registration_gpu.py)
+  const int64_t xw = hrf_xcorr_workspace_bytes(NL, H, W);
+  const int64_t xb = xw > 0 ? xw : hrf_register_workspace_bytes(H, W);
+  HRF_REQUIRE(xb > 0, "tile_ctx: registration workspace size");
   const int64_t tb = hrf_pixtable_bytes(H * W, C, BOUNDS, NL);
   HRF_REQUIRE(tb > 0, "tile_ctx: pixel table size");
   hrf_tile_ctx *t = new hrf_tile_ctx();
   t->H = H;
   t->W = W;
+  t->pow2 = xw > 0;
   auto fail = [&](hrf_status st) {
     hrf_tile_ctx_destroy(t);
     return st;
@@ -190,7 +195,14 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
   double *proj[NL];
   for (int l = 0; l < NL; ++l) proj[l] = t->proj + l * n;
   HRF_TRY(hrf_channel_max_multi(lasers_host, CH, NL, n, proj, s));
-  HRF_TRY(hrf_xcorr_shifts_dev(t->proj, NL, H, W, t->xwork, 15, t->shifts, s));
+  if (t->pow2) {
+    HRF_TRY(hrf_xcorr_shifts_dev(t->proj, NL, H, W, t->xwork, 15, t->shifts, s));
+  } else {  // row 0 = (0, 0); the reference's transform is taken once (src == NULL reuses it)
+    HRF_HIP(hipMemsetAsync(t->shifts, 0, 2 * sizeof(int32_t), s));
+    for (int l = 1; l < NL; ++l)
+      HRF_TRY(hrf_register_translation_dev(l == 1 ? proj[0] : nullptr, proj[l], H, W, t->xwork, 15, t->shifts + 2 * l,
+                                           s));
+  }
   // ecoli :58-72 registered assembly (coverage mask) -> image_cn + the pixel table
   HRF_TRY(hrf_register_assemble_pixtable(lasers_host, CH, t->shifts, NL, H, W, 1, nullptr, t->cn, 1, t->table,
                                          t->flags, s));

@@ -495,7 +495,8 @@ def process_tile_native(lasers, lib: Library, calibration=None, per_pixel: bool 
     tile.hip): ecoli measurement.py:44-162 (-c T) + image_classification.py:43-71 + collect
     :92-98, the per-pixel classifier on the side stream with `overlap`.  The same results as the
     composed path bit for bit (tests/test_tile_gpu.py).  lasers: the five E. coli acquisitions
-    (H, W powers of two)."""
+    (W a multiple of 16; the registration FFT is xcorr.hip for power-of-two H and W, hipFFT
+    otherwise)."""
     main = torch.cuda.current_stream(lasers[0].device)
     side = _side_stream(main) if (per_pixel and overlap) else None
     refx = lib.refx_table() if per_pixel else None

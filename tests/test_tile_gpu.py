@@ -76,6 +76,22 @@ def test_tile_native_equals_composed(mods, variant, calibrated):
     _check(nat, ref)
 
 
+def test_tile_native_non_power_of_two(mods):
+    """a 384 x 320 tile (not powers of two): the native call registers through hipFFT per target
+    and equals the composed path bit for bit"""
+    K, P, S = mods
+    H, W = 384, 320
+    lib = _lib(P, S)
+    lasers = _lasers(S, H, W, 20190114)
+    cal = S.flat_field(H, W, device="cuda")
+    assert not K.xcorr_supported(5, H, W)
+    nat = P.process_tile_native(lasers, lib, calibration=cal, variant=1)
+    ref = P.process_tile(P.register_tile(lasers), lib, calibration=cal, per_pixel=True, variant=1)
+    torch.cuda.synchronize()
+    assert nat.ncells > 10
+    _check(nat, ref)
+
+
 def test_tile_native_no_overlap_no_pixels(mods):
     K, P, S = mods
     H = W = 256
