@@ -31,9 +31,14 @@ returning part of it.
 The biofilm script's loaders (hiprfish_imaging_biofilm_analysis.py:55-120) are here too:
 `load_ztslice(path, z, t, series)`, the z-stacks `load_image_zstack_fixed_t(path, t)` ->
 (H, W, Z, C) (np.stack over z on axis 2, `load_image_tile` = t 0) and the z-window
-`load_image_zstack_fixed_t_memory_efficient`, and the OME sizes `get_{x,y,c,z,t}_range` /
-`get_image_count` from the directory.  A `series` selects a mosaic tile (M index) unstitched,
-as Bio-Formats' per-tile series do; series=None stitches the scene.
+`load_image_zstack_fixed_t_memory_efficient`, the per-tile `load_ztslice_tile` /
+`load_image_zstack_fixed_t_tile`, and the OME sizes `get_{x,y,c,z,t}_range` / `get_image_count`
+/ `get_tile_size` from the directory.  Series convention: every mosaic tile (M index) is a
+series, as in the Bio-Formats of the reference's era (the biofilm script takes
+get_tile_size = sqrt(image_count) and stitches the per-tile series itself, :93-96, :1066), so
+get_image_count is the tile count and get_x_range / get_y_range are series 0's (one tile's)
+size; `series=k` reads tile k unstitched.  series=None (this reader's default) stitches the
+scene -- for the single-tile acquisitions the measurement scripts load the two agree.
 
 Bio-Formats itself is absent here, so parity with load_image is unpinned; the layout follows
 the published ZISRAW specification and is exercised on files written to it (tests/test_czi.py).
@@ -303,12 +308,34 @@ def dims(path):
     return out
 
 
+def _series0_size(path):
+    """(X, Y) of series 0: the first mosaic tile when the scene has several (Bio-Formats of the
+    reference's era gives every tile its own series, so ome.image(0).Pixels is one tile), else
+    the scene"""
+    buf = _open(path)
+    try:
+        ent = _level0(read_directory(buf))
+    finally:
+        _close(buf)
+    if not ent:
+        raise CziError("%s: no level-0 subblocks" % path)
+    scene = min(e.start("S") for e in ent)
+    ent = [e for e in ent if e.start("S") == scene]
+    m0 = min(e.start("M") for e in ent)
+    ent = [e for e in ent if e.start("M") == m0]
+    x = max(e.start("X") + e.dims["X"][1] for e in ent) - min(e.start("X") for e in ent)
+    y = max(e.start("Y") + e.dims["Y"][1] for e in ent) - min(e.start("Y") for e in ent)
+    return x, y
+
+
 def get_x_range(path):
-    return dims(path)["X"]
+    """ome.image(0).Pixels.SizeX (biofilm :63-67): one tile's width when tiles are series"""
+    return _series0_size(path)[0]
 
 
 def get_y_range(path):
-    return dims(path)["Y"]
+    """ome.image(0).Pixels.SizeY (biofilm :69-73)"""
+    return _series0_size(path)[1]
 
 
 def get_c_range(path):
@@ -324,7 +351,24 @@ def get_t_range(path):
 
 
 def get_image_count(path):
+    """ome.image_count (biofilm :98-101): the series count = mosaic tiles of the first scene
+    (load_image(path, series=k) reads tile k unstitched)"""
     return dims(path)["M"]
+
+
+def get_tile_size(path):
+    """int(sqrt(ome.image_count)) (biofilm :93-96): tiles per side of a square mosaic"""
+    return int(np.sqrt(get_image_count(path)))
+
+
+def load_ztslice_tile(path, z_index, t_index, tile, rescale=True):
+    """bioformats.load_image(path, z=, t=, series=tile) (biofilm :59-61)"""
+    return load_image(path, rescale=rescale, z=z_index, t=t_index, series=tile)
+
+
+def load_image_zstack_fixed_t_tile(path, t, tile, rescale=True):
+    """(H, W, Z, C) of one tile (biofilm :116-119)"""
+    return load_image_zstack_fixed_t_memory_efficient(path, t, 0, get_z_range(path), tile, rescale)
 
 
 def load_ztslice(path, z_index, t_index, series=None, rescale=True):

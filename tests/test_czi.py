@@ -78,6 +78,10 @@ def test_zstack_loaders_and_sizes(tmp_path):
     d = czi.dims(p)
     assert (d["X"], d["Y"], d["Z"], d["C"], d["T"], d["M"]) == (30, 20, 4, 6, 1, 2)
     assert czi.get_z_range(p) == 4 and czi.get_c_range(p) == 6 and czi.get_image_count(p) == 2
+    # series 0 (ome.image(0)) is one tile: 15 of the 30 columns; get_tile_size = sqrt(count)
+    assert (czi.get_x_range(p), czi.get_y_range(p)) == (15, 20) and czi.get_tile_size(p) == 1
+    assert np.array_equal(czi.load_image_zstack_fixed_t_tile(p, 0, 1, rescale=False), vol[:, 15:])
+    assert np.array_equal(czi.load_ztslice_tile(p, 3, 0, 0, rescale=False), vol[:, :15, 3])
     got = czi.load_image_zstack_fixed_t(p, 0)
     assert got.dtype == np.float32 and got.shape == (20, 30, 4, 6)
     assert np.array_equal(got, vol.astype(np.float32) / np.float32(65535.0))
