@@ -261,6 +261,50 @@ HRF_DM_FN double hrf_div_rcp(double x, double d, double r) {
   return fma(e, r, q);
 }
 
+/* BEGIN EXPTAB (gen_logtab.py) */
+HRF_DM_TAB double hrf_exp2tab64[64] = {
+  1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+  1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+  1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+  1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+  1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+  1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+  1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+  1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+  1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+  1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+  1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+  1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+  1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+  1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+  1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+  1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951,
+};
+#define HRF_EXP_INVL 92.33248261689366
+#define HRF_EXP_L2HI 0.010830424696249145
+#define HRF_EXP_L2LO 3.623510646634843e-19
+/* END EXPTAB */
+
+/* e^x for x in [-8, 0] (the NL-means weights, nlmeans.hip / oracle_nl_means): x = (64 m + j)
+ * ln2/64 + r with k = rint(x * 64/ln2), |r| <= ln2/128 (Cody-Waite, two FMAs), then
+ * 2^(j/64) (1 + q) with q = r + r^2/2 + ... + r^5/120 (truncation < 4e-17 relative) and an
+ * exact scale by 2^m.  tab = hrf_exp2tab64 (the kernel passes its LDS copy).  Same operations
+ * in the same order on both sides, so the kernel's weights equal the oracle's bit for bit. */
+HRF_DM_FN double hrf_exp_neg_tab(double x, const double *tab) {
+    const double k = rint(x * HRF_EXP_INVL);
+    const int ki = (int)k;
+    double r = fma(-k, HRF_EXP_L2HI, x);
+    r = fma(-k, HRF_EXP_L2LO, r);
+    double q = 1.0 / 120.0;
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    q = fma(q, r, 1.0);
+    q = q * r;
+    const double t = tab[ki & 63];
+    return ldexp(fma(t, q, t), ki >> 6);
+}
+
 /* x >= 0 (umap's squared distances): x^y */
 HRF_DM_FN double hrf_det_pow(double x, double y) {
   if (x == 0.0) return y > 0.0 ? 0.0 : (y == 0.0 ? 1.0 : INFINITY);

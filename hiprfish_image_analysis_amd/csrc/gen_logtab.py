@@ -1,6 +1,7 @@
 """Generate the constant tables of hrf_cr_log / hrf_cr_log10 (detmath.h) with Python's decimal
 module: ln(k/128) for k = 96..192 as double-double (hi, lo) pairs, ln 2, 1/3, 1/5 and 1/ln 10 as
-double-doubles.  Rewrites the block between the BEGIN/END LOGTAB markers of detmath.h.
+double-doubles; 2^(j/64) for j = 0..63 (hrf_exp_neg_tab, the NL-means weights).  Rewrites the
+blocks between the BEGIN/END LOGTAB and BEGIN/END EXPTAB markers of detmath.h.
 
 Run: python csrc/gen_logtab.py
 """
@@ -39,6 +40,18 @@ def main():
     src = open(path).read()
     a = src.index("/* BEGIN LOGTAB")
     b = src.index("/* END LOGTAB */") + len("/* END LOGTAB */")
+    src = src[:a] + "\n".join(out) + src[b:]
+    e = [float(D(2) ** (D(j) / D(64))) for j in range(64)]
+    inv = float(D(64) / D(2).ln())
+    l2 = D(2).ln() / D(64)
+    l2hi = float(l2)
+    l2lo = float(l2 - D(l2hi))
+    out = ["/* BEGIN EXPTAB (gen_logtab.py) */", "HRF_DM_TAB double hrf_exp2tab64[64] = {"]
+    out += ["  %s," % ", ".join(repr(v) for v in e[i:i + 4]) for i in range(0, 64, 4)]
+    out += ["};", "#define HRF_EXP_INVL %s" % repr(inv), "#define HRF_EXP_L2HI %s" % repr(l2hi),
+            "#define HRF_EXP_L2LO %s" % repr(l2lo), "/* END EXPTAB */"]
+    a = src.index("/* BEGIN EXPTAB")
+    b = src.index("/* END EXPTAB */") + len("/* END EXPTAB */")
     open(path, "w").write(src[:a] + "\n".join(out) + src[b:])
     print("wrote", path)
 

@@ -18,6 +18,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../hiprfish_image_analysis_amd/csrc/detmath.h"
+
 #define EXPORT __attribute__((visibility("default")))
 
 /* ------------------------------------------------------------------------------------
@@ -944,39 +946,28 @@ EXPORT void oracle_nl_means_skimage(const double *img, int64_t H, int64_t W, int
 }
 
 /* The same weights per pixel, in the summation order AND arithmetic of libhrf's
- * nl_means_kernel, so the two are bit-identical (tests/test_nlmeans_gpu.py) and the whole
- * community chain can be compared without handing the GPU image to the oracle:
- * out[p] = (2 P[p] + sum_s w_s P[p+s]) / (2 + sum_s w_s) over the full (2d+1)^2 window
- * (s != 0) in raster order of s; patch distance = sum over 7 rows (top to bottom) of the
- * row's 7 squared differences (left to right); skimage's cut max(D,0)/h2s2 <= 5 as the
- * exact threshold D <= lim on D; w = e^{-max(D,0) * (1/h2s2)} by Cody-Waite reduction and
- * the degree-13 Taylor polynomial (exp_neg_small below, the kernel's).  Agrees with the
- * integral-image restatement above within 1e-12. */
-static double exp_neg_small(double x) {
-    const double k = rint(x * 1.4426950408889634);
-    double r = fma(-k, 6.93147180369123816490e-01, x);
-    r = fma(-k, 1.90821492927058770002e-10, r);
-    double p = 1.0 / 6227020800.0;
-    p = fma(p, r, 1.0 / 479001600.0);
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    return ldexp(p, (int)k);
-}
+ * nl_means_pairs_kernel, so the two are bit-identical (tests/test_nlmeans_gpu.py) and the
+ * whole community chain can be compared without handing the GPU image to the oracle:
+ * out[p] = (2 P[p] + sum_s w_s P[p+s]) / (2 + sum_s w_s) over the (2d+1)^2 window, s != 0,
+ * taken as skimage takes it -- each unordered pair once: for s in the half window H+ (sr > 0,
+ * or sr == 0 and sc > 0) in raster order, first the pair (p, p+s), then (p-s, p).  Patch
+ * distance of the pair (a, a+s) = sum7 over 7 rows (top to bottom) of the row's sum7 of 7
+ * squared differences (left to right), sum7 the kernel's fixed tree -- symmetric in a and
+ * a+s, so both ends see the same weight; skimage's cut
+ * max(D,0)/h2s2 <= 5 as the exact threshold D <= lim on D (a cut pair adds w = 0);
+ * w = e^{-max(D,0) * (1/h2s2)} by hrf_exp_neg_tab (detmath.h, shared with the kernel).
+ * Agrees with the integral-image restatement above within 1e-12. */
+/* nlmeans.hip sum7: ((v0 + v1) + (v2 + v3)) + ((v4 + v5) + v6) */
+static double sum7(const double *v) { return ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + v[6]); }
 
 EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, int dist, double h, double sigma,
                             double *out) {
     const int s = patch % 2 == 0 ? patch + 1 : patch;
     const int off = s / 2;
+    if (s != 7) { /* sum7: the kernel is built for patch 7 only */
+        for (int64_t i = 0; i < H * W; ++i) out[i] = NAN;
+        return;
+    }
     const int64_t pw = off + dist, wp = W + 2 * pw;
     double *P = reflect_pad(img, H, W, pw);
     const double h2 = h * h, s2 = (double)s * (double)s, h2s2 = 1.0 * h2 * s2, var = sigma * sigma;
@@ -992,26 +983,27 @@ EXPORT void oracle_nl_means(const double *img, int64_t H, int64_t W, int patch, 
         for (int64_t c = 0; c < W; ++c) {
             const double *p = P + (r + pw) * wp + (c + pw);
             double acc = p[0] + p[0], ws = 2.0;
-            for (int sr = -dist; sr <= dist; ++sr)
-                for (int sc = -dist; sc <= dist; ++sc) {
-                    if (sr == 0 && sc == 0) continue;
-                    const double *q = p + sr * wp + sc;
-                    double D = 0.0;
-                    for (int du = -off; du <= off; ++du) {
-                        double hs = 0.0;
-                        for (int dv = -off; dv <= off; ++dv) {
-                            const double t = p[du * wp + dv] - q[du * wp + dv];
-                            const double sq = var == 0.0 ? t * t : t * t - var;
-                            hs = dv == -off ? sq : hs + sq;
+            for (int sr = 0; sr <= dist; ++sr)
+                for (int sc = sr == 0 ? 1 : -dist; sc <= dist; ++sc)
+                    for (int end = 0; end < 2; ++end) {
+                        /* the pair (a, a + s): a = p first, then a = p - s; the partner's value */
+                        const double *a = end == 0 ? p : p - sr * wp - sc;
+                        const double *b = a + sr * wp + sc;
+                        double hs[7], sq[7];
+                        for (int du = -off; du <= off; ++du) {
+                            for (int dv = -off; dv <= off; ++dv) {
+                                const double t = a[du * wp + dv] - b[du * wp + dv];
+                                sq[dv + off] = var == 0.0 ? t * t : t * t - var;
+                            }
+                            hs[du + off] = sum7(sq);
                         }
-                        D = du == -off ? hs : D + hs;
-                    }
-                    if (D <= lim) {
-                        const double w = exp_neg_small(-(D > 0.0 ? D : 0.0) * inv);
+                        const double D = sum7(hs);
+                        /* a cut pair adds w = 0, as the kernel's pixel phase does */
+                        const double w = D <= lim ? hrf_exp_neg_tab(-(D > 0.0 ? D : 0.0) * inv, hrf_exp2tab64) : 0.0;
                         ws += w;
-                        acc += w * q[0];
+                        const double t = w * (end == 0 ? b[0] : a[0]);
+                        acc += t;
                     }
-                }
             out[r * W + c] = acc / ws;
         }
     free(P);
