@@ -396,7 +396,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                "per-pixel classification, counts", "concurrent": T, "steps": steps,
                    "value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
                    "ms_per_tile": round(sec / (steps * T) * 1e3, 3),
-                   "roofline": {"kernel": "nl_means_kernel<false>", "bound": "valu-f64", "kernel_ms": round(ms_nl, 4),
+                   "roofline": {"kernel": "nl_means_pairs_kernel<false, 8, 4, 1024, 48>", "bound": "valu-f64", "kernel_ms": round(ms_nl, 4),
                                 "algorithmic_ops_per_pixel": NL_OPS_PER_PIXEL, "achieved": round(ach, 3),
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s", "frac": round(ach / F64_VALU_PEAK_TOPS, 4)}}
     del ctiles, s, norm, ccal

@@ -305,6 +305,26 @@ HRF_DM_FN double hrf_exp_neg_tab(double x, const double *tab) {
     return ldexp(fma(t, q, t), ki >> 6);
 }
 
+/* The same value for x in [-8, 0] from a widened table tabw[i] = 2^(-i/64), i = 0..739
+ * (= ldexp(hrf_exp2tab64[-i & 63], -i >> 6), exact): fma(t 2^m, q, t 2^m) = 2^m fma(t, q, t)
+ * exactly in the normal range, so the result equals hrf_exp_neg_tab's bit for bit without
+ * the ldexp and the index split. */
+#define HRF_EXP_WIDE_N 740
+HRF_DM_FN double hrf_exp_neg_tabw(double x, const double *tabw) {
+    const double k = rint(x * HRF_EXP_INVL);
+    const int ki = (int)k;
+    double r = fma(-k, HRF_EXP_L2HI, x);
+    r = fma(-k, HRF_EXP_L2LO, r);
+    double q = 1.0 / 120.0;
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    q = fma(q, r, 1.0);
+    q = q * r;
+    const double t = tabw[-ki];
+    return fma(t, q, t);
+}
+
 /* x >= 0 (umap's squared distances): x^y */
 HRF_DM_FN double hrf_det_pow(double x, double y) {
   if (x == 0.0) return y > 0.0 ? 0.0 : (y == 0.0 ? 1.0 : INFINITY);

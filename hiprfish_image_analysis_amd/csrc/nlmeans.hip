@@ -21,8 +21,8 @@
 // pixels with the (48+28) x (64+28) reflect-padded f64 neighbourhood in LDS; per shift three
 // barrier-separated phases build the pair's row sums, distances + weights and the two
 // accumulations through LDS (141 KB: one workgroup, 16 waves per CU).  All 7-term sums use one
-// fixed tree (sum7) and -ffp-contract=off, the exponential is hrf_exp_neg_tab (detmath.h): the
-// oracle repeats the same operations, so results are bit-identical.  HBM traffic is 16 B per
+// fixed tree (sum7) and -ffp-contract=off, the exponential is hrf_exp_neg_tabw (detmath.h, equal
+// to the oracle's hrf_exp_neg_tab bit for bit): results are bit-identical.  HBM traffic is 16 B per
 // pixel: the kernel is f64-VALU bound.
 //
 // nl_means_kernel (HRF_NLM_PERPIXEL=1, timing A/B only) is the round-3 per-pixel walk: every
@@ -238,7 +238,7 @@ constexpr int NP_BW = 81;                                   // >= 64 + 16 (last 
 constexpr int np_wh(int th, int cseg) { return (th + NL_DIST + cseg - 1) / cseg * cseg; }
 constexpr int np_hsh(int th, int cseg) { return np_wh(th, cseg) + 2 * NL_OFF; }
 constexpr int np_lds(int th, int cseg) {
-  return ((th + 2 * NL_HALO) * NP_LW + (np_hsh(th, cseg) + np_wh(th, cseg)) * NP_BW + 64) * 8;
+  return ((th + 2 * NL_HALO) * NP_LW + (np_hsh(th, cseg) + np_wh(th, cseg)) * NP_BW + HRF_EXP_WIDE_N) * 8;
 }
 
 template <bool VAR, int RSEG, int CSEG, int NT, int NP_TH>
@@ -253,9 +253,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? 2 : 4) void nl_means_pairs_kernel(c
   __shared__ double P[NP_LH * NP_LW];
   __shared__ double HS[NP_HSH * NP_BW];
   __shared__ double WB[NP_WH * NP_BW];
-  __shared__ double ET[64];  // hrf_exp2tab64
+  __shared__ double ET[HRF_EXP_WIDE_N];  // 2^(-i/64): hrf_exp_neg_tabw
   const int tid = threadIdx.x;
-  if (tid < 64) ET[tid] = hrf_exp2tab64[tid];
+  for (int i = tid; i < HRF_EXP_WIDE_N; i += NT) ET[i] = ldexp(hrf_exp2tab64[-i & 63], -i >> 6);
   const int64_t r0 = (int64_t)blockIdx.y * NP_TH, c0 = (int64_t)blockIdx.x * NP_TW;
   for (int idx = tid; idx < NP_LH * NP_LW; idx += NP_THREADS) {
     const int lr = idx / NP_LW, lc = idx - lr * NP_LW;
@@ -316,8 +316,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? 2 : 4) void nl_means_pairs_kernel(c
           // lim = the largest D with fl(D / h2s2) <= 5 (host): exactly skimage's cut, no division
           // branch-free: the CSEG exponentials are independent chains the scheduler can
           // interleave; the clamp only touches cut pairs (x < -5.0001), whose w is 0 anyway
-          const double x = -(D > 0.0 ? D : 0.0) * inv;
-          const double e = hrf_exp_neg_tab(fmax(x, -8.0), ET);
+          // sigma = 0: D is a sum of squares, never negative, and max(D, 0) is D itself
+          const double x = -(VAR ? (D > 0.0 ? D : 0.0) : D) * inv;
+          const double e = hrf_exp_neg_tabw(fmax(x, -8.0), ET);
           wb[k * NP_BW] = D <= lim ? e : 0.0;
         }
       }
@@ -356,7 +357,7 @@ void launch_pairs(int rseg, int cseg, int nt, int th, hipStream_t st, const doub
     nl_means_pairs_kernel<VAR, R, C, T, TH><<<g, T, 0, st>>>(img, H, W, inv, lim, var, out);          \
     return;                                                                                           \
   }
-  HRF_NP(8, 4, 512, 16) HRF_NP(8, 4, 1024, 32) HRF_NP(8, 4, 1024, 48) HRF_NP(16, 4, 1024, 48) HRF_NP(8, 8, 1024, 48)
+  HRF_NP(8, 4, 1024, 32) HRF_NP(8, 4, 1024, 48) HRF_NP(16, 4, 1024, 48) HRF_NP(8, 8, 1024, 48)
   HRF_NP(8, 4, 768, 48)
 #undef HRF_NP
   dim3 g((unsigned)hrf::cdiv(W, NP_TW), (unsigned)hrf::cdiv(H, 48));

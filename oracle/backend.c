@@ -497,3 +497,26 @@ __attribute__((visibility("default"))) int64_t oracle_div_rcp_check(uint64_t see
   }
   return bad;
 }
+
+/* nlmeans.hip's widened-table exponential against detmath.h hrf_exp_neg_tab (the oracle's):
+ * n values spread over [-8, 0] plus every rounding boundary k ln2/64 and its neighbours;
+ * returns the count of results that differ in any bit. */
+__attribute__((visibility("default"))) int64_t oracle_exp_tabw_check(int64_t n) {
+  static double tabw[HRF_EXP_WIDE_N];
+  for (int i = 0; i < HRF_EXP_WIDE_N; ++i) tabw[i] = ldexp(hrf_exp2tab64[-i & 63], -i >> 6);
+  int64_t bad = 0;
+  for (int64_t i = 0; i <= n; ++i) {
+    const double x = -8.0 * (double)i / (double)n;
+    const double a = hrf_exp_neg_tab(x, hrf_exp2tab64), b = hrf_exp_neg_tabw(x, tabw);
+    if (memcmp(&a, &b, 8) != 0) ++bad;
+  }
+  for (int k = 0; k <= 739; ++k) {
+    double x = -(k + 0.5) / HRF_EXP_INVL;
+    for (int d = 0; d < 5; ++d) x = nextafter(x, 0.0);
+    for (int d = 0; d < 10 && x >= -8.0; ++d, x = nextafter(x, -9.0)) {
+      const double a = hrf_exp_neg_tab(x, hrf_exp2tab64), b = hrf_exp_neg_tabw(x, tabw);
+      if (memcmp(&a, &b, 8) != 0) ++bad;
+    }
+  }
+  return bad;
+}

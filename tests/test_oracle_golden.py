@@ -294,3 +294,12 @@ def test_flat_field_division_through_reciprocal(orc):
     f = orc.lib().oracle_div_rcp_check
     f.restype = ctypes.c_int64
     assert f(ctypes.c_uint64(7), ctypes.c_int64(20_000_000)) == 0
+
+
+def test_nl_means_widened_exp_table(orc):
+    """nlmeans.hip's exponential (hrf_exp_neg_tabw: 740-entry table, no ldexp) equals the
+    oracle's hrf_exp_neg_tab bit for bit over [-8, 0] and at every rounding boundary of k"""
+    import ctypes
+    f = orc.lib().oracle_exp_tabw_check
+    f.restype = ctypes.c_int64
+    assert f(ctypes.c_int64(4_000_000)) == 0
