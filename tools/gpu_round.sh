@@ -20,4 +20,5 @@ cut -c1-300 $o/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $o/prof -o run -- python3 bench.py --steps 30 --warmup 5 --no-extras --no-cpu-baseline > $o/prof_bench.json 2> $o/prof.err || { echo "profile failed"; exit 1; }
 bash tools/gpu_pmc.sh $tag t || { echo "pmc failed"; exit 1; }
 bash tools/gpu_pmc_hbm.sh || { echo "pmc hbm failed"; exit 1; }
+bash tools/gpu_pmc_nlm.sh $tag || { echo "pmc nlm failed"; exit 1; }
 echo round done
