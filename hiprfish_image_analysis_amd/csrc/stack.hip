@@ -771,7 +771,8 @@ __global__ void calibrate_kernel(const float *__restrict__ stack, int64_t npix, 
 // foreground pixel's value is its laser's source pixel shifted by (dr_q, dc_q), 0 outside the
 // laser's frame or -- apply_mask -- outside any laser's frame (register_assemble's stack, which
 // then never has to exist).  CAL: a per-pixel flat field on channels [cal0, cal1).
-template <bool CAL>
+// DIV (HRF_LSL_DIV=1, timing A/B only): the per-channel f64 division instead of the reciprocal
+template <bool CAL, bool DIV = false>
 __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                                 const int32_t *__restrict__ lab, int32_t maxlab,
                                                                 const float *__restrict__ cal, int cal0, int cal1,
@@ -876,7 +877,7 @@ __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_
             const double r = __builtin_bit_cast(
                 double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(rb >> 32), idx[j]) << 32) |
                             (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rb, idx[j]));
-            if (df != 0.0f && __builtin_isfinite(df)) {
+            if (!DIV && df != 0.0f && __builtin_isfinite(df)) {
               a0 += k0 ? hrf_div_rcp((double)x0[j], d, r) : (double)x0[j];
               a1 += k1 ? hrf_div_rcp((double)x1[j], d, r) : (double)x1[j];
             } else {
@@ -1021,9 +1022,14 @@ hrf_status hrf_label_sums_lasers(const float *const *src_host, const int32_t *ch
   HRF_REQUIRE(labels, "label_sums_lasers: null labels");
   const int64_t nblk = hrf::cdiv(hrf::cdiv(H * W, 64), 4);
   if (cal) {
+    static const bool div = getenv("HRF_LSL_DIV") != nullptr;
     const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<true>, 256, 0, nblk);
-    label_sums_lasers_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0, cal_c1, sums,
-                                                       (unsigned long long *)counts);
+    if (div)
+      label_sums_lasers_kernel<true, true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0,
+                                                                cal_c1, sums, (unsigned long long *)counts);
+    else
+      label_sums_lasers_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0, cal_c1,
+                                                         sums, (unsigned long long *)counts);
   } else {
     const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<false>, 256, 0, nblk);
     label_sums_lasers_kernel<false><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, nullptr, 0, 0, sums,
