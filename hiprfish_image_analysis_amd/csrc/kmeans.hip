@@ -274,7 +274,7 @@ __global__ void km_minmax_kernel(const double *__restrict__ x, const uint8_t *__
 }
 
 // value and potential scales (oracle_kmeans_scale / kmeans_sk.c)
-__global__ void km_scale_kernel(KmState *st) {
+__device__ __forceinline__ void km_scale(KmState *st) {
   const double amax = __longlong_as_double((long long)st->amax_bits);
   int e = 0;
   frexp(amax > 0 ? amax : 1.0, &e);
@@ -368,10 +368,16 @@ __device__ __forceinline__ u128 km_q2(long long v) {
   return (u128)a * a;
 }
 
-__global__ void km_bucket_init_kernel(KmState *st, double *geo) {
+__device__ __forceinline__ void km_bucket_init(KmState *st, double *geo) {
   const double mn = ord_dec(st->lo_bits), mx = ord_dec(st->hi_bits);
   geo[0] = mn;
   geo[1] = mx > mn ? (double)KM_NB / (mx - mn) : 0.0;
+}
+
+// the scales and (n > 0) the bucket geometry, one launch
+__global__ void km_scale_kernel(KmState *st, double *geo) {
+  km_scale(st);
+  if (geo) km_bucket_init(st, geo);
 }
 
 __device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long long v, unsigned long long *sh,
@@ -722,7 +728,7 @@ __global__ __launch_bounds__(PT) void km_bucket_prefix_kernel(const double *__re
 }
 
 // tol = 1e-4 * var(x) from the exact sums (kmeans_sk.c)
-__global__ void km_tol_kernel(KmState *st) {
+__device__ __forceinline__ void km_tol(KmState *st) {
   const long long nv = (long long)st->nvalid;
   if (!nv) {
     st->tol = 0;
@@ -1423,15 +1429,16 @@ __device__ bool same_clustering(const SkRun &a, const SkRun &b) {
 // both hold a positive sample, else sklearn's cluster 0 (the reference's NaN comparison);
 // 2 (k = 2, ecoli :75-84) the larger cluster mean when both are non-empty, else cluster 0
 template <int K>
-__global__ void km_best_kernel(KmState *st, int nrun, int rule) {
-  if (threadIdx.x != 0) return;
+__device__ void km_best(KmState *st, int nrun, int rule, bool write, int *best_out, int *top_out) {
   int best = 0;
   for (int r = 1; r < nrun; ++r)
     if (st->run[r].inertia < st->run[best].inertia && !same_clustering<K>(st->run[r], st->run[best])) best = r;
-  st->best = best;
   const SkRun &B = st->run[best];
-  for (int j = 0; j < K; ++j) st->center[j] = B.cen[j];
-  st->iters = B.iters;
+  if (write) {
+    st->best = best;
+    for (int j = 0; j < K; ++j) st->center[j] = B.cen[j];
+    st->iters = B.iters;
+  }
   long long n_of[KMAX];
   long long c0 = 0;
   for (int p = 0; p < K; ++p) {
@@ -1451,12 +1458,14 @@ __global__ void km_best_kernel(KmState *st, int nrun, int rule) {
     const bool pos_lo = nl - zl > 0, pos_hi = nh - zh > 0;
     top = (pos_lo && pos_hi) ? hi_id : 0;
   }
-  st->top = top;
+  if (write) st->top = top;
+  *best_out = best;
+  *top_out = top;
 }
 
 // samples <= 0 (rule 1), counted on the sorted array: whole buckets below, the straddling one
-__global__ void km_count_le0_kernel(const double *__restrict__ xs, const unsigned long long *__restrict__ off,
-                                    const double *__restrict__ geo, KmState *st) {
+__device__ __forceinline__ void km_count_le0(const double *__restrict__ xs, const unsigned long long *__restrict__ off,
+                                             const double *__restrict__ geo, KmState *st) {
   __shared__ unsigned long long acc;
   const int64_t nv = (int64_t)st->nvalid;
   if (threadIdx.x == 0) acc = 0;
@@ -1476,14 +1485,27 @@ __global__ void km_count_le0_kernel(const double *__restrict__ xs, const unsigne
   if (threadIdx.x == 0) st->nle0 = mn > 0.0 ? 0 : lo + (long long)acc;
 }
 
+// tol, then the samples <= 0: one launch
+__global__ void km_tol_le0_kernel(const double *__restrict__ xs, const unsigned long long *__restrict__ off,
+                                  const double *__restrict__ geo, KmState *st) {
+  if (threadIdx.x == 0) km_tol(st);
+  km_count_le0(xs, off, geo, st);
+}
+
+// the winner of the runs (every block works it out from the runs' records; block 0 stores it),
+// then the labels / top mask
 template <int K>
 __global__ void km_label_kernel(const double *__restrict__ x, const uint8_t *__restrict__ valid, int64_t n,
-                                const KmState *st, int32_t *__restrict__ labels, uint8_t *__restrict__ top) {
+                                KmState *st, int32_t *__restrict__ labels, uint8_t *__restrict__ top, int nrun,
+                                int rule) {
+  __shared__ int sbest, stop;
+  if (threadIdx.x == 0) km_best<K>(st, nrun, rule, blockIdx.x == 0, &sbest, &stop);
+  __syncthreads();
   double c[K];
-  const SkRun &B = st->run[st->best];
+  const SkRun &B = st->run[sbest];
 #pragma unroll
   for (int j = 0; j < K; ++j) c[j] = B.lcen[j];
-  const int jt = st->top;
+  const int jt = stop;
   const bool err = st->error != 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const bool ok = (!valid || valid[i]) && !err;
@@ -1620,11 +1642,10 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
     // after this frame is gone
     km_state_init_kernel<<<1, 256, 0, s>>>(st);
     if (n > 0) km_minmax_kernel<<<std::min<unsigned>(g, 512), 256, 0, s>>>(x, valid, n, st);
-    km_scale_kernel<<<1, 1, 0, s>>>(st);
+    km_scale_kernel<<<1, 1, 0, s>>>(st, n > 0 ? ws.geo : nullptr);
     HRF_LAUNCHED();
     if (n > 0) {
       const unsigned nch = (unsigned)nblocks(n);
-      km_bucket_init_kernel<<<1, 1, 0, s>>>(st, ws.geo);
       const int L = nch_b(n) + 1;
       km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch);
       if (hrf_status r = scan_u32(ws.cntA, (int64_t)KD * nch, ws.sbsum, s)) return r;
@@ -1646,8 +1667,7 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
         km_sel_scatter_kernel<<<nsb, 256, 0, s>>>(x, valid, n, boff, ws.xr, ws.nsel);
         HRF_LAUNCHED();
       }
-      km_tol_kernel<<<1, 1, 0, s>>>(st);
-      km_count_le0_kernel<<<1, 1024, 0, s>>>(ws.xs, ws.off, ws.geo, st);
+      km_tol_le0_kernel<<<1, 1024, 0, s>>>(ws.xs, ws.off, ws.geo, st);
       HRF_LAUNCHED();
     }
   }
@@ -1678,8 +1698,7 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
     HRF_LAUNCHED();
   }
   km_lloyd_kernel<K><<<n_init, KS_T, 0, s>>>(ws.xs, ws.bq, ws.bq2, ws.off, ws.geo, st, max_iter);
-  km_best_kernel<K><<<1, 64, 0, s>>>(st, n_init, rule);
-  km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top);
+  km_label_kernel<K><<<g, 256, 0, s>>>(x, valid, n, st, labels, top, n_init, rule);
   HRF_LAUNCHED();
   if (fin) HRF_HIP(hipMemcpyAsync(fin, st, sizeof(KmState), hipMemcpyDeviceToHost, s));
   return HRF_OK;
@@ -1775,14 +1794,14 @@ hrf_status hrf_kmeans_1d_sorted(const double *x, const uint8_t *valid, int64_t n
 }  // extern "C"
 
 // The pair without its synchronisation (the native E. coli driver): the NaN flag lands in
-// *err_pinned (pinned host memory) and the caller checks it after its next synchronisation.
+// *err_pinned (pinned host memory), or stays on the device for the caller's own read-back
+// (err_pinned == nullptr), and the caller checks it after its next synchronisation.
 hrf_status hrf::kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32_t k1, int32_t k2, int32_t max_iter,
                                                int32_t n_init, int32_t rule1, int32_t rule2, uint8_t *top1,
                                                uint8_t *top2, void *work, int64_t work_bytes, hipStream_t s,
                                                int32_t *err_pinned) {
   if (hrf_status r = check_args(k1, n, max_iter, n_init, rule1, work, x)) return r;
   if (hrf_status r = check_args(k2, n, max_iter, n_init, rule2, work, x)) return r;
-  HRF_REQUIRE(err_pinned, "kmeans_1d_pair: null error slot");
   const int64_t need = hrf_kmeans_sorted_workspace_bytes(n);
   HRF_REQUIRE(need > 0 && work_bytes >= need, "kmeans_1d_pair: workspace too small");
   size_t tb = 0;
@@ -1790,8 +1809,16 @@ hrf_status hrf::kmeans_1d_sorted_pair_deferred(const double *x, int64_t n, int32
   const SortWs ws = carve(work, n, tb);
   if (hrf_status r = km_launch_k(k1, x, nullptr, n, max_iter, n_init, rule1, nullptr, top1, ws, 0, s, nullptr)) return r;
   if (hrf_status r = km_launch_k(k2, x, nullptr, n, max_iter, n_init, rule2, nullptr, top2, ws, 1, s, nullptr)) return r;
-  HRF_HIP(hipMemcpyAsync(err_pinned, &ws.st->error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  // err_pinned == nullptr: the caller reads the flag itself (hrf::kmeans_error_flag)
+  if (err_pinned) HRF_HIP(hipMemcpyAsync(err_pinned, &ws.st->error, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   return HRF_OK;
+}
+
+// device address of the NaN flag of the last fit in this workspace (n values)
+const int32_t *hrf::kmeans_error_flag(void *work, int64_t n) {
+  size_t tb = 0;
+  if (sort_tmp_bytes(n, &tb) != HRF_OK) return nullptr;
+  return &carve(work, n, tb).st->error;
 }
 
 extern "C" {

@@ -440,6 +440,33 @@ __global__ void dilate_kernel(const uint8_t *__restrict__ m, int64_t H, int64_t 
   }
 }
 
+// dilate(erode(m)) with the cross in one pass (the eroded image is not stored): a pixel is set
+// when it or one of its in-image 4-neighbours q survives the erosion, q's erosion reading its
+// own 4-neighbours with `border` outside the image -- erode_kernel then dilate_kernel, fused
+__device__ __forceinline__ int eroded_at(const uint8_t *__restrict__ m, int64_t H, int64_t W, int border, int64_t r,
+                                         int64_t c) {
+  const int64_t i = r * W + c;
+  int v = m[i] != 0;
+  v = v && (r > 0 ? m[i - W] != 0 : border);
+  v = v && (r + 1 < H ? m[i + W] != 0 : border);
+  v = v && (c > 0 ? m[i - 1] != 0 : border);
+  v = v && (c + 1 < W ? m[i + 1] != 0 : border);
+  return v;
+}
+
+__global__ void opening_kernel(const uint8_t *__restrict__ m, int64_t H, int64_t W, int border,
+                               uint8_t *__restrict__ o) {
+  const int64_t n = H * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / W, c = i - r * W;
+    const int v = eroded_at(m, H, W, border, r, c) || (r > 0 && eroded_at(m, H, W, border, r - 1, c)) ||
+                  (r + 1 < H && eroded_at(m, H, W, border, r + 1, c)) ||
+                  (c > 0 && eroded_at(m, H, W, border, r, c - 1)) ||
+                  (c + 1 < W && eroded_at(m, H, W, border, r, c + 1));
+    o[i] = (uint8_t)v;
+  }
+}
+
 __global__ void count_u8_kernel(const uint8_t *__restrict__ m, int64_t n, unsigned long long *__restrict__ cnt) {
   unsigned long long c = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -632,13 +659,24 @@ hrf_status hrf_remove_small_objects_labels(const int32_t *labels, int64_t n, int
                                            int32_t *out, int32_t *cnt_ws, hrf_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) return HRF_OK;
-  HRF_REQUIRE(labels && out && cnt_ws && maxlab >= 0, "remove_small_objects_labels: bad arguments");
+  HRF_REQUIRE(cnt_ws && maxlab >= 0, "remove_small_objects_labels: bad arguments");
   HRF_HIP(hipMemsetAsync(cnt_ws, 0, sizeof(int32_t) * ((size_t)maxlab + 1), s));
+  return hrf::remove_small_objects_labels_zeroed(labels, n, maxlab, min_size, out, cnt_ws, s);
+}
+
+}  // extern "C"
+
+hrf_status hrf::remove_small_objects_labels_zeroed(const int32_t *labels, int64_t n, int32_t maxlab,
+                                                   int64_t min_size, int32_t *out, int32_t *cnt_ws, hipStream_t s) {
+  if (n == 0) return HRF_OK;
+  HRF_REQUIRE(labels && out && cnt_ws && maxlab >= 0, "remove_small_objects_labels: bad arguments");
   label_counts_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(n, RUN_PX * 4), 4096), 256, 0, s>>>(labels, n, maxlab, cnt_ws);
   rso_labels_finish_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(labels, cnt_ws, n, maxlab, min_size, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }
+
+extern "C" {
 
 hrf_status hrf_relabel_sequential(const int32_t *labels, int64_t n, int32_t maxlab, int32_t *out, int32_t *map_ws,
                                   int32_t *nlab_dev, hrf_stream_t stream) {
@@ -660,6 +698,20 @@ hrf_status hrf_binary_erosion(const uint8_t *mask, int64_t H, int64_t W, int32_t
   HRF_LAUNCHED();
   return HRF_OK;
 }
+
+}  // extern "C"
+
+// hrf_binary_erosion(mask, border_value) then hrf_binary_dilation, one launch
+hrf_status hrf::binary_opening(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,
+                               hipStream_t s) {
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(mask && out && mask != out, "binary_opening: bad buffers (in-place not supported)");
+  opening_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(mask, H, W, border_value != 0, out);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+extern "C" {
 
 hrf_status hrf_binary_dilation(const uint8_t *mask, int64_t H, int64_t W, uint8_t *out, hrf_stream_t stream) {
   if (H * W == 0) return HRF_OK;

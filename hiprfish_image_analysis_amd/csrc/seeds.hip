@@ -353,7 +353,8 @@ __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *
                                                                  int32_t mode, int32_t area_max,
                                                                  int32_t min_obj, int32_t *__restrict__ list,
                                                                  int32_t *__restrict__ count,
-                                                                 uint8_t *__restrict__ be_out) {
+                                                                 uint8_t *__restrict__ be_out,
+                                                                 int32_t *__restrict__ ovf) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int comp = blockIdx.x + 1;
   const int cls = seed_class(box, comp, mode);
@@ -450,8 +451,12 @@ __global__ __launch_bounds__(RS_T) void erosion_seed_runs_kernel(const int32_t *
   // over capacity (or the iteration cap): the pixel kernel redoes this component -- unless its
   // box exceeds the pixel kernel's capacity (SEED_BIG_RUNS): then count[1] tells the caller
   if (threadIdx.x == 0) {
-    if ((int64_t)bh * bw > SEED_LDS_PX_MAX) atomicAdd(count + 1, 1);
-    else list[atomicAdd(count, 1)] = comp;
+    if ((int64_t)bh * bw > SEED_LDS_PX_MAX) {
+      atomicAdd(count + 1, 1);
+      if (ovf) atomicAdd(ovf, 1);  // the caller's copy of count[1] (no device-to-device copy)
+    } else {
+      list[atomicAdd(count, 1)] = comp;
+    }
   }
 }
 
@@ -640,9 +645,11 @@ int64_t hrf::seed_px_scratch_bytes() { return (int64_t)SEED_PX_WG * (int64_t)SEE
 hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t W, int32_t ncomp, const int32_t *box,
                                       const int32_t *hb, int32_t area_max, int32_t min_obj, uint8_t *be_out,
                                       hipStream_t s, int32_t *ovf_dev, char *px_scratch) {
-  HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
-  if (ovf_dev) HRF_HIP(hipMemsetAsync(ovf_dev, 0, sizeof(int32_t), s));
-  if (ncomp == 0) return HRF_OK;
+  if (ncomp == 0) {
+    HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+    if (ovf_dev) HRF_HIP(hipMemsetAsync(ovf_dev, 0, sizeof(int32_t), s));
+    return HRF_OK;
+  }
   // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
   // Components the run kernel cannot hold (run arrays over capacity) are listed with the
   // class-1 ones and redone by the pixel kernel, so every box it receives fits SEED_LDS_PX_MAX.
@@ -672,10 +679,18 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   HRF_HIP(hipMallocAsync((void **)&dlist, list_bytes + (px_scratch ? 0 : (size_t)npx_wg * SEED_SLICE), s));
   if (!px_scratch) px_scratch = reinterpret_cast<char *>(dlist) + list_bytes;
   int32_t *dcount = dlist + ncomp + 1;  // [0] pixel-kernel list length, [1] large-box overflows
-  HRF_HIP(hipMemsetAsync(dcount, 0, 2 * sizeof(int32_t), s));
+  // the seed image, the counters and the caller's overflow slot cleared by one launch
+  ZeroPub zp;
+  HRF_REQUIRE(zp.zero(dcount, 2 * sizeof(int32_t)) && zp.zero(ovf_dev, sizeof(int32_t)),
+              "erosion_seeds: clear list");
+  if ((H * W) % 4 == 0) {
+    zp.zero(be_out, H * W);
+  } else {
+    HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
+  }
+  if (hrf_status r_ = zero_publish(zp, s)) return r_;
   erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, mode, area_max, min_obj, dlist,
-                                                                 dcount, be_out);
-  if (ovf_dev) HRF_HIP(hipMemcpyAsync(ovf_dev, dcount + 1, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+                                                                 dcount, be_out, ovf_dev);
   static const bool dbg = getenv("HRF_SEEDS_DEBUG") != nullptr;
   if (dbg) {  // diagnostics: how many components the pixel kernel receives (synchronises)
     int32_t hc[2] = {0, 0};

@@ -27,6 +27,7 @@ struct hrf_seg_ctx {
   void *ws_state = nullptr;
   int32_t *ws_flag = nullptr;
   int32_t *hpin = nullptr;  // pinned host slots for counts read back at a later synchronisation
+  int32_t *hpin_dev = nullptr, *hbox_dev = nullptr;  // their device addresses (hrf::zero_publish)
   void *km = nullptr;
   int64_t km_bytes = 0;
   char *seed_px = nullptr;  // erosion seeding's pixel-kernel scratch
@@ -58,18 +59,25 @@ hrf_status ensure_labels(hrf_seg_ctx *c, int64_t maxlab, hipStream_t s) {
   hipFree(c->props);
   if (c->hbox) hipHostFree(c->hbox);
   c->hbox = nullptr;
+  c->hbox_dev = nullptr;
   int64_t cap = 1024;
   while (cap < maxlab + 1) cap *= 2;
   if (hrf_status r = dalloc(&c->box, 4 * cap)) return r;
   if (hrf_status r = dalloc(&c->cnt, cap)) return r;
   if (hrf_status r = dalloc(&c->mom, 6 * cap)) return r;
   if (hrf_status r = dalloc(&c->props, 8 * cap)) return r;
-  if (hipHostMalloc((void **)&c->hbox, sizeof(int32_t) * 4 * cap, hipHostMallocDefault) != hipSuccess) {
+  if (::hrf::host_alloc_mapped((void **)&c->hbox, sizeof(int32_t) * 4 * cap) != hipSuccess ||
+      !(c->hbox_dev = ::hrf::mapped(c->hbox))) {
+    if (c->hbox) hipHostFree(c->hbox);
     c->hbox = nullptr;
     c->lab_cap = 0;
     ::hrf::set_error("seg_ctx: pinned host allocation failed");
     return HRF_EHIP;
   }
+  // the chain clears cnt and mom at the watershed's synchronisation (capacity-wide); buffers
+  // allocated after it are cleared here
+  HRF_HIP(hipMemsetAsync(c->cnt, 0, sizeof(int32_t) * cap, s));
+  HRF_HIP(hipMemsetAsync(c->mom, 0, sizeof(int64_t) * 6 * cap, s));
   c->lab_cap = cap;
   return HRF_OK;
 }
@@ -133,8 +141,8 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
       (r = dalloc(&c->dint, 16)) || (r = dalloc(&c->ws_flag, 8)))
     return fail(r);
   if ((r = dalloc((char **)&c->ws_state, (size_t)hrf_watershed_workspace_bytes(H, W)))) return fail(r);
-  if (hipHostMalloc((void **)&c->hpin, 16 * sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
-    c->hpin = nullptr;
+  if (::hrf::host_alloc_mapped((void **)&c->hpin, 16 * sizeof(int32_t)) != hipSuccess ||
+      !(c->hpin_dev = ::hrf::mapped(c->hpin))) {
     ::hrf::set_error("seg_ctx: pinned host allocation failed");
     return fail(HRF_EHIP);
   }
@@ -174,35 +182,45 @@ hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *c) {
   return HRF_OK;
 }
 
-// ecoli :73-127 from image_cn (f64, H x W)
+// ecoli :73-127 from image_cn (f64, H x W).  Clears and host read-backs ride on the chain's two
+// synchronisations (components + boxes, watershed batch) as ZeroPub launches; `extra` (the
+// native tile's per-label buffers) is cleared at the watershed's.
 static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_t *seg_out, int32_t *maxlab_host,
-                                        hipStream_t s) {
+                                        hipStream_t s, const ::hrf::ZeroPub *extra) {
   const int64_t H = c->H, W = c->W, n = c->n;
   uint8_t *rough = c->m[0], *interior = c->m[1], *a = c->m[2], *b = c->m[3], *d = c->m[4];
   int32_t *lab1 = c->l[0], *seeds = c->l[1], *ws = c->l[2], *lab3 = c->l[3];
   // :73-94; the NaN check (sklearn raises) is read at the component-count synchronisation below
   HRF_TRY(::hrf::kmeans_1d_sorted_pair_deferred(cn, c->n, 2, 3, 300, 10, 2, 0, rough, interior, c->km, c->km_bytes, s,
-                                                c->hpin + 3));
+                                                nullptr));
+  const int32_t *km_err = ::hrf::kmeans_error_flag(c->km, c->n);
+  HRF_REQUIRE(km_err, "segment_ecoli: kmeans workspace");
   HRF_TRY(hrf_remove_small_holes(interior, H, W, 64, 1, a, c->parent, c->size, s));   // :95
-  HRF_TRY(hrf_binary_erosion(a, H, W, 1, b, s));
-  HRF_TRY(hrf_binary_dilation(b, H, W, d, s));
+  HRF_TRY(::hrf::binary_opening(a, H, W, 1, d, s));                                 // erosion, dilation
   HRF_TRY(hrf_remove_small_objects_mask(d, H, W, 50, 1, a, c->parent, c->size, s));  // :96 cell_sm = a
   // :97-110.  Components, their count and their boxes come back in ONE synchronisation: the
   // boxes are computed for every label the current capacity holds (labels above it are
   // ignored by the box kernel) and redone in the rare case the count exceeds it.
   HRF_TRY(hrf_label(a, 0, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
-  HRF_HIP(hipMemcpyAsync(c->hpin + 1, c->dint, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HRF_TRY(ensure_labels(c, 1, s));
   int32_t guess = (int32_t)(c->lab_cap - 1);
   HRF_TRY(hrf_label_boxes(lab1, H, W, guess, c->box, s));
-  HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)guess + 1), hipMemcpyDeviceToHost, s));
+  {
+    ::hrf::ZeroPub zp;
+    zp.pub(c->dint, c->hpin_dev + 1, 1);
+    zp.pub(km_err, c->hpin_dev + 3, 1);
+    zp.pub(c->box, c->hbox_dev, 4 * (guess + 1));
+    HRF_TRY(::hrf::zero_publish(zp, s));
+  }
   HRF_HIP(hipStreamSynchronize(s));
   HRF_REQUIRE(!c->hpin[3], "kmeans_1d_pair: input contains NaN (sklearn KMeans raises ValueError)");
   const int32_t ncomp = c->hpin[1];
   if (ncomp > guess) {
     HRF_TRY(ensure_labels(c, ncomp, s));
     HRF_TRY(hrf_label_boxes(lab1, H, W, ncomp, c->box, s));
-    HRF_HIP(hipMemcpyAsync(c->hbox, c->box, sizeof(int32_t) * 4 * ((size_t)ncomp + 1), hipMemcpyDeviceToHost, s));
+    ::hrf::ZeroPub zp;
+    zp.pub(c->box, c->hbox_dev, 4 * (ncomp + 1));
+    HRF_TRY(::hrf::zero_publish(zp, s));
     HRF_HIP(hipStreamSynchronize(s));
   }
   // Large-box components go to the run kernel too; how many overflowed it lands in hpin[2]
@@ -211,18 +229,23 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   for (int attempt = 0;; ++attempt) {
     HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s,
                                          attempt == 0 ? c->dint + 8 : nullptr, c->seed_px));
-    if (attempt == 0) HRF_HIP(hipMemcpyAsync(c->hpin + 2, c->dint + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
-    HRF_TRY(label_conn2_deferred(c, d, seeds, s));                                 // :111-112
-    HRF_TRY(hrf_watershed_ex(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, c->ws_stats,
-                             c->ws_stats + 1, s));  // :113
+    HRF_TRY(hrf_label(d, 0, H, W, 2, seeds, c->parent, c->blk, c->dint, s));        // :111-112
+    // read back at the watershed's synchronisation: the seed count, the run kernel's overflow
+    // count; cleared there: the per-label counts and moments (capacity-wide) and `extra`
+    ::hrf::ZeroPub zp = extra ? *extra : ::hrf::ZeroPub();
+    HRF_REQUIRE(zp.pub(c->dint, c->hpin_dev + 0, 1) && (attempt > 0 || zp.pub(c->dint + 8, c->hpin_dev + 2, 1)) &&
+                    zp.zero(c->cnt, sizeof(int32_t) * c->lab_cap) && zp.zero(c->mom, sizeof(int64_t) * 6 * c->lab_cap),
+                "segment_ecoli: too many read-backs");
+    HRF_TRY(::hrf::watershed_ex_extra(cn, 1, seeds, rough, H, W, ws, c->ws_state, c->ws_flag, 100000, c->ws_stats,
+                                      c->ws_stats + 1, s, &zp));  // :113
     if (attempt > 0 || c->hpin[2] == 0) break;
   }
   const int32_t nseeds = c->hpin[0];  // read back by the watershed's synchronisation
   HRF_TRY(ensure_labels(c, nseeds, s));
-  HRF_TRY(hrf_remove_small_objects_labels(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114
+  HRF_TRY(::hrf::remove_small_objects_labels_zeroed(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114
   HRF_TRY(hrf_clear_border(lab1, H, W, lab3, c->parent, c->size, s));          // :115
-  HRF_TRY(hrf_region_moments(lab3, H, W, nseeds, c->mom, s));                   // :116
+  HRF_TRY(::hrf::region_moments_zeroed(lab3, H, W, nseeds, c->mom, s));         // :116
   HRF_TRY(hrf_region_props(c->mom, nseeds, c->props, s));
   HRF_TRY(hrf_shape_filter(lab3, H, W, c->props, nseeds, 15.0, 35.0, seg_out, s));   // :117-126
   *maxlab_host = nseeds;
@@ -240,14 +263,26 @@ hrf_status hrf_segment_ecoli(hrf_seg_ctx *c, const float *stack, int32_t C, int3
   HRF_REQUIRE(c && stack && seg_out && maxlab_host && C >= 1, "segment_ecoli: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   HRF_TRY(hrf_channel_sum(stack, c->n, C, nullptr, 1, 0, c->cn, s));            // :71-72
-  return segment_ecoli_from_cn(c, c->cn, seg_out, maxlab_host, s);
+  return segment_ecoli_from_cn(c, c->cn, seg_out, maxlab_host, s, nullptr);
 }
 
 hrf_status hrf_segment_ecoli_cn(hrf_seg_ctx *c, const double *image_cn, int32_t *seg_out, int32_t *maxlab_host,
                                 hrf_stream_t stream) {
   HRF_REQUIRE(c && image_cn && seg_out && maxlab_host, "segment_ecoli_cn: bad arguments");
-  return segment_ecoli_from_cn(c, image_cn, seg_out, maxlab_host, (hipStream_t)stream);
+  return segment_ecoli_from_cn(c, image_cn, seg_out, maxlab_host, (hipStream_t)stream, nullptr);
 }
+
+}  // extern "C"
+
+// the native tile's entry: hrf_segment_ecoli_cn with the tile's per-label buffers cleared at the
+// watershed's synchronisation
+hrf_status hrf::segment_ecoli_cn_extra(hrf_seg_ctx *c, const double *image_cn, int32_t *seg_out,
+                                       int32_t *maxlab_host, hipStream_t s, const ZeroPub *extra) {
+  HRF_REQUIRE(c && image_cn && seg_out && maxlab_host, "segment_ecoli_cn: bad arguments");
+  return segment_ecoli_from_cn(c, image_cn, seg_out, maxlab_host, s, extra);
+}
+
+extern "C" {
 
 hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t C, const float *cal, int64_t cal_sp,
                                     int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, int32_t *seg_out,
@@ -268,8 +303,7 @@ hrf_status hrf_segment_multispecies(hrf_seg_ctx *c, const float *stack, int32_t 
   HRF_TRY(hrf_pad_edge_f64(nl, H, W, 5, c->pad, s));                            // :109
   HRF_TRY(hrf_enhance_2d(c->pad, H + 10, W + 10, W + 10, 11, 9, fin, s));      // :110-124
   HRF_TRY(kmeans_top(c, fin, 2, 1, 0, rough, s));                               // :125-135
-  HRF_TRY(hrf_binary_erosion(rough, H, W, 1, a, s));                            // :136
-  HRF_TRY(hrf_binary_dilation(a, H, W, b, s));
+  HRF_TRY(::hrf::binary_opening(rough, H, W, 1, b, s));                          // :136 erosion, dilation
   HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 1, a, c->parent, c->size, s));  // :137
   HRF_TRY(hrf_fill_holes(a, H, W, b, c->parent, c->size, s));                  // :138
   HRF_TRY(hrf_fill_holes(rough, H, W, d, c->parent, c->size, s));              // :139

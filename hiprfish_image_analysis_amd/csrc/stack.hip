@@ -1018,6 +1018,22 @@ hrf_status hrf_label_sums_lasers(const float *const *src_host, const int32_t *ch
   hipStream_t s = (hipStream_t)stream;
   HRF_HIP(hipMemsetAsync(sums, 0, sizeof(double) * ((size_t)maxlab + 1) * C, s));
   HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * ((size_t)maxlab + 1), s));
+  return hrf::label_sums_lasers_zeroed(src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, labels, maxlab,
+                                       cal, cal_c0, cal_c1, sums, counts, s);
+}
+
+}  // extern "C"
+
+hrf_status hrf::label_sums_lasers_zeroed(const float *const *src_host, const int32_t *channels_host,
+                                         const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                         int32_t apply_mask, const int32_t *labels, int32_t maxlab, const float *cal,
+                                         int32_t cal_c0, int32_t cal_c1, double *sums, int64_t *counts,
+                                         hipStream_t s) {
+  Lasers L;
+  if (hrf_status st = lasers_of(src_host, channels_host, shifts_dev, nlaser, &L)) return st;
+  const int C = L.c0[nlaser];
+  HRF_REQUIRE(C <= 128 && maxlab >= 0 && H >= 0 && W >= 0, "label_sums_lasers: C must be <= 128");
+  HRF_REQUIRE(sums && counts, "label_sums_lasers: null output");
   if (H * W == 0) return HRF_OK;
   HRF_REQUIRE(labels, "label_sums_lasers: null labels");
   const int64_t nblk = hrf::cdiv(hrf::cdiv(H * W, 64), 4);
@@ -1038,6 +1054,8 @@ hrf_status hrf_label_sums_lasers(const float *const *src_host, const int32_t *ch
   HRF_LAUNCHED();
   return HRF_OK;
 }
+
+extern "C" {
 
 hrf_status hrf_channel_sum(const float *stack, int64_t npix, int32_t C, const uint8_t *mask, int32_t mode,
                            int32_t negate, double *out, hrf_stream_t stream) {

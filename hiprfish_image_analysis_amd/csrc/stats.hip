@@ -481,11 +481,21 @@ hrf_status hrf_region_moments(const int32_t *labels, int64_t H, int64_t W, int32
   hipStream_t s = (hipStream_t)stream;
   HRF_REQUIRE(maxlab >= 0 && mom, "region_moments: bad arguments");
   HRF_HIP(hipMemsetAsync(mom, 0, sizeof(int64_t) * 6 * ((size_t)maxlab + 1), s));
+  return hrf::region_moments_zeroed(labels, H, W, maxlab, mom, s);
+}
+
+}  // extern "C"
+
+hrf_status hrf::region_moments_zeroed(const int32_t *labels, int64_t H, int64_t W, int32_t maxlab, int64_t *mom,
+                                      hipStream_t s) {
+  HRF_REQUIRE(maxlab >= 0 && mom, "region_moments: bad arguments");
   if (H * W == 0) return HRF_OK;
   moments_kernel<<<hrf::stream_grid(H * W), 256, 0, s>>>(labels, H, W, maxlab, (unsigned long long *)mom);
   HRF_LAUNCHED();
   return HRF_OK;
 }
+
+extern "C" {
 
 hrf_status hrf_region_props(const int64_t *mom, int32_t maxlab, double *props, hrf_stream_t stream) {
   HRF_REQUIRE(maxlab >= 0 && mom && props, "region_props: bad arguments");
@@ -531,9 +541,9 @@ namespace hrf {
 // hrf_barcode_counts / hrf_paint_ids with the cell count held on the device (hrf_tile_ecoli):
 // n_dev <= nmax rows; paint writes code[l - 1] + add
 hrf_status barcode_counts_devn(const int32_t *bc, int64_t nmax, const int32_t *n_dev, int32_t R, int64_t *counts,
-                               hipStream_t s) {
+                               hipStream_t s, bool zeroed) {
   HRF_REQUIRE(R >= 1 && counts, "barcode_counts: bad arguments");
-  HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * R, s));
+  if (!zeroed) HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * R, s));
   if (nmax == 0) return HRF_OK;
   barcode_counts_kernel<<<hrf::stream_grid(nmax), 256, 0, s>>>(bc, nmax, R, (unsigned long long *)counts, n_dev);
   HRF_LAUNCHED();

@@ -82,6 +82,9 @@ hrf_status ensure_cap(hrf_tile_ctx *t, int64_t maxlab, hipStream_t s) {
   HRF_TRY(dalloc(&t->counts, (size_t)cap));
   HRF_TRY(dalloc(&t->rol, (size_t)cap));
   HRF_TRY(dalloc(&t->fx, (size_t)cap * NL));
+  // later tiles clear sums and counts at the chain's watershed synchronisation
+  HRF_HIP(hipMemsetAsync(t->sums, 0, sizeof(double) * (size_t)cap * C, s));
+  HRF_HIP(hipMemsetAsync(t->counts, 0, sizeof(int64_t) * (size_t)cap, s));
   t->cap = cap;
   return HRF_OK;
 }
@@ -90,7 +93,7 @@ hrf_status ensure_cap(hrf_tile_ctx *t, int64_t maxlab, hipStream_t s) {
 hrf_status tile_cells(hrf_tile_ctx *t, const int32_t *seg, const double *lib, const double *lib_flags, int32_t R,
                       int32_t variant, double flag_thr, int32_t cell_cap, int32_t *labels, double *avgint,
                       double *avgint_norm, int32_t *cell_idx, double *cell_dist, int32_t *ident, int64_t *counts,
-                      int32_t *ncells_dev, hipStream_t s) {
+                      int32_t *ncells_dev, hipStream_t s, bool counts_zeroed) {
   const int32_t maxlab = t->maxlab;
   HRF_REQUIRE(cell_cap >= maxlab, "tile_ecoli: cell buffers hold %d rows, the tile needs %d", cell_cap, maxlab);
   HRF_REQUIRE(variant == 0 || lib_flags, "tile_ecoli: the gated variants need the library's presence flags");
@@ -108,7 +111,7 @@ hrf_status tile_cells(hrf_tile_ctx *t, const int32_t *seg, const double *lib, co
   HRF_TRY(hrf::cells_lib_prep(lib, R, C, BOUNDS, NL, t->refT, ny, s));
   HRF_TRY(hrf::classify_cells_devn(avgint_norm, maxlab, ncells_dev, t->refT, ny, R, C, BOUNDS, NL, variant,
                                    variant ? t->fx : nullptr, variant ? lib_flags : nullptr, cell_idx, cell_dist, s));
-  HRF_TRY(hrf::barcode_counts_devn(cell_idx, maxlab, ncells_dev, R, counts, s));              // collect :92-98
+  HRF_TRY(hrf::barcode_counts_devn(cell_idx, maxlab, ncells_dev, R, counts, s, counts_zeroed));  // collect :92-98
   HRF_TRY(hrf::paint_ids_devn(seg, t->H * t->W, cell_idx, maxlab, ncells_dev, 1, ident, s));   // :65-71
   return HRF_OK;
 }
@@ -221,7 +224,13 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
     return HRF_OK;
   };
   int32_t maxlab = 0;
-  hrf_status st = hrf_segment_ecoli_cn(t->seg, t->cn, seg, &maxlab, stream);            // :73-127
+  // the per-label sums and counts (their current capacity) and the barcode counts are cleared
+  // inside the chain's watershed read-back launch (no fill kernels of their own)
+  ::hrf::ZeroPub zp;
+  zp.zero(t->sums, sizeof(double) * (size_t)t->cap * C);
+  zp.zero(t->counts, sizeof(int64_t) * (size_t)t->cap);
+  zp.zero(counts, sizeof(int64_t) * (size_t)R);
+  hrf_status st = ::hrf::segment_ecoli_cn_extra(t->seg, t->cn, seg, &maxlab, s, &zp);   // :73-127
   if (st) {
     join();
     return st;
@@ -229,14 +238,14 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
   t->maxlab = maxlab;
   *maxlab_host = maxlab;
   if ((st = ensure_cap(t, maxlab, s)) ||
-      (st = hrf_label_sums_lasers(lasers_host, CH, t->shifts, NL, H, W, 1, seg, maxlab, cal, 0, 32, t->sums,
-                                  t->counts, s))) {                                     // :147-155
+      (st = ::hrf::label_sums_lasers_zeroed(lasers_host, CH, t->shifts, NL, H, W, 1, seg, maxlab, cal, 0, 32,
+                                            t->sums, t->counts, s))) {                   // :147-155
     join();
     return st;
   }
   if (maxlab <= cell_cap)
     st = tile_cells(t, seg, lib, lib_flags, R, variant, flag_thr, cell_cap, labels, avgint, avgint_norm, cell_idx,
-                    cell_dist, ident, counts, ncells_dev, s);
+                    cell_dist, ident, counts, ncells_dev, s, true);
   if (hrf_status j = join()) return st ? st : j;
   return st;
 }
@@ -247,7 +256,7 @@ hrf_status hrf_tile_ecoli_cells(hrf_tile_ctx *t, const int32_t *seg, const doubl
                                 int32_t *ident, int64_t *counts, int32_t *ncells_dev, hrf_stream_t stream) {
   HRF_REQUIRE(t && seg && lib && R >= 1 && ident && counts && ncells_dev, "tile_ecoli_cells: bad arguments");
   return tile_cells(t, seg, lib, lib_flags, R, variant, flag_thr, cell_cap, labels, avgint, avgint_norm, cell_idx,
-                    cell_dist, ident, counts, ncells_dev, (hipStream_t)stream);
+                    cell_dist, ident, counts, ncells_dev, (hipStream_t)stream, false);
 }
 
 }  // extern "C"

@@ -60,8 +60,14 @@ __global__ __launch_bounds__(256) void ws_init_kernel(const double *__restrict__
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
                                                       WsState a, WsState b, int32_t *__restrict__ ptr,
                                                       int32_t *__restrict__ tile_work,
-                                                      int32_t *__restrict__ tile_marker) {
+                                                      int32_t *__restrict__ tile_marker,
+                                                      int32_t *__restrict__ tile_flags, int32_t *__restrict__ flags) {
+  // the first pass batch's zeroed state, instead of fills: this tile's change flags of
+  // generations 0 and 1, and (block 0) the 8 host-read flags
   const int tid = threadIdx.x;
+  const int64_t ntl = (int64_t)gridDim.x * gridDim.y, tl = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+  if (tid < 2) tile_flags[tid * ntl + tl] = 0;
+  if (tl == 0 && tid < 8) flags[tid] = 0;
   int work = 0, mark = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -421,7 +427,18 @@ int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W) {
 hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask, int64_t H,
                             int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws, int32_t max_passes,
                             int32_t *passes_host, int32_t *ties_host, hrf_stream_t stream) {
-  hipStream_t s = (hipStream_t)stream;
+  return hrf::watershed_ex_extra(image, negate, markers, mask, H, W, out_labels, state_ws, flag_ws, max_passes,
+                                 passes_host, ties_host, (hipStream_t)stream, nullptr);
+}
+
+}  // extern "C"
+
+// hrf_watershed_ex whose batch read-backs also run the caller's clears and read-backs (extra:
+// the native chains fold theirs into the watershed's synchronisation, common.hpp ZeroPub)
+hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
+                                   int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
+                                   int32_t max_passes, int32_t *passes_host, int32_t *ties_host, hipStream_t s,
+                                   const ZeroPub *extra) {
   const int64_t n = H * W;
   HRF_REQUIRE(H >= 0 && W >= 0 && H <= 65535 * (int64_t)WT && W <= 65535 * (int64_t)WT && n < ((int64_t)1 << 31),
               "watershed: bad shape");
@@ -429,6 +446,11 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   if (passes_host) *passes_host = 0;
   if (n == 0) return HRF_OK;
   HRF_REQUIRE(image && markers && out_labels && state_ws && flag_ws, "watershed: null buffer");
+  // the batch flags' pinned host slots (one set per host thread, kept for the process)
+  static thread_local int32_t *pin = nullptr;
+  if (!pin) HRF_HIP(host_alloc_mapped((void **)&pin, 64));
+  int32_t *pin_dev = mapped(pin);
+  HRF_REQUIRE(pin_dev, "watershed: pinned flags have no device address");
   dim3 grid((unsigned)hrf::cdiv(W, WT), (unsigned)hrf::cdiv(H, WT));
   const int64_t ntiles = (int64_t)grid.x * grid.y;
   WsBuffers B = carve(state_ws, n, ntiles);
@@ -437,11 +459,11 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   HRF_REQUIRE(out_labels != markers, "watershed: out_labels must not alias markers");
   B.a.lab = out_labels;
   WsState a = B.a, b = B.b;
-  ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw, B.tm);
-  HRF_LAUNCHED();
   int32_t *tf = B.tf;  // per-tile change flags, three rotating generations
+  ws_init_kernel<<<grid, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, B.tw, B.tm, tf, flag_ws);
+  HRF_LAUNCHED();
   int32_t hflag[4] = {0, 0, 0, 0};  // host copies of flag_ws[0..3]
-  HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 8, s));
+  bool zeroed = true;  // ws_init_kernel zeroed tf's generations 0/1 and flag_ws[0..7]
   int passes = 0;
   static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
   // persistent pass grids (HRF_WS_TILEGRID=1: one workgroup per tile, as before)
@@ -454,10 +476,11 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   // first batch of 8 covers the typical tile (~7 passes) with a single synchronisation, later
   // batches 4.  Passes after convergence skip every tile (no tile changed).
   auto run = [&](bool relabel, int32_t *count_out) -> hrf_status {
-    HRF_HIP(hipMemsetAsync(tf, 0, sizeof(int32_t) * 2 * ntiles, s));  // generations of passes 0 and 1
+    if (!zeroed) HRF_HIP(hipMemsetAsync(tf, 0, sizeof(int32_t) * 2 * ntiles, s));  // generations 0 and 1
     int local = 0;
     for (int batch = 8;; batch = 4) {
-      HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 3, s));
+      if (!zeroed) HRF_HIP(hipMemsetAsync(flag_ws, 0, sizeof(int32_t) * 3, s));
+      zeroed = false;
       for (int k = 0; k < batch; ++k) {
         int32_t *cur = tf + (local % 3) * ntiles;
         const int32_t *prev = local == 0 ? B.tm : tf + ((local + 2) % 3) * ntiles;
@@ -485,8 +508,13 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
       WsGeom g{image, negate, markers, mask, H, W, a.lam, a.hop};
       ws_contest_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(g, a.lab, B.ptr, B.list, flag_ws + 2);
       HRF_LAUNCHED();
-      HRF_HIP(hipMemcpyAsync(hflag, flag_ws, sizeof(int32_t) * 3, hipMemcpyDeviceToHost, s));
-      HRF_HIP(hipStreamSynchronize(s));
+      {  // the batch's flags (and the caller's extras) in one launch, read after the synchronisation
+        ZeroPub zp = extra ? *extra : ZeroPub();
+        HRF_REQUIRE(zp.pub(flag_ws, pin_dev, 3), "watershed: too many read-backs");
+        if (hrf_status r = zero_publish(zp, s)) return r;
+        HRF_HIP(hipStreamSynchronize(s));
+        for (int k = 0; k < 3; ++k) hflag[k] = pin[k];
+      }
       if (dbg)
         fprintf(stderr, "hrf_watershed: %s batch, passes %d, changed %d %d, contests %d\n",
                 relabel ? "relabel" : "relax", passes, hflag[0], hflag[1], hflag[2]);
@@ -568,6 +596,8 @@ hrf_status hrf_watershed_ex(const double *image, int32_t negate, const int32_t *
   if (passes_host) *passes_host = passes;
   return HRF_OK;
 }
+
+extern "C" {
 
 hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask, int64_t H,
                          int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws, int32_t max_passes,
