@@ -12,6 +12,7 @@
 // coalesced global traffic.  All arithmetic is f64 in the reference's order (numpy's
 // 8-accumulator pairwise mean, numpy percentile lerp), compiled with -ffp-contract=off, so
 // results are bit-identical to the reference chain.
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -102,21 +103,94 @@ __global__ __launch_bounds__(256) void enhance2d_kernel(const double *__restrict
 constexpr int E3_TX = 4, E3_TY = 4, E3_TZ = 32;
 constexpr int E3_LX = E3_TX + 10, E3_LY = E3_TY + 10, E3_LZ = E3_TZ + 10;
 
-template <int MODE>
-__global__ __launch_bounds__(256) void enhance3d_kernel(const double *__restrict__ pad, int64_t xp, int64_t yp,
+// One output voxel (b: its centre in the LDS tile).  FAST: the tile holds no NaN, no infinity and
+// no negative zero, so every `a < b ? a : b` of the reference's min/max and of the selection
+// network picks the same value as v_min_f64 / v_max_f64 -- one instruction instead of a compare,
+// two 64-bit selects and their hazard nops (values equal => same bits, no signed zeros).
+#ifndef E3_GROUP_N
+#define E3_GROUP_N 4
+#endif
+constexpr int E3_GROUP = E3_GROUP_N;
+
+template <int MODE, bool FAST>
+__device__ __forceinline__ void enhance3d_voxel(const double *__restrict__ b, int64_t vox,
+                                                double *__restrict__ out) {
+  double v[72];
+#pragma unroll
+  for (int t = 0; t < 72; ++t) {
+    double mn = 0.0, mx = 0.0, c = 0.0;
+#pragma unroll
+    for (int l = 0; l < 11; ++l) {
+      const double q = b[(LP3D_11_9_9[t][l][0] * E3_LY + LP3D_11_9_9[t][l][1]) * E3_LZ + LP3D_11_9_9[t][l][2]];
+      if (l == 0) {
+        mn = q;
+        mx = q;
+      } else if (FAST) {
+        mn = __builtin_fmin(q, mn);
+        mx = __builtin_fmax(q, mx);
+      } else {
+        mn = q < mn ? q : mn;
+        mx = q > mx ? q : mx;
+      }
+      if (l == 5) c = q;
+    }
+    double r = mx - mn;
+    if (1e-8 > r) r = 1e-8;  // builtin max(range, 1e-8) (neighbor.pyx:259)
+    v[t] = (c - mn) / r;
+    // at most E3_GROUP directions' taps in flight: the 72 results stay within the register
+    // budget of two waves per SIMD instead of the scheduler hoisting hundreds of LDS reads
+    if (t % E3_GROUP == E3_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+  }
+  if (MODE == 1) {
+#pragma unroll
+    for (int t = 0; t < 72; ++t) out[vox * 72 + t] = v[t];
+    return;
+  }
+  // numpy pairwise mean over 72 (8 accumulators seeded with the first 8)
+  double acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = v[q];
+#pragma unroll
+  for (int i = 8; i < 72; i += 8)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += v[i + q];
+  const double avg = (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))) / 72.0;
+#pragma unroll
+  for (int q = 0; q < SEL72_N; ++q) {
+    const double a = v[SEL72[q][0]], bb = v[SEL72[q][1]];
+    if (FAST) {
+      v[SEL72[q][0]] = __builtin_fmin(a, bb);
+      v[SEL72[q][1]] = __builtin_fmax(a, bb);
+    } else {
+      v[SEL72[q][0]] = a < bb ? a : bb;
+      v[SEL72[q][1]] = a < bb ? bb : a;
+    }
+  }
+  // np.percentile(.., 25/75) over 72: positions 17.75 (t >= .5 form) and 53.25
+  const double lq = v[18] - (v[18] - v[17]) * 0.25;
+  const double uq = v[53] + (v[54] - v[53]) * 0.25;
+  const double qcv = nan_to_num((uq - lq) / (uq + lq));
+  out[vox] = avg * (1.0 - qcv);
+}
+
+template <int MODE, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void enhance3d_kernel(const double *__restrict__ pad, int64_t xp, int64_t yp,
                                                         int64_t zp, double *__restrict__ out, int64_t X, int64_t Y,
                                                         int64_t Z) {
   __shared__ double tile[E3_LX * E3_LY * E3_LZ];
   const int tid = threadIdx.x;
   const int64_t x0 = (int64_t)blockIdx.z * E3_TX, y0 = (int64_t)blockIdx.y * E3_TY, z0 = (int64_t)blockIdx.x * E3_TZ;
+  int special = 0;  // a NaN, an infinity or a negative zero in the tile: the reference's compare-select path
   for (int idx = tid; idx < E3_LX * E3_LY * E3_LZ; idx += 256) {
     const int lx = idx / (E3_LY * E3_LZ);
     const int rem = idx - lx * (E3_LY * E3_LZ);
     const int ly = rem / E3_LZ, lz = rem - ly * E3_LZ;
     const int64_t gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
-    tile[idx] = (gx < xp && gy < yp && gz < zp) ? pad[(gx * yp + gy) * zp + gz] : 0.0;
+    const double v = (gx < xp && gy < yp && gz < zp) ? pad[(gx * yp + gy) * zp + gz] : 0.0;
+    special |= !__builtin_isfinite(v) || (v == 0.0 && __builtin_signbit(v));
+    tile[idx] = v;
   }
-  __syncthreads();
+  const bool fast = !__syncthreads_or(special);
   const int tz = tid & 31, ty = (tid >> 5) & 3, th = tid >> 7;
 #pragma unroll 1
   for (int k = 0; k < 2; ++k) {
@@ -124,52 +198,9 @@ __global__ __launch_bounds__(256) void enhance3d_kernel(const double *__restrict
     const int64_t x = x0 + tx, y = y0 + ty, z = z0 + tz;
     if (x >= X || y >= Y || z >= Z) continue;
     const double *b = tile + (tx * E3_LY + ty) * E3_LZ + tz;
-    double v[72];
-#pragma unroll
-    for (int t = 0; t < 72; ++t) {
-      double mn = 0.0, mx = 0.0, c = 0.0;
-#pragma unroll
-      for (int l = 0; l < 11; ++l) {
-        const double q = b[(LP3D_11_9_9[t][l][0] * E3_LY + LP3D_11_9_9[t][l][1]) * E3_LZ + LP3D_11_9_9[t][l][2]];
-        if (l == 0) {
-          mn = q;
-          mx = q;
-        } else {
-          mn = q < mn ? q : mn;
-          mx = q > mx ? q : mx;
-        }
-        if (l == 5) c = q;
-      }
-      double r = mx - mn;
-      if (1e-8 > r) r = 1e-8;  // builtin max(range, 1e-8) (neighbor.pyx:259)
-      v[t] = (c - mn) / r;
-    }
     const int64_t vox = (x * Y + y) * Z + z;
-    if (MODE == 1) {
-#pragma unroll
-      for (int t = 0; t < 72; ++t) out[vox * 72 + t] = v[t];
-      continue;
-    }
-    // numpy pairwise mean over 72 (8 accumulators seeded with the first 8)
-    double acc[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] = v[q];
-#pragma unroll
-    for (int i = 8; i < 72; i += 8)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += v[i + q];
-    const double avg = (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))) / 72.0;
-#pragma unroll
-    for (int q = 0; q < SEL72_N; ++q) {
-      const double a = v[SEL72[q][0]], bb = v[SEL72[q][1]];
-      v[SEL72[q][0]] = a < bb ? a : bb;
-      v[SEL72[q][1]] = a < bb ? bb : a;
-    }
-    // np.percentile(.., 25/75) over 72: positions 17.75 (t >= .5 form) and 53.25
-    const double lq = v[18] - (v[18] - v[17]) * 0.25;
-    const double uq = v[53] + (v[54] - v[53]) * 0.25;
-    const double qcv = nan_to_num((uq - lq) / (uq + lq));
-    out[vox] = avg * (1.0 - qcv);
+    if (fast) enhance3d_voxel<MODE, true>(b, vox, out);
+    else enhance3d_voxel<MODE, false>(b, vox, out);
   }
 }
 
@@ -391,7 +422,12 @@ hrf_status hrf_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t zp,
   HRF_REQUIRE(pad && final_, "enhance_3d: null buffer");
   dim3 grid((unsigned)hrf::cdiv(Z, E3_TZ), (unsigned)hrf::cdiv(Y, E3_TY), (unsigned)hrf::cdiv(X, E3_TX));
   HRF_REQUIRE(grid.y <= 65535 && grid.z <= 65535, "enhance_3d: volume too large");
-  enhance3d_kernel<0><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
+  // HRF_E3_WPE=2: built for two waves per SIMD (spills) instead of one (A/B)
+  static const int wpe = getenv("HRF_E3_WPE") ? atoi(getenv("HRF_E3_WPE")) : 1;
+  if (wpe == 2)
+    enhance3d_kernel<0, 2><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
+  else
+    enhance3d_kernel<0><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -775,12 +775,25 @@ __global__ void km_pp_first_kernel(const double *__restrict__ xr, KmState *st, D
 // The candidate's cell is an interval of values (1-D): the range is bounded by whole buckets
 // around the midpoints to the neighbouring centres, widened by a margin far above the rounding
 // of the squares.  Work per round: one raster pass, one sweep of the cells.
-__global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict__ xr, const KmState *st, Draws d,
+// c == 1: the runs' first centres (km_pp_first_kernel's work) are taken here -- every block
+// reads them from the draws, block 0 stores them for the later kernels
+__global__ __launch_bounds__(PT) void km_pp_pass_kernel(const double *__restrict__ xr, KmState *st, Draws d,
                                                         U128 *__restrict__ part, int nblk, int c) {
   __shared__ U128 sh[PT / 64];
   __shared__ double cen[NRUN][KMAX];
-  if (threadIdx.x < NRUN * KMAX) cen[threadIdx.x / KMAX][threadIdx.x % KMAX] = st->run[threadIdx.x / KMAX].cen[threadIdx.x % KMAX];
+  if (threadIdx.x < NRUN * KMAX && !(c == 1 && threadIdx.x % KMAX == 0))
+    cen[threadIdx.x / KMAX][threadIdx.x % KMAX] = st->run[threadIdx.x / KMAX].cen[threadIdx.x % KMAX];
   const int64_t nv = (int64_t)st->nvalid;
+  if (c == 1 && (int)threadIdx.x < d.nrun) {
+    const int r = threadIdx.x;
+    const long long idx = d.first[r] < nv ? d.first[r] : nv - 1;
+    const double c0 = nv > 0 ? xr[idx] : 0.0;
+    cen[r][0] = c0;
+    if (blockIdx.x == 0) {
+      st->run[r].cen[0] = c0;
+      st->run[r].ncen = 1;
+    }
+  }
   const double scaleS = ldexp(1.0, st->S);
   const int64_t base = (int64_t)blockIdx.x * PB + threadIdx.x;
   double v[PB / PT];
@@ -1688,7 +1701,7 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   const Draws d = make_draws(std::max<int64_t>(nv, 1), K, n_init, 0u);
   const double *xr = valid ? ws.xr : x;
   const int nblk = (int)nblocks(nv);
-  km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d);
+  if (K == 1) km_pp_first_kernel<<<1, 64, 0, s>>>(xr, st, d);  // K > 1: the first pass takes them
   HRF_LAUNCHED();
   for (int c = 1; c < K; ++c) {
     km_pp_pass_kernel<<<nblk, PT, 0, s>>>(xr, st, d, ws.part, nblk, c);

@@ -1,6 +1,6 @@
 """Time individual libhrf kernels on resident 2048x2048 inputs (HIP events, mean of 5).
 
-python tools/time_kernels.py [nlmeans] [classify] [stream] [path] [pathcal]
+python tools/time_kernels.py [nlmeans] [enhance3d] [classify] [stream] [path] [pathcal]
 """
 import sys
 
@@ -33,6 +33,14 @@ def main():
         ms = timed(lambda: K.nl_means_2d(s, h=0.02))
         print("nl_means_2d 2048^2: %.3f ms  (%.1f Mpix/s, %.2f G pixel-shifts/s)" % (ms, H * W / ms / 1e3,
                                                                                   H * W * 528 / ms / 1e6))
+    if "enhance3d" in what:
+        # the cfg4 volume: 1024 x 1024 x 64, edge-padded by 5 (biofilm :810-817)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(4)
+        vol = torch.rand((1024, 1024, 64), dtype=torch.float64, device="cuda", generator=g)
+        pad = K.pad_edge_3d(vol, 5)
+        ms = timed(lambda: K.enhance_3d(pad), 3)
+        print("enhance_3d 1024x1024x64: %.3f ms  (%.1f Mvoxel/s)" % (ms, 1024 * 1024 * 64 / ms / 1e3))
     if "classify" in what:
         g = torch.Generator(device="cuda")
         g.manual_seed(0)
