@@ -296,6 +296,10 @@ __global__ __launch_bounds__(256) void cc_number_onepass_kernel(const int32_t *_
   if (tid == 0) sblk = (int32_t)atomicAdd(ticket, 1u);
   __syncthreads();
   const int32_t b = sblk;
+  if (b >= nb) {  // a ticket counter not reset (corrupted workspace): fail the call, write nothing
+    if (tid == 0) *total = INT32_MIN / 2;
+    return;
+  }
   int flags[4], pc[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -649,7 +653,7 @@ hrf_status hrf_label(const void *img, int32_t dtype, int64_t H, int64_t W, int32
 int64_t hrf::label_onepass_ws_bytes(int64_t n) { return 8 * (hrf::cdiv(n, NB) + 2) + 64; }
 
 // hrf_label with the numbering in one pass (cc_number_onepass_kernel).  ws: label_onepass_ws_bytes(n)
-// bytes, zeroed once when allocated; *epoch: the caller's call counter (advanced here)
+// bytes; *epoch: the caller's call counter, 0 before the first call (advanced here)
 hrf_status hrf::label_onepass(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
                               int32_t *parent_ws, void *ws, uint32_t *epoch, int32_t *nlab_dev, hipStream_t s) {
   if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, s)) return st;
@@ -658,8 +662,11 @@ hrf_status hrf::label_onepass(const uint8_t *mask, int64_t H, int64_t W, int32_t
   const int64_t nb = hrf::cdiv(n, NB);
   unsigned *ticket = (unsigned *)ws;
   unsigned long long *status = (unsigned long long *)((char *)ws + 64);
+  // the workspace is cleared on the first call's own stream (a hipMemset at allocation is not
+  // ordered before work on a non-blocking stream); epoch 0 = not cleared yet
+  if (*epoch == 0) HRF_HIP(hipMemsetAsync(ws, 0, (size_t)label_onepass_ws_bytes(n), s));
   *epoch = (*epoch + 1) & 0x3fffffffu;
-  if (*epoch == 0) *epoch = 1;  // 0 is the zeroed buffer's epoch
+  if (*epoch == 0) *epoch = 1;  // 0 is the cleared buffer's epoch
   cc_number_onepass_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, (int32_t)nb, status, ticket, *epoch, labels,
                                                          nlab_dev);
   cc_fill_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent_ws, n, labels);
