@@ -151,10 +151,6 @@ struct ZeroPub {
   }
 };
 hrf_status zero_publish(const ZeroPub &z, hipStream_t s);
-// hrf_label(mask, u8, conn) with the component numbering in one launch (label.hip)
-int64_t label_onepass_ws_bytes(int64_t n);
-hrf_status label_onepass(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels, int32_t *parent_ws,
-                         void *ws, uint32_t *epoch, int32_t *nlab_dev, hipStream_t s);
 // hrf_binary_erosion(border_value) followed by hrf_binary_dilation, fused (label.hip)
 hrf_status binary_opening(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,
                           hipStream_t s);

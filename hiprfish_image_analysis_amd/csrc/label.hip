@@ -279,86 +279,6 @@ __global__ __launch_bounds__(256) void cc_rank_roots_kernel(const int32_t *__res
   }
 }
 
-// cc_count_roots + scan_blocks + cc_rank_roots in one pass (decoupled look-back): a block takes
-// a ticket (the order blocks started in, so it only ever waits on blocks already running),
-// publishes its root count, adds its predecessors' published counts -- stopping at the first
-// inclusive prefix -- and publishes its own inclusive prefix.  Status words carry the call's
-// epoch (no clearing between calls): [epoch:30][flag:2][value:32], flag 1 = block count,
-// 2 = inclusive prefix.  The last ticket writes the total and resets the ticket counter.
-__global__ __launch_bounds__(256) void cc_number_onepass_kernel(const int32_t *__restrict__ parent, int64_t n,
-                                                                int32_t nb, unsigned long long *__restrict__ status,
-                                                                unsigned *__restrict__ ticket, uint32_t epoch,
-                                                                int32_t *__restrict__ labels,
-                                                                int32_t *__restrict__ total) {
-  __shared__ int32_t wc[16];
-  __shared__ int32_t sblk, sprefix;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) sblk = (int32_t)atomicAdd(ticket, 1u);
-  __syncthreads();
-  const int32_t b = sblk;
-  if (b >= nb) {  // a ticket counter not reset (corrupted workspace): fail the call, write nothing
-    if (tid == 0) *total = INT32_MIN / 2;
-    return;
-  }
-  int flags[4], pc[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t p = (int64_t)b * NB + k * 256 + tid;
-    flags[k] = (p < n && parent[p] == p);
-    const unsigned long long m = __ballot(flags[k]);
-    pc[k] = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wc[k * 4 + w] = __popcll(m);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int32_t agg = 0;
-    for (int q = 0; q < 16; ++q) agg += wc[q];
-    const unsigned long long tag = (unsigned long long)(epoch & 0x3fffffffu) << 34;
-    int32_t prefix = 0;
-    if (b == 0) {
-      __hip_atomic_store(status, tag | (2ull << 32) | (uint32_t)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(status + b, tag | (1ull << 32) | (uint32_t)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned spins = 0;
-      for (int32_t j = b - 1; j >= 0;) {
-        const unsigned long long v = __hip_atomic_load(status + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned fl = (unsigned)(v >> 32) & 3u;
-        if ((v >> 34) != (epoch & 0x3fffffffu) || fl == 0) {
-          // predecessor has not published yet (it is running: its ticket is smaller).  A bounded
-          // wait: a corrupted status fails the call (negative total) instead of hanging the GPU
-          if (++spins > (1u << 26)) {
-            prefix = INT32_MIN / 2;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += (int32_t)(uint32_t)v;
-        if (fl == 2) break;
-        --j;
-      }
-      __hip_atomic_store(status + b, tag | (2ull << 32) | (uint32_t)(prefix + agg), __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (b == nb - 1) {
-      *total = prefix + agg;
-      *ticket = 0u;  // every block has its ticket: the counter is free for the next call
-    }
-    sprefix = prefix;
-  }
-  __syncthreads();
-  const int32_t base = sprefix;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t p = (int64_t)b * NB + k * 256 + tid;
-    if (p >= n) continue;
-    int before = 0;
-    for (int q = 0; q < k * 4 + w; ++q) before += wc[q];
-    if (flags[k]) labels[p] = base + before + pc[k] + 1;
-    else if (parent[p] < 0) labels[p] = 0;
-  }
-}
-
 __global__ void cc_fill_kernel(const int32_t *__restrict__ parent, int64_t n, int32_t *__restrict__ labels) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
     const int32_t q = parent[p];
@@ -649,30 +569,6 @@ hrf_status hrf_label(const void *img, int32_t dtype, int64_t H, int64_t W, int32
 }
 
 }  // extern "C"
-
-int64_t hrf::label_onepass_ws_bytes(int64_t n) { return 8 * (hrf::cdiv(n, NB) + 2) + 64; }
-
-// hrf_label with the numbering in one pass (cc_number_onepass_kernel).  ws: label_onepass_ws_bytes(n)
-// bytes; *epoch: the caller's call counter, 0 before the first call (advanced here)
-hrf_status hrf::label_onepass(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
-                              int32_t *parent_ws, void *ws, uint32_t *epoch, int32_t *nlab_dev, hipStream_t s) {
-  if (hrf_status st = hrf_cc_roots(mask, 0, H, W, conn, parent_ws, s)) return st;
-  const int64_t n = H * W;
-  HRF_REQUIRE(n > 0 && n < (int64_t)INT32_MAX && labels && ws && epoch && nlab_dev, "label: bad arguments");
-  const int64_t nb = hrf::cdiv(n, NB);
-  unsigned *ticket = (unsigned *)ws;
-  unsigned long long *status = (unsigned long long *)((char *)ws + 64);
-  // the workspace is cleared on the first call's own stream (a hipMemset at allocation is not
-  // ordered before work on a non-blocking stream); epoch 0 = not cleared yet
-  if (*epoch == 0) HRF_HIP(hipMemsetAsync(ws, 0, (size_t)label_onepass_ws_bytes(n), s));
-  *epoch = (*epoch + 1) & 0x3fffffffu;
-  if (*epoch == 0) *epoch = 1;  // 0 is the cleared buffer's epoch
-  cc_number_onepass_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, (int32_t)nb, status, ticket, *epoch, labels,
-                                                         nlab_dev);
-  cc_fill_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent_ws, n, labels);
-  HRF_LAUNCHED();
-  return HRF_OK;
-}
 
 extern "C" {
 

@@ -32,8 +32,6 @@ struct hrf_seg_ctx {
   void *km = nullptr;
   int64_t km_bytes = 0;
   char *seed_px = nullptr;  // erosion seeding's pixel-kernel scratch
-  void *lab_ws = nullptr;   // one-pass component numbering: ticket + epoch-tagged block status
-  uint32_t lab_epoch = 0;  // 0: lab_ws not cleared yet (cleared on the first call's stream)
   // the last chain's watershed: passes, contested pixels, resolution rounds, decisions between
   // equal-valued markers of different labels (hrf_watershed_ex ties_host) -- hrf_seg_ctx_stats
   int32_t ws_stats[4] = {0, 0, 0, 0};
@@ -153,8 +151,6 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
   if (c->km_bytes <= 0) return fail(HRF_EHIP);
   if ((r = dalloc((char **)&c->km, (size_t)c->km_bytes))) return fail(r);
   if ((r = dalloc(&c->seed_px, (size_t)::hrf::seed_px_scratch_bytes()))) return fail(r);
-  const int64_t lb = ::hrf::label_onepass_ws_bytes(c->n);
-  if ((r = dalloc((char **)&c->lab_ws, (size_t)lb))) return fail(r);
 
   *out = c;
   return HRF_OK;
@@ -180,7 +176,6 @@ hrf_status hrf_seg_ctx_destroy(hrf_seg_ctx *c) {
   if (c->hbox) hipHostFree(c->hbox);
   hipFree(c->km);
   hipFree(c->seed_px);
-  hipFree(c->lab_ws);
   hipFree(c->box);
   hipFree(c->cnt);
   hipFree(c->mom);
@@ -208,9 +203,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   // :97-110.  Components, their count and their boxes come back in ONE synchronisation: the
   // boxes are computed for every label the current capacity holds (labels above it are
   // ignored by the box kernel) and redone in the rare case the count exceeds it.
-  static const bool onepass = !getenv("HRF_LABEL_ONEPASS") || atoi(getenv("HRF_LABEL_ONEPASS")) != 0;
-  if (onepass) HRF_TRY(::hrf::label_onepass(a, H, W, 2, lab1, c->parent, c->lab_ws, &c->lab_epoch, c->dint, s));
-  else HRF_TRY(hrf_label(a, 0, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
+  HRF_TRY(hrf_label(a, 0, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
   HRF_TRY(ensure_labels(c, 1, s));
   int32_t guess = (int32_t)(c->lab_cap - 1);
   HRF_TRY(hrf_label_boxes(lab1, H, W, guess, c->box, s));
@@ -240,8 +233,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
     HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s,
                                          attempt == 0 ? c->dint + 8 : nullptr, c->seed_px));
     HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
-    if (onepass) HRF_TRY(::hrf::label_onepass(d, H, W, 2, seeds, c->parent, c->lab_ws, &c->lab_epoch, c->dint, s));
-    else HRF_TRY(hrf_label(d, 0, H, W, 2, seeds, c->parent, c->blk, c->dint, s));  // :111-112
+    HRF_TRY(hrf_label(d, 0, H, W, 2, seeds, c->parent, c->blk, c->dint, s));        // :111-112
     // read back at the watershed's synchronisation: the seed count, the run kernel's overflow
     // count; cleared there: the per-label counts and moments (capacity-wide) and `extra`
     ::hrf::ZeroPub zp = extra ? *extra : ::hrf::ZeroPub();
