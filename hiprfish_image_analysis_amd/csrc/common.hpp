@@ -51,13 +51,15 @@ struct Err {
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-// Grid for a grid-stride elementwise kernel: enough blocks to fill 256 CUs x 8 (cap
-// HRF_STREAM_GRID_MAX, for A/B of the dispatch count beside the concurrent classifier).
+// Grid for a grid-stride elementwise kernel: at most 512 blocks (two per CU).  Beside the
+// concurrent classifier every dispatched block waits for a CU slot, so fewer, longer blocks win:
+// 1037-1050 vs 1027-1042 Mpix/s against 2048 (5 of 6 interleaved pairs; 256: 1032, 1024: 1030).
+// HRF_STREAM_GRID_MAX overrides the cap (A/B).
 inline int64_t stream_grid_max() {
   static const int64_t cap = [] {
     const char *e = getenv("HRF_STREAM_GRID_MAX");
     const long v = e ? atol(e) : 0;
-    return v > 0 ? (int64_t)v : (int64_t)2048;
+    return v > 0 ? (int64_t)v : (int64_t)512;
   }();
   return cap;
 }
