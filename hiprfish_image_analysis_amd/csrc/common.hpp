@@ -53,7 +53,8 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Grid for a grid-stride elementwise kernel: at most 512 blocks (two per CU).  Beside the
 // concurrent classifier every dispatched block waits for a CU slot, so fewer, longer blocks win:
-// 1037-1050 vs 1027-1042 Mpix/s against 2048 (5 of 6 interleaved pairs; 256: 1032, 1024: 1030).
+// 1037-1050 vs 1027-1042 Mpix/s against 2048 (means of 3; 4 of 6 interleaved pairs; 256: 1032,
+// 1024: 1030).
 // HRF_STREAM_GRID_MAX overrides the cap (A/B).
 inline int64_t stream_grid_max() {
   static const int64_t cap = [] {
