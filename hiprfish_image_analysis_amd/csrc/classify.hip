@@ -2102,11 +2102,19 @@ hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nro
   HRF_REQUIRE(variant >= 0 && variant <= 2, "classify_cells: variant must be 0, 1 or 2");
   HRF_REQUIRE(variant == 0 || (fx && fr), "classify_cells: gated variants need presence flags");
   if (nmax == 0) return HRF_OK;
-  classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(nmax, CELLS_CB), CELLS_NT,
-                                                  sizeof(double) * CELLS_CB * C, s>>>(
-      x, nmax, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nrows_dev);
-  HRF_LAUNCHED();
-  return HRF_OK;
+  // HRF_CELLS_SHAPE=<cells per workgroup><threads> (A/B, e.g. 4256): smaller workgroups find a
+  // CU slot beside the concurrent classifier sooner
+  static const int shape = getenv("HRF_CELLS_SHAPE") ? atoi(getenv("HRF_CELLS_SHAPE")) : 0;
+#define HRF_CB(CB, NT)                                                                                 \
+  if (shape == CB * 10000 + NT || (shape == 0 && CB == CELLS_CB && NT == CELLS_NT)) {                   \
+    classify_cells_blk_kernel<CB, NT><<<(unsigned)hrf::cdiv(nmax, CB), NT, sizeof(double) * CB * C, s>>>( \
+        x, nmax, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nrows_dev);                           \
+    HRF_LAUNCHED();                                                                                    \
+    return HRF_OK;                                                                                     \
+  }
+  HRF_CB(4, 1024) HRF_CB(4, 256) HRF_CB(8, 256) HRF_CB(4, 512) HRF_CB(2, 256)
+#undef HRF_CB
+  HRF_REQUIRE(false, "classify_cells: unknown HRF_CELLS_SHAPE");
 }
 
 }  // namespace hrf
