@@ -549,9 +549,17 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
     WsGeom g{image, negate, markers, mask, H, W, a.lam, a.hop};
     const int32_t *todo = B.list;
     int32_t ntodo = ncontest;
-    for (int32_t cap = 4096, threads = 256;; cap *= 16, threads = threads > 16 ? threads / 16 : 1) {
+    // as many walkers as the scratch budget holds (HRF_WS_SCRATCH_MB, default 1024 MB: ~4 k walkers
+    // of 244 KB at the first capacity; round 3 ran 256), each deciding its share of the list
+    static const int64_t budget = [] {
+      const char *e = getenv("HRF_WS_SCRATCH_MB");
+      const long v = e ? atol(e) : 1024;
+      return (int64_t)(v > 0 ? v : 1024) << 20;
+    }();
+    for (int32_t cap = 4096;; cap *= 16) {
       const int32_t hcap = 2 * cap, gcap = cap;
       const int64_t stride = walker_bytes(cap, hcap, gcap);
+      const int64_t threads = budget / stride > 0 ? budget / stride : 1;
       const int64_t nth = ntodo < threads ? ntodo : threads;
       if (nth * stride > scratch_bytes) {
         const hipError_t fe = scratch ? hipFreeAsync(scratch, s) : hipSuccess;
