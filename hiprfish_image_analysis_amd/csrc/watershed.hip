@@ -35,6 +35,11 @@
 
 #include "common.hpp"
 #include "ws_core.hpp"
+#ifdef HRF_WSW_DEBUG
+__device__ int g_wsw_dbg = 0;
+#define WSW_DBG(...) do { if (g_wsw_dbg && threadIdx.x == 0 && blockIdx.x == 0) printf(__VA_ARGS__); } while (0)
+#endif
+#include "ws_wave.hpp"
 
 namespace {
 
@@ -378,6 +383,50 @@ __global__ void ws_resolve_kernel(WsGeom g, const int32_t *__restrict__ list, in
   if (lay) atomicAdd(layout, lay);
 }
 
+// ws_resolve_kernel with one 64-lane workgroup per walker (ws_wave.hpp): the same decisions, each
+// walk's frontier processed 64 members at a time.  Scratch layout as ws_resolve_kernel's (the
+// hash is the hkey array; hgen and ml are unused).
+__global__ __launch_bounds__(64) void ws_resolve_wave_kernel(WsGeom g, const int32_t *__restrict__ list,
+                                                             int32_t count, int32_t *__restrict__ ptr,
+                                                             char *__restrict__ scratch, int64_t stride, int64_t nw,
+                                                             int32_t cap, int32_t hcap, int32_t gcap, int pbits,
+                                                             int gbits, int32_t *__restrict__ retry,
+                                                             int32_t *__restrict__ nretry, int32_t *__restrict__ layout) {
+  const int64_t t = blockIdx.x;
+  if (t >= nw) return;  // scratch exists for nw walkers only
+  char *base = scratch + t * stride;
+  WalkerW w;
+  w.pa = (int32_t *)base;
+  w.ga = w.pa + cap;
+  w.pb = w.ga + cap;
+  w.gb = w.pb + cap;
+  w.slots = w.gb + cap;
+  w.hs = (unsigned long long *)(w.slots + cap);
+  uint32_t *hgen = (uint32_t *)(w.hs + hcap);
+  double *ml = (double *)(hgen + hcap);
+  w.hit = (int32_t *)(ml + gcap);
+  w.mr = w.hit + gcap;
+  w.alive = (uint8_t *)(w.mr + gcap);
+  w.cap = cap;
+  w.hcap = hcap;
+  w.gcap = gcap;
+  w.pbits = pbits;
+  w.gbits = gbits;
+  w.genb = 64 - pbits - gbits;
+  w.gen = 1;
+  for (int32_t i = threadIdx.x; i < hcap; i += 64) w.hs[i] = 0ull;
+  __syncthreads();
+  int32_t lay = 0;
+  for (int64_t li = t; li < count; li += nw) {
+    const int32_t x = list[li];
+    if (ptr[x] >= 0) continue;  // decided with its basin component by another walker (uniform read)
+    const bool ok = ws_resolve_one_wave(g, x, ptr, w, &lay);
+    if (!ok && threadIdx.x == 0) retry[atomicAdd(nretry, 1)] = x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && lay) atomicAdd(layout, lay);
+}
+
 // labels of every non-marker pixel back to 0 (both ping-pong buffers): relabel from markers
 __global__ void ws_reset_labels_kernel(const int32_t *__restrict__ markers, const uint8_t *__restrict__ mask, int64_t n,
                                        int32_t *__restrict__ la, int32_t *__restrict__ lb) {
@@ -570,9 +619,18 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
         scratch_bytes = nth * stride;
       }
       HRF_HIP(hipMemsetAsync(flag_ws + 3, 0, sizeof(int32_t), s));
-      ws_resolve_kernel<<<(unsigned)hrf::cdiv(nth, 64), 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, nth,
-                                                                     cap, hcap, gcap, B.retry, flag_ws + 3,
-                                                                     flag_ws + 4);
+      // HRF_WS_WAVE=0: one thread per walker (the serial walk of ws_core.hpp) instead of a wave
+      static const bool wave = !getenv("HRF_WS_WAVE") || atoi(getenv("HRF_WS_WAVE")) != 0;
+      int pbits = 1, gbits = 1;
+      while (pbits < 31 && ((int64_t)1 << pbits) < n) ++pbits;
+      while (gbits < 31 && ((int64_t)1 << gbits) <= gcap) ++gbits;
+      if (wave && 64 - pbits - gbits >= 8)
+        ws_resolve_wave_kernel<<<(unsigned)nth, 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, nth, cap, hcap,
+                                                            gcap, pbits, gbits, B.retry, flag_ws + 3, flag_ws + 4);
+      else
+        ws_resolve_kernel<<<(unsigned)hrf::cdiv(nth, 64), 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, nth,
+                                                                       cap, hcap, gcap, B.retry, flag_ws + 3,
+                                                                       flag_ws + 4);
       HRF_LAUNCHED();
       HRF_HIP(hipMemcpyAsync(hflag + 3, flag_ws + 3, sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HRF_HIP(hipStreamSynchronize(s));
