@@ -98,3 +98,29 @@ def test_watershed_continuous_has_no_contest(K, orc):
     got = host(K.watershed(dev(f), dev(markers), None, ties=ties))
     assert ties == [0, 0, 0]
     assert np.array_equal(got, orc.watershed(f, markers, None))
+
+
+@pytest.mark.parametrize("n", [512, 1024])
+def test_watershed_adversarial_plateaus_equal_heap(K, orc, n):
+    """bench.py's tie-path image (`extras.cfg3.watershed_tie_path`: 4 levels in 4x4 blocks,
+    3x3 markers with distinct values per label, 10 % outside the mask) at 512^2 (8.9 k contested
+    pixels, 5 resolution rounds) and 1024^2: the wave-cooperative resolver's label map equals the
+    restated heap's pixel for pixel -- or, where a decision came down to equal-valued markers of
+    different labels (at 1024^2 the 1e-3 label offsets overlap the integer levels), the ws_order.c
+    model of the documented rule"""
+    rng = np.random.default_rng(7)
+    f = np.kron(rng.integers(0, 4, (n // 4, n // 4)), np.ones((4, 4))).astype(np.float64)
+    markers = np.zeros((n, n), np.int32)
+    for lab in range(1, n * n // 300 + 1):
+        r, c = rng.integers(1, n - 1), rng.integers(1, n - 1)
+        markers[r - 1:r + 2, c - 1:c + 2] = lab
+    f = f + 1e-3 * markers
+    mask = rng.random((n, n)) < 0.9
+    ties = []
+    got = host(K.watershed(dev(f), dev(markers), dev(mask), ties=ties))
+    assert ties[0] > 1000
+    if ties[2] == 0:
+        assert np.array_equal(got, orc.watershed(f, markers, mask))
+    else:
+        model, _ = orc.watershed_ordered(f, markers, mask)
+        assert np.array_equal(got, model)
