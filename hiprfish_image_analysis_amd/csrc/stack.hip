@@ -898,6 +898,149 @@ __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_
   }
 }
 
+// label_sums_lasers_kernel for W % 64 == 0: every 64-pixel chunk lies in one row, so a lane's
+// laser covers a contiguous range [lo, lo + span) of the chunk's pixels, and its pixel idx reads
+// base + (idx - lo) * cl -- the per-pixel row / column, coverage test and 64-bit address of the
+// general kernel (≈100 VALU and 13 quarter-rate 64-bit multiplies per labelled pixel, which
+// bound it) become one compare and one 24-bit multiply-add per lane.  Same per-wave partial sums
+// as the general kernel (runs of equal labels in raster order, f64 per lane, the same atomics);
+// a pixel outside the coverage (apply_mask) counts with a zero spectrum, as there.
+template <bool CAL>
+__global__ __launch_bounds__(256) void label_sums_lasers_row_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+                                                                    const int32_t *__restrict__ lab, int32_t maxlab,
+                                                                    const float *__restrict__ cal, int cal0, int cal1,
+                                                                    double *__restrict__ sums,
+                                                                    unsigned long long *__restrict__ counts) {
+  constexpr int LB = 16;
+  __shared__ int sdr[LMAX], sdc[LMAX];
+  load_shifts(L, sdr, sdc);
+  const int C = L.c0[L.n];
+  const int64_t npix = H * W;
+  const int lane = hrf::lane_id();
+  const int64_t nchunks = npix >> 6;  // W % 64 == 0
+  const int64_t cpr = W >> 6;         // chunks per row
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t ch = (int64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c0 = lane, c1 = lane + 64;
+  const bool v0 = c0 < C, v1 = c1 < C;
+  const bool k0 = CAL && c0 >= cal0 && c0 < cal1, k1 = CAL && c1 >= cal0 && c1 < cal1;
+  int q0 = 0, q1 = 0;
+#pragma unroll
+  for (int q = 1; q < LMAX; ++q) {
+    if (q < L.n && c0 >= L.c0[q]) q0 = q;
+    if (q < L.n && c1 >= L.c0[q]) q1 = q;
+  }
+  const int cl0 = L.c0[q0 + 1] - L.c0[q0], cl1 = L.c0[q1 + 1] - L.c0[q1];
+  const float *s0 = L.src[q0] + (c0 - L.c0[q0]), *s1 = L.src[q1] + (c1 - L.c0[q1]);
+  const int dr0 = sdr[q0], dc0 = sdc[q0], dr1 = sdr[q1], dc1 = sdc[q1];
+  auto load_label = [&](int64_t c) -> int32_t {
+    const int64_t p = (c << 6) + lane;
+    int32_t l = c < nchunks ? __builtin_nontemporal_load(lab + p) : 0;
+    return (l < 0 || l > maxlab) ? 0 : l;
+  };
+  // the lane's laser over the chunk (row r, columns cs .. cs + 63): pixels [lo, lo + span),
+  // pixel lo at base
+  auto span_of = [&](int64_t r, int64_t cs, bool v, int dr, int dc, const float *src, int cl, const float **base,
+                     int *lo) -> unsigned {
+    const int64_t rr = r - dr, col = cs - dc;
+    const int64_t a = col < 0 ? -col : 0, b = W - col < 64 ? W - col : 64;
+    const bool ok = v && rr >= 0 && rr < H && b > a;
+    *lo = ok ? (int)a : 0;
+    *base = ok ? src + (rr * W + col + a) * cl : src;
+    return ok ? (unsigned)(b - a) : 0u;
+  };
+  int32_t lnext = load_label(ch);
+  for (; ch < nchunks; ch += nwaves) {
+    const int32_t l = lnext;
+    lnext = load_label(ch + nwaves);
+    unsigned long long fg = __ballot(l != 0);
+    if (!fg) continue;
+    const int64_t p0 = ch << 6;
+    const int64_t r = ch / cpr, cs = (ch - r * cpr) << 6;
+    float pcal = 1.0f;
+    double prc = 1.0;  // lane = pixel: one division per 64 pixels, 1 / flat field
+    if (CAL) {
+      pcal = cal[p0 + lane];
+      prc = 1.0 / (double)pcal;
+    }
+    unsigned long long okmask = ~0ull;
+    if (apply_mask) {
+      bool okl = true;
+      for (int q = 0; q < L.n; ++q) okl = okl && covered(r, cs + lane, H, W, sdr[q], sdc[q]);
+      okmask = __ballot(okl);
+    }
+    const float *b0, *b1;
+    int lo0, lo1;
+    const unsigned sp0 = span_of(r, cs, v0, dr0, dc0, s0, cl0, &b0, &lo0);
+    const unsigned sp1 = span_of(r, cs, v1, dr1, dc1, s1, cl1, &b1, &lo1);
+    int32_t run = 0;  // wave-uniform
+    unsigned long long n = 0;
+    double a0 = 0.0, a1 = 0.0;
+    while (fg) {
+      int idx[LB];
+      int nb = 0;
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        idx[j] = fg ? __ffsll((long long)fg) - 1 : -1;
+        if (fg) {
+          fg &= fg - 1;
+          ++nb;
+        }
+      }
+      float x0[LB], x1[LB];
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        x0[j] = x1[j] = 0.0f;
+        if (j < nb && ((okmask >> idx[j]) & 1ull)) {
+          const unsigned u0 = (unsigned)(idx[j] - lo0), u1 = (unsigned)(idx[j] - lo1);
+          if (u0 < sp0) x0[j] = __builtin_nontemporal_load(b0 + __umul24(u0, (unsigned)cl0));
+          if (u1 < sp1) x1[j] = __builtin_nontemporal_load(b1 + __umul24(u1, (unsigned)cl1));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < LB; ++j) {
+        if (j < nb) {
+          const int32_t lj = __builtin_amdgcn_readlane(l, idx[j]);
+          if (lj != run) {
+            if (run) {
+              double *row = sums + (int64_t)run * C;
+              if (v0) atomicAdd(row + c0, a0);
+              if (v1) atomicAdd(row + c1, a1);
+              if (lane == 0) atomicAdd(counts + run, n);
+            }
+            run = lj;
+            a0 = a1 = 0.0;
+            n = 0;
+          }
+          ++n;
+          if (CAL) {
+            const float df = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, pcal), idx[j]));
+            const double d = (double)df;
+            const unsigned long long rb = __builtin_bit_cast(unsigned long long, prc);
+            const double rc = __builtin_bit_cast(
+                double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(rb >> 32), idx[j]) << 32) |
+                            (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rb, idx[j]));
+            if (df != 0.0f && __builtin_isfinite(df)) {
+              a0 += k0 ? hrf_div_rcp((double)x0[j], d, rc) : (double)x0[j];
+              a1 += k1 ? hrf_div_rcp((double)x1[j], d, rc) : (double)x1[j];
+            } else {
+              a0 += k0 ? (double)x0[j] / d : (double)x0[j];
+              a1 += k1 ? (double)x1[j] / d : (double)x1[j];
+            }
+          } else {
+            a0 += (double)x0[j];
+            a1 += (double)x1[j];
+          }
+        }
+      }
+    }
+    double *row = sums + (int64_t)run * C;
+    if (v0) atomicAdd(row + c0, a0);
+    if (v1) atomicAdd(row + c1, a1);
+    if (lane == 0) atomicAdd(counts + run, n);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1037,6 +1180,21 @@ hrf_status hrf::label_sums_lasers_zeroed(const float *const *src_host, const int
   if (H * W == 0) return HRF_OK;
   HRF_REQUIRE(labels, "label_sums_lasers: null labels");
   const int64_t nblk = hrf::cdiv(hrf::cdiv(H * W, 64), 4);
+  // HRF_LSL_ROW=0: the general kernel on every width (A/B)
+  static const bool row_ok = !getenv("HRF_LSL_ROW") || atoi(getenv("HRF_LSL_ROW")) != 0;
+  if (row_ok && W % 64 == 0) {
+    if (cal) {
+      const unsigned grid = hrf::resident_grid(label_sums_lasers_row_kernel<true>, 256, 0, nblk);
+      label_sums_lasers_row_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0,
+                                                              cal_c1, sums, (unsigned long long *)counts);
+    } else {
+      const unsigned grid = hrf::resident_grid(label_sums_lasers_row_kernel<false>, 256, 0, nblk);
+      label_sums_lasers_row_kernel<false><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, nullptr, 0, 0,
+                                                               sums, (unsigned long long *)counts);
+    }
+    HRF_LAUNCHED();
+    return HRF_OK;
+  }
   if (cal) {
     static const bool div = getenv("HRF_LSL_DIV") != nullptr;
     const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<true>, 256, 0, nblk);

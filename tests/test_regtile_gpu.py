@@ -40,10 +40,10 @@ def test_assembly_pixtable_equals_stack_path(mods, H, W, apply_mask):
     assert torch.equal(a2[0], a[0]) and torch.equal(a2[1], a[1])
 
 
+@pytest.mark.parametrize("H,W", [(256, 320), (200, 328)])  # W % 64 == 0: the row-chunk kernel
 @pytest.mark.parametrize("apply_mask,with_cal", [(True, True), (True, False), (False, True)])
-def test_label_sums_lasers_equal_stack(mods, apply_mask, with_cal):
+def test_label_sums_lasers_equal_stack(mods, apply_mask, with_cal, H, W):
     K, P, S = mods
-    H, W = 256, 320
     stack, truth, _, _ = S.tile(H, W, seed=9)
     lasers = S.laser_split(stack)
     shifts = P.estimate_shifts(lasers, device=True)
