@@ -1022,7 +1022,8 @@ __global__ __launch_bounds__(256) void label_sums_lasers_row_kernel(Lasers L, in
                             (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rb, idx[j]));
             if (df != 0.0f && __builtin_isfinite(df)) {
               a0 += k0 ? hrf_div_rcp((double)x0[j], d, rc) : (double)x0[j];
-              a1 += k1 ? hrf_div_rcp((double)x1[j], d, rc) : (double)x1[j];
+              // channels 64.. calibrated on no lane (the E. coli flat field covers 0..31): a plain sum
+              a1 += (cal1 > 64 && k1) ? hrf_div_rcp((double)x1[j], d, rc) : (double)x1[j];
             } else {
               a0 += k0 ? (double)x0[j] / d : (double)x0[j];
               a1 += k1 ? (double)x1[j] / d : (double)x1[j];
