@@ -209,7 +209,7 @@ def _event_ms(fn, n=5):
 # rocprofv3 lists them under -- the hbm_kernels rows and tools/time_kernels.py path's PMC passes
 HBM_KERNELS = {"channel_max_multi": "channel_max_multi_pf_kernel",
                "assemble_pixtable": "assemble_ecoli_kernel<false, 3>",
-               "label_sums_lasers_cal": "label_sums_lasers_kernel<true>"}
+               "label_sums_lasers_cal": "label_sums_lasers_row_kernel<true>"}
 
 
 def path_kernel_rows(lasers, cal, lib):
