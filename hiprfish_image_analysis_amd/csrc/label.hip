@@ -260,23 +260,27 @@ __global__ __launch_bounds__(256) void cc_count_scan_kernel(const int32_t *__res
                                                             int32_t *__restrict__ blk, int32_t nb,
                                                             unsigned *__restrict__ ticket,
                                                             int32_t *__restrict__ total) {
-  __shared__ int32_t ws[4];
+  __shared__ int32_t ws[2][4];
   __shared__ int32_t wsum[4];
   __shared__ int last;
   const int tid = threadIdx.x;
-  int cnt = 0;
+  // grid-stride over the NB-pixel chunks: a few hundred blocks, so a few hundred ticket
+  // acquire/releases (each an L2 write-back + invalidate on gfx950), not one per chunk
+  for (int64_t b = blockIdx.x, it = 0; b < nb; b += gridDim.x, ++it) {
+    int cnt = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t p = (int64_t)blockIdx.x * NB + k * 256 + tid;
-    cnt += (p < n && parent[p] == p);
+    for (int k = 0; k < 4; ++k) {
+      const int64_t p = b * NB + k * 256 + tid;
+      cnt += (p < n && parent[p] == p);
+    }
+    cnt = hrf::wave_sum(cnt);
+    if ((tid & 63) == 0) ws[it & 1][tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) blk[b] = ws[it & 1][0] + ws[it & 1][1] + ws[it & 1][2] + ws[it & 1][3];
   }
-  cnt = hrf::wave_sum(cnt);
-  if ((tid & 63) == 0) ws[tid >> 6] = cnt;
-  __syncthreads();
   if (tid == 0) {
-    blk[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
     __threadfence();
-    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nb - 1);
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
@@ -769,15 +773,19 @@ hrf_status hrf::label_ticketed(const uint8_t *mask, int64_t H, int64_t W, int32_
   const int64_t n = H * W;
   HRF_REQUIRE(n > 0 && mask && labels && parent_ws && blk_ws && nlab_dev, "label: bad arguments");
   const int64_t nb = hrf::cdiv(n, NB);
-  // HRF_CC_TICKET=1: the counting pass's last block scans (one launch less).  Off by default:
-  // the ticket's agent-scope acquire/release compiles to an L2 writeback + invalidate
-  // (buffer_wbl2 sc1 / buffer_inv sc1) in each of the 4096 blocks, which flushes the XCD's L2
-  // under the concurrent classifier: 905 vs 1034 Mpix/s (profiles/r4h_ticket_ab.txt)
-  static const bool use_ticket = getenv("HRF_CC_TICKET") && atoi(getenv("HRF_CC_TICKET")) != 0;
+  // The counting pass's last block scans (one launch less; HRF_CC_TICKET=0: the separate scan
+  // kernel).  The ticket's
+  // agent-scope acquire/release compiles to an L2 writeback + invalidate (buffer_wbl2 sc1 /
+  // buffer_inv sc1) per block: with one block per 1024-pixel chunk (4096 per 2048^2 tile) that
+  // flushed the XCD's L2 under the concurrent classifier, 905 vs 1034 Mpix/s
+  // (profiles/r4h_ticket_ab.txt); the counting pass now strides over the chunks with <= 256
+  // blocks: 1023 vs 1027 Mpix/s without the ticket, within the runs' spread (1011-1037)
+  static const bool use_ticket = !getenv("HRF_CC_TICKET") || atoi(getenv("HRF_CC_TICKET")) != 0;
   unsigned *ticket = use_ticket ? (unsigned *)(blk_ws + nb + 1) : nullptr;
   if (hrf_status st = run_cc(MaskV{mask, false}, H, W, conn, parent_ws, s, nullptr, nullptr, ticket)) return st;
   if (use_ticket) {
-    cc_count_scan_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, blk_ws, (int32_t)nb, ticket, nlab_dev);
+    cc_count_scan_kernel<<<(unsigned)std::min<int64_t>(nb, 256), 256, 0, s>>>(parent_ws, n, blk_ws, (int32_t)nb, ticket,
+                                                                            nlab_dev);
   } else {
     cc_count_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, blk_ws);
     scan_blocks_kernel<<<1, 1024, 0, s>>>(blk_ws, nb, nlab_dev);
