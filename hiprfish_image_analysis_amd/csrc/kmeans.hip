@@ -1691,17 +1691,21 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   if (!reuse) {
     // initial state written by a kernel: an asynchronous copy from a host stack object may run
     // after this frame is gone
-    // HRF_KM_TICKET=0: scan_u32 with its separate block-sum scan kernel (A/B: 1037 vs 1034
-    // Mpix/s, within noise; the scans have ~256 blocks, so ~256 L2 writeback + invalidates)
-    static const bool km_ticket = !getenv("HRF_KM_TICKET") || atoi(getenv("HRF_KM_TICKET")) != 0;
+    // HRF_KM_TICKET=1: scan_u32's block sums scanned by the summing launch's last block (one
+    // launch less per scan; its 256 blocks each write back and invalidate their XCD's L2 at the
+    // ticket).  Off: alone within noise (1037 vs 1034, 1024 vs 1025 Mpix/s), but the launch-count
+    // fusions together cost 1.3 % (profiles/r4i_fusion_ab.txt)
+    static const bool km_ticket = getenv("HRF_KM_TICKET") && atoi(getenv("HRF_KM_TICKET")) != 0;
     km_state_init_kernel<<<1, 256, 0, s>>>(st);
     if (n > 0) km_minmax_kernel<<<std::min<unsigned>(g, 512), 256, 0, s>>>(x, valid, n, st);
-    if (n == 0) km_scale_kernel<<<1, 1, 0, s>>>(st, nullptr);  // n > 0: km_hist_a_kernel takes it
+    static const bool scale_split = getenv("HRF_KM_SCALE_SPLIT") && atoi(getenv("HRF_KM_SCALE_SPLIT")) != 0;  // A/B
+    // n > 0: km_hist_a_kernel takes it
+    if (n == 0 || scale_split) km_scale_kernel<<<1, 1, 0, s>>>(st, n > 0 ? ws.geo : nullptr);
     HRF_LAUNCHED();
     if (n > 0) {
       const unsigned nch = (unsigned)nblocks(n);
       const int L = nch_b(n) + 1;
-      km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, st);
+      km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, scale_split ? nullptr : st);
       if (hrf_status r = scan_u32(ws.cntA, (int64_t)KD * nch, ws.sbsum, s, km_ticket ? &st->scan_ticket : nullptr)) return r;
       km_scatter_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, ws.tmpx);
       km_segments_kernel<<<1, KD, 0, s>>>(ws.cntA, (int)nch, st, ws.seg, ws.cB);

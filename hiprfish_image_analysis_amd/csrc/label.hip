@@ -773,14 +773,14 @@ hrf_status hrf::label_ticketed(const uint8_t *mask, int64_t H, int64_t W, int32_
   const int64_t n = H * W;
   HRF_REQUIRE(n > 0 && mask && labels && parent_ws && blk_ws && nlab_dev, "label: bad arguments");
   const int64_t nb = hrf::cdiv(n, NB);
-  // The counting pass's last block scans (one launch less; HRF_CC_TICKET=0: the separate scan
-  // kernel).  The ticket's
+  // HRF_CC_TICKET=1: the counting pass's last block scans (one launch less).  The ticket's
   // agent-scope acquire/release compiles to an L2 writeback + invalidate (buffer_wbl2 sc1 /
   // buffer_inv sc1) per block: with one block per 1024-pixel chunk (4096 per 2048^2 tile) that
   // flushed the XCD's L2 under the concurrent classifier, 905 vs 1034 Mpix/s
   // (profiles/r4h_ticket_ab.txt); the counting pass now strides over the chunks with <= 256
-  // blocks: 1023 vs 1027 Mpix/s without the ticket, within the runs' spread (1011-1037)
-  static const bool use_ticket = !getenv("HRF_CC_TICKET") || atoi(getenv("HRF_CC_TICKET")) != 0;
+  // blocks: 1023 vs 1027 Mpix/s without the ticket, within the runs' spread (1011-1037), but
+  // off by default with the other launch-count fusions (profiles/r4i_fusion_ab.txt)
+  static const bool use_ticket = getenv("HRF_CC_TICKET") && atoi(getenv("HRF_CC_TICKET")) != 0;
   unsigned *ticket = use_ticket ? (unsigned *)(blk_ws + nb + 1) : nullptr;
   if (hrf_status st = run_cc(MaskV{mask, false}, H, W, conn, parent_ws, s, nullptr, nullptr, ticket)) return st;
   if (use_ticket) {
