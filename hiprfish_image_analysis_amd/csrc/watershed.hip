@@ -27,9 +27,11 @@
 //     once), fixes its parent, labels are re-propagated from the markers (ws_pass_kernel in
 //     relabel mode: resolved pixels copy their parent, others the least candidate label) and
 //     step 2 repeats until no undecided contest is left.
-// One departure from skimage remains, reported in ties_host[2]: when two competing strings
-// are equal down to markers of the same value, skimage's choice depends on where its binary
-// heap happens to hold the two age-0 items; here the marker with the smaller raster index wins.
+//  4. when two competing strings are equal down to markers of the same value (counted in
+//     ties_host[2]), skimage's choice depends on where its binary heap happens to hold the two
+//     age-0 items; the resolver then takes the smaller raster index and the tile is flooded
+//     once more by ws_heap_flood_kernel, one workgroup running skimage's heap itself, whose
+//     labels replace the relaxation's.
 #include <algorithm>
 #include <cstdlib>
 
@@ -437,6 +439,198 @@ __global__ void ws_reset_labels_kernel(const int32_t *__restrict__ markers, cons
   }
 }
 
+// ---- exact replay of skimage's binary heap (equal-valued markers) ------------------------
+// When a decision comes down to equal-valued markers of different labels (all age 0), skimage
+// pops them in whatever order its binary heap holds them -- a function of every push and pop
+// before.  No parallel formulation reproduces that, so such a tile is flooded once more by one
+// workgroup that runs skimage's algorithm itself (_watershed.pyx / heap_general.pxi of the
+// reference era, restated in oracle_watershed): markers pushed in raster order with age 0,
+// (value, age) binary heap with strict-less sift up and down, the four neighbours visited up,
+// left, right, down, a pixel labelled when pushed.  The top 13 levels of the heap (8191 items)
+// live in LDS as separate value / age / index arrays, deeper items in global memory (16 B each).
+// Serial by nature; rare (no bench tile needs it).
+struct alignas(16) HeapItem {
+  double v;
+  uint32_t age;
+  int32_t idx;
+};
+constexpr int32_t HEAP_LDS = 8191;
+constexpr size_t HEAP_LDS_BYTES = (size_t)HEAP_LDS * 16;
+
+struct HeapView {
+  double *lv;
+  uint32_t *la;
+  int32_t *li;
+  HeapItem *g;  // indexed by heap position (positions < HEAP_LDS unused)
+  __device__ __forceinline__ HeapItem get(int32_t p) const {
+    if (p < HEAP_LDS) return HeapItem{lv[p], la[p], li[p]};
+    return g[p];
+  }
+  __device__ __forceinline__ void put(int32_t p, const HeapItem &x) const {
+    if (p < HEAP_LDS) {
+      lv[p] = x.v;
+      la[p] = x.age;
+      li[p] = x.idx;
+    } else {
+      g[p] = x;
+    }
+  }
+};
+
+// heap_general.pxi smaller(): value first (IEEE compare, NaN never smaller), then age
+__device__ __forceinline__ bool heap_smaller(const HeapItem &a, const HeapItem &b) {
+  if (a.v != b.v) return a.v < b.v;
+  return a.age < b.age;
+}
+
+// heappush: the new item sifts up while strictly smaller than its parent
+__device__ void heap_push(const HeapView &h, int32_t &n, const HeapItem &x) {
+  int32_t c = n++;
+  while (c > 0) {
+    const int32_t p = (c + 1) / 2 - 1;
+    const HeapItem P = h.get(p);
+    if (!heap_smaller(x, P)) break;
+    h.put(c, P);
+    c = p;
+  }
+  h.put(c, x);
+}
+
+// heappop: the last item moves to the root and sifts down to the smaller child (left wins
+// unless the right one is strictly smaller) while that child is strictly smaller than it
+__device__ HeapItem heap_pop(const HeapView &h, int32_t &n) {
+  const HeapItem top = h.get(0);
+  n -= 1;
+  if (n == 0) return top;
+  const HeapItem x = h.get(n);
+  int32_t i = 0;
+  for (;;) {
+    const int32_t l = 2 * i + 1;
+    if (l >= n) break;
+    const int32_t r = l + 1;
+    const HeapItem L = h.get(l);
+    const HeapItem R = h.get(r);  // position n (one past the heap) is allocated: read, unused
+    int32_t s = i;
+    HeapItem b = x;
+    if (heap_smaller(L, x)) {
+      s = l;
+      b = L;
+    }
+    if (r < n && heap_smaller(R, b)) {
+      s = r;
+      b = R;
+    }
+    if (s == i) break;
+    h.put(i, b);
+    i = s;
+  }
+  h.put(i, x);
+  return top;
+}
+
+// One 1024-thread workgroup.  Phase 1 (all threads): out = markers where in the mask, and the
+// list of marker pixels in raster order (order-preserving compaction by ballots + a 16-wave
+// scan).  Phase 2 (thread 0): the flood.  heap: (n + 2) items; list: n int32.
+__global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__restrict__ f, int negate,
+                                                             const int32_t *__restrict__ markers,
+                                                             const uint8_t *__restrict__ mask, int32_t H, int32_t W,
+                                                             int32_t *__restrict__ out, HeapItem *__restrict__ heap,
+                                                             int32_t *__restrict__ list) {
+  extern __shared__ char heap_smem[];
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t n = H * W;
+  if (tid == 0) base_s = 0;
+  __syncthreads();
+  for (int32_t c0 = 0; c0 < n; c0 += 1024) {
+    const int32_t i = c0 + tid;
+    int32_t m = 0;
+    if (i < n) {
+      m = (!mask || mask[i]) ? markers[i] : 0;
+      out[i] = m;
+    }
+    const uint64_t bal = __ballot(m != 0);
+    if (lane == 0) wsum[wv] = __popcll(bal);
+    __syncthreads();
+    int32_t off = base_s;
+    for (int k = 0; k < wv; ++k) off += wsum[k];
+    if (m) list[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+    __syncthreads();
+    if (tid == 0) {
+      int32_t t = base_s;
+      for (int k = 0; k < 16; ++k) t += wsum[k];
+      base_s = t;
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  __threadfence_block();  // the other waves' list and label stores, seen by thread 0's loads
+  HeapView h{(double *)heap_smem, (uint32_t *)(heap_smem + HEAP_LDS * 8), (int32_t *)(heap_smem + HEAP_LDS * 12),
+             heap};
+  const int32_t nm = base_s;
+  int32_t hn = 0;
+  for (int32_t k = 0; k < nm; ++k) {
+    const int32_t i = list[k];
+    heap_push(h, hn, HeapItem{negate ? -f[i] : f[i], 0u, i});
+  }
+  uint32_t age = 1;
+  while (hn > 0) {
+    const HeapItem e = heap_pop(h, hn);
+    const int32_t x = e.idx, r = x / W, c = x - r * W;
+    const bool ok[4] = {r > 0, c > 0, c + 1 < W, r + 1 < H};
+    const int32_t nb[4] = {x - W, x - 1, x + 1, x + W};
+    // the four neighbours' state, read before any of them is written (distinct pixels)
+    bool free_[4];
+    double v[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int32_t q = ok[d] ? nb[d] : x;
+      free_[d] = ok[d] && (!mask || mask[q]) && out[q] == 0;
+      v[d] = negate ? -f[q] : f[q];
+    }
+    const int32_t lab = out[x];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      if (!free_[d]) continue;
+      age += 1;
+      out[nb[d]] = lab;
+      heap_push(h, hn, HeapItem{v[d], age, nb[d]});
+    }
+  }
+}
+
+int64_t heap_flood_scratch_bytes(int64_t n) { return ((n + 2) * 16 + n * 4 + 255) & ~(int64_t)255; }
+
+hrf_status heap_flood(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask, int64_t H,
+                      int64_t W, int32_t *out, hipStream_t s) {
+  const int64_t n = H * W;
+  HRF_REQUIRE(n < ((int64_t)1 << 31) - 2, "watershed heap replay: image too large");
+  if (n == 0) return HRF_OK;
+  char *scratch = nullptr;
+  HRF_HIP(hipMallocAsync((void **)&scratch, (size_t)heap_flood_scratch_bytes(n), s));
+  static const bool attr = [] {
+    return hipFuncSetAttribute((const void *)ws_heap_flood_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)HEAP_LDS_BYTES) == hipSuccess;
+  }();
+  hrf_status st = HRF_OK;
+  if (!attr) {
+    ::hrf::set_error("watershed heap replay: cannot reserve %d bytes of LDS", (int)HEAP_LDS_BYTES);
+    st = HRF_EHIP;
+  } else {
+    ws_heap_flood_kernel<<<1, 1024, HEAP_LDS_BYTES, s>>>(image, negate, markers, mask, (int32_t)H, (int32_t)W, out,
+                                                         (HeapItem *)scratch,
+                                                         (int32_t *)(scratch + (n + 2) * 16));
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      ::hrf::set_error("watershed heap replay: launch failed: %s", hipGetErrorString(e));
+      st = HRF_EHIP;
+    }
+  }
+  HRF_HIP(hipFreeAsync(scratch, s));
+  return st;
+}
+
 int64_t walker_bytes(int32_t cap, int32_t hcap, int32_t gcap) {
   int64_t b = 5 * (int64_t)cap * 4 + (int64_t)hcap * 12 + (int64_t)gcap * (8 + 4 + 4 + 1);
   return (b + 255) & ~(int64_t)255;
@@ -649,16 +843,21 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
     if (hrf_status r = run(true, &ncontest)) return r;
     HRF_REQUIRE(rounds < 4096, "watershed: tie resolution does not terminate");
   }
+  int32_t layout = 0;  // decisions between equal-valued markers of different labels
+  if (rounds) {
+    HRF_HIP(hipMemcpyAsync(hflag + 3, flag_ws + 4, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HRF_HIP(hipStreamSynchronize(s));
+    layout = hflag[3];
+  }
   if (ties_host) {
     ties_host[0] = total;
     ties_host[1] = rounds;
-    if (rounds) {
-      HRF_HIP(hipMemcpyAsync(hflag + 3, flag_ws + 4, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-      HRF_HIP(hipStreamSynchronize(s));
-      ties_host[2] = hflag[3];
-    }
+    ties_host[2] = layout;
   }
   if (a.lab != out_labels) HRF_HIP(hipMemcpyAsync(out_labels, a.lab, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  // skimage decides those by its heap's layout: flood the tile again with the heap itself
+  if (layout > 0)
+    if (hrf_status r = heap_flood(image, negate, markers, mask, H, W, out_labels, s)) return r;
   if (passes_host) *passes_host = passes;
   return HRF_OK;
 }
@@ -670,6 +869,15 @@ hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *mar
                          int32_t *passes_host, hrf_stream_t stream) {
   return hrf_watershed_ex(image, negate, markers, mask, H, W, out_labels, state_ws, flag_ws, max_passes, passes_host,
                           nullptr, stream);
+}
+
+hrf_status hrf_watershed_heap(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
+                              int64_t H, int64_t W, int32_t *out_labels, hrf_stream_t stream) {
+  HRF_REQUIRE(H >= 0 && W >= 0, "watershed_heap: bad shape");
+  if (H * W == 0) return HRF_OK;
+  HRF_REQUIRE(image && markers && out_labels, "watershed_heap: null buffer");
+  HRF_REQUIRE(out_labels != markers, "watershed_heap: out_labels must not alias markers");
+  return heap_flood(image, negate, markers, mask, H, W, out_labels, (hipStream_t)stream);
 }
 
 }  // extern "C"

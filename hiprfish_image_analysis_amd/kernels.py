@@ -584,7 +584,8 @@ def max_i32(a, sync=True):
 def watershed(image, markers, mask=None, negate=False, max_passes=100000, ties: list | None = None):
     """skimage.morphology.watershed(+/-image, markers, mask=mask), 4-connectivity, with the
     heap's (value, age) order on ties.  `ties` (a list) receives [pixels that needed the exact
-    order, resolution rounds, equal-valued-marker decisions] (hrf_watershed_ex)."""
+    order, resolution rounds, equal-valued-marker decisions] (hrf_watershed_ex); a tile with
+    such a decision is flooded again by skimage's binary heap on the device (watershed_heap)."""
     import ctypes
     image = _dev(image, torch.float64, "image")
     mk = _i32(markers, "markers")
@@ -600,6 +601,18 @@ def watershed(image, markers, mask=None, negate=False, max_passes=100000, ties: 
               max_passes, ctypes.addressof(passes), ctypes.addressof(st), _stream())
     if ties is not None:
         ties[:] = list(st)
+    return out
+
+
+def watershed_heap(image, markers, mask=None, negate=False):
+    """skimage's heap flood itself on the device, one workgroup (hrf_watershed_heap): the exact
+    tie path of watershed(); serial, for tests and small images"""
+    image = _dev(image, torch.float64, "image")
+    mk = _i32(markers, "markers")
+    H, W = image.shape
+    m = _u8(mask, "mask") if mask is not None else None
+    out = torch.empty((H, W), dtype=torch.int32, device=image.device)
+    _lib.call("hrf_watershed_heap", _ptr(image), int(negate), _ptr(mk), _ptr(m), H, W, _ptr(out), _stream())
     return out
 
 

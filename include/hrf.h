@@ -306,8 +306,11 @@ HRF_API hrf_status hrf_max_i32(const int32_t *a, int64_t n, int32_t *max_dev, hr
  * hrf_watershed_workspace_bytes(H, W) device bytes; flag_ws: >= 8 int32.  Synchronises after
  * 8 relaxation passes, then per 4; HRF_EINVAL if not converged within max_passes.
  * ties_host (nullable, 3 int32): pixels whose label needed the exact order, resolution
- * rounds, and decisions between equal-valued markers (skimage: binary-heap layout; here
- * raster order) -- see DESIGN.md "Watershed". */
+ * rounds, and decisions between equal-valued markers of different labels (skimage decides
+ * those by its binary heap's layout: when there is one, the tile is flooded again by
+ * hrf_watershed_heap's kernel and its labels are returned) -- see DESIGN.md "Watershed".
+ * hrf_watershed_heap: skimage's heap flood itself, run by one workgroup (serial; exact on any
+ * input, slow on large images -- the tie path of hrf_watershed_ex, exported for tests). */
 HRF_API int64_t hrf_watershed_workspace_bytes(int64_t H, int64_t W);
 HRF_API hrf_status hrf_watershed(const double *image, int32_t negate, const int32_t *markers, const uint8_t *mask,
                                  int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
@@ -316,6 +319,9 @@ HRF_API hrf_status hrf_watershed_ex(const double *image, int32_t negate, const i
                                     int64_t H, int64_t W, int32_t *out_labels, void *state_ws, int32_t *flag_ws,
                                     int32_t max_passes, int32_t *passes_host, int32_t *ties_host,
                                     hrf_stream_t stream);
+HRF_API hrf_status hrf_watershed_heap(const double *image, int32_t negate, const int32_t *markers,
+                                      const uint8_t *mask, int64_t H, int64_t W, int32_t *out_labels,
+                                      hrf_stream_t stream);
 
 /* ==== native segmentation drivers (segment.hip) ==========================================
  * One call runs a whole segmentation chain -- the same library calls, in the same order, as

@@ -20,7 +20,9 @@
  *    share an ancestor, so the push index never matters for labels.
  *  - rank of a marker = raster index.  skimage orders equal-valued markers (all age 0)
  *    by the internal layout of its binary heap; decisions that come down to that are
- *    counted in stats[2] ("heap-layout" decisions).
+ *    counted in stats[2] ("heap-layout" decisions), and then -- as libhrf floods such a tile
+ *    again with skimage's heap (watershed.hip ws_heap_flood_kernel) -- the model returns the
+ *    heap flood's labels (oracle_watershed).
  * stats: [0] contested pixels, [1] walk steps, [2] heap-layout decisions, [3] rounds
  */
 #include <math.h>
@@ -29,6 +31,10 @@
 #include <string.h>
 
 #define EXPORT __attribute__((visibility("default")))
+
+/* hrf_oracle.c: the heap flood restated from skimage */
+void oracle_watershed(const double *img, const int32_t *markers, const uint8_t *mask, int64_t H, int64_t W,
+                      int32_t *out);
 
 typedef struct {
     int64_t *a;
@@ -328,4 +334,5 @@ EXPORT void oracle_watershed_ordered(const double *img, const int32_t *markers, 
     free(c.hop);
     free(c.stamp);
     free(ptr);
+    if (stats[2] > 0) oracle_watershed(img, markers, mask, H, W, out);
 }

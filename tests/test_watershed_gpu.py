@@ -3,10 +3,10 @@ restated from skimage (oracle_watershed: (value, age) order, labels on push), on
 integer images and on bioformats-like quantised E. coli / community tiles.
 
 skimage's binary heap orders equal-valued markers (all age 0) by its internal layout; when a
-decision comes down to that, libhrf takes the marker with the smaller raster index and reports
-the decision (ties[2]).  Tests whose markers cannot produce such a decision (distinct values
-per label) require ties[2] == 0 and the heap's map; tests with arbitrary markers require the
-heap's map whenever ties[2] == 0 and otherwise the ws_order.c model of the same rule."""
+decision comes down to that (ties[2] > 0), libhrf floods the tile again with skimage's heap on
+the device (ws_heap_flood_kernel).  Every test requires the heap's map, unconditionally; tests
+whose markers cannot produce such a decision (distinct values per label) also require
+ties[2] == 0, and the arbitrary-marker tests require the fallback to have run on some seeds."""
 import numpy as np
 import pytest
 
@@ -61,16 +61,69 @@ def test_watershed_plateaus_equal_heap(K, orc, seed):
     assert np.array_equal(got_neg, ref)
 
 
+_LAYOUT_SEEDS = []
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_watershed_plateaus_any_markers(K, orc, seed):
     H, W = [(50, 60), (128, 128), (97, 211)][seed % 3]
     f, markers, mask = plateau_case(100 + seed, H, W, 2 + seed % 3, False, seed % 2 == 1)
+    mk = mask if seed % 4 else None
     ties = []
-    got = host(K.watershed(dev(f), dev(markers), dev(mask) if seed % 4 else None, ties=ties))
-    model, st = orc.watershed_ordered(f, markers, mask if seed % 4 else None)
-    assert np.array_equal(got, model)
-    if ties[2] == 0:
-        assert np.array_equal(got, orc.watershed(f, markers, mask if seed % 4 else None))
+    got = host(K.watershed(dev(f), dev(markers), dev(mk) if mk is not None else None, ties=ties))
+    assert np.array_equal(got, orc.watershed(f, markers, mk))
+    _, st = orc.watershed_ordered(f, markers, mk)
+    assert bool(ties[2]) == bool(st[2])   # the device meets an equal-marker decision where the CPU model does
+    if ties[2]:
+        _LAYOUT_SEEDS.append(seed)
+    if seed == 7:
+        assert _LAYOUT_SEEDS, "no seed exercised the heap replay"
+
+
+def _heap_case(seed, H, W):
+    rng = np.random.default_rng(seed)
+    nv = 1 + seed % 5
+    f = rng.integers(0, nv, (H, W)).astype(np.float64)
+    if seed % 3 == 1:
+        f = rng.random((H, W))
+    if seed % 5 == 2:
+        f[rng.random((H, W)) < 0.05] = np.nan      # NaN never compares smaller, as in the heap
+    if seed % 5 == 3:
+        f[rng.random((H, W)) < 0.2] = -0.0          # -0.0 == 0.0: the age decides
+    markers = np.zeros((H, W), np.int32)
+    k = max(1, H * W // 50)
+    markers.flat[rng.choice(H * W, k, replace=False)] = rng.integers(-3, 9, k)
+    mask = (rng.random((H, W)) < 0.8) if seed % 2 else None
+    return f, markers, mask
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_watershed_heap_replay_equals_oracle(K, orc, seed):
+    """the tie path's kernel alone (hrf_watershed_heap): skimage's heap flood on the device
+    equals oracle_watershed bit for bit -- NaN and signed-zero values, negative labels, no
+    mask, 1-pixel-wide images -- and, at 160x150 and 256x256 with every pixel a marker's
+    neighbour chain, heaps deeper than the 8191 LDS-resident items"""
+    H, W = [(1, 57), (33, 1), (45, 61), (160, 150), (256, 256)][seed % 5]
+    f, markers, mask = _heap_case(seed, H, W)
+    ref = orc.watershed(f, markers, mask)
+    got = host(K.watershed_heap(dev(f), dev(markers), dev(mask) if mask is not None else None))
+    assert np.array_equal(got, ref)
+    got_neg = host(K.watershed_heap(dev(-f), dev(markers), dev(mask) if mask is not None else None, negate=True))
+    assert np.array_equal(got_neg, ref)
+
+
+def test_watershed_heap_replay_all_markers(K, orc):
+    """every pixel a marker at one value: the heap holds all 300x300 age-0 items at once (deep
+    levels in global memory) and pops them in its layout's order"""
+    H, W = 300, 300
+    rng = np.random.default_rng(11)
+    f = np.zeros((H, W))
+    markers = rng.integers(1, 5, (H, W)).astype(np.int32)
+    markers[rng.random((H, W)) < 0.3] = 0
+    ref = orc.watershed(f, markers, None)
+    assert np.array_equal(host(K.watershed_heap(dev(f), dev(markers))), ref)
+    ties = []
+    assert np.array_equal(host(K.watershed(dev(f), dev(markers), None, ties=ties)), ref)
 
 
 def test_watershed_constant_image(K, orc):
@@ -104,10 +157,9 @@ def test_watershed_continuous_has_no_contest(K, orc):
 def test_watershed_adversarial_plateaus_equal_heap(K, orc, n):
     """bench.py's tie-path image (`extras.cfg3.watershed_tie_path`: 4 levels in 4x4 blocks,
     3x3 markers with distinct values per label, 10 % outside the mask) at 512^2 (8.9 k contested
-    pixels, 5 resolution rounds) and 1024^2: the wave-cooperative resolver's label map equals the
-    restated heap's pixel for pixel -- or, where a decision came down to equal-valued markers of
-    different labels (at 1024^2 the 1e-3 label offsets overlap the integer levels), the ws_order.c
-    model of the documented rule"""
+    pixels, 5 resolution rounds) and 1024^2 (where the 1e-3 label offsets overlap the integer
+    levels, so some decisions come down to equal-valued markers and the heap replay runs): the
+    label map equals the restated heap's pixel for pixel"""
     rng = np.random.default_rng(7)
     f = np.kron(rng.integers(0, 4, (n // 4, n // 4)), np.ones((4, 4))).astype(np.float64)
     markers = np.zeros((n, n), np.int32)
@@ -118,9 +170,6 @@ def test_watershed_adversarial_plateaus_equal_heap(K, orc, n):
     mask = rng.random((n, n)) < 0.9
     ties = []
     got = host(K.watershed(dev(f), dev(markers), dev(mask), ties=ties))
+    print(f"n={n} ties={ties}")
     assert ties[0] > 1000
-    if ties[2] == 0:
-        assert np.array_equal(got, orc.watershed(f, markers, mask))
-    else:
-        model, _ = orc.watershed_ordered(f, markers, mask)
-        assert np.array_equal(got, model)
+    assert np.array_equal(got, orc.watershed(f, markers, mask))

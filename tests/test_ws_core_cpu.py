@@ -55,9 +55,12 @@ def test_device_resolution_code_equals_heap(emul, orc, block):
         if seed % 2:
             f = f + 1e-3 * markers
         got, ties = emul(f, markers, mask)
-        model, _ = orc.watershed_ordered(f, markers, mask)
-        assert np.array_equal(got, model), seed
+        model, st = orc.watershed_ordered(f, markers, mask)
+        # the emulator replays the resolution only; an equal-valued-marker decision (ties[2]) is
+        # where libhrf floods again with the heap (watershed.hip), as the model does (st[2])
+        assert bool(ties[2]) == bool(st[2]), seed
         if ties[2] == 0:
+            assert np.array_equal(got, model), seed
             assert np.array_equal(got, orc.watershed(f, markers, mask)), seed
         else:
             layout_cases += 1
