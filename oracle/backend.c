@@ -466,6 +466,13 @@ __attribute__((visibility("default"))) void oracle_cr_log(const double *x, int64
   for (int64_t i = 0; i < n; ++i) out[i] = mode ? hrf_cr_log10(x[i]) : hrf_cr_log(x[i]);
 }
 
+/* the C library's own log / log10 (glibc here), element by element: what numpy 1.16 -- the
+ * reference era's numpy, whose np.log called libm -- computes for image_cn (ecoli :72).  Used by
+ * tests/test_image_cn_log.py to show the segmentation does not depend on the last ulp. */
+__attribute__((visibility("default"))) void oracle_libm_log(const double *x, int64_t n, int mode, double *out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = mode ? log10(x[i]) : log(x[i]);
+}
+
 /* hrf_div_rcp (detmath.h) against the IEEE division on n float32 pairs: random bit patterns
  * (finite, d nonzero), plus directed significands (all ones, 1 + ulp, powers of two) -> the
  * number of pairs whose results differ (tests/test_oracle_golden.py). */

@@ -62,6 +62,15 @@ def cr_log(x):
     return out
 
 
+def libm_log(x, base10=False):
+    """the C library's log (glibc on the host), one call per element: numpy 1.16's np.log (the
+    reference era's numpy called libm); tests/test_image_cn_log.py"""
+    a = _c(x, np.float64)
+    out = np.empty_like(a)
+    lib().oracle_libm_log(_p(a), I64(a.size), 1 if base10 else 0, _p(out))
+    return out
+
+
 def cr_log10(x):
     """correctly rounded log10 (hrf_cr_log10): log10(sum + 1), biofilm :831"""
     a = _c(x, np.float64)
