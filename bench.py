@@ -51,10 +51,6 @@ KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7
                2: "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 3>",
                "t": "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3>"}
 REGTILE = os.environ.get("HRF_REGTILE", "1") != "0"   # A/B switch: 0 = register_stack + in-kernel operand build
-# HRF_LOOKAHEAD=1: each worker starts tile i+1 (registration + per-pixel classifier) before it
-# finishes tile i -- neutral with six tiles in flight (1046.7 vs 1048.5 Mpix/s, three interleaved
-# pairs), so off by default
-LOOKAHEAD = os.environ.get("HRF_LOOKAHEAD", "0") == "1"
 # one native call per tile (hrf_tile_ecoli: registration, both classifications, segmentation,
 # spectra, counts, identification map); HRF_TILE_NATIVE=0: the composed path (register_tile +
 # process_tile, ~15 foreign calls and a cell-count synchronisation per tile)
@@ -543,28 +539,19 @@ def main():
     def worker(j, first, nsteps, timed):
         # worker j drives tiles first*T + j, (first+1)*T + j, ... on its own stream, with no
         # barrier between steps: a tile's segmentation chain starts while the previous tile's
-        # classifier still runs, so the GPU never drains at a step boundary.  With LOOKAHEAD
-        # the worker registers tile i+1 and enqueues its per-pixel classifier before it runs
-        # tile i's segmentation chain (every tile is still registered, classified, segmented
-        # and counted inside the region it is timed in).  Counts are summed on the worker's
-        # stream (one all-reduce per job, after the join).
+        # classifier still runs, so the GPU never drains at a step boundary.  Counts are summed
+        # on the worker's stream (one all-reduce per job, after the join).
         acc = None
         res = None
         seq = [tiles[(i * T + j) % len(tiles)] for i in range(first, first + nsteps)]
-        nxt = tile_start(j, seq[0], timed) if (LOOKAHEAD and not NATIVE and seq) else None
-        for k, tile in enumerate(seq):
+        for tile in seq:
             if NATIVE and REGTILE:
                 with torch.cuda.stream(streams[j]):
                     res = P.process_tile_native(tile[0], lib, calibration=tile[1], per_pixel=per_pixel, variant=1,
                                                 overlap=not args.no_overlap, pixel_events=ev if timed else None)
                     acc = res.counts.clone() if acc is None else acc.add_(res.counts)
                 continue
-            if LOOKAHEAD:
-                cur = nxt
-                nxt = tile_start(j, seq[k + 1], timed) if k + 1 < len(seq) else None
-            else:
-                cur = tile_start(j, tile, timed)
-            res = tile_finish(j, cur)
+            res = tile_finish(j, tile_start(j, tile, timed))
             with torch.cuda.stream(streams[j]):
                 acc = res.counts.clone() if acc is None else acc.add_(res.counts)
         return res, acc

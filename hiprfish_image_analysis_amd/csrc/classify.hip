@@ -608,7 +608,10 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
 // keys: score bits with the low 4 mantissa bits replaced by 15 - register (so the max also
 // names the register, lower rows winning ties), a max tree per block and one compare per
 // block -- about half the VALU of a compare-and-select per score.  The 4 dropped bits are
-// <= 2^-19 relative (< 1e-5 of a distance); blocks still compete in row order.
+// <= 2^-19 relative (< 1e-5 of a distance): the keyed score IS the truncated one (it is the
+// distance reported), and its argmax keeps the reference's tie rule on it -- within a block the
+// code makes the lowest row win equal scores, across blocks (and chunks) only a strictly greater
+// score replaces the running best, so equal scores anywhere in the library go to the lowest r.
 template <int KS16, int ROWB, int NW, int NSEG, bool ZS, bool KEYED>
 __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w, int h,
                                           const h8 (&bh0)[KS16], const h8 (&bl0)[KS16], const h8 (&bh1)[KS16],
@@ -656,12 +659,12 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
         }
       }
     }
-    if (KEYED && hi == 16) {  // the pending block is complete
-      if (bk0 > key0) {
+    if (KEYED && hi == 16) {  // the pending block is complete: a later block wins on a greater score only
+      if ((bk0 >> 4) > (key0 >> 4)) {
         key0 = bk0;
         bi0 = pr;
       }
-      if (bk1 > key1) {
+      if ((bk1 >> 4) > (key1 >> 4)) {
         key1 = bk1;
         bi1 = pr;
       }
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   }
 }
 
-// ---- the same sweep on v_mfma_f32_16x16x32_f16 -------------------------------------------
+// ---- the same sweep on v_mfma_f32_16x16x32_f16 (E. coli layout) -------------------------------
 // Same table, same split-fp16 products, same argmax rules; the MFMA shape differs: A = 16
 // library rows x 32 columns (lane: row lane & 15, columns 32t + 8Q..+7, Q = lane >> 4), B = 32
 // columns x 16 pixels (lane: pixel lane & 15, the same columns), C = 16 x 16 (lane: pixel lane &
@@ -784,281 +787,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
 // shape holds a higher clock than 32x32x16 under load (MI355X_MICROARCH.md, matrix-core DVFS).
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// B operand of the 16-pixel sub-group g (0/1) of a staged 32-pixel group: lane pixel
-// jj = (lane & 15) + 16 g, columns 32t + 8Q + q.  The four quarter-lanes of a pixel split its
-// columns; segment norms are summed over them (two shuffles).  Arithmetic as build_b_lay.
-template <class L, int KT>
-__device__ __forceinline__ void build_b_lay16(const float *stg, int lane, int g, h8 (&bh)[KT], h8 (&bl)[KT],
-                                              uint32_t &zx, uint32_t &neg) {
-  const int jj = (lane & 15) + 16 * g, Q = lane >> 4;
-  const float *pc = stg + jj * L::C + 8 * Q;
-  float raw[KT][8];
-  int sg[KT][8];
-  float nn[L::NSEG];
-  uint32_t nzs[L::NSEG];
-  uint32_t sgn = 0;
-#pragma unroll
-  for (int s = 0; s < L::NSEG; ++s) {
-    nn[s] = 0.0f;
-    nzs[s] = 0u;
-  }
-#pragma unroll
-  for (int t = 0; t < KT; ++t)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = 32 * t + 8 * Q + q;
-      int seg = -2;
-      if (k == L::C) seg = -1;
-      else if (k < L::C) {
-        seg = 0;
-#pragma unroll
-        for (int u = 1; u < L::NSEG; ++u) seg += k >= L::b(u) ? 1 : 0;
-      }
-      sg[t][q] = seg;
-      const float r = pc[32 * t + q];  // past the row end: another pixel's value, masked here
-      const float x = seg >= 0 ? r : 0.0f;
-      raw[t][q] = x;
-      const uint32_t xb = __float_as_uint(x);
-      sgn |= xb;
-      const float x2 = x * x;
-#pragma unroll
-      for (int s = 0; s < L::NSEG; ++s) {
-        nn[s] += seg == s ? x2 : 0.0f;
-        nzs[s] |= seg == s ? (xb << 1) : 0u;
-      }
-    }
-  neg = sgn >> 31;
-  float inv[L::NSEG];
-  zx = 0;
-#pragma unroll
-  for (int s = 0; s < L::NSEG; ++s) {
-    float t = nn[s] + __shfl_xor(nn[s], 16, 64);
-    t += __shfl_xor(t, 32, 64);
-    uint32_t nz = nzs[s] | __shfl_xor(nzs[s], 16, 64);
-    nz |= __shfl_xor(nz, 32, 64);
-    inv[s] = nz ? rsqrtf(t) : 0.0f;
-    zx |= (nz ? 0u : 1u) << s;
-    if (nz && !(t >= 1e-30f)) {  // f32 underflow: redo in f64
-      double td = 0.0;
-#pragma unroll
-      for (int tt = 0; tt < KT; ++tt)
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (sg[tt][q] == s) td += (double)raw[tt][q] * (double)raw[tt][q];
-      td += __shfl_xor(td, 16, 64);
-      td += __shfl_xor(td, 32, 64);
-      inv[s] = (float)(1.0 / sqrt(td));
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    h8 vh, vl;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int seg = sg[t][q];
-      float m = seg == -1 ? 1.0f : 0.0f;
-#pragma unroll
-      for (int s = 0; s < L::NSEG; ++s) m = seg == s ? inv[s] : m;
-      float x = seg >= 0 ? raw[t][q] * m : m;
-      asm volatile("" : "+v"(x));  // round to f32 first: no fused multiply-to-f16
-      const _Float16 hv = (_Float16)x;
-      vh[q] = hv;
-      vl[q] = (_Float16)(x - (float)hv);
-    }
-    bh[t] = vh;
-    bl[t] = vl;
-  }
-}
-
-template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF>
-__device__ __forceinline__ void lay_sweep16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
-                                            const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t (&zx)[4],
-                                            float (&best)[4], int (&bi)[4]) {
-  constexpr int KP = 32 * KT;
-  constexpr int CHB = RCH * ROWB;
-  constexpr int NPC = CHB / 1024;
-  const int rl = lane & 15, Q = lane >> 4;
-  // NBUF = 3: chunk c + 2 streams in while c feeds the MFMAs and c + 1 lands; NBUF = 2: c + 1
-  // streams in while c feeds them (less LDS per workgroup: room for other kernels on the CU)
-  auto issue = [&](int c) {
-    const char *g = gref + (int64_t)c * CHB + lane * 16;
-    char *l = ldsb + (c % NBUF) * CHB;
-    for (int q = w; q < NPC; q += NW)
-      __builtin_amdgcn_global_load_lds((glb_void_t *)(g + q * 1024), (lds_void_t *)(l + q * 1024), 16, 0, 0);
-  };
-  constexpr int MINE_LO = NPC / NW;                  // pieces per wave: MINE_LO or MINE_LO + 1
-  const int mine = (NPC - w + NW - 1) / NW;
-  issue(0);
-  if (NBUF == 3 && nch > 1) issue(1);
-  f32x4 pv[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pv[g][i] = -__builtin_inff();
-  int pr = 0;  // first row of the pending block
-  h8 bz[4];    // ZS: the pixels' zero-segment indicators (Q == 0 lanes, k < NSEG)
-#pragma unroll
-  for (int g = 0; g < 4; ++g)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) bz[g][q] = (_Float16)((Q == 0 && q < NSEG && ((zx[g] >> q) & 1u)) ? 1.0f : 0.0f);
-  int key[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) key[g] = INT32_MIN;
-  // epilogue of the pending block, groups [g0, g1): this lane's rows pr + 4Q + i
-  auto epi = [&](int g0, int g1) {
-#pragma unroll
-    for (int g = g0; g < g1; ++g) {
-      if (KEYED) {
-        int bk = INT32_MIN;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bk = max(bk, (__float_as_int(pv[g][i]) & -16) | (15 - i));
-        if (bk > key[g]) {
-          key[g] = bk;
-          bi[g] = pr;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (pv[g][i] > best[g]) {
-            best[g] = pv[g][i];
-            bi[g] = pr + i;
-          }
-      }
-    }
-  };
-  for (int c = 0; c < nch; ++c) {
-    // chunk c landed for this wave: only chunk c + 1's pieces may still be outstanding (loads
-    // retire in order; hipcc does not count LDS-DMA before the barrier, see lay_sweep)
-    if (NBUF == 2 || c + 1 >= nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (mine > MINE_LO) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MINE_LO) : "memory");
-    __syncthreads();  // every wave's pieces of c landed; everyone is past chunk c - 1
-    if (c + NBUF - 1 < nch) issue(c + NBUF - 1);
-    const char *buf = ldsb + (c % NBUF) * CHB;
-#pragma unroll
-    for (int rb = 0; rb < RCH; rb += 16) {
-      f32x4 acc[4];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const char *row = buf + (rb + rl) * ROWB + 16 * Q;
-      h8 az;
-      if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + rl) * ROWB + 4 * KP);
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
-        const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 64 * t);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
-        epi((4 * t) / KT, (4 * (t + 1)) / KT);  // previous block, slice t
-      }
-      if (ZS) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz[g], acc[g], 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) pv[g] = acc[g];
-      pr = c * RCH + rb;
-    }
-  }
-  epi(0, 4);  // the last block
-  if (KEYED) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bi[g] += 15 - (key[g] & 15);
-      best[g] = __int_as_float(key[g] & -16);
-    }
-  }
-}
-
-template <class L, int NW, int NBUF>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay16_kernel(const float *__restrict__ stack,
-                                                                       int64_t P, const _Float16 *__restrict__ refh,
-                                                                       int32_t R, int32_t Rpad,
-                                                                       int32_t *__restrict__ best_idx,
-                                                                       float *__restrict__ best_dist) {
-  constexpr int KT = (L::C + 1 + 31) / 32;
-  constexpr int KP = 32 * KT;
-  static_assert(KP == 16 * lay_ks16<L>(), "the 16x16x32 path needs K padded to a multiple of 32");
-  constexpr int ROWB = 4 * KP + L::PADB;
-  static_assert((RCH * ROWB) % 1024 == 0, "chunk must be whole 1 KiB pieces");
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
-  h8 bh[4][KT], bl[4][KT];
-  uint32_t zx[4], ng[4];
-  float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
-  {
-    float4 v[LDV];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      load_group(stack, P, L::C, pbase + 32 * half, lane, v);
-#pragma unroll
-      for (int i = 0; i < LDV; ++i) {
-        const int e4 = lane + 64 * i;
-        if (e4 < 8 * L::C) reinterpret_cast<float4 *>(stg)[e4] = v[i];
-      }
-      __syncthreads();
-      build_b_lay16<L, KT>(stg, lane, 0, bh[2 * half], bl[2 * half], zx[2 * half], ng[2 * half]);
-      build_b_lay16<L, KT>(stg, lane, 1, bh[2 * half + 1], bl[2 * half + 1], zx[2 * half + 1], ng[2 * half + 1]);
-      __syncthreads();
-    }
-  }
-  const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
-  float best[4];
-  int bi[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    best[g] = -__builtin_inff();
-    bi[g] = 0;
-  }
-  const char *gref = reinterpret_cast<const char *>(refh);
-  char *ldsb = reinterpret_cast<char *>(lds);
-  const int nch = Rpad / RCH;
-  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
-  const bool keyed = !libneg && !__syncthreads_or((ng[0] | ng[1] | ng[2] | ng[3]) != 0);
-#define HRF_SWEEP16(Z, K) \
-  lay_sweep16<KT, ROWB, NW, L::NSEG, Z, K, NBUF>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
-  if (keyed) {
-    if (zs) HRF_SWEEP16(true, true);
-    else HRF_SWEEP16(false, true);
-  } else {
-    if (zs) HRF_SWEEP16(true, false);
-    else HRF_SWEEP16(false, false);
-  }
-#undef HRF_SWEEP16
-  const int Q = lane >> 4;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    float b = best[g];
-    int idx = bi[g] + 4 * Q;
-#pragma unroll
-    for (int o = 16; o <= 32; o <<= 1) {
-      const float ob = __shfl_xor(b, o, 64);
-      const int oi = __shfl_xor(idx, o, 64);
-      if (ob > b || (ob == b && oi < idx)) {
-        b = ob;
-        idx = oi;
-      }
-    }
-    const int64_t p = pbase + 16 * g + (lane & 15);
-    if (Q == 0 && p < P) {
-      best_idx[p] = idx;
-      best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
-    }
-  }
-}
-
 // ---- round 3: the 16x16x32 sweep with a lane-per-pixel prologue and per-chunk argmax keys ----
-// Same table, products, scores and tie rules as classify_pixels_lay16_kernel; what changes is the
-// instruction count around the MFMAs (the lay16 kernel issues ~2.3 VALU per MFMA over its life,
-// which with two waves per SIMD leaves the matrix pipe idle ~40 % of the time):
+// Same table, products, scores and tie rules as the 32x32x16 form; what changes against round 2's
+// first 16x16x32 kernel (lay16, removed in round 5 after losing every A/B) is the instruction
+// count around the MFMAs (lay16 issued ~2.3 VALU per MFMA over its life, which with two waves per
+// SIMD left the matrix pipe idle ~40 % of the time):
 //  * prologue: in the B-operand layout a lane's columns 32t + 8Q + q belong to a segment that
-//    depends on the lane quarter Q, a runtime value, so build_b_lay16 selects among all NSEG
-//    segments for every value (~830 v_cndmask per wave).  Here the segment norms are taken by
+//    depends on the lane quarter Q, a runtime value, so lay16's operand build selected among all
+//    NSEG segments for every value (~830 v_cndmask per wave).  Here the segment norms are taken by
 //    one lane per staged pixel walking its C channels -- every channel's segment a compile-time
 //    constant -- and the pixel is normalised in place in LDS; the B-operand lanes then only read
 //    and split into hi/lo fp16;
@@ -1072,8 +808,8 @@ using hrf_pix::lay_seg;
 
 // One staged 32-pixel group (row-major, stride C floats, at stg): lanes 0..31 (pixel = lane)
 // take the segment norms, flag all-zero segments (zx) and negative values (neg), and rewrite
-// the pixel normalised.  Same arithmetic as build_b_lay16 (f32 sums, v_rsq, f64 redo when a
-// sum underflows f32), summed in channel order.
+// the pixel normalised.  Same arithmetic as build_b_lay (f32 sums, v_rsq, f64 redo when a sum
+// underflows f32), summed in channel order.
 template <class L>
 __device__ __forceinline__ void norm_pixels_w16(float *stg, int lane, uint32_t &zx, uint32_t &neg) {
   zx = 0;
@@ -1174,7 +910,8 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
 #pragma unroll
   for (int g = 0; g < 4; ++g) key[g] = ck[g] = INT32_MIN;
   // fold the pending block into the chunk keys, groups [g0, g1); after the chunk's last block,
-  // the chunk key against the running best (strictly greater: earlier chunks win ties)
+  // the chunk key against the running best (strictly greater score, the position code left out:
+  // earlier chunks win ties, so equal scores keep the lowest row across the whole library)
   auto epi = [&](int g0, int g1) {
     const int pb = (pr / 16) % NB;
 #pragma unroll
@@ -1200,7 +937,7 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
       const int cb = pr - 16 * pb;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        if (ck[g] > key[g]) {
+        if ((ck[g] >> 4) > (key[g] >> 4)) {
           key[g] = ck[g];
           bi[g] = cb;
         }
@@ -1512,98 +1249,15 @@ int64_t table_rowb(int mode, int lay, int kp) {
   return 4 * kp + 16;
 }
 
-// ---- per cell, f64, gated variants; one workgroup per cell ----
-// The library is read channel-major (refT[c * R + r], transposed once per call), so the 256
-// threads of a workgroup -- one library row each -- read consecutive addresses per channel:
-// coalesced, instead of 64 cache lines per load with row-major rows.  Same arithmetic order.
-__device__ double seg_dist(const double *x, const double *y, int64_t ys, int lo, int hi) {
-  double d = 0, nx = 0, ny = 0;
-  for (int i = lo; i < hi; ++i) {
-    const double yi = y[i * ys];
-    d += x[i] * yi;
-    nx += x[i] * x[i];
-    ny += yi * yi;
-  }
-  if (nx == 0.0 && ny == 0.0) return 0.0;
-  if (nx == 0.0 || ny == 0.0) return 1.0;
-  return 1.0 - d / sqrt(nx * ny);
-}
-
-__global__ void transpose_f64_kernel(const double *__restrict__ a, int32_t R, int32_t C, double *__restrict__ t) {
-  const int64_t n = (int64_t)R * C;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = e / C, c = e - r * C;
-    t[c * R + r] = a[e];
-  }
-}
-
-__global__ __launch_bounds__(256) void classify_cells_kernel(const double *__restrict__ X, int64_t N,
-                                                             const double *__restrict__ ref, int32_t R, int32_t C,
-                                                             Bounds bd, int32_t variant,
-                                                             const double *__restrict__ fx,
-                                                             const double *__restrict__ fr,
-                                                             int32_t *__restrict__ arg, double *__restrict__ dmin,
-                                                             const int32_t *__restrict__ n_dev) {
-  extern __shared__ double xs[];
-  __shared__ double sbest[256];
-  __shared__ int sidx[256];
-  const int64_t i = blockIdx.x;
-  if (n_dev && i >= *n_dev) return;  // rows past the device-held count (hrf_tile_ecoli)
-  const int tid = threadIdx.x;
-  for (int c = tid; c < C; c += 256) xs[c] = X[i * C + c];
-  __syncthreads();
-  const int S = bd.nseg;
-  double best = __builtin_inf();
-  int bi = 0x7fffffff;
-  for (int r = tid; r < R; r += 256) {
-    const double *y = ref + r;  // channel-major: element c at y[c * R]
-    double d;
-    if (variant == 0) {
-      double s = 0;
-      for (int k = 0; k < S; ++k) s += seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
-      d = s / S;
-    } else {
-      double chk = 0;
-      for (int k = 0; k < S; ++k) chk += fabs(fx[i * S + k] - fr[(int64_t)r * S + k]);
-      if (chk < 0.01) {
-        double s = 0;
-        for (int k = 0; k < S; ++k) s += fx[i * S + k] == 0 ? 0.0 : seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
-        d = variant == 1 ? s / S : 0.5 * s / S;
-      } else if (variant == 2) {
-        d = 1.0;
-      } else {
-        double s = 0;
-        for (int k = 0; k < S; ++k) s += seg_dist(xs, y, R, bd.b[k], bd.b[k + 1]);
-        d = s / S;
-      }
-    }
-    if (d < best) {
-      best = d;
-      bi = r;
-    }
-  }
-  sbest[tid] = best;
-  sidx[tid] = bi;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      const double b2 = sbest[tid + o];
-      const int i2 = sidx[tid + o];
-      if (b2 < sbest[tid] || (b2 == sbest[tid] && i2 < sidx[tid])) {
-        sbest[tid] = b2;
-        sidx[tid] = i2;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    arg[i] = sidx[0] == 0x7fffffff ? 0 : sidx[0];
-    dmin[i] = sbest[0];
-  }
-}
+// ---- per cell, f64, gated variants ----
+// The library is read channel-major (refT[c * R + r], transposed once per call), so the threads of
+// a workgroup -- one library row each -- read consecutive addresses per channel: coalesced,
+// instead of 64 cache lines per load with row-major rows.  A segment's distance is
+// 1 - x.y / sqrt(|x|^2 |y|^2) with the three sums in channel order (0 when both are zero, 1 when
+// one is), the restatement's seg_dist.
 
 // library prep for the blocked kernel: refT = channel-major library (t[c * R + r]) and ny[r * S + s]
-// = the segment's sum of squares in channel order (seg_dist's ny, bit for bit)
+// = the segment's sum of squares in channel order (the restatement's |y|^2, bit for bit)
 __global__ void cells_lib_prep_kernel(const double *__restrict__ a, int32_t R, int32_t C, Bounds bd,
                                       double *__restrict__ t, double *__restrict__ ny) {
   const int64_t n = (int64_t)R * C;
@@ -1624,11 +1278,11 @@ __global__ void cells_lib_prep_kernel(const double *__restrict__ a, int32_t R, i
   }
 }
 
-// classify_cells_kernel for CB cells per workgroup: each library value read from L2 feeds CB
-// cells, and only the dot products run per (cell, row) -- the segment norms are taken once, the
-// cells' in the workgroup (nx) and the library's by cells_lib_prep_kernel (ny), in seg_dist's
-// channel order, so every distance equals classify_cells_kernel's bit for bit.  Rows are visited
-// in increasing order per thread and ties go to the smaller row, as there.
+// CB cells per workgroup: each library value read from L2 feeds CB cells, and only the dot
+// products run per (cell, row) -- the segment norms are taken once, the cells' in the workgroup
+// (nx) and the library's by cells_lib_prep_kernel (ny), in channel order, so every distance is the
+// restatement's bit for bit (round 1's one-workgroup-per-cell kernel, removed in round 5, computed
+// the same values).  Rows are visited in increasing order per thread and ties go to the smaller row.
 template <int CB, int NT>
 __global__ __launch_bounds__(NT) void classify_cells_blk_kernel(const double *__restrict__ X, int64_t N,
                                                                  const double *__restrict__ refT,
@@ -1763,23 +1417,13 @@ template <class L, int NW, int NB, int CR, int OCC>
 hrf_status launch_w16_lay(const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad, int32_t *best_idx,
                           float *best_dist, hipStream_t s) {
   constexpr int KT = (L::C + 1 + 31) / 32;
-  size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
+  const size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
   HRF_REQUIRE(shm * OCC <= 160 * 1024 + 1024, "classify: w16 configuration exceeds the LDS");
-  // HRF_CLASSIFY_MAXWG = m: at most m workgroups per CU (the LDS request padded to 160 KB / m),
-  // leaving registers and LDS on every CU for the segmentation kernels running beside it
-  static const int maxwg = getenv("HRF_CLASSIFY_MAXWG") ? atoi(getenv("HRF_CLASSIFY_MAXWG")) : 0;
-  if (maxwg > 0 && maxwg < OCC) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
   (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   classify_pixels_w16_kernel<L, NW, NB, CR, OCC><<<(unsigned)hrf::cdiv(P, 64 * NW), 64 * NW, shm, s>>>(
       stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist);
   return HRF_OK;
-}
-template <int NW, int NB, int CR, int OCC>
-hrf_status launch_w16(int lay, const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad,
-                      int32_t *best_idx, float *best_dist, hipStream_t s) {
-  return lay == 1 ? launch_w16_lay<LayEcoli, NW, NB, CR, OCC>(stack, P, refx, R, rpad, best_idx, best_dist, s)
-                  : launch_w16_lay<LayMulti, NW, NB, CR, OCC>(stack, P, refx, R, rpad, best_idx, best_dist, s);
 }
 
 hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Bounds *bd) {
@@ -1863,89 +1507,24 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
   if (mode == 2) {
     const int lay = layout_id(bd, C);
     HRF_REQUIRE(lay != 0, "classify: mode 2 needs the E. coli or multispecies channel layout");
-    // waves per workgroup: the library chunks streamed through LDS are shared by NW*64 pixels
-    static const int nw = getenv("HRF_CLASSIFY_NW") ? atoi(getenv("HRF_CLASSIFY_NW")) : 4;
-    const size_t rowb = (size_t)table_rowb(2, lay, kp);
-    const size_t shm = std::max<size_t>((size_t)2 * RCH * rowb, sizeof(float) * nw * 32 * C);
-#define HRF_LAY(LAY, NWV)                                                                                      \
-  (void)hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LAY, NWV>,                                \
-                            hipFuncAttributeMaxDynamicSharedMemorySize,                                       \
-                            (int)shm);                                                                        \
-  classify_pixels_lay_kernel<LAY, NWV><<<(unsigned)hrf::cdiv(P, 64 * NWV), 64 * NWV, shm, s>>>(                 \
-      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
-    // the 16x16x32 MFMA form of the same sweep, default for the E. coli layout (R = 1023: +2 %
-    // end to end in interleaved A/B pairs; isolated within 1 %); the 32x32x16 form for the
-    // community layout (R = 127, where it is 25 % faster).  HRF_CLASSIFY_MFMA16=0/1 forces one.
-    static const int m16_env = getenv("HRF_CLASSIFY_MFMA16") ? atoi(getenv("HRF_CLASSIFY_MFMA16")) : -1;
-    const int m16 = m16_env >= 0 ? m16_env : (lay == 1);
-    // chunk buffers of the 16x16x32 form (HRF_CLASSIFY_NBUF=2/3): two by default -- isolated
-    // the same, but 52 instead of 78 KB of LDS per workgroup leaves room on the CU for the
-    // segmentation kernels running beside it (+2 % end to end, interleaved A/B, 2 of 3 pairs)
-    static const int nbuf = getenv("HRF_CLASSIFY_NBUF") ? atoi(getenv("HRF_CLASSIFY_NBUF")) : 2;
-    const size_t shm16 = std::max<size_t>((size_t)(nbuf == 2 ? 2 : 3) * RCH * rowb, sizeof(float) * 4 * 32 * C);
-#define HRF_LAY16N(LAY, NB)                                                                                    \
-  (void)hipFuncSetAttribute((const void *)classify_pixels_lay16_kernel<LAY, 4, NB>,                            \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm16);                           \
-  classify_pixels_lay16_kernel<LAY, 4, NB><<<(unsigned)hrf::cdiv(P, 256), 256, shm16, s>>>(                      \
-      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist)
-#define HRF_LAY16(LAY)   \
-  if (nbuf == 2) {       \
-    HRF_LAY16N(LAY, 2);  \
-  } else {               \
-    HRF_LAY16N(LAY, 3);  \
-  }
-    // round-3 kernel (classify_pixels_w16_kernel), the default for the E. coli layout in its
-    // measured-best configuration (4 waves, 2 buffers of 64 rows, three workgroups per CU:
-    // 1.76 vs 1.83 ms isolated for the lay16 kernel on a 2048^2 tile, R = 1023);
-    // HRF_CLASSIFY_W16 = "NW,NBUF,CR[,OCC]" picks another configuration, "0" the lay16 kernel
-    static const int w16env = [] {
-      const char *e = getenv("HRF_CLASSIFY_W16");
-      if (!e || !*e) return -1;
-      int a = 0, b = 0, c = 0, o = 2;
-      if (sscanf(e, "%d,%d,%d,%d", &a, &b, &c, &o) < 3) return 0;
-      return o * 100000 + a * 10000 + b * 1000 + c;
-    }();
-    const int w16cfg = w16env >= 0 ? w16env : (lay == 1 && m16_env < 0 ? 342064 : 0);
-    if (m16 && w16cfg) {
-      hrf_status st = HRF_EINVAL;
-      switch (w16cfg) {
-        case 242064: st = launch_w16<4, 2, 64, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        case 243064: st = launch_w16<4, 3, 64, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        case 242032: st = launch_w16<4, 2, 32, 2>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        case 342064: st = launch_w16<4, 2, 64, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        case 342032: st = launch_w16<4, 2, 32, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        case 343032: st = launch_w16<4, 3, 32, 3>(lay, stack, P, refx, R, rpad, best_idx, best_dist, s); break;
-        default: HRF_REQUIRE(false, "classify: HRF_CLASSIFY_W16 configuration not built");
-      }
-      if (st) return st;
-      HRF_LAUNCHED();
-      return HRF_OK;
-    }
-    if (m16) {
-      if (lay == 1) {
-        HRF_LAY16(LayEcoli);
-      } else {
-        HRF_LAY16(LayMulti);
-      }
-      HRF_LAUNCHED();
-      return HRF_OK;
-    }
-#undef HRF_LAY16N
-#undef HRF_LAY16
     if (lay == 1) {
-      if (nw == 8) {
-        HRF_LAY(LayEcoli, 8);
-      } else {
-        HRF_LAY(LayEcoli, 4);
-      }
-    } else {
-      if (nw == 8) {
-        HRF_LAY(LayMulti, 8);
-      } else {
-        HRF_LAY(LayMulti, 4);
-      }
+      // E. coli layout: the 16x16x32 sweep with the lane-per-pixel prologue
+      // (classify_pixels_w16_kernel) in its measured-best configuration -- 4 waves, 2 buffers of
+      // 64 rows, three workgroups per CU (1.76 vs 1.83 ms for round 2's lay16 form, 2.13-2.20 for
+      // the 32x32x16 form, on a 2048^2 tile at R = 1023; DESIGN.md "Per-pixel classifier")
+      if (hrf_status st = launch_w16_lay<LayEcoli, 4, 2, 64, 3>(stack, P, refx, R, rpad, best_idx, best_dist, s))
+        return st;
+      HRF_LAUNCHED();
+      return HRF_OK;
     }
-#undef HRF_LAY
+    // community layout (R = 127: a two-chunk sweep, where the 32x32x16 form's shorter prologue
+    // wins, 0.34 vs 0.44 ms): 4 waves per workgroup share the library chunks streamed through LDS
+    const size_t rowb = (size_t)table_rowb(2, lay, kp);
+    const size_t shm = std::max<size_t>((size_t)2 * RCH * rowb, sizeof(float) * 4 * 32 * C);
+    (void)hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayMulti, 4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    classify_pixels_lay_kernel<LayMulti, 4><<<(unsigned)hrf::cdiv(P, 256), 256, shm, s>>>(
+        stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist);
     HRF_LAUNCHED();
     return HRF_OK;
   }
@@ -2047,14 +1626,7 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
   auto go = [&](auto lay_tag) -> hrf_status {
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
-    size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
-    // HRF_CLASSIFY_MAXWG = m < 3: at most m workgroups per CU (as launch_w16_lay)
-    static const int maxwg = getenv("HRF_CLASSIFY_MAXWG") ? atoi(getenv("HRF_CLASSIFY_MAXWG")) : 0;
-    if (maxwg > 0 && maxwg < 3) shm = std::max<size_t>(shm, (size_t)(160 * 1024) / (size_t)maxwg - 4096);
-    // HRF_CLASSIFY_SHM = bytes: the LDS request raised to that (e.g. 56 KB: two workgroups per CU
-    // and 48 KB of LDS and a third of the VGPRs left for the chain kernels on the same CU)
-    static const long shm_env = getenv("HRF_CLASSIFY_SHM") ? atol(getenv("HRF_CLASSIFY_SHM")) : 0;
-    if (shm_env > 0) shm = std::max<size_t>(shm, (size_t)shm_env);
+    const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
     (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
@@ -2102,19 +1674,11 @@ hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nro
   HRF_REQUIRE(variant >= 0 && variant <= 2, "classify_cells: variant must be 0, 1 or 2");
   HRF_REQUIRE(variant == 0 || (fx && fr), "classify_cells: gated variants need presence flags");
   if (nmax == 0) return HRF_OK;
-  // HRF_CELLS_SHAPE=<cells per workgroup><threads> (A/B, e.g. 4256): smaller workgroups find a
-  // CU slot beside the concurrent classifier sooner
-  static const int shape = getenv("HRF_CELLS_SHAPE") ? atoi(getenv("HRF_CELLS_SHAPE")) : 0;
-#define HRF_CB(CB, NT)                                                                                 \
-  if (shape == CB * 10000 + NT || (shape == 0 && CB == CELLS_CB && NT == CELLS_NT)) {                   \
-    classify_cells_blk_kernel<CB, NT><<<(unsigned)hrf::cdiv(nmax, CB), NT, sizeof(double) * CB * C, s>>>( \
-        x, nmax, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nrows_dev);                           \
-    HRF_LAUNCHED();                                                                                    \
-    return HRF_OK;                                                                                     \
-  }
-  HRF_CB(4, 1024) HRF_CB(4, 256) HRF_CB(8, 256) HRF_CB(4, 512) HRF_CB(2, 256)
-#undef HRF_CB
-  HRF_REQUIRE(false, "classify_cells: unknown HRF_CELLS_SHAPE");
+  classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(nmax, CELLS_CB), CELLS_NT,
+                                                  sizeof(double) * CELLS_CB * C, s>>>(
+      x, nmax, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nrows_dev);
+  HRF_LAUNCHED();
+  return HRF_OK;
 }
 
 }  // namespace hrf
@@ -2147,17 +1711,10 @@ hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int
   double *refT = nullptr;
   HRF_HIP(hipMallocAsync((void **)&refT, sizeof(double) * (size_t)R * (C + bd.nseg), s));
   double *ny = refT + (size_t)R * C;
-  static const bool per_cell = getenv("HRF_CELLS_PERCELL") != nullptr;  // A/B: one workgroup per cell
-  if (per_cell) {
-    transpose_f64_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(ref, R, C, refT);
-    classify_cells_kernel<<<(unsigned)N, 256, sizeof(double) * C, s>>>(x, N, refT, R, C, bd, variant, fx, fr, arg,
-                                                                       dmin, nullptr);
-  } else {
-    cells_lib_prep_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(ref, R, C, bd, refT, ny);
-    classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(N, CELLS_CB), CELLS_NT,
-                                                    sizeof(double) * CELLS_CB * C, s>>>(
-        x, N, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nullptr);
-  }
+  cells_lib_prep_kernel<<<hrf::stream_grid((int64_t)R * C), 256, 0, s>>>(ref, R, C, bd, refT, ny);
+  classify_cells_blk_kernel<CELLS_CB, CELLS_NT><<<(unsigned)hrf::cdiv(N, CELLS_CB), CELLS_NT,
+                                                  sizeof(double) * CELLS_CB * C, s>>>(
+      x, N, refT, ny, R, C, bd, variant, fx, fr, arg, dmin, nullptr);
   HRF_LAUNCHED();
   HRF_HIP(hipFreeAsync(refT, s));
   return HRF_OK;

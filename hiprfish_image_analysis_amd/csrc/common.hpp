@@ -55,18 +55,10 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // concurrent classifier every dispatched block waits for a CU slot, so fewer, longer blocks win:
 // 1037-1050 vs 1027-1042 Mpix/s against 2048 (means of 3; 4 of 6 interleaved pairs; 256: 1032,
 // 1024: 1030).
-// HRF_STREAM_GRID_MAX overrides the cap (A/B).
-inline int64_t stream_grid_max() {
-  static const int64_t cap = [] {
-    const char *e = getenv("HRF_STREAM_GRID_MAX");
-    const long v = e ? atol(e) : 0;
-    return v > 0 ? (int64_t)v : (int64_t)512;
-  }();
-  return cap;
-}
+constexpr int64_t STREAM_GRID_MAX = 512;
 inline unsigned stream_grid(int64_t n, int block = 256) {
   int64_t g = cdiv(n, block);
-  if (g > stream_grid_max()) g = stream_grid_max();
+  if (g > STREAM_GRID_MAX) g = STREAM_GRID_MAX;
   if (g < 1) g = 1;
   return (unsigned)g;
 }
@@ -123,13 +115,6 @@ hrf_status classify_cells_devn(const double *x, int64_t nmax, const int32_t *nro
                                hipStream_t s);
 hrf_status barcode_counts_devn(const int32_t *bc, int64_t nmax, const int32_t *n_dev, int32_t R, int64_t *counts,
                                hipStream_t s, bool zeroed = false);
-// paint_ids_devn + barcode_counts_devn on counts the caller cleared, one launch (stats.hip)
-hrf_status paint_count_devn(const int32_t *labels, int64_t n, const int32_t *code, int32_t nmax,
-                            const int32_t *ncell_dev, int32_t add, int32_t *out, int32_t R, int64_t *counts,
-                            hipStream_t s);
-// hrf_region_props + hrf_shape_filter with the minor axis taken from the moments per pixel
-hrf_status shape_filter_mom(const int32_t *labels, int64_t H, int64_t W, const int64_t *mom, int32_t maxlab,
-                            double minor_lo, double minor_hi, int32_t *out, hipStream_t s);
 hrf_status paint_ids_devn(const int32_t *labels, int64_t n, const int32_t *code, int32_t nmax, const int32_t *ncell_dev,
                           int32_t add, int32_t *out, hipStream_t s);
 // One kernel that clears device buffers and copies device words into pinned host memory the
@@ -161,9 +146,9 @@ struct ZeroPub {
   }
 };
 hrf_status zero_publish(const ZeroPub &z, hipStream_t s);
-// hrf_label(mask, u8, conn) with the block counts scanned inside the counting launch (label.hip)
-int64_t label_ticketed_ws_words(int64_t n);
-hrf_status label_ticketed(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
+// hrf_label(mask, u8, conn) with the component count left in device memory (label.hip)
+int64_t label_dev_ws_words(int64_t n);
+hrf_status label_dev(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
                           int32_t *parent_ws, int32_t *blk_ws, int32_t *nlab_dev, hipStream_t s);
 // hrf_binary_erosion(border_value) followed by hrf_binary_dilation, fused (label.hip)
 hrf_status binary_opening(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,

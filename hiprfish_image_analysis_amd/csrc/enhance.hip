@@ -103,10 +103,11 @@ __global__ __launch_bounds__(256) void enhance2d_kernel(const double *__restrict
 constexpr int E3_TX = 4, E3_TY = 4, E3_TZ = 32;
 constexpr int E3_LX = E3_TX + 10, E3_LY = E3_TY + 10, E3_LZ = E3_TZ + 10;
 
-// One output voxel (b: its centre in the LDS tile).  FAST: the tile holds no NaN, no infinity and
-// no negative zero, so every `a < b ? a : b` of the reference's min/max and of the selection
-// network picks the same value as v_min_f64 / v_max_f64 -- one instruction instead of a compare,
-// two 64-bit selects and their hazard nops (values equal => same bits, no signed zeros).
+// One output voxel (b: its centre in the LDS tile).  FAST: the tile holds no NaN, no infinity, no
+// negative zero and no magnitude above 2^1023 (so no window's range overflows and every normalised
+// tap is a number in [0, 1]), so every `a < b ? a : b` of the reference's min/max and of the
+// selection network picks the same value as v_min_f64 / v_max_f64 -- one instruction instead of a
+// compare, two 64-bit selects and their hazard nops (values equal => same bits, no signed zeros).
 #ifndef E3_GROUP_N
 #define E3_GROUP_N 4
 #endif
@@ -180,14 +181,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ double tile[E3_LX * E3_LY * E3_LZ];
   const int tid = threadIdx.x;
   const int64_t x0 = (int64_t)blockIdx.z * E3_TX, y0 = (int64_t)blockIdx.y * E3_TY, z0 = (int64_t)blockIdx.x * E3_TZ;
-  int special = 0;  // a NaN, an infinity or a negative zero in the tile: the reference's compare-select path
+  // a NaN, an infinity, a negative zero -- or a magnitude above 2^1023, where a window's max - min
+  // could overflow to inf and (c - mn) / r give inf / inf = NaN, on which fmin / fmax and the
+  // reference's `a < b ? a : b` disagree -- sends the tile down the reference's compare-select path
+  int special = 0;
   for (int idx = tid; idx < E3_LX * E3_LY * E3_LZ; idx += 256) {
     const int lx = idx / (E3_LY * E3_LZ);
     const int rem = idx - lx * (E3_LY * E3_LZ);
     const int ly = rem / E3_LZ, lz = rem - ly * E3_LZ;
     const int64_t gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
     const double v = (gx < xp && gy < yp && gz < zp) ? pad[(gx * yp + gy) * zp + gz] : 0.0;
-    special |= !__builtin_isfinite(v) || (v == 0.0 && __builtin_signbit(v));
+    special |= !(__builtin_fabs(v) <= 0x1p1023) || (v == 0.0 && __builtin_signbit(v));
     tile[idx] = v;
   }
   const bool fast = !__syncthreads_or(special);
@@ -423,12 +427,8 @@ hrf_status hrf_enhance_3d(const double *pad, int64_t xp, int64_t yp, int64_t zp,
   dim3 grid((unsigned)hrf::cdiv(Z, E3_TZ), (unsigned)hrf::cdiv(Y, E3_TY), (unsigned)hrf::cdiv(X, E3_TX));
   HRF_REQUIRE(grid.y <= 65535 && grid.z <= 65535, "enhance_3d: volume too large");
   // built for two waves per SIMD (106 VGPRs of spills) rather than one: 12.2 vs 17.0 ms on the
-  // 1024x1024x64 volume (HRF_E3_WPE=1 for the one-wave build)
-  static const int wpe = getenv("HRF_E3_WPE") ? atoi(getenv("HRF_E3_WPE")) : 2;
-  if (wpe == 2)
-    enhance3d_kernel<0, 2><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
-  else
-    enhance3d_kernel<0><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
+  // 1024x1024x64 volume (round 4)
+  enhance3d_kernel<0, 2><<<grid, 256, 0, (hipStream_t)stream>>>(pad, xp, yp, zp, final_, X, Y, Z);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -196,7 +196,6 @@ struct KmState {
   U128 sumq2;
   double center[KMAX];
   int iters;
-  unsigned scan_ticket, scan_pad;  // scan_u32's last-block ticket (cleared by km_state_init_kernel)
   SkRun run[NRUN];
 };
 
@@ -406,35 +405,16 @@ __device__ __forceinline__ unsigned long long block_excl_scan_u64(unsigned long 
 constexpr int KSC_B = 4096;  // entries per scan block (256 threads x 16)
 
 __global__ __launch_bounds__(256) void km_scan_sum_kernel(const unsigned *__restrict__ a, long long n,
-                                                          unsigned *__restrict__ bsum, unsigned *__restrict__ ticket) {
+                                                          unsigned *__restrict__ bsum) {
   const long long i0 = (long long)blockIdx.x * KSC_B;
   unsigned long long s = 0;
   for (int e = threadIdx.x; e < KSC_B; e += 256)
     if (i0 + e < n) s += a[i0 + e];
   s = hrf::wave_sum(s);
   __shared__ unsigned long long sh[4];
-  __shared__ int last;
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    bsum[blockIdx.x] = (unsigned)(sh[0] + sh[1] + sh[2] + sh[3]);
-    __threadfence();
-    last = ticket && __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  // the last block in: every block sum is published -- km_scan_blocks_kernel's scan, here
-  __threadfence();
-  unsigned long long carry = 0;
-  for (int b0 = 0; b0 < (int)gridDim.x; b0 += 256) {
-    const int i = b0 + threadIdx.x;
-    unsigned long long tot;
-    const unsigned v = i < (int)gridDim.x ? __hip_atomic_load(bsum + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    const unsigned long long e = block_excl_scan_u64(v, sh, &tot);
-    if (i < (int)gridDim.x) bsum[i] = (unsigned)(carry + e);
-    carry += tot;
-  }
-  if (threadIdx.x == 0) *ticket = 0u;
+  if (threadIdx.x == 0) bsum[blockIdx.x] = (unsigned)(sh[0] + sh[1] + sh[2] + sh[3]);
 }
 
 __global__ __launch_bounds__(256) void km_scan_blocks_kernel(unsigned *__restrict__ bsum, int nb) {
@@ -1670,12 +1650,12 @@ __global__ void km_state_init_kernel(KmState *st) {
   if (threadIdx.x == 0) st->lo_bits = ~0ull;
 }
 
-// ticket: a zeroed counter (KmState::scan_ticket) -- the block sums are then scanned by the
-// summing launch's last block; nullptr: the separate scan kernel
-hrf_status scan_u32(unsigned *a, int64_t n, unsigned *bsum, hipStream_t s, unsigned *ticket) {
+// (a last-block scan behind an agent-scope ticket saved one launch per scan but wrote back and
+// invalidated the XCD's L2 in every block; it cost end to end and was removed in round 5)
+hrf_status scan_u32(unsigned *a, int64_t n, unsigned *bsum, hipStream_t s) {
   const int nb = (int)((n + KSC_B - 1) / KSC_B);
-  km_scan_sum_kernel<<<nb, 256, 0, s>>>(a, n, bsum, ticket);
-  if (!ticket) km_scan_blocks_kernel<<<1, 256, 0, s>>>(bsum, nb);
+  km_scan_sum_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
+  km_scan_blocks_kernel<<<1, 256, 0, s>>>(bsum, nb);
   km_scan_apply_kernel<<<nb, 256, 0, s>>>(a, n, bsum);
   HRF_LAUNCHED();
   return HRF_OK;
@@ -1691,26 +1671,20 @@ hrf_status km_sk_launch(const double *x, const uint8_t *valid, int64_t n, int ma
   if (!reuse) {
     // initial state written by a kernel: an asynchronous copy from a host stack object may run
     // after this frame is gone
-    // HRF_KM_TICKET=1: scan_u32's block sums scanned by the summing launch's last block (one
-    // launch less per scan; its 256 blocks each write back and invalidate their XCD's L2 at the
-    // ticket).  Off: alone within noise (1037 vs 1034, 1024 vs 1025 Mpix/s), but the launch-count
-    // fusions together cost 1.3 % (profiles/r4i_fusion_ab.txt)
-    static const bool km_ticket = getenv("HRF_KM_TICKET") && atoi(getenv("HRF_KM_TICKET")) != 0;
     km_state_init_kernel<<<1, 256, 0, s>>>(st);
     if (n > 0) km_minmax_kernel<<<std::min<unsigned>(g, 512), 256, 0, s>>>(x, valid, n, st);
-    static const bool scale_split = getenv("HRF_KM_SCALE_SPLIT") && atoi(getenv("HRF_KM_SCALE_SPLIT")) != 0;  // A/B
-    // n > 0: km_hist_a_kernel takes it
-    if (n == 0 || scale_split) km_scale_kernel<<<1, 1, 0, s>>>(st, n > 0 ? ws.geo : nullptr);
+    // n > 0: km_hist_a_kernel takes the scales and the bucket geometry
+    if (n == 0) km_scale_kernel<<<1, 1, 0, s>>>(st, nullptr);
     HRF_LAUNCHED();
     if (n > 0) {
       const unsigned nch = (unsigned)nblocks(n);
       const int L = nch_b(n) + 1;
-      km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, scale_split ? nullptr : st);
-      if (hrf_status r = scan_u32(ws.cntA, (int64_t)KD * nch, ws.sbsum, s, km_ticket ? &st->scan_ticket : nullptr)) return r;
+      km_hist_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, st);
+      if (hrf_status r = scan_u32(ws.cntA, (int64_t)KD * nch, ws.sbsum, s)) return r;
       km_scatter_a_kernel<<<nch, 256, 0, s>>>(x, valid, n, ws.geo, ws.cntA, (int)nch, ws.tmpx);
       km_segments_kernel<<<1, KD, 0, s>>>(ws.cntA, (int)nch, st, ws.seg, ws.cB);
       km_hist_b_kernel<<<L - 1, 256, 0, s>>>(ws.tmpx, ws.geo, ws.seg, ws.cB, ws.cntB, L);
-      if (hrf_status r = scan_u32(ws.cntB, (int64_t)KD * L, ws.sbsum, s, km_ticket ? &st->scan_ticket : nullptr)) return r;
+      if (hrf_status r = scan_u32(ws.cntB, (int64_t)KD * L, ws.sbsum, s)) return r;
       km_bucket_off_kernel<<<KD, KD, 0, s>>>(ws.cntB, L, ws.seg, ws.cB, ws.off);
       km_scatter_b_kernel<<<L - 1, 256, 0, s>>>(ws.tmpx, ws.geo, ws.seg, ws.cB, ws.cntB, L, ws.off, ws.xs);
       km_chunk_sum_kernel<<<nch, PT, 0, s>>>(ws.xs, st, ws.cq, ws.cq2);

@@ -151,10 +151,8 @@ __global__ __launch_bounds__(256) void cc_local_kernel(V val, int64_t H, int64_t
 // image instead of one thread per pixel that mostly exits at once.
 constexpr int CC_BORDER_PX = CC_T + 2 * (CC_T - 1);
 template <class V, int CONN>
-__global__ void cc_border_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent,
-                                 unsigned *__restrict__ ticket) {
+__global__ void cc_border_kernel(V val, int64_t H, int64_t W, int32_t *__restrict__ parent) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ticket && t == 0) *ticket = 0u;  // the numbering pass's last-block ticket (label_ticketed)
   const int64_t tiles_x = (W + CC_T - 1) / CC_T;
   const int64_t tile = t / CC_BORDER_PX;
   if (tile >= tiles_x * ((H + CC_T - 1) / CC_T)) return;
@@ -250,60 +248,6 @@ __global__ __launch_bounds__(1024) void scan_blocks_kernel(int32_t *__restrict__
     __syncthreads();
   }
   if (tid == 0) *total = carry;
-}
-
-// cc_count_roots_kernel + scan_blocks_kernel in one launch: every block publishes its root count;
-// the block that takes the last ticket (all counts are in) scans them and writes the total.  No
-// block ever waits for another (unlike a look-back), so it is safe beside concurrent kernels.
-// ticket: zero before the launch (cc_border_kernel clears it), reset to zero by the last block.
-__global__ __launch_bounds__(256) void cc_count_scan_kernel(const int32_t *__restrict__ parent, int64_t n,
-                                                            int32_t *__restrict__ blk, int32_t nb,
-                                                            unsigned *__restrict__ ticket,
-                                                            int32_t *__restrict__ total) {
-  __shared__ int32_t ws[2][4];
-  __shared__ int32_t wsum[4];
-  __shared__ int last;
-  const int tid = threadIdx.x;
-  // grid-stride over the NB-pixel chunks: a few hundred blocks, so a few hundred ticket
-  // acquire/releases (each an L2 write-back + invalidate on gfx950), not one per chunk
-  for (int64_t b = blockIdx.x, it = 0; b < nb; b += gridDim.x, ++it) {
-    int cnt = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t p = b * NB + k * 256 + tid;
-      cnt += (p < n && parent[p] == p);
-    }
-    cnt = hrf::wave_sum(cnt);
-    if ((tid & 63) == 0) ws[it & 1][tid >> 6] = cnt;
-    __syncthreads();
-    if (tid == 0) blk[b] = ws[it & 1][0] + ws[it & 1][1] + ws[it & 1][2] + ws[it & 1][3];
-  }
-  if (tid == 0) {
-    __threadfence();
-    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  // exclusive scan of blk[0, nb) in place: thread t owns a contiguous segment
-  const int per = (nb + 255) / 256;
-  const int b0 = tid * per, b1 = min(nb, b0 + per);
-  int32_t sum = 0;
-  for (int i = b0; i < b1; ++i) sum += __hip_atomic_load(blk + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int32_t inc = hrf::wave_inclusive_scan(sum);
-  if ((tid & 63) == 63) wsum[tid >> 6] = inc;
-  __syncthreads();
-  int32_t off = inc - sum;
-  for (int q = 0; q < (tid >> 6); ++q) off += wsum[q];
-  for (int i = b0; i < b1; ++i) {
-    const int32_t v = blk[i];
-    blk[i] = off;
-    off += v;
-  }
-  if (tid == 255) {
-    *total = off;
-    *ticket = 0u;
-  }
 }
 
 // labels[root] = 1 + rank(root); background 0.  Non-roots filled by cc_fill_kernel.
@@ -559,15 +503,15 @@ __global__ void max_i32_kernel(const int32_t *__restrict__ a, int64_t n, int32_t
 // the compression pass itself (cleared by the tile pass)
 template <class V>
 hrf_status run_cc(V val, int64_t H, int64_t W, int conn, int32_t *parent, hipStream_t s, int32_t *zero = nullptr,
-                  int32_t *sizes = nullptr, unsigned *ticket = nullptr) {
+                  int32_t *sizes = nullptr) {
   dim3 g((unsigned)hrf::cdiv(W, CC_T), (unsigned)hrf::cdiv(H, CC_T));
   const unsigned gb = (unsigned)hrf::cdiv(hrf::cdiv(W, CC_T) * hrf::cdiv(H, CC_T) * CC_BORDER_PX, 256);
   if (conn == 2) {
     cc_local_kernel<V, 2><<<g, 256, 0, s>>>(val, H, W, parent, sizes);
-    cc_border_kernel<V, 2><<<gb, 256, 0, s>>>(val, H, W, parent, ticket);
+    cc_border_kernel<V, 2><<<gb, 256, 0, s>>>(val, H, W, parent);
   } else {
     cc_local_kernel<V, 1><<<g, 256, 0, s>>>(val, H, W, parent, sizes);
-    cc_border_kernel<V, 1><<<gb, 256, 0, s>>>(val, H, W, parent, ticket);
+    cc_border_kernel<V, 1><<<gb, 256, 0, s>>>(val, H, W, parent);
   }
   if (sizes)
     cc_compress_sizes_kernel<<<(unsigned)std::min<int64_t>(hrf::cdiv(H * W, RUN_PX * 4), 4096), 256, 0, s>>>(
@@ -761,41 +705,29 @@ hrf_status hrf_binary_erosion(const uint8_t *mask, int64_t H, int64_t W, int32_t
 
 }  // extern "C"
 
-// hrf_binary_erosion(mask, border_value) then hrf_binary_dilation, one launch
-// hrf_label(mask, u8) with the block counts scanned by the counting pass's last block (one
-// launch less).  blk_ws: label_ticketed_ws_words(n) int32 (the ticket after the block counts)
-int64_t hrf::label_ticketed_ws_words(int64_t n) { return hrf::cdiv(n, NB) + 4; }
+// hrf_label(mask, u8) with the component count left in device memory (nlab_dev) for a later
+// read-back.  blk_ws: label_dev_ws_words(n) int32.  (Round 4 also built a last-block scan behind
+// an agent-scope ticket here -- one launch less, an L2 write-back + invalidate per block; it lost
+// end to end and was removed in round 5, profiles/r4h_ticket_ab.txt, r4i_fusion_ab.txt.)
+int64_t hrf::label_dev_ws_words(int64_t n) { return hrf::cdiv(n, NB) + 4; }
 
-hrf_status hrf::label_ticketed(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
-                               int32_t *parent_ws, int32_t *blk_ws, int32_t *nlab_dev, hipStream_t s) {
+hrf_status hrf::label_dev(const uint8_t *mask, int64_t H, int64_t W, int32_t conn, int32_t *labels,
+                          int32_t *parent_ws, int32_t *blk_ws, int32_t *nlab_dev, hipStream_t s) {
   if (hrf_status st = check_hw(H, W, "label")) return st;
   HRF_REQUIRE(conn == 1 || conn == 2, "label: connectivity must be 1 or 2");
   const int64_t n = H * W;
   HRF_REQUIRE(n > 0 && mask && labels && parent_ws && blk_ws && nlab_dev, "label: bad arguments");
   const int64_t nb = hrf::cdiv(n, NB);
-  // HRF_CC_TICKET=1: the counting pass's last block scans (one launch less).  The ticket's
-  // agent-scope acquire/release compiles to an L2 writeback + invalidate (buffer_wbl2 sc1 /
-  // buffer_inv sc1) per block: with one block per 1024-pixel chunk (4096 per 2048^2 tile) that
-  // flushed the XCD's L2 under the concurrent classifier, 905 vs 1034 Mpix/s
-  // (profiles/r4h_ticket_ab.txt); the counting pass now strides over the chunks with <= 256
-  // blocks: 1023 vs 1027 Mpix/s without the ticket, within the runs' spread (1011-1037), but
-  // off by default with the other launch-count fusions (profiles/r4i_fusion_ab.txt)
-  static const bool use_ticket = getenv("HRF_CC_TICKET") && atoi(getenv("HRF_CC_TICKET")) != 0;
-  unsigned *ticket = use_ticket ? (unsigned *)(blk_ws + nb + 1) : nullptr;
-  if (hrf_status st = run_cc(MaskV{mask, false}, H, W, conn, parent_ws, s, nullptr, nullptr, ticket)) return st;
-  if (use_ticket) {
-    cc_count_scan_kernel<<<(unsigned)std::min<int64_t>(nb, 256), 256, 0, s>>>(parent_ws, n, blk_ws, (int32_t)nb, ticket,
-                                                                            nlab_dev);
-  } else {
-    cc_count_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, blk_ws);
-    scan_blocks_kernel<<<1, 1024, 0, s>>>(blk_ws, nb, nlab_dev);
-  }
+  if (hrf_status st = run_cc(MaskV{mask, false}, H, W, conn, parent_ws, s)) return st;
+  cc_count_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, blk_ws);
+  scan_blocks_kernel<<<1, 1024, 0, s>>>(blk_ws, nb, nlab_dev);
   cc_rank_roots_kernel<<<(unsigned)nb, 256, 0, s>>>(parent_ws, n, blk_ws, labels);
   cc_fill_kernel<<<hrf::stream_grid(n), 256, 0, s>>>(parent_ws, n, labels);
   HRF_LAUNCHED();
   return HRF_OK;
 }
 
+// hrf_binary_erosion(mask, border_value) then hrf_binary_dilation, one launch
 hrf_status hrf::binary_opening(const uint8_t *mask, int64_t H, int64_t W, int32_t border_value, uint8_t *out,
                                hipStream_t s) {
   if (H * W == 0) return HRF_OK;

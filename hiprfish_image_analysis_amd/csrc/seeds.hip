@@ -653,13 +653,9 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   // 0: run-length kernel (32 KB LDS), 1: pixel kernel (160 KB LDS), 2: whole-image loop.
   // Components the run kernel cannot hold (run arrays over capacity) are listed with the
   // class-1 ones and redone by the pixel kernel, so every box it receives fits SEED_LDS_PX_MAX.
-  static const int use_runs = [] {
-    const char *e = getenv("HRF_SEEDS_RUNS");
-    return e ? atoi(e) : 1;
-  }();
   // ovf_dev given: large boxes may go to the run kernel; ovf_dev receives the number of those
   // that overflowed it (then the caller redoes the stage with ovf_dev == nullptr)
-  const int mode = (use_runs ? 1 : 0) | (ovf_dev ? SEED_BIG_RUNS : 0);
+  const int mode = 1 | (ovf_dev ? SEED_BIG_RUNS : 0);
   int64_t br0 = H, bc0 = W, br1 = -1, bc1 = -1;
   for (int c = 1; c <= ncomp; ++c) {
     if (seed_class(hb, c, mode) != 2) continue;
@@ -684,23 +680,13 @@ hrf_status hrf::erosion_seeds_hostbox(const int32_t *labels, int64_t H, int64_t 
   HRF_REQUIRE(zp.zero(dcount, 2 * sizeof(int32_t)) && zp.zero(ovf_dev, sizeof(int32_t)),
               "erosion_seeds: clear list");
   if ((H * W) % 4 == 0) {
-    zp.zero(be_out, H * W);
+    HRF_REQUIRE(zp.zero(be_out, H * W), "erosion_seeds: clear seeds");
   } else {
     HRF_HIP(hipMemsetAsync(be_out, 0, (size_t)(H * W), s));
   }
   if (hrf_status r_ = zero_publish(zp, s)) return r_;
   erosion_seed_runs_kernel<<<(unsigned)ncomp, RS_T, RS_LDS, s>>>(labels, H, W, box, mode, area_max, min_obj, dlist,
                                                                  dcount, be_out, ovf_dev);
-  static const bool dbg = getenv("HRF_SEEDS_DEBUG") != nullptr;
-  if (dbg) {  // diagnostics: how many components the pixel kernel receives (synchronises)
-    int32_t hc[2] = {0, 0};
-    HRF_HIP(hipMemcpyAsync(hc, dcount, sizeof(hc), hipMemcpyDeviceToHost, s));
-    HRF_HIP(hipStreamSynchronize(s));
-    int n1 = 0;
-    for (int c = 1; c <= ncomp; ++c) n1 += seed_class(hb, c, mode) == 1;
-    fprintf(stderr, "hrf_erosion_seeds: %d components, %d class 1, %d to the pixel kernel, %d large-box overflows\n",
-            ncomp, n1, hc[0], hc[1]);
-  }
   erosion_seed_kernel<<<(unsigned)npx_wg, 256, 0, s>>>(labels, H, W, box, dlist, dcount, area_max, min_obj,
                                                         px_scratch, be_out);
   HRF_LAUNCHED();

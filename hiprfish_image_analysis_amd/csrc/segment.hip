@@ -138,7 +138,7 @@ hrf_status hrf_seg_ctx_create(int64_t H, int64_t W, hrf_seg_ctx **out) {
     if ((r = dalloc(&p, n))) return fail(r);
   for (auto &p : c->l)
     if ((r = dalloc(&p, n))) return fail(r);
-  if ((r = dalloc(&c->parent, n)) || (r = dalloc(&c->size, n)) || (r = dalloc(&c->blk, (size_t)::hrf::label_ticketed_ws_words(c->n))) ||
+  if ((r = dalloc(&c->parent, n)) || (r = dalloc(&c->size, n)) || (r = dalloc(&c->blk, (size_t)::hrf::label_dev_ws_words(c->n))) ||
       (r = dalloc(&c->dint, 16)) || (r = dalloc(&c->ws_flag, 8)))
     return fail(r);
   if ((r = dalloc((char **)&c->ws_state, (size_t)hrf_watershed_workspace_bytes(H, W)))) return fail(r);
@@ -203,15 +203,15 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   // :97-110.  Components, their count and their boxes come back in ONE synchronisation: the
   // boxes are computed for every label the current capacity holds (labels above it are
   // ignored by the box kernel) and redone in the rare case the count exceeds it.
-  HRF_TRY(::hrf::label_ticketed(a, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
+  HRF_TRY(::hrf::label_dev(a, H, W, 2, lab1, c->parent, c->blk, c->dint, s));
   HRF_TRY(ensure_labels(c, 1, s));
   int32_t guess = (int32_t)(c->lab_cap - 1);
   HRF_TRY(hrf_label_boxes(lab1, H, W, guess, c->box, s));
   {
     ::hrf::ZeroPub zp;
-    zp.pub(c->dint, c->hpin_dev + 1, 1);
-    zp.pub(km_err, c->hpin_dev + 3, 1);
-    zp.pub(c->box, c->hbox_dev, 4 * (guess + 1));
+    HRF_REQUIRE(zp.pub(c->dint, c->hpin_dev + 1, 1) && zp.pub(km_err, c->hpin_dev + 3, 1) &&
+                    zp.pub(c->box, c->hbox_dev, 4 * (guess + 1)),
+                "segment_ecoli: too many read-backs");
     HRF_TRY(::hrf::zero_publish(zp, s));
   }
   HRF_HIP(hipStreamSynchronize(s));
@@ -222,7 +222,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
     HRF_TRY(ensure_labels(c, ncomp, s));
     HRF_TRY(hrf_label_boxes(lab1, H, W, ncomp, c->box, s));
     ::hrf::ZeroPub zp;
-    zp.pub(c->box, c->hbox_dev, 4 * (ncomp + 1));
+    HRF_REQUIRE(zp.pub(c->box, c->hbox_dev, 4 * (ncomp + 1)), "segment_ecoli: too many read-backs");
     HRF_TRY(::hrf::zero_publish(zp, s));
     HRF_HIP(hipStreamSynchronize(s));
   }
@@ -233,7 +233,7 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
     HRF_TRY(::hrf::erosion_seeds_hostbox(lab1, H, W, ncomp, c->box, c->hbox, 600, 10, b, s,
                                          attempt == 0 ? c->dint + 8 : nullptr, c->seed_px));
     HRF_TRY(hrf_remove_small_objects_mask(b, H, W, 10, 2, d, c->parent, c->size, s));  // :111
-    HRF_TRY(::hrf::label_ticketed(d, H, W, 2, seeds, c->parent, c->blk, c->dint, s));  // :111-112
+    HRF_TRY(::hrf::label_dev(d, H, W, 2, seeds, c->parent, c->blk, c->dint, s));  // :111-112
     // read back at the watershed's synchronisation: the seed count, the run kernel's overflow
     // count; cleared there: the per-label counts and moments (capacity-wide) and `extra`
     ::hrf::ZeroPub zp = extra ? *extra : ::hrf::ZeroPub();
@@ -250,16 +250,10 @@ static hrf_status segment_ecoli_from_cn(hrf_seg_ctx *c, const double *cn, int32_
   HRF_TRY(::hrf::remove_small_objects_labels_zeroed(ws, n, nseeds, 100, lab1, c->cnt, s));    // :114
   HRF_TRY(hrf_clear_border(lab1, H, W, lab3, c->parent, c->size, s));          // :115
   HRF_TRY(::hrf::region_moments_zeroed(lab3, H, W, nseeds, c->mom, s));         // :116
-  // the props pass + shape filter (default) or the filter straight from the moments
-  // (HRF_SF_PROPS=0: one launch less, but every labelled pixel recomputes its label's
-  // eigenvalues: 1013 vs 1017 Mpix/s, profiles/r4i_fusion_ab.txt)
-  static const bool sf_props = !getenv("HRF_SF_PROPS") || atoi(getenv("HRF_SF_PROPS")) != 0;
-  if (sf_props) {
-    HRF_TRY(hrf_region_props(c->mom, nseeds, c->props, s));
-    HRF_TRY(hrf_shape_filter(lab3, H, W, c->props, nseeds, 15.0, 35.0, seg_out, s));
-  } else {
-    HRF_TRY(::hrf::shape_filter_mom(lab3, H, W, c->mom, nseeds, 15.0, 35.0, seg_out, s));   // :117-126
-  }
+  // the props pass + shape filter (:116-126; the filter straight from the moments -- one launch
+  // less, every labelled pixel recomputing its label's eigenvalues -- lost, removed in round 5)
+  HRF_TRY(hrf_region_props(c->mom, nseeds, c->props, s));
+  HRF_TRY(hrf_shape_filter(lab3, H, W, c->props, nseeds, 15.0, 35.0, seg_out, s));
   *maxlab_host = nseeds;
   return HRF_OK;
 }

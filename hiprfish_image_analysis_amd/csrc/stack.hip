@@ -222,9 +222,9 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 // Strips t = blockIdx.x, + gridDim.x, ... (row t / nsx, columns (t % nsx) * 64 ..): launched on a
 // resident grid (round 3), a 2048^2 tile is ~1.5 k workgroup dispatches instead of 65 k -- under
 // the concurrent classifier every dispatch waits for a CU slot.  Per strip unchanged.
-// PF: the next strip's loads are issued right after this strip is staged in LDS and stay in flight
-// through its image_cn and pixel-table phases (barriers there order LDS only, lds_barrier).
-template <bool PF, int WPE = 2>
+// (Round 3 also built a prefetching form -- the next strip's loads in flight through this strip's
+// image_cn and pixel-table phases -- equal end to end; removed in round 5.)
+template <int WPE = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
@@ -240,7 +240,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
   constexpr int UT = 8 + 6 + 5 + 4 + 2;
   float v[UT];
-  if (PF && (int64_t)blockIdx.x < nstrip) lay_load<0, 5>(L, sdr, sdc, blockIdx.x / nsx, (blockIdx.x % nsx) * AS_P, H, W, tid, v);
   for (int64_t t = blockIdx.x; t < nstrip; t += gridDim.x) {
   const int64_t r = t / nsx;
   const int64_t c0 = (t - r * nsx) * AS_P;
@@ -252,9 +251,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     okp[tid] = (uint8_t)ok;
     fl[tid] = 0;
   }
-  if (PF) {
-    lay_store<0, 5>(tile, tid, v);
-  } else if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
+  if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
     lay_load<0, 2>(L, sdr, sdc, r, c0, H, W, tid, v);
     lay_store<0, 2>(tile, tid, v);
     lay_load<2, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
@@ -263,13 +260,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
     lay_store<0, 5>(tile, tid, v);
   }
-  if (PF) {
-    hrf_pix::lds_barrier();
-    const int64_t tn = t + gridDim.x;  // the next strip's loads: in flight until its lay_store
-    if (tn < nstrip) lay_load<0, 5>(L, sdr, sdc, tn / nsx, (tn % nsx) * AS_P, H, W, tid, v);
-  } else {
-    __syncthreads();
-  }
+  __syncthreads();
   float *out = dst ? dst + (r * W + c0) * (int64_t)C : nullptr;
   const int n = dst ? np * C : 0;
   if (!dst) {
@@ -320,47 +311,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
   }
   if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
-    if (PF) hrf_pix::lds_barrier();
-    else __syncthreads();
-    hrf_pix::prep_tile_ecoli<PF>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl,
+    __syncthreads();
+    hrf_pix::prep_tile_ecoli<false>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl,
                                  cn_out ? cns : nullptr, cn_mode, cn_out);
   }
-  if (PF) hrf_pix::lds_barrier();  // the next strip rewrites tile, okp and fl
-  else __syncthreads();
+  __syncthreads();  // the next strip rewrites tile, okp and fl
   }
 }
 
-// E. coli assembly launch: a resident grid (HRF_ASSEMBLE_STRIPGRID=1: one workgroup per strip)
-// of the kernel built for three workgroups per CU (165 VGPRs, no spills).  Interleaved on one box:
-// 1035 vs 991 Mpix/s end to end against the 2-per-CU build (197 VGPRs), isolated 1.03 vs 1.38 ms;
-// with the next strip prefetched (HRF_ASSEMBLE_PF=1) 1035 either way; 4 per CU
-// (HRF_ASSEMBLE_WPE=4) spills and loses (985).
-template <bool PF, int WPE>
+// E. coli assembly launch: a resident grid of the kernel built for three workgroups per CU with
+// the pixel table (165 VGPRs, no spills; 1035 vs 991 Mpix/s end to end against the 2-per-CU build,
+// isolated 1.03 vs 1.38 ms; 4 per CU spills and loses, 985) and for four without it (the
+// stack-writing form: 0.650 vs 0.687 ms).  One workgroup per strip instead of the resident grid
+// lost in round 3 (the switch was removed in round 5).
+template <int WPE>
 void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                        uint4 *table, uint8_t *flags, hipStream_t s) {
   const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
-  static const bool per_strip = getenv("HRF_ASSEMBLE_STRIPGRID") != nullptr;
-  const unsigned grid =
-      per_strip ? (unsigned)nstrip : hrf::resident_grid(assemble_ecoli_kernel<PF, WPE>, 256, 0, nstrip);
-  assemble_ecoli_kernel<PF, WPE><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
+  const unsigned grid = hrf::resident_grid(assemble_ecoli_kernel<WPE>, 256, 0, nstrip);
+  assemble_ecoli_kernel<WPE><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
 }
 
 void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                      uint4 *table, uint8_t *flags, hipStream_t s) {
-  // the stack-writing form (no table) runs the 4-per-CU build: 0.650 vs 0.687 ms (2 per CU, prefetch)
-  static const char *epf = getenv("HRF_ASSEMBLE_PF"), *ewpe = getenv("HRF_ASSEMBLE_WPE");
-  const bool pf = epf && atoi(epf) == 1;
-  const int wpe = ewpe ? atoi(ewpe) : (table == nullptr ? 4 : 3);
-  if (wpe == 4) {
-    if (pf) launch_assemble_t<true, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-    else launch_assemble_t<false, 4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-  } else if (wpe == 3) {
-    if (pf) launch_assemble_t<true, 3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-    else launch_assemble_t<false, 3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-  } else {
-    if (pf) launch_assemble_t<true, 2>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-    else launch_assemble_t<false, 2>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-  }
+  if (table == nullptr) launch_assemble_t<4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  else launch_assemble_t<3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
 }
 
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
@@ -771,8 +746,7 @@ __global__ void calibrate_kernel(const float *__restrict__ stack, int64_t npix, 
 // foreground pixel's value is its laser's source pixel shifted by (dr_q, dc_q), 0 outside the
 // laser's frame or -- apply_mask -- outside any laser's frame (register_assemble's stack, which
 // then never has to exist).  CAL: a per-pixel flat field on channels [cal0, cal1).
-// DIV (HRF_LSL_DIV=1, timing A/B only): the per-channel f64 division instead of the reciprocal
-template <bool CAL, bool DIV = false>
+template <bool CAL>
 __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                                 const int32_t *__restrict__ lab, int32_t maxlab,
                                                                 const float *__restrict__ cal, int cal0, int cal1,
@@ -877,7 +851,7 @@ __global__ __launch_bounds__(256) void label_sums_lasers_kernel(Lasers L, int64_
             const double r = __builtin_bit_cast(
                 double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(rb >> 32), idx[j]) << 32) |
                             (unsigned)__builtin_amdgcn_readlane((int)(unsigned)rb, idx[j]));
-            if (!DIV && df != 0.0f && __builtin_isfinite(df)) {
+            if (df != 0.0f && __builtin_isfinite(df)) {
               a0 += k0 ? hrf_div_rcp((double)x0[j], d, r) : (double)x0[j];
               a1 += k1 ? hrf_div_rcp((double)x1[j], d, r) : (double)x1[j];
             } else {
@@ -1074,7 +1048,7 @@ static hrf_status register_assemble(const float *const *src_host, const int32_t 
     dim3 grid((unsigned)hrf::cdiv(W, AS_P), (unsigned)H);
     bool ecoli = nlaser == 5 && W % 4 == 0 && (((uintptr_t)dst & 15) == 0);
     for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
-    if (ecoli && !getenv("HRF_ASSEMBLE_GENERIC")) {
+    if (ecoli) {
       launch_assemble(L, H, W, apply_mask, dst, cn_out, cn_mode, nullptr, nullptr, (hipStream_t)stream);
       HRF_LAUNCHED();
       return HRF_OK;
@@ -1181,9 +1155,7 @@ hrf_status hrf::label_sums_lasers_zeroed(const float *const *src_host, const int
   if (H * W == 0) return HRF_OK;
   HRF_REQUIRE(labels, "label_sums_lasers: null labels");
   const int64_t nblk = hrf::cdiv(hrf::cdiv(H * W, 64), 4);
-  // HRF_LSL_ROW=0: the general kernel on every width (A/B)
-  static const bool row_ok = !getenv("HRF_LSL_ROW") || atoi(getenv("HRF_LSL_ROW")) != 0;
-  if (row_ok && W % 64 == 0) {
+  if (W % 64 == 0) {
     if (cal) {
       const unsigned grid = hrf::resident_grid(label_sums_lasers_row_kernel<true>, 256, 0, nblk);
       label_sums_lasers_row_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0,
@@ -1197,14 +1169,9 @@ hrf_status hrf::label_sums_lasers_zeroed(const float *const *src_host, const int
     return HRF_OK;
   }
   if (cal) {
-    static const bool div = getenv("HRF_LSL_DIV") != nullptr;
     const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<true>, 256, 0, nblk);
-    if (div)
-      label_sums_lasers_kernel<true, true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0,
-                                                                cal_c1, sums, (unsigned long long *)counts);
-    else
-      label_sums_lasers_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0, cal_c1,
-                                                         sums, (unsigned long long *)counts);
+    label_sums_lasers_kernel<true><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, cal, cal_c0, cal_c1, sums,
+                                                       (unsigned long long *)counts);
   } else {
     const unsigned grid = hrf::resident_grid(label_sums_lasers_kernel<false>, 256, 0, nblk);
     label_sums_lasers_kernel<false><<<grid, 256, 0, s>>>(L, H, W, apply_mask, labels, maxlab, nullptr, 0, 0, sums,

@@ -393,33 +393,12 @@ __global__ void paint_kernel(const int32_t *__restrict__ lab, int64_t n, const i
   }
 }
 
-// paint_kernel and barcode_counts_kernel in one launch (the native tile's last two steps)
-__global__ void paint_count_kernel(const int32_t *__restrict__ lab, int64_t n, const int32_t *__restrict__ code,
-                                   int32_t ncell, int32_t *__restrict__ out, const int32_t *__restrict__ ncell_dev,
-                                   int32_t add, int32_t R, unsigned long long *__restrict__ counts) {
-  if (ncell_dev) ncell = min(ncell, *ncell_dev);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x, i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t i = i0; i < n; i += stride) {
-    const int32_t l = lab[i];
-    out[i] = (l >= 1 && l <= ncell) ? code[l - 1] + add : 0;
-  }
-  const int64_t n_up = ((int64_t)ncell + 63) / 64 * 64;
-  for (int64_t i = i0; i < n_up; i += stride) {
-    const int32_t b = i < ncell ? code[i] : -1;
-    const bool ok = b >= 0 && b < R;
-    hrf::agg_atomic_add<unsigned long long>(counts, ok ? b : 0, 1ull, ok);
-  }
-}
-
 // ecoli measurement.py:116-126: keep a cell iff !(minor < lo || minor > hi) and paint only its
 // interior after two cross erosions of its own mask (border_value True) == every in-image
 // pixel within L1 distance 2 carries the same label.
-// MOM: the minor axis straight from the moments (props_kernel's s[4] by the same operations,
-// label_eigvals), so the native chain needs no props pass
-template <bool MOM>
 __global__ void shape_filter_kernel(const int32_t *__restrict__ lab, int64_t H, int64_t W,
-                                    const double *__restrict__ props, const unsigned long long *__restrict__ mom,
-                                    int32_t maxlab, double lo, double hi, int32_t *__restrict__ out) {
+                                    const double *__restrict__ props, int32_t maxlab, double lo, double hi,
+                                    int32_t *__restrict__ out) {
   const int64_t n = H * W;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
     const int32_t l = lab[p];
@@ -427,18 +406,8 @@ __global__ void shape_filter_kernel(const int32_t *__restrict__ lab, int64_t H, 
     bool valid = false;
     double mn = 0.0;
     if (l > 0 && l <= maxlab) {
-      if (MOM) {
-        const int64_t A = (int64_t)mom[(int64_t)l * 6];
-        if (A != 0) {
-          double ta, tb, tc, l1, l2;
-          label_eigvals(mom, l, A, ta, tb, tc, l1, l2);
-          mn = 4.0 * sqrt(l2);
-          valid = true;
-        }
-      } else {
-        valid = props[(int64_t)l * 8 + 7] != 0.0;
-        mn = props[(int64_t)l * 8 + 4];
-      }
+      valid = props[(int64_t)l * 8 + 7] != 0.0;
+      mn = props[(int64_t)l * 8 + 4];
     }
     if (valid) {
       if (!(mn < lo || mn > hi)) {
@@ -481,8 +450,7 @@ hrf_status hrf_label_sums_cal(const float *stack, const int32_t *labels, int64_t
   HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * ((size_t)maxlab + 1), s));
   if (npix == 0) return HRF_OK;
   HRF_REQUIRE(stack && labels, "label_sums: null input");
-  static const bool lds_variant = getenv("HRF_LS_LDS") != nullptr;  // A/B switch
-  if (C <= 128 && !lds_variant) {
+  if (C <= 128) {
     const int64_t nchunks = hrf::cdiv(npix, 64);
     const int mode = cal == nullptr ? 0 : (cal_sc == 0 ? 1 : 2);
     const int64_t nblk = hrf::cdiv(nchunks, 4);
@@ -555,8 +523,8 @@ hrf_status hrf_shape_filter(const int32_t *labels, int64_t H, int64_t W, const d
                             double minor_lo, double minor_hi, int32_t *out, hrf_stream_t stream) {
   if (H * W == 0) return HRF_OK;
   HRF_REQUIRE(labels && props && out && labels != out && maxlab >= 0, "shape_filter: bad arguments");
-  shape_filter_kernel<false><<<hrf::stream_grid(H * W), 256, 0, (hipStream_t)stream>>>(
-      labels, H, W, props, nullptr, maxlab, minor_lo, minor_hi, out);
+  shape_filter_kernel<<<hrf::stream_grid(H * W), 256, 0, (hipStream_t)stream>>>(labels, H, W, props, maxlab,
+                                                                                  minor_lo, minor_hi, out);
   HRF_LAUNCHED();
   return HRF_OK;
 }
@@ -592,27 +560,6 @@ hrf_status barcode_counts_devn(const int32_t *bc, int64_t nmax, const int32_t *n
   if (!zeroed) HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * R, s));
   if (nmax == 0) return HRF_OK;
   barcode_counts_kernel<<<hrf::stream_grid(nmax), 256, 0, s>>>(bc, nmax, R, (unsigned long long *)counts, n_dev);
-  HRF_LAUNCHED();
-  return HRF_OK;
-}
-
-hrf_status shape_filter_mom(const int32_t *labels, int64_t H, int64_t W, const int64_t *mom, int32_t maxlab,
-                            double minor_lo, double minor_hi, int32_t *out, hipStream_t s) {
-  if (H * W == 0) return HRF_OK;
-  HRF_REQUIRE(labels && mom && out && labels != out && maxlab >= 0, "shape_filter: bad arguments");
-  shape_filter_kernel<true><<<hrf::stream_grid(H * W), 256, 0, s>>>(
-      labels, H, W, nullptr, (const unsigned long long *)mom, maxlab, minor_lo, minor_hi, out);
-  HRF_LAUNCHED();
-  return HRF_OK;
-}
-
-hrf_status paint_count_devn(const int32_t *labels, int64_t n, const int32_t *code, int32_t nmax,
-                            const int32_t *ncell_dev, int32_t add, int32_t *out, int32_t R, int64_t *counts,
-                            hipStream_t s) {
-  HRF_REQUIRE(R >= 1 && counts, "barcode_counts: bad arguments");
-  if (n == 0 && nmax == 0) return HRF_OK;
-  paint_count_kernel<<<hrf::stream_grid(n > nmax ? n : nmax), 256, 0, s>>>(labels, n, code, nmax, out, ncell_dev, add,
-                                                                            R, (unsigned long long *)counts);
   HRF_LAUNCHED();
   return HRF_OK;
 }

@@ -111,17 +111,10 @@ hrf_status tile_cells(hrf_tile_ctx *t, const int32_t *seg, const double *lib, co
   HRF_TRY(hrf::cells_lib_prep(lib, R, C, BOUNDS, NL, t->refT, ny, s));
   HRF_TRY(hrf::classify_cells_devn(avgint_norm, maxlab, ncells_dev, t->refT, ny, R, C, BOUNDS, NL, variant,
                                    variant ? t->fx : nullptr, variant ? lib_flags : nullptr, cell_idx, cell_dist, s));
-  // counts and paint as two launches (default) or one (HRF_PAINT_SPLIT=0: 1013 vs 1019 Mpix/s,
-  // profiles/r4i_fusion_ab.txt)
-  static const bool split = !getenv("HRF_PAINT_SPLIT") || atoi(getenv("HRF_PAINT_SPLIT")) != 0;
-  if (split) {
-    HRF_TRY(hrf::barcode_counts_devn(cell_idx, maxlab, ncells_dev, R, counts, s, counts_zeroed));
-    HRF_TRY(hrf::paint_ids_devn(seg, t->H * t->W, cell_idx, maxlab, ncells_dev, 1, ident, s));
-    return HRF_OK;
-  }
-  if (!counts_zeroed) HRF_HIP(hipMemsetAsync(counts, 0, sizeof(int64_t) * (size_t)R, s));
-  // identification map (:65-71) and per-barcode counts (collect :92-98), one launch
-  HRF_TRY(hrf::paint_count_devn(seg, t->H * t->W, cell_idx, maxlab, ncells_dev, 1, ident, R, counts, s));
+  // per-barcode counts (collect :92-98) and the identification map (:65-71); one fused launch
+  // lost (1013 vs 1019 Mpix/s, profiles/r4i_fusion_ab.txt) and was removed in round 5
+  HRF_TRY(hrf::barcode_counts_devn(cell_idx, maxlab, ncells_dev, R, counts, s, counts_zeroed));
+  HRF_TRY(hrf::paint_ids_devn(seg, t->H * t->W, cell_idx, maxlab, ncells_dev, 1, ident, s));
   return HRF_OK;
 }
 
@@ -235,10 +228,17 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
   int32_t maxlab = 0;
   // the per-label sums and counts (their current capacity) and the barcode counts are cleared
   // inside the chain's watershed read-back launch (no fill kernels of their own)
+  // Entry budget: these 3 clears + the segmentation's 2 clears and 3 read-backs at the watershed
+  // batch (segment.hip) must fit ZeroPub::N per kind; every add is checked, since a dropped clear
+  // would add the previous tile's sums into this one.
+  static_assert(::hrf::ZeroPub::N >= 5, "ZeroPub: the tile's and the segmentation's clears share one launch");
   ::hrf::ZeroPub zp;
-  zp.zero(t->sums, sizeof(double) * (size_t)t->cap * C);
-  zp.zero(t->counts, sizeof(int64_t) * (size_t)t->cap);
-  zp.zero(counts, sizeof(int64_t) * (size_t)R);
+  if (!(zp.zero(t->sums, sizeof(double) * (size_t)t->cap * C) && zp.zero(t->counts, sizeof(int64_t) * (size_t)t->cap) &&
+        zp.zero(counts, sizeof(int64_t) * (size_t)R))) {
+    join();
+    ::hrf::set_error("tile_ecoli: per-label clears do not fit the read-back launch");
+    return HRF_EINVAL;
+  }
   hrf_status st = ::hrf::segment_ecoli_cn_extra(t->seg, t->cn, seg, &maxlab, s, &zp);   // :73-127
   if (st) {
     join();

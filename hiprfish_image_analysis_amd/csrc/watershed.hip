@@ -22,9 +22,9 @@
 //     ping-pong global passes until no tile changes (ws_pass_kernel);
 //  2. ws_contest_kernel lists the pixels whose candidates carry different labels.  None (every
 //     input without competing equal values, and the quantised E. coli tiles measured) -> done;
-//  3. otherwise ws_resolve_kernel decides each listed pixel by walking the candidates' strings
-//     (one thread per pixel, sets of tied ancestors, hash-deduplicated, a basin component at
-//     once), fixes its parent, labels are re-propagated from the markers (ws_pass_kernel in
+//  3. otherwise ws_resolve_wave_kernel decides each listed pixel by walking the candidates'
+//     strings (one 64-lane workgroup per walker, sets of tied ancestors, hash-deduplicated, a
+//     basin component at once), fixes its parent, labels are re-propagated from the markers (ws_pass_kernel in
 //     relabel mode: resolved pixels copy their parent, others the least candidate label) and
 //     step 2 repeats until no undecided contest is left.
 //  4. when two competing strings are equal down to markers of the same value (counted in
@@ -124,7 +124,7 @@ __device__ __forceinline__ bool better(double l1, int32_t h1, int32_t d1, int32_
 // + gridDim.x, ... (ntx x nty tiles), so a pass costs a resident grid's dispatches instead of one
 // per tile -- most tiles are skipped after the first passes, and under the concurrent classifier
 // every dispatch waits for a CU's LDS.
-template <bool RELABEL, bool JACOBI = false>
+template <bool RELABEL>
 __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__ f, int negate,
                                                       const int32_t *__restrict__ markers,
                                                       const uint8_t *__restrict__ mask, int64_t H, int64_t W,
@@ -179,8 +179,8 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
     }
   }
   __syncthreads();
-  // each thread owns 4 interior pixels: Jacobi (row = tid/32 + 8k, col = tid%32); red-black
-  // (row = 4 (tid/32) + k, col = tid%32), so a thread's pixels alternate in colour with k.
+  // each thread owns 4 interior pixels, row = 4 (tid/32) + k, col = tid%32, so a thread's pixels
+  // alternate in colour with k (red-black order below).
   // The owned pixels' own values stay in registers (only a pixel's own value is ever read:
   // 9 KB less LDS per workgroup, room beside the classifier's workgroups on a CU).
   int own[4];
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   double fvk[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    own[k] = (JACOBI ? ((tid >> 5) + 8 * k + 1) : (4 * (tid >> 5) + k + 1)) * WL + (tid & 31) + 1;
+    own[k] = (4 * (tid >> 5) + k + 1) * WL + (tid & 31) + 1;
     par[k] = -1;
     {
       const int64_t gr = r0 + (own[k] / WL), gc = c0 + (own[k] % WL);
@@ -276,38 +276,28 @@ __global__ __launch_bounds__(256) void ws_pass_kernel(const double *__restrict__
   bool any_change = false;
   for (int it = 0; it < 4 * WT * WT; ++it) {
     bool ch = false;
-    if (JACOBI) {
-      double nl[4];
-      int32_t nh[4], nd[4], nb[4];
+    // Red-black (checkerboard) relaxation: a pixel's four neighbours have the other colour, so
+    // one colour's pixels update in place from the other's current state (no two neighbours
+    // ever update together, nothing is staged) and a label travels two pixels per iteration.
+    // The update is monotone, so it reaches the Jacobi form's least fixpoint (the Jacobi form
+    // was 3.03 vs 2.16 ms per tile in the bench; removed in round 5).  Colour of pixel k:
+    // (k + tid) & 1; every lane updates two pixels per colour.
 #pragma unroll
-      for (int k = 0; k < 4; ++k) ch |= relax(own[k], fvk[k], par[k], nl[k], nh[k], nd[k], nb[k]);
-      __syncthreads();  // every read of the old state is done before the writes
+    for (int colour = 0; colour < 2; ++colour) {
+      const bool odd = (colour ^ (tid & 1)) != 0;  // this lane's pixels of the colour: k = odd, odd + 2
 #pragma unroll
-      for (int k = 0; k < 4; ++k) store(own[k], nl[k], nh[k], nd[k], nb[k]);
-    } else {
-      // Red-black (checkerboard) relaxation: a pixel's four neighbours have the other colour, so
-      // one colour's pixels update in place from the other's current state (no two neighbours
-      // ever update together, nothing is staged) and a label travels two pixels per iteration.
-      // The update is monotone, so it reaches the Jacobi form's least fixpoint
-      // (HRF_WS_JACOBI=1 keeps that form).  Colour of pixel k: (k + tid) & 1; every lane updates
-      // two pixels per colour.
-#pragma unroll
-      for (int colour = 0; colour < 2; ++colour) {
-        const bool odd = (colour ^ (tid & 1)) != 0;  // this lane's pixels of the colour: k = odd, odd + 2
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int i = odd ? own[2 * j + 1] : own[2 * j];
-          const double fv = odd ? fvk[2 * j + 1] : fvk[2 * j];
-          const int32_t pa = odd ? par[2 * j + 1] : par[2 * j];
-          double nl;
-          int32_t nh, nd, nb;
-          if (relax(i, fv, pa, nl, nh, nd, nb)) {
-            store(i, nl, nh, nd, nb);
-            ch = true;
-          }
+      for (int j = 0; j < 2; ++j) {
+        const int i = odd ? own[2 * j + 1] : own[2 * j];
+        const double fv = odd ? fvk[2 * j + 1] : fvk[2 * j];
+        const int32_t pa = odd ? par[2 * j + 1] : par[2 * j];
+        double nl;
+        int32_t nh, nd, nb;
+        if (relax(i, fv, pa, nl, nh, nd, nb)) {
+          store(i, nl, nh, nd, nb);
+          ch = true;
         }
-        if (colour == 0) __syncthreads();  // red written before black reads it
       }
+      if (colour == 0) __syncthreads();  // red written before black reads it
     }
     any_change |= ch;
     if (!__syncthreads_or(ch)) break;
@@ -708,12 +698,9 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
   int32_t hflag[4] = {0, 0, 0, 0};  // host copies of flag_ws[0..3]
   bool zeroed = true;  // ws_init_kernel zeroed tf's generations 0/1 and flag_ws[0..7]
   int passes = 0;
-  static const bool dbg = getenv("HRF_WS_DEBUG") != nullptr;
-  // persistent pass grids (HRF_WS_TILEGRID=1: one workgroup per tile, as before)
-  static const bool tilegrid = getenv("HRF_WS_TILEGRID") != nullptr;
-  static const bool jacobi = getenv("HRF_WS_JACOBI") != nullptr;  // A/B: the Jacobi relaxation
-  const unsigned pgrid_t = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
-  const unsigned pgrid_f = tilegrid ? (unsigned)ntiles : hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
+  // persistent pass grids (one workgroup per tile lost in round 3)
+  const unsigned pgrid_t = hrf::resident_grid(ws_pass_kernel<true>, 256, 0, ntiles);
+  const unsigned pgrid_f = hrf::resident_grid(ws_pass_kernel<false>, 256, 0, ntiles);
 
   // Passes run in batches with one host read per batch (change flag + contest count): the
   // first batch of 8 covers the typical tile (~7 passes) with a single synchronisation, later
@@ -729,15 +716,9 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
         const int32_t *prev = local == 0 ? B.tm : tf + ((local + 2) % 3) * ntiles;
         int32_t *next = tf + ((local + 1) % 3) * ntiles;
         int32_t *chg = flag_ws + (k == batch - 1 ? 0 : 1);
-        if (relabel && jacobi)
-          ws_pass_kernel<true, true><<<pgrid_t, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg,
-                                                             prev, cur, next, B.tw, (int)grid.x, (int)grid.y);
-        else if (relabel)
+        if (relabel)
           ws_pass_kernel<true><<<pgrid_t, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
                                                        cur, next, B.tw, (int)grid.x, (int)grid.y);
-        else if (jacobi)
-          ws_pass_kernel<false, true><<<pgrid_f, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg,
-                                                              prev, cur, next, B.tw, (int)grid.x, (int)grid.y);
         else
           ws_pass_kernel<false><<<pgrid_f, 256, 0, s>>>(image, negate, markers, mask, H, W, a, b, B.ptr, chg, prev,
                                                         cur, next, B.tw, (int)grid.x, (int)grid.y);
@@ -758,9 +739,6 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
         HRF_HIP(hipStreamSynchronize(s));
         for (int k = 0; k < 3; ++k) hflag[k] = pin[k];
       }
-      if (dbg)
-        fprintf(stderr, "hrf_watershed: %s batch, passes %d, changed %d %d, contests %d\n",
-                relabel ? "relabel" : "relax", passes, hflag[0], hflag[1], hflag[2]);
       if (!hflag[0]) {
         *count_out = hflag[2];
         return HRF_OK;
@@ -792,13 +770,9 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
     WsGeom g{image, negate, markers, mask, H, W, a.lam, a.hop};
     const int32_t *todo = B.list;
     int32_t ntodo = ncontest;
-    // as many walkers as the scratch budget holds (HRF_WS_SCRATCH_MB, default 1024 MB: ~4 k walkers
-    // of 244 KB at the first capacity; round 3 ran 256), each deciding its share of the list
-    static const int64_t budget = [] {
-      const char *e = getenv("HRF_WS_SCRATCH_MB");
-      const long v = e ? atol(e) : 1024;
-      return (int64_t)(v > 0 ? v : 1024) << 20;
-    }();
+    // as many walkers as a 1 GB scratch budget holds (~4 k walkers of 244 KB at the first
+    // capacity; round 3 ran 256), each deciding its share of the list
+    constexpr int64_t budget = (int64_t)1024 << 20;
     for (int32_t cap = 4096;; cap *= 16) {
       const int32_t hcap = 2 * cap, gcap = cap;
       const int64_t stride = walker_bytes(cap, hcap, gcap);
@@ -813,12 +787,13 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
         scratch_bytes = nth * stride;
       }
       HRF_HIP(hipMemsetAsync(flag_ws + 3, 0, sizeof(int32_t), s));
-      // HRF_WS_WAVE=0: one thread per walker (the serial walk of ws_core.hpp) instead of a wave
-      static const bool wave = !getenv("HRF_WS_WAVE") || atoi(getenv("HRF_WS_WAVE")) != 0;
+      // one 64-lane workgroup per walker; one thread per walker (the serial walk of ws_core.hpp,
+      // 28x slower on the adversarial image) only when the hash slots' [generation | group |
+      // pixel] words cannot hold 8 generation bits
       int pbits = 1, gbits = 1;
       while (pbits < 31 && ((int64_t)1 << pbits) < n) ++pbits;
       while (gbits < 31 && ((int64_t)1 << gbits) <= gcap) ++gbits;
-      if (wave && 64 - pbits - gbits >= 8)
+      if (64 - pbits - gbits >= 8)
         ws_resolve_wave_kernel<<<(unsigned)nth, 64, 0, s>>>(g, todo, ntodo, B.ptr, scratch, stride, nth, cap, hcap,
                                                             gcap, pbits, gbits, B.retry, flag_ws + 3, flag_ws + 4);
       else
@@ -828,7 +803,6 @@ hrf_status hrf::watershed_ex_extra(const double *image, int32_t negate, const in
       HRF_LAUNCHED();
       HRF_HIP(hipMemcpyAsync(hflag + 3, flag_ws + 3, sizeof(int32_t), hipMemcpyDeviceToHost, s));
       HRF_HIP(hipStreamSynchronize(s));
-      if (dbg) fprintf(stderr, "hrf_watershed: round %d resolved %d (cap %d), retry %d\n", rounds, ntodo, cap, hflag[3]);
       if (!hflag[3]) break;
       // a group holds at most n pixels, and the queue each at most 4 times: beyond that an
       // overflow means a corrupted state, not a large plateau

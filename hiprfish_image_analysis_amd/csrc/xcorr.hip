@@ -363,11 +363,10 @@ __global__ __launch_bounds__(XT) void xc_shifts_kernel(const RowBest *__restrict
   }
 }
 
-// a resident grid for the walking passes (HRF_XCORR_FULLGRID=1: one workgroup per job, as before)
+// a resident grid for the walking passes (one workgroup per job lost in round 3's A/B)
 template <class Kern>
 unsigned xgrid(Kern k, int64_t njobs) {
-  static const bool full = getenv("HRF_XCORR_FULLGRID") != nullptr;
-  return full ? (unsigned)njobs : hrf::resident_grid(k, XT, 0, njobs);
+  return hrf::resident_grid(k, XT, 0, njobs);
 }
 
 int ilog2(int64_t n) {

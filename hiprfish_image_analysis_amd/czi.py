@@ -37,8 +37,10 @@ The biofilm script's loaders (hiprfish_imaging_biofilm_analysis.py:55-120) are h
 series, as in the Bio-Formats of the reference's era (the biofilm script takes
 get_tile_size = sqrt(image_count) and stitches the per-tile series itself, :93-96, :1066), so
 get_image_count is the tile count and get_x_range / get_y_range are series 0's (one tile's)
-size; `series=k` reads tile k unstitched.  series=None (this reader's default) stitches the
-scene -- for the single-tile acquisitions the measurement scripts load the two agree.
+size; every loader reads series 0 -- one tile -- unless told otherwise, as bioformats.load_image
+does without a series (python-bioformats leaves the reader on series 0), and `series=k` reads tile
+k.  `stitch=True` (this reader's extension) places every tile of the scene by its X / Y start
+instead; for the single-tile acquisitions the measurement scripts load the two agree.
 
 Bio-Formats itself is absent here, so parity with load_image is unpinned; the layout follows
 the published ZISRAW specification and is exercised on files written to it (tests/test_czi.py).
@@ -166,8 +168,14 @@ def _jxr_lib():
         import os
         path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhrfjxr.so")
         if not os.path.exists(path):
-            raise CziError("JpegXrFile subblock but libhrfjxr.so is not built (jxrlib absent at build time)")
-        lib = ctypes.CDLL(path)
+            raise CziError("JpegXrFile subblock but libhrfjxr.so is not built (jxrlib's headers and "
+                           "libjxrglue.so were not found at build time; _build.JXR_INC / JXR_LIB)")
+        try:
+            lib = ctypes.CDLL(path)
+        except OSError as e:
+            raise CziError("JpegXrFile subblock but libhrfjxr.so cannot load jxrlib (libjxrglue.so / libjpegxr.so, "
+                           "linked from %s; set LD_LIBRARY_PATH or rebuild with HRF_JXR_LIBDIR): %s"
+                           % (os.environ.get("HRF_JXR_LIBDIR", "/opt/conda/lib"), e)) from e
         lib.hrf_jxr_info.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p]
         lib.hrf_jxr_decode.argtypes = [ctypes.c_char_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64]
@@ -237,13 +245,14 @@ def _level0(entries):
             and e.dims["X"][1] == e.dims["X"][2] and e.dims["Y"][1] == e.dims["Y"][2]]
 
 
-def _plane(buf, entries, path, z, t, series):
+def _plane(buf, entries, path, z, t, series, stitch=False):
     sel = [e for e in _level0(entries) if e.start("Z") == z and e.start("T") == t]
     if not sel:
         raise CziError("%s: no level-0 subblocks at z=%d, t=%d" % (path, z, t))
     scene = min(e.start("S") for e in sel)
     sel = [e for e in sel if e.start("S") == scene]
-    if series is not None:
+    if not stitch:
+        series = 0 if series is None else series
         tiles = sorted({e.start("M") for e in sel})
         if not 0 <= series < len(tiles):
             raise CziError("%s: series %d of %d mosaic tiles" % (path, series, len(tiles)))
@@ -276,12 +285,13 @@ def _rescaled(out, scale, rescale):
     return out
 
 
-def load_image(path, rescale=True, z=0, t=0, series=None):
+def load_image(path, rescale=True, z=0, t=0, series=None, stitch=False):
     """bioformats.load_image(path, z=, t=, series=) for a CZI spectral acquisition: (H, W, C)
-    float32 (rescaled by the pixel type's maximum) or the raw sample type with rescale=False"""
+    float32 (rescaled by the pixel type's maximum) or the raw sample type with rescale=False.
+    series None = series 0 (one mosaic tile), as Bio-Formats; stitch=True: the whole scene"""
     buf = _open(path)
     try:
-        out, scale = _plane(buf, read_directory(buf), path, z, t, series)
+        out, scale = _plane(buf, read_directory(buf), path, z, t, series, stitch)
     finally:
         _close(buf)
     return _rescaled(out, scale, rescale)
@@ -371,19 +381,22 @@ def load_image_zstack_fixed_t_tile(path, t, tile, rescale=True):
     return load_image_zstack_fixed_t_memory_efficient(path, t, 0, get_z_range(path), tile, rescale)
 
 
-def load_ztslice(path, z_index, t_index, series=None, rescale=True):
-    return load_image(path, rescale=rescale, z=z_index, t=t_index, series=series)
+def load_ztslice(path, z_index, t_index, series=0, rescale=True, stitch=False):
+    """bioformats.load_image(path, z=, t=) (biofilm :55-57): series 0 -- one tile, the size
+    get_x_range / get_y_range report"""
+    return load_image(path, rescale=rescale, z=z_index, t=t_index, series=series, stitch=stitch)
 
 
-def load_image_zstack_fixed_t_memory_efficient(path, t, z_min, z_max, series=None, rescale=True):
-    """(H, W, z_max - z_min, C): planes z_min..z_max-1 stacked on axis 2, the file mapped once"""
+def load_image_zstack_fixed_t_memory_efficient(path, t, z_min, z_max, series=0, rescale=True, stitch=False):
+    """(H, W, z_max - z_min, C): planes z_min..z_max-1 of series 0 (or `series`, or the stitched
+    scene) stacked on axis 2, the file mapped once (biofilm :103-114)"""
     buf = _open(path)
     try:
         ent = read_directory(buf)
         planes = []
         scale = 1.0
         for z in range(z_min, z_max):
-            a, scale = _plane(buf, ent, path, z, t, series)
+            a, scale = _plane(buf, ent, path, z, t, series, stitch)
             planes.append(a)
     finally:
         _close(buf)
@@ -392,9 +405,11 @@ def load_image_zstack_fixed_t_memory_efficient(path, t, z_min, z_max, series=Non
     return _rescaled(np.stack(planes, axis=2), scale, rescale)
 
 
-def load_image_zstack_fixed_t(path, t, series=None, rescale=True):
-    return load_image_zstack_fixed_t_memory_efficient(path, t, 0, get_z_range(path), series, rescale)
+def load_image_zstack_fixed_t(path, t, series=0, rescale=True, stitch=False):
+    """biofilm :75-91: every z plane of series 0 at time t -> (H, W, Z, C)"""
+    return load_image_zstack_fixed_t_memory_efficient(path, t, 0, get_z_range(path), series, rescale, stitch)
 
 
-def load_image_tile(path, rescale=True):
-    return load_image_zstack_fixed_t(path, 0, rescale=rescale)
+def load_image_tile(path, rescale=True, stitch=False):
+    """biofilm :120-122: the z-stack at t 0 of series 0"""
+    return load_image_zstack_fixed_t(path, 0, rescale=rescale, stitch=stitch)

@@ -43,10 +43,6 @@ def erosion_seeds_global(cell_sm: torch.Tensor, area_max: int = 600, min_obj: in
 # The segmentation chains run as one native call (segment.hip, same calls in the same order)
 # unless intermediates are requested (`keep`) or HRF_NATIVE_SEG=0.
 NATIVE_SEG = os.environ.get("HRF_NATIVE_SEG", "1") != "0"
-# the registration estimate of all lasers as one batch of FFTs (HRF_BATCH_REG=1).  Off by default:
-# with four tiles in flight the batched transforms cost 1-7 % end to end against one transform
-# pair per target (4 of 4 interleaved pairs; DESIGN.md "Tried and not kept")
-BATCH_REGISTRATION = os.environ.get("HRF_BATCH_REG", "0") == "1"
 # power-of-two tiles: the registration cross-correlations through xcorr.hip (six launches for all
 # lasers) instead of hipFFT; HRF_XCORR=0 keeps hipFFT
 XCORR = os.environ.get("HRF_XCORR", "1") != "0"
@@ -121,8 +117,6 @@ def estimate_shifts(lasers, reduce: str = "max", clamp: int | None = 15, device:
         proj = K.channel_max_multi(lasers, stacked=True)                 # one launch for all lasers
         if device and len(lasers) >= 2 and XCORR and K.xcorr_supported(*proj.shape):
             return K.xcorr_shifts_dev(proj, clamp)                      # hand-written FFT pipeline
-        if device and len(lasers) >= 2 and BATCH_REGISTRATION:
-            return K.register_translations_batch_dev(proj, clamp)       # batched FFTs
         proj = list(proj.unbind(0))
     elif reduce == "sum" and device and len(lasers) >= 2 and XCORR and K.xcorr_supported(len(lasers), H, W):
         proj = torch.empty((len(lasers), H, W), dtype=torch.float64, device=lasers[0].device)

@@ -28,11 +28,15 @@ def test_spectral_gray16_rescaled(tmp_path):
 
 
 def test_mosaic_tiles_stitched(tmp_path):
+    """a 3-tile mosaic: Bio-Formats' default is series 0 (one tile); stitch=True places all"""
     rng = np.random.default_rng(2)
     st = rng.integers(0, 65536, (24, 60, 3), dtype=np.uint16)
     p = str(tmp_path / "m.czi")
     write_spectral(p, st, tiles=3)
-    assert np.array_equal(czi.load_image(p, rescale=False), st)
+    assert np.array_equal(czi.load_image(p, rescale=False, stitch=True), st)
+    assert np.array_equal(czi.load_image(p, rescale=False), st[:, :20])
+    # the loaders' arrays have the sizes the OME queries report (biofilm :55-73)
+    assert czi.load_ztslice(p, 0, 0).shape[:2] == (czi.get_y_range(p), czi.get_x_range(p)) == (24, 20)
 
 
 def test_gray8_float_and_plane_selection(tmp_path):
@@ -61,7 +65,7 @@ def test_zstd_subblocks(tmp_path, compression, hilo):
     st = rng.integers(0, 4096, (33, 47, 5), dtype=np.uint16)
     p = str(tmp_path / "zs.czi")
     write_spectral(p, st, tiles=2, compression=compression, hilo=hilo)
-    assert np.array_equal(czi.load_image(p, rescale=False), st)
+    assert np.array_equal(czi.load_image(p, rescale=False, stitch=True), st)
     f = rng.random((6, 9)).astype(np.float32)
     pf = str(tmp_path / "zf.czi")
     write_czi(pf, [(f, {"C": 0})], compression=compression)
@@ -82,13 +86,19 @@ def test_zstack_loaders_and_sizes(tmp_path):
     assert (czi.get_x_range(p), czi.get_y_range(p)) == (15, 20) and czi.get_tile_size(p) == 1
     assert np.array_equal(czi.load_image_zstack_fixed_t_tile(p, 0, 1, rescale=False), vol[:, 15:])
     assert np.array_equal(czi.load_ztslice_tile(p, 3, 0, 0, rescale=False), vol[:, :15, 3])
+    # the reference-named loaders read series 0, the size get_x_range / get_y_range report
     got = czi.load_image_zstack_fixed_t(p, 0)
-    assert got.dtype == np.float32 and got.shape == (20, 30, 4, 6)
-    assert np.array_equal(got, vol.astype(np.float32) / np.float32(65535.0))
-    assert np.array_equal(czi.load_image_tile(p, rescale=False), vol)
+    assert got.dtype == np.float32 and got.shape == (20, 15, 4, 6)
+    assert got.shape[:2] == (czi.get_y_range(p), czi.get_x_range(p))
+    assert np.array_equal(got, vol[:, :15].astype(np.float32) / np.float32(65535.0))
+    assert np.array_equal(czi.load_image_tile(p, rescale=False), vol[:, :15])
     assert np.array_equal(czi.load_image_zstack_fixed_t_memory_efficient(p, 0, 1, 3, rescale=False),
-                          vol[:, :, 1:3])
-    assert np.array_equal(czi.load_ztslice(p, 2, 0, rescale=False), vol[:, :, 2])
+                          vol[:, :15, 1:3])
+    assert np.array_equal(czi.load_ztslice(p, 2, 0, rescale=False), vol[:, :15, 2])
+    assert czi.load_ztslice(p, 2, 0).shape[:2] == (czi.get_y_range(p), czi.get_x_range(p))
+    # stitching is explicit
+    assert np.array_equal(czi.load_image_tile(p, rescale=False, stitch=True), vol)
+    assert np.array_equal(czi.load_ztslice(p, 2, 0, rescale=False, stitch=True), vol[:, :, 2])
     # series = one mosaic tile, unstitched
     assert np.array_equal(czi.load_image(p, rescale=False, z=1, series=1), vol[:, 15:, 1])
     with pytest.raises(czi.CziError, match="series"):
@@ -110,9 +120,9 @@ def test_jpegxr_subblocks_lossless(tmp_path, dtype, tiles):
     pu, pj = str(tmp_path / "u.czi"), str(tmp_path / "j.czi")
     write_spectral(pu, st, tiles=tiles)
     write_spectral(pj, st, tiles=tiles, compression=4, jxr_quality=1)
-    got = czi.load_image(pj)
-    assert np.array_equal(got, czi.load_image(pu))
-    assert np.array_equal(czi.load_image(pj, rescale=False), st)
+    got = czi.load_image(pj, stitch=True)
+    assert np.array_equal(got, czi.load_image(pu, stitch=True))
+    assert np.array_equal(czi.load_image(pj, rescale=False, stitch=True), st)
 
 
 @pytest.mark.skipif(not JXR, reason="jxrlib's encoder is not in this image")
@@ -147,3 +157,23 @@ def test_unsupported_raise(tmp_path):
     bad.write_bytes(b"NOTACZI" + b"\0" * 100)
     with pytest.raises(czi.CziError):
         czi.load_image(str(bad))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not JXR, reason="jxrlib's encoder is not in this image")
+def test_jpegxr_on_the_gpu_box(tmp_path):
+    """the lossless JPEG-XR case where the measurement scripts run: the shim loads jxrlib on the
+    GPU box, and the decoded acquisition goes through the device channel sum as the
+    uncompressed one does (ecoli measurement.py:145, :71)"""
+    torch = pytest.importorskip("torch")
+    from hiprfish_image_analysis_amd import kernels as K
+    rng = np.random.default_rng(8)
+    st = rng.integers(0, 4096, (64, 96, 6), dtype=np.uint16)
+    pu, pj = str(tmp_path / "u_405.czi"), str(tmp_path / "j_405.czi")
+    write_spectral(pu, st)
+    write_spectral(pj, st, compression=4, jxr_quality=1)
+    a, b = io.load_laser_stack(pj), io.load_laser_stack(pu)
+    assert np.array_equal(a, b)
+    sa = K.channel_sum(torch.from_numpy(a).cuda())
+    sb = K.channel_sum(torch.from_numpy(b).cuda())
+    assert torch.equal(sa, sb)

@@ -82,6 +82,22 @@ def test_enhance_3d_vs_oracle(K, orc, shape):
     same(K.line_profile_3d_norm(dev(pad)).cpu().numpy(), orc.line_profile_3d_norm(pad))
 
 
+def test_enhance_3d_special_values(K, orc):
+    """tiles with NaN, infinities, negative zeros and finite values whose window ranges overflow
+    (max - min > DBL_MAX: inf / inf = NaN taps) take the reference's compare-select arithmetic;
+    equal to the restatement, NaNs in place"""
+    rng = np.random.default_rng(21)
+    pad = rng.random((24, 22, 50))
+    pad[3, 4, 5] = np.nan
+    pad[12, 7, 40] = np.inf
+    pad[14, 15, 20] = -np.inf
+    pad[2:6, 2:6, 30:34] = -0.0
+    pad[18, 17, 8] = 1.5e308                # finite, span with the next value > DBL_MAX
+    pad[18, 18, 8] = -1.5e308
+    pad[20, 3, 45] = 1e308                  # finite, span within DBL_MAX but above 2^1023
+    same(K.enhance_3d(dev(pad)).cpu().numpy(), orc.enhance_3d(pad))
+
+
 def test_enhance_3d_flat_volume(K, orc):
     pad = np.full((13, 12, 14), 0.3)
     same(K.enhance_3d(dev(pad)).cpu().numpy(), orc.enhance_3d(pad))

@@ -419,7 +419,10 @@ def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
                           rng.choice(512 * 384, 1000, replace=False)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
     for mode in (1, 2):
-        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 4000)
+        # cell pixels here are the rendered cells' (edges included, where the dome profile is dim),
+        # not a segmentation's interior as in the full-size tests: 0.98
+        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 4000,
+                           min_cell_sep=0.98)
 
 
 def test_classify_pixels_mode2_negative_values(K, orc, S):
@@ -436,7 +439,7 @@ def test_classify_pixels_mode2_negative_values(K, orc, S):
     for lib in (ref, ref - 0.01):                   # then a library with negative entries
         refx = K.classify_prepare(dev(lib.astype(np.float32)), bounds, mode=2)
         gi, gd = [host(t).ravel()[sel] for t in K.classify_pixels(st, refx, R, bounds)]
-        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 1500)
+        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 1500, min_cell_sep=0.98)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
@@ -678,8 +681,9 @@ def test_classify_pixels_equal_scores_take_lowest_row(K, S, nbit, bounds, mode):
     rng = np.random.default_rng(9)
     n = 64 * 96
     rows = np.array([p[0] for p in pairs])[rng.integers(0, len(pairs), n)]
-    x = ref[rows] * rng.uniform(0.5, 1.0, (n, 1)).astype(np.float32) + \
-        np.abs(rng.normal(0, 0.01, (n, C))).astype(np.float32)
+    # multiplicative noise: a row's all-zero segments stay zero in its pixels (the metric puts 1 on a
+    # segment zero in one operand only), so the copied row and its copy are the best rows
+    x = (ref[rows] * rng.uniform(0.5, 1.0, (n, 1)) * (1 + rng.normal(0, 0.01, (n, C)))).astype(np.float32)
     x[: n // 8] -= 0.02                             # negative values: the unkeyed argmax
     stack = dev(x.reshape(64, 96, C))
     if mode == "table":
@@ -690,4 +694,4 @@ def test_classify_pixels_equal_scores_take_lowest_row(K, S, nbit, bounds, mode):
         idx = host(K.classify_pixels(stack, refx, R, bounds)[0]).ravel()
     copies = np.array([p[1] for p in pairs])
     assert not np.isin(idx, copies).any(), np.unique(idx[np.isin(idx, copies)])
-    assert (idx == rows).mean() > 0.9
+    assert (idx == rows)[n // 8:].mean() > 0.9     # the tie is the argmin's: the pairs are exercised

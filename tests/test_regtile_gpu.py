@@ -83,3 +83,41 @@ def test_register_tile_falls_back(mods):
     stack, _, _, _ = S.tile(64, 72, seed=1)
     out = P.register_tile(S.laser_split(stack))
     assert isinstance(out, tuple) and out[0].shape == (64, 72, 95)
+
+
+@pytest.mark.parametrize("W", [192, 200])   # the strip kernel (W % 64 == 0) and the general one
+@pytest.mark.parametrize("apply_mask", [True, False])
+def test_label_sums_lasers_adversarial(mods, W, apply_mask):
+    """the lasers label sums on a random label map against label_sums of the assembled stack:
+    many small labels per 64 x 8 unit (the per-wave table fills and flushes early), labels past
+    maxlab and negative ones (background), shifts that move a laser by more than a 64-pixel
+    chunk (whole chunks uncovered), a flat field with zeros, infinities and denormals (the
+    division path), H not a multiple of the unit height"""
+    K, P, S = mods
+    H = 75
+    rng = np.random.default_rng(W + apply_mask)
+    chans = [32, 23, 20, 14, 6]
+    lasers = [torch.from_numpy(rng.random((H, W, c), dtype=np.float32)).cuda() for c in chans]
+    shifts = torch.tensor([[0, 0], [3, -5], [-7, 2], [12, 70], [-20, -67]], dtype=torch.int32).cuda()
+    maxlab = 60
+    lab = rng.integers(-3, maxlab + 8, (H, W)).astype(np.int32)
+    lab[rng.random((H, W)) < 0.3] = 0
+    lab[10:40, 30:90] = 7                             # one long run across chunks and rows
+    seg = torch.from_numpy(lab).cuda()
+    cal = rng.uniform(0.5, 1.5, (H, W)).astype(np.float32)
+    cal[0, :5] = 0.0
+    cal[1, :3] = np.inf
+    cal[2, :3] = 1e-40
+    cal = torch.from_numpy(cal).cuda()
+    reg = K.register_assemble(lasers, shifts, apply_mask)
+    clean = torch.where((seg < 0) | (seg > maxlab), torch.zeros_like(seg), seg)
+    for c in (None, cal):
+        ws, wc = K.label_sums(reg, clean, maxlab, cal=c, cal_range=(0, 32) if c is not None else None)
+        gs, gc = K.label_sums_lasers(lasers, shifts, seg, maxlab, apply_mask, cal=c)
+        assert torch.equal(gc, wc)
+        fin = torch.isfinite(ws)
+        assert torch.equal(fin, torch.isfinite(gs))
+        torch.testing.assert_close(gs[fin], ws[fin], rtol=1e-12, atol=0)
+        assert torch.equal(torch.isnan(gs), torch.isnan(ws))
+        inf = torch.isinf(ws)
+        assert torch.equal(gs[inf], ws[inf])
