@@ -72,7 +72,8 @@ def test_process_tile_classification_and_counts(mods, orc):
     sel = np.concatenate([rng.choice(cells, 3000, replace=False), rng.choice(P_, 1000, replace=False)])
     x = host(stack).reshape(P_, -1)[sel].astype(np.float64)
     pi, pd = host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel]
-    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 3000)
+    # a 512^2 tile: 0.98 (the full-size cfg3 / cfg2 tests hold 0.99, tests/test_fullsize_gpu.py)
+    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 3000, min_cell_sep=0.98)
 
 
 def test_concurrent_tiles_equal_isolated(mods):
