@@ -1117,7 +1117,8 @@ hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const in
   for (int i = 0; i < nlaser && ecoli; ++i) ecoli = channels_host[i] == EcoliLasers<0>::cl(i);
   HRF_REQUIRE(ecoli && W % 16 == 0 && H <= 65535 && H >= 1 && W >= 16,
               "register_assemble_pixtable: the five E. coli lasers and W a multiple of 16");
-  HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && table && flags, "register_assemble_pixtable: null output");
+  HRF_REQUIRE(cn_out && cn_mode >= 0 && cn_mode <= 2 && (table != nullptr) == (flags != nullptr),
+              "register_assemble_pixtable: null output");
   HRF_REQUIRE(!dst || ((uintptr_t)dst & 15) == 0, "register_assemble_pixtable: dst must be 16-byte aligned");
   launch_assemble(L, H, W, apply_mask, dst, cn_out, cn_mode, (uint4 *)table, flags, (hipStream_t)stream);
   HRF_LAUNCHED();

@@ -663,6 +663,18 @@ def register_assemble_pixtable(lasers, shifts_dev, apply_mask=True, cn_mode=1, b
     return cn, pt, stack
 
 
+def register_assemble_cn_only(lasers, shifts_dev, apply_mask=True, cn_mode=1):
+    """the E. coli registered assembly writing image_cn only (hrf_register_assemble_pixtable with
+    no table: the tile path without the per-pixel classifier) -> image_cn f64 (H, W)"""
+    import ctypes
+    srcs, ch, ptrs, sd = _laser_args(lasers, shifts_dev)
+    H, W = srcs[0].shape[:2]
+    cn = torch.empty((H, W), dtype=torch.float64, device=srcs[0].device)
+    _lib.call("hrf_register_assemble_pixtable", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd), len(srcs),
+              H, W, int(bool(apply_mask)), None, _ptr(cn), int(cn_mode), None, None, _stream())
+    return cn
+
+
 def label_sums_lasers(lasers, shifts_dev, labels, maxlab, apply_mask=True, cal=None, cal_range=(0, 32)):
     """label_sums of the registered stack, read from the per-laser acquisitions (no stack);
     cal: a per-pixel (H, W) flat field on channels cal_range"""

@@ -114,7 +114,7 @@ HRF_API hrf_status hrf_register_assemble_cn_dev(const float *const *src_host, co
  * above) and the per-pixel classifier's prepared operands (table: hrf_pixtable_bytes(H * W, ...)
  * bytes, flags: H * W bytes; see hrf_pixtable_prepare) from the same LDS strip; dst (nullable)
  * also receives the registered stack -- without it the stack never exists (the per-cell spectra
- * then come from hrf_label_sums_lasers) */
+ * then come from hrf_label_sums_lasers).  table and flags both NULL: image_cn only */
 HRF_API hrf_status hrf_register_assemble_pixtable(const float *const *src_host, const int32_t *channels_host,
                                                   const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
                                                   int32_t apply_mask, float *dst, double *cn_out, int32_t cn_mode,

@@ -33,9 +33,11 @@ def test_assembly_pixtable_equals_stack_path(mods, H, W, apply_mask):
     a = K.classify_pixels_table(pt, refx, ref.shape[0])
     b = K.classify_pixels(want_stack, refx, ref.shape[0], S.ECOLI_BOUNDS, mode=2)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
-    # without the stack output: the same table and image_cn
+    # without the stack output: the same table and image_cn; without the table: the same image_cn
     cn2, pt2, st2 = K.register_assemble_pixtable(lasers, shifts, apply_mask)
     assert st2 is None and torch.equal(cn2, cn)
+    if W % 16 == 0:
+        assert torch.equal(K.register_assemble_cn_only(lasers, shifts, apply_mask), cn)
     a2 = K.classify_pixels_table(pt2, refx, ref.shape[0])
     assert torch.equal(a2[0], a[0]) and torch.equal(a2[1], a[1])
 
