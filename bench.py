@@ -204,7 +204,7 @@ def _event_ms(fn, n=5):
 # The streaming kernels of the timed path (hrf_tile_ecoli, tile.hip) and the kernel symbols
 # rocprofv3 lists them under -- the hbm_kernels rows and tools/time_kernels.py path's PMC passes
 HBM_KERNELS = {"channel_max_multi": "channel_max_multi_pf_kernel",
-               "assemble_pixtable": "assemble_ecoli_kernel<false, 3>",
+               "assemble_pixtable": "assemble_ecoli_kernel<3>",
                "label_sums_lasers_cal": "label_sums_lasers_row_kernel<true>"}
 
 
@@ -261,32 +261,38 @@ def _hbm_kernels(lasers, cal, lib):
     return out
 
 
-def _watershed_ties(dev, n=512):
-    """The watershed's tie path on an adversarial n x n image: a plateau-heavy integer image (4
+def _watershed_ties(dev, sizes=(512, 1024)):
+    """The watershed's tie path on adversarial n x n images: a plateau-heavy integer image (4
     levels in 4x4 blocks, multi-pixel markers with distinct values per label, 10 % of pixels outside
-    the mask) forces contests that the resolver decides exactly; the same markers on a continuous
-    image have none.  Mean time of hrf_watershed_ex (HIP events) and the tie statistics of each.
-    (The bench tiles -- continuous, k/4095, k/255 -- have no contest; see the quantised lines.)"""
+    the mask) forces contests that the resolver decides exactly; at 1024^2 the 1e-3 label offsets
+    overlap the integer levels, so some decisions come down to equal-valued markers of different
+    labels and the tile is flooded again by skimage's binary heap on the device (the heap replay,
+    watershed.hip); the same markers on a continuous image have none.  Mean time of
+    hrf_watershed_ex (HIP events) and the tie statistics of each.  (The bench tiles -- continuous,
+    k/4095, k/255 -- have at most a contest or two; see the quantised lines.)"""
     import torch
 
     from hiprfish_image_analysis_amd import kernels as K
-    rng = np.random.default_rng(7)
-    f = np.kron(rng.integers(0, 4, (n // 4, n // 4)), np.ones((4, 4))).astype(np.float64)
-    markers = np.zeros((n, n), np.int32)
-    for lab in range(1, n * n // 300 + 1):
-        r, c = rng.integers(1, n - 1), rng.integers(1, n - 1)
-        markers[r - 1:r + 2, c - 1:c + 2] = lab
-    f = f + 1e-3 * markers
-    mask = rng.random((n, n)) < 0.9
-    mk, mm = torch.from_numpy(markers).to(dev), torch.from_numpy(mask).to(dev)
-    out = {"size": [n, n]}
-    for name, img in (("plateaus", f), ("continuous", f + rng.random((n, n)))):
-        x = torch.from_numpy(img).to(dev)
-        ties = []
-        K.watershed(x, mk, mm, ties=ties)
-        ms = _event_ms(lambda: K.watershed(x, mk, mm), 3)
-        out[name] = {"ms": round(ms, 3), "contested_px": int(ties[0]), "resolution_rounds": int(ties[1]),
-                     "equal_marker_decisions": int(ties[2])}
+    out = {}
+    for n in sizes:
+        rng = np.random.default_rng(7)
+        f = np.kron(rng.integers(0, 4, (n // 4, n // 4)), np.ones((4, 4))).astype(np.float64)
+        markers = np.zeros((n, n), np.int32)
+        for lab in range(1, n * n // 300 + 1):
+            r, c = rng.integers(1, n - 1), rng.integers(1, n - 1)
+            markers[r - 1:r + 2, c - 1:c + 2] = lab
+        f = f + 1e-3 * markers
+        mask = rng.random((n, n)) < 0.9
+        mk, mm = torch.from_numpy(markers).to(dev), torch.from_numpy(mask).to(dev)
+        rec = {"size": [n, n]}
+        for name, img in (("plateaus", f), ("continuous", f + rng.random((n, n)))):
+            x = torch.from_numpy(img).to(dev)
+            ties = []
+            K.watershed(x, mk, mm, ties=ties)
+            ms = _event_ms(lambda: K.watershed(x, mk, mm), 3 if n <= 512 else 1)
+            rec[name] = {"ms": round(ms, 3), "contested_px": int(ties[0]), "resolution_rounds": int(ties[1]),
+                         "equal_marker_decisions": int(ties[2]), "heap_replay": bool(ties[2] > 0)}
+        out["n%d" % n] = rec
     return out
 
 
@@ -392,7 +398,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                "per-pixel classification, counts", "concurrent": T, "steps": steps,
                    "value": round(H * W * steps * T / sec / 1e6, 3), "unit": "Mpixel-spectra/s",
                    "ms_per_tile": round(sec / (steps * T) * 1e3, 3),
-                   "roofline": {"kernel": "nl_means_pairs_kernel<false, 8, 4, 1024, 48>", "bound": "valu-f64", "kernel_ms": round(ms_nl, 4),
+                   "roofline": {"kernel": "nl_means_pairs_kernel<false, 8, 4, 1024, 52>", "bound": "valu-f64", "kernel_ms": round(ms_nl, 4),
                                 "algorithmic_ops_per_pixel": NL_OPS_PER_PIXEL, "achieved": round(ach, 3),
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s", "frac": round(ach / F64_VALU_PEAK_TOPS, 4)}}
     del ctiles, s, norm, ccal
@@ -413,7 +419,7 @@ def _extras(dev, T, streams, pool, tiles, lib_main):
                                "line_profile_memory_efficient_v2 + biofilm :812-817 post-chain (72 directions x 11 "
                                "taps per voxel)", "value": round(X * Y * Z / ms_chain / 1e3, 3), "unit": "Mvoxel/s",
                    "ms": round(ms_chain, 3),
-                   "roofline": {"kernel": "enhance3d_kernel<0>", "bound": "valu-f64", "kernel_ms": round(ms_e3, 3),
+                   "roofline": {"kernel": "enhance3d_kernel<0, 2>", "bound": "valu-f64", "kernel_ms": round(ms_e3, 3),
                                 "algorithmic_ops_per_voxel": E3_OPS_PER_VOXEL, "achieved": round(ach3, 3),
                                 "peak": F64_VALU_PEAK_TOPS, "unit": "Tops/s",
                                 "frac": round(ach3 / F64_VALU_PEAK_TOPS, 4)}}
