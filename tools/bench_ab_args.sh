@@ -1,5 +1,6 @@
 #!/bin/bash
 # Interleaved comparison of bench argument sets: bash tools/bench_ab_args.sh <reps> "<args A>" "<args B>" ...
+# (leading NAME=value words of a set are put in the environment of that run)
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/ab_args.log
@@ -7,7 +8,11 @@ out=gpurun_out/ab_args.log
 reps=$1; shift
 for rep in $(seq $reps); do
   for a in "$@"; do
-    r=$(timeout -k 10 240 python3 bench.py --no-cpu-baseline --no-extras --steps 40 --warmup 5 $a 2>/dev/null) || exit 1
+    envs=(); args=()
+    for w in $a; do
+      if [ ${#args[@]} -eq 0 ] && [[ $w =~ ^[A-Z_][A-Z0-9_]*= ]]; then envs+=("$w"); else args+=("$w"); fi
+    done
+    r=$(env HRF_NONE=1 "${envs[@]}" timeout -k 10 240 python3 bench.py --no-cpu-baseline --no-extras --steps 40 --warmup 5 "${args[@]}" 2>/dev/null) || exit 1
     echo "[$a] $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d.get("roofline", {}).get("kernel_ms"))')" >> $out
   done
 done
