@@ -204,7 +204,7 @@ def _event_ms(fn, n=5):
 # The streaming kernels of the timed path (hrf_tile_ecoli, tile.hip) and the kernel symbols
 # rocprofv3 lists them under -- the hbm_kernels rows and tools/time_kernels.py path's PMC passes
 HBM_KERNELS = {"channel_max_multi": "channel_max_multi_pf_kernel",
-               "assemble_pixtable": "assemble_ecoli_kernel<3>",
+               "assemble_pixtable": "assemble_ecoli_kernel<4, true>",
                "label_sums_lasers_cal": "label_sums_lasers_row_kernel<true>"}
 
 

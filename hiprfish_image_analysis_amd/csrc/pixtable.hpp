@@ -117,30 +117,22 @@ __device__ __forceinline__ void prep_tile(float *tile, const uint8_t *ok, int np
   }
 }
 
-// The same for the E. coli layout with the norm pass spread over the block's four waves (wave =
-// a segment group, lane = pixel: segments 0 | 1 | 2 | 3 + 4, at most 32 channels per wave instead
-// of 95 per lane): the assembly kernel calls this on its strip.  Same arithmetic per segment (the
-// segments' sums are independent), so the table is bit-identical to prep_tile's.
-// workgroup barrier ordering LDS only (s_barrier after the LDS counter drains): unlike
-// __syncthreads it does not wait for the wave's global loads, so loads issued before it stay in
-// flight across it (the E. coli assembly prefetches its next strip that way)
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// Caller contract: fl[0..63] is zero and the tile is staged (both ordered by a barrier before
-// the call); the f64 channel sums the caller left in cns[0..np) (nullable) are turned into
-// image_cn by wave 2 (log(s + 1e-2), cn_mode 1, or log10(s + 1), cn_mode 2) beside its segment.
-template <bool LDSB = false>
-__device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, int np, int64_t p0,
-                                                uint4 *__restrict__ table, uint8_t *__restrict__ flags,
-                                                uint32_t *fl /* LDS, 64 words, zero */, const double *cns,
-                                                int cn_mode, double *__restrict__ cn_out) {
+// The same for the E. coli layout, in two phases the assembly kernel runs on its strip (round 5:
+// the tile is read, never rewritten, so the norms share a barrier interval with the channel sums):
+//  ecoli_norms: the segment norms spread over the block's four waves (wave = a segment group, lane
+//    = pixel: segments 0 | 1 | 2 | 3 + 4), each pixel's reciprocal segment norms into invs[s * 64 +
+//    pixel] and its flag bits into fl (zero on entry);
+//  ecoli_table (after a barrier): the table entries, x = raw * inv of its segment.
+// Same arithmetic per segment as prep_tile (f32 sums in channel order, v_rsq, the f64 redo, one f32
+// multiply per value), so the table is bit-identical to prep_tile's.
+__device__ __forceinline__ void ecoli_norms(const float *tile, const uint8_t *ok, int np, float *invs, uint32_t *fl) {
   using L = LayEcoli;
-  constexpr int C = L::C, KT = lay_kt<L>();
+  constexpr int C = L::C;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   auto seg = [&](auto sc) {
     constexpr int s = decltype(sc)::value;
     if (lane >= np) return;
-    float *px = tile + lane * C;
+    const float *px = tile + lane * C;
     const bool use = !ok || ok[lane];
     float nn = 0.0f;
     uint32_t sg = 0;
@@ -163,50 +155,62 @@ __device__ __forceinline__ void prep_tile_ecoli(float *tile, const uint8_t *ok, 
       inv = nz ? (float)(1.0 / sqrt(td)) : 0.0f;
       zx = nz ? 0u : (1u << s);
     }
-#pragma unroll 4
-    for (int c = L::b(s); c < L::b(s + 1); ++c) px[c] = use ? px[c] * inv : 0.0f;
+    invs[s * 64 + lane] = inv;
     const uint32_t f = zx | ((sg >> 31) << 7);
     if (f) atomicOr(&fl[lane], f);
   };
   if (w == 0) seg(std::integral_constant<int, 0>{});
   else if (w == 1) seg(std::integral_constant<int, 1>{});
-  else if (w == 2) {
-    seg(std::integral_constant<int, 2>{});
-    if (cns && lane < np) {
-      double sv = 0.0 + cns[lane];
-      if (cn_mode == 1) sv = hrf_cr_log(sv + 1e-2);
-      else if (cn_mode == 2) sv = hrf_cr_log10(sv + 1.0);
-      cn_out[p0 + lane] = sv;
-    }
-  } else {
+  else if (w == 2) seg(std::integral_constant<int, 2>{});
+  else {
     seg(std::integral_constant<int, 3>{});
     seg(std::integral_constant<int, 4>{});
   }
-  if (LDSB) lds_barrier();
-  else __syncthreads();
-  if (tid < np) flags[p0 + tid] = (uint8_t)fl[tid];
-  // one item = one (group, k-block, lane): its 8 values once, the hi and the lo entry from them
-  const int ne = (np + 15) / 16 * KT * 64;
-#pragma unroll 1
-  for (int e = tid; e < ne; e += 256) {
-    const int ln = e & 63, gt = e >> 6;
-    const int g = gt / KT, t = gt - g * KT;
-    const int i = 16 * g + (ln & 15), Q = ln >> 4;
-    const float *pc = tile + (i < np ? i : 0) * C;
+}
+
+// runtime segment of E. coli column k (k < 95) and its segment's end
+__device__ __forceinline__ int ecoli_seg(int k) { return (k >= 32) + (k >= 55) + (k >= 75) + (k >= 89); }
+__device__ __forceinline__ int ecoli_end(int s) { return s == 0 ? 32 : s == 1 ? 55 : s == 2 ? 75 : s == 3 ? 89 : 95; }
+
+// One item per (group g, k-block t, lane): wave w takes the three (g, t) with 3g + t in {w, w + 4,
+// w + 8} -- one per k-block, so t is a compile-time constant in each.
+__device__ __forceinline__ void ecoli_table(const float *tile, const uint8_t *ok, int np, int64_t p0, const float *invs,
+                                            uint4 *__restrict__ table) {
+  constexpr int C = LayEcoli::C, KT = lay_kt<LayEcoli>();
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, Q = lane >> 4;
+  const int ng = (np + 15) / 16;
+#pragma unroll 1  // (unrolled, the three items' values spill at four waves per SIMD)
+  for (int t = 0; t < KT; ++t) {
+    const int j = ((t - w) % 3 + 3) % 3;
+    const int g = (w + 4 * j - t) / 3;
+    if (g >= ng) continue;
+    const int i = 16 * g + (lane & 15);
+    const int ii = i < np ? i : 0;
+    const float *pc = tile + ii * C;
+    const bool use = i < np && (!ok || ok[ii]);
+    const int k0 = 32 * t + 8 * Q;
+    const int sa = ecoli_seg(k0), sb = ecoli_seg(min(k0 + 7, C - 1));
+    const float ia = invs[sa * 64 + ii], ib = invs[sb * 64 + ii];
+    const int split = ecoli_end(sa) - k0;  // first q of segment sb
     union {
       _Float16 h[8];
       uint4 u;
     } hi, lo;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int k = 32 * t + 8 * Q + q;
-      float x = k < C ? pc[k] : (k == C ? 1.0f : 0.0f);
-      if (i >= np) x = 0.0f;
+      const int k = k0 + q;
+      float x;
+      if (32 * t + 24 + q < C) {  // every lane quarter's column is a channel
+        x = use ? pc[k] * (q < split ? ia : ib) : 0.0f;
+      } else {
+        x = k < C ? (use ? pc[k < C ? k : 0] * (q < split ? ia : ib) : 0.0f) : (k == C ? 1.0f : 0.0f);
+        if (i >= np) x = 0.0f;
+      }
       const _Float16 hv = (_Float16)x;
       hi.h[q] = hv;
       lo.h[q] = (_Float16)(x - (float)hv);
     }
-    uint4 *dst = table + (p0 / 16 + g) * (int64_t)(KT * 2 * 64) + t * 128 + ln;
+    uint4 *dst = table + (p0 / 16 + g) * (int64_t)(KT * 2 * 64) + t * 128 + lane;
     dst[0] = hi.u;
     dst[64] = lo.u;
   }

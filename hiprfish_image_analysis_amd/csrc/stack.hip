@@ -204,6 +204,27 @@ __device__ __forceinline__ void lay_load(const Lasers &L, const int *sdr, const 
   if constexpr (q + 1 < NL) lay_load<q + 1, NL>(L, sdr, sdc, r, c0, H, W, tid, v + U);
 }
 
+// The same loads through buffer descriptors (round 5): an element outside the laser's coverage
+// gets an out-of-range offset and reads 0 (the descriptor's range check), so the 25 loads issue
+// back to back with no exec-mask branches around them.  Offsets are 32-bit: each laser buffer
+// holds < 2 GiB (checked by the launch).  rbase[q] = ((r - dr) * W + c0 - dc) * cl, cok[q] packs
+// the strip's valid column range for laser q (wave-uniform, computed once per strip).
+template <int q, int NL>
+__device__ __forceinline__ void lay_load_buf(const __amdgpu_buffer_rsrc_t *rs, const int *rbase, const int *clo,
+                                             const int *chi, int tid, float *v) {
+  constexpr int cl = EcoliLasers<0>::cl(q);
+  constexpr int U = (AS_P * cl + 255) / 256;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + 256 * u;
+    const int pp = e / cl;
+    const bool ok = e < AS_P * cl && pp >= clo[q] && pp < chi[q];
+    const int off = ok ? (rbase[q] + e) * 4 : -1;
+    v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs[q], off, 0, 0));
+  }
+  if constexpr (q + 1 < NL) lay_load_buf<q + 1, NL>(rs, rbase, clo, chi, tid, v + U);
+}
+
 template <int q, int NL>
 __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) {
   constexpr int cl = EcoliLasers<0>::cl(q), off = EcoliLasers<0>::off(q);
@@ -221,10 +242,12 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 
 // Strips t = blockIdx.x, + gridDim.x, ... (row t / nsx, columns (t % nsx) * 64 ..): launched on a
 // resident grid (round 3), a 2048^2 tile is ~1.5 k workgroup dispatches instead of 65 k -- under
-// the concurrent classifier every dispatch waits for a CU slot.  Per strip unchanged.
+// the concurrent classifier every dispatch waits for a CU slot.  Per strip: loads -> barrier ->
+// channel sums and segment norms (the tile only read) -> barrier -> flags, image_cn's log and the
+// table entries -> barrier.
 // (Round 3 also built a prefetching form -- the next strip's loads in flight through this strip's
 // image_cn and pixel-table phases -- equal end to end; removed in round 5.)
-template <int WPE = 2>
+template <int WPE, bool BUF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
@@ -234,16 +257,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ uint8_t okp[AS_P];
   __shared__ int sdr[LMAX], sdc[LMAX];
   __shared__ uint32_t fl[AS_P];
-  __shared__ double cns[AS_P];  // the strip's channel sums, to prep_tile_ecoli (pixel-table mode)
+  __shared__ double cns[AS_P];  // the strip's channel sums (pixel-table mode: logged in the table phase)
+  __shared__ float invs[5 * AS_P];  // reciprocal segment norms (hrf_pix::ecoli_norms)
   load_shifts(L, sdr, sdc);
   const int tid = threadIdx.x;
-  const int64_t nsx = (W + AS_P - 1) / AS_P, nstrip = nsx * H;
   constexpr int UT = 8 + 6 + 5 + 4 + 2;
   float v[UT];
-  for (int64_t t = blockIdx.x; t < nstrip; t += gridDim.x) {
-  const int64_t r = t / nsx;
-  const int64_t c0 = (t - r * nsx) * AS_P;
-  const int np = (int)min((int64_t)AS_P, W - c0);
+  // strips t = blockIdx.x, + gridDim.x, ...: (row, column strip) stepped incrementally in 32 bits
+  // (H * W < 2^31), no per-strip 64-bit division
+  const int nsx = (int)((W + AS_P - 1) / AS_P), Hi = (int)H, Wi = (int)W;
+  const int gstep_r = (int)(gridDim.x / nsx), gstep_c = (int)(gridDim.x % nsx);
+  int ri = (int)(blockIdx.x / nsx), csi = (int)(blockIdx.x % nsx);
+  for (; ri < Hi; ri += gstep_r + (csi + gstep_c >= nsx), csi = csi + gstep_c >= nsx ? csi + gstep_c - nsx : csi + gstep_c) {
+  const int64_t r = ri;
+  const int64_t c0 = (int64_t)csi * AS_P;
+  const int np = min(AS_P, Wi - csi * AS_P);
   if (tid < AS_P) {
     bool ok = tid < np;
     if (apply_mask)
@@ -251,7 +279,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     okp[tid] = (uint8_t)ok;
     fl[tid] = 0;
   }
-  if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
+  if (BUF) {
+    // per laser: the strip's source offset and its valid pixel range [clo, chi) (row outside the
+    // laser's coverage: empty)
+    int rbase[5], clo[5], chi[5];
+    __amdgpu_buffer_rsrc_t rs[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int dr = __builtin_amdgcn_readfirstlane(sdr[q]), dc = __builtin_amdgcn_readfirstlane(sdc[q]);
+      rs[q] = __builtin_amdgcn_make_buffer_rsrc((void *)L.src[q], (short)0, (int)(H * W * EcoliLasers<0>::cl(q) * 4),
+                                                0x00020000);
+      const bool row_ok = ri >= (dr > 0 ? dr : 0) && ri < Hi + (dr < 0 ? dr : 0);
+      const int cmin = dc > 0 ? dc : 0, cmax = min(Wi + (dc < 0 ? dc : 0), Wi);
+      const int c0i = csi * AS_P;
+      clo[q] = row_ok ? max(cmin - c0i, 0) : AS_P;
+      chi[q] = row_ok ? min(cmax - c0i, np) : 0;
+      rbase[q] = ((ri - dr) * Wi + (c0i - dc)) * EcoliLasers<0>::cl(q);
+    }
+    if (WPE >= 4) {
+      lay_load_buf<0, 2>(rs, rbase, clo, chi, tid, v);
+      lay_store<0, 2>(tile, tid, v);
+      lay_load_buf<2, 5>(rs, rbase, clo, chi, tid, v);
+      lay_store<2, 5>(tile, tid, v);
+    } else {
+      lay_load_buf<0, 5>(rs, rbase, clo, chi, tid, v);
+      lay_store<0, 5>(tile, tid, v);
+    }
+  } else if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
     lay_load<0, 2>(L, sdr, sdc, r, c0, H, W, tid, v);
     lay_store<0, 2>(tile, tid, v);
     lay_load<2, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
@@ -282,11 +336,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int e = tid; e < n; e += 256) out[e] = (!apply_mask || okp[e / C]) ? tile[e] : 0.0f;
   }
   if (cn_out) {
+    // 8 lanes per pixel; a 32-lane group takes pixels g, g + 8, g + 16, g + 24 (g = tid >> 5), so
+    // with the odd row stride its reads fall in 32 distinct banks
     const int j = tid & 7;
     constexpr int main_n = C - (C % 8);
-#pragma unroll
+#pragma unroll 1
     for (int half = 0; half < 2; ++half) {
-      const int pi = half * 32 + (tid >> 3);
+      const int pi = half * 32 + (tid >> 5) + 8 * ((tid >> 3) & 3);
       const float *a = tile + (pi < np ? pi : 0) * C;
       const bool ok = pi < np && (!apply_mask || okp[pi]);
       double rr = ok ? (double)a[j] : 0.0;
@@ -299,7 +355,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       if (j == 0)
         for (int i = main_n; i < C; ++i) res += ok ? (double)a[i] : 0.0;
       if (j == 0 && pi < np) {
-        if (ptab) {  // the log is taken once per pixel in prep_tile_ecoli
+        if (ptab) {  // the log is taken once per pixel in the table phase
           cns[pi] = res;
         } else {
           double sv = 0.0 + res;
@@ -311,31 +367,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
   }
   if (ptab) {  // the classifier's operands from the same tile (pixtable.hpp); W % 16 == 0
+    const uint8_t *okm = apply_mask ? okp : nullptr;
+    hrf_pix::ecoli_norms(tile, okm, np, invs, fl);  // beside the channel sums: the tile is only read
     __syncthreads();
-    hrf_pix::prep_tile_ecoli<false>(tile, apply_mask ? okp : nullptr, np, r * W + c0, ptab, pflags, fl,
-                                 cn_out ? cns : nullptr, cn_mode, cn_out);
+    const int64_t p0 = r * W + c0;
+    if (tid < np) {
+      pflags[p0 + tid] = (uint8_t)fl[tid];
+      if (cn_out) {
+        double sv = 0.0 + cns[tid];
+        if (cn_mode == 1) sv = hrf_cr_log(sv + 1e-2);
+        else if (cn_mode == 2) sv = hrf_cr_log10(sv + 1.0);
+        cn_out[p0 + tid] = sv;
+      }
+    }
+    hrf_pix::ecoli_table(tile, okm, np, p0, invs, ptab);
   }
-  __syncthreads();  // the next strip rewrites tile, okp and fl
+  __syncthreads();  // the next strip rewrites tile, okp, fl, invs and cns
   }
 }
 
-// E. coli assembly launch: a resident grid of the kernel built for three workgroups per CU with
-// the pixel table (165 VGPRs, no spills; 1035 vs 991 Mpix/s end to end against the 2-per-CU build,
-// isolated 1.03 vs 1.38 ms; 4 per CU spills and loses, 985) and for four without it (the
-// stack-writing form: 0.650 vs 0.687 ms).  One workgroup per strip instead of the resident grid
-// lost in round 3 (the switch was removed in round 5).
-template <int WPE>
-void launch_assemble_t(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
+// E. coli assembly launch: a resident grid of the kernel built for four workgroups per CU (128
+// VGPRs, no spills).  Round 5: the pixel-table form no longer normalises the tile in place (the
+// norms share the channel sums' barrier interval, the table applies them), the channel-sum reads
+// are bank-conflict free and the loads go through buffer descriptors: 0.98 -> 0.92 ms alone,
+// per-pixel-off line +4 % (profiles/r5_asm_ab.txt); it was three per CU (165 VGPRs) in rounds 3-4,
+// where four spilled.  One workgroup per strip instead of the resident grid lost in round 3.
+template <bool BUF>
+void launch_assemble_b(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                        uint4 *table, uint8_t *flags, hipStream_t s) {
   const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
-  const unsigned grid = hrf::resident_grid(assemble_ecoli_kernel<WPE>, 256, 0, nstrip);
-  assemble_ecoli_kernel<WPE><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
+  const unsigned grid = hrf::resident_grid(assemble_ecoli_kernel<4, BUF>, 256, 0, nstrip);
+  assemble_ecoli_kernel<4, BUF><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
 }
 
 void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                      uint4 *table, uint8_t *flags, hipStream_t s) {
-  if (table == nullptr) launch_assemble_t<4>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
-  else launch_assemble_t<3>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  // buffer-descriptor loads while every laser buffer (H W 32 floats at most) is < 2 GiB
+  if (H * W * 32 * 4 < ((int64_t)1 << 31))
+    launch_assemble_b<true>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
+  else
+    launch_assemble_b<false>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags, s);
 }
 
 // numpy pairwise_sum over n f32 values (as f64), n <= 512
