@@ -123,3 +123,51 @@ def test_label_sums_lasers_adversarial(mods, W, apply_mask):
         assert torch.equal(torch.isnan(gs), torch.isnan(ws))
         inf = torch.isinf(ws)
         assert torch.equal(gs[inf], ws[inf])
+
+
+@pytest.mark.parametrize("apply_mask", [True, False])
+def test_assembly_pixtable_large_shifts(mods, apply_mask):
+    """the E. coli assembly's buffer-descriptor loads against register_assemble + pixtable_prepare
+    on random spectra: shifts past a 64-pixel strip in both directions and past whole rows,
+    a width with a partial last strip (W % 64 == 16), zeros, negative values and an all-zero
+    segment in some pixels"""
+    K, P, S = mods
+    H, W = 75, 208
+    rng = np.random.default_rng(11 + apply_mask)
+    chans = [32, 23, 20, 14, 6]
+    las = [rng.random((H, W, c), dtype=np.float32) for c in chans]
+    las[0][5:9] = 0.0                                  # an all-zero first segment
+    las[2][20:22, :, 3] = -0.25                        # negative values (the flag's bit 7)
+    lasers = [torch.from_numpy(x).cuda() for x in las]
+    shifts = torch.tensor([[0, 0], [3, -5], [-7, 2], [12, 70], [-20, -67]], dtype=torch.int32).cuda()
+    want_stack, want_cn = K.register_assemble(lasers, shifts, apply_mask, cn_mode=1)
+    cn, pt, st = K.register_assemble_pixtable(lasers, shifts, apply_mask, want_stack=True)
+    assert torch.equal(st, want_stack) and torch.equal(cn, want_cn)
+    ref_pt = K.pixtable_prepare(want_stack, S.ECOLI_BOUNDS)
+    assert torch.equal(pt.flags, ref_pt.flags)
+    nb = H * W // 16 * 6144                            # the groups' entries (past them: allocation padding)
+    assert torch.equal(pt.table[:nb], ref_pt.table[:nb])
+    assert torch.equal(K.register_assemble_cn_only(lasers, shifts, apply_mask), cn)
+
+
+def test_assembly_pixtable_past_2gib_lasers(mods):
+    """4096 x 4096: the 32-channel laser is 2 GiB, past the buffer-descriptor loads' 32-bit range,
+    so the assembly takes its flat-address loads; the same table and image_cn as the composed path
+    on a band of rows (bit for bit)"""
+    K, P, S = mods
+    H = W = 4096
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    lasers = [torch.rand((H, W, c), generator=g, device="cuda") for c in (32, 23, 20, 14, 6)]
+    shifts = torch.tensor([[0, 0], [2, -3], [-4, 1], [5, 6], [-1, -7]], dtype=torch.int32).cuda()
+    cn, pt, _ = K.register_assemble_pixtable(lasers, shifts, False)
+    band = [l[1000:1064].contiguous() for l in lasers]
+    # the band's own assembly with the same shifts differs only where a shift reaches outside the
+    # band (|dr| <= 5): compare its rows 8 .. 55
+    want_stack, want_cn = K.register_assemble(band, shifts, False, cn_mode=1)
+    full_mask_rows = slice(1008, 1056)
+    assert torch.equal(cn[full_mask_rows], want_cn[8:56])
+    ref_pt = K.pixtable_prepare(want_stack[8:56].contiguous(), S.ECOLI_BOUNDS)
+    rows = pt.table[:H * W // 16 * 6144].view(H * W // 16, -1)[1008 * W // 16:1056 * W // 16]
+    assert torch.equal(rows, ref_pt.table[:48 * W // 16 * 6144].view(48 * W // 16, -1))
+    del lasers, band
