@@ -228,7 +228,10 @@ def path_kernel_rows(lasers, cal, lib):
     tb = int(_lib.lib().hrf_pixtable_bytes(HW, C, b.ctypes.data, len(b) - 1))
     torch.cuda.synchronize()
     return {
-        "channel_max_multi": (lambda: K.channel_max_multi(lasers, stacked=True), HW * (4 * C + 5 * 8)),
+        # the tile path's launch: 512 workgroups (tile.hip TILE_CHANMAX_WG); the default grid's time is
+        # reported beside it (_hbm_kernels)
+        "channel_max_multi": (lambda: K.channel_max_multi(lasers, stacked=True, max_workgroups=512),
+                              HW * (4 * C + 5 * 8)),
         "assemble_pixtable": (lambda: K.register_assemble_pixtable(lasers, shifts, True, cn_mode=1),
                               HW * 4 * C + tb + HW // 16 + HW * 8),
         "label_sums_lasers_cal": (lambda: K.label_sums_lasers(lasers, shifts, seg, maxlab, True, cal=cal,
@@ -242,6 +245,7 @@ def _hbm_kernels(lasers, cal, lib):
     algorithmic bytes per launch / mean launch time (HIP events) against the 8 TB/s peak, with the
     HBM traffic of the same launches from the committed PMC passes (profiles/hbm_kernels_pmc.json,
     tools/gpu_pmc_hbm.sh)."""
+    from hiprfish_image_analysis_amd import kernels as K
     rows, info = path_kernel_rows(lasers, cal, lib)
     pmc = {}
     try:
@@ -257,6 +261,11 @@ def _hbm_kernels(lasers, cal, lib):
                      "achieved_GBps": round(gbs, 1), "peak_GBps": 8000.0, "frac": round(gbs / 8000.0, 4),
                      "traffic": rec.get("hbm_bytes_per_launch"),
                      "traffic_ratio": rec.get("traffic_ratio"), "pmc_round": pmc.get("round")}
+    ms = _event_ms(lambda: K.channel_max_multi(lasers, stacked=True), 10)
+    out["channel_max_multi"]["default_grid"] = {
+        "ms": round(ms, 4), "frac": round(out["channel_max_multi"]["algorithmic_bytes"] / (ms * 1e-3) / 8e12, 4),
+        "note": "the same projections on the default 4096-workgroup grid (the fastest alone); the tile "
+                "path runs them on 512 workgroups, slower alone but +1.4 % end to end (DESIGN.md)"}
     out["tile"] = info
     return out
 

@@ -1309,7 +1309,14 @@ hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, double *
 
 hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *channels_host, int32_t nlaser,
                                  int64_t npix, double *const *out_host, hrf_stream_t stream) {
+  return hrf_channel_max_multi_grid(src_host, channels_host, nlaser, npix, out_host, 0, stream);
+}
+
+hrf_status hrf_channel_max_multi_grid(const float *const *src_host, const int32_t *channels_host, int32_t nlaser,
+                                      int64_t npix, double *const *out_host, int32_t max_workgroups,
+                                      hrf_stream_t stream) {
   HRF_REQUIRE(nlaser >= 1 && nlaser <= LMAX && src_host && channels_host && out_host, "channel_max_multi: bad lasers");
+  HRF_REQUIRE(max_workgroups >= 0, "channel_max_multi: bad workgroup budget");
   if (npix == 0) return HRF_OK;
   MaxJob J{};
   J.n = nlaser;
@@ -1327,7 +1334,9 @@ hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *ch
     cmax = std::max(cmax, (int)channels_host[i]);
   }
   const int64_t chunks = hrf::cdiv(npix, CM_P);
-  const int64_t total = std::min<int64_t>(chunks * nlaser, 4096);
+  // 4096 workgroups by default (two rounds on 256 CUs, the fastest alone); the tile path passes a
+  // smaller budget (tile.hip)
+  const int64_t total = std::min<int64_t>(chunks * nlaser, max_workgroups > 0 ? max_workgroups : 4096);
   int wg = 0;
   for (int i = 0; i < nlaser; ++i) {
     J.wg0[i] = wg;

@@ -25,6 +25,7 @@ constexpr int NL = 5;                                    // E. coli lasers 405, 
 constexpr int32_t CH[NL] = {32, 23, 20, 14, 6};          // channels per laser (ecoli :51-70)
 constexpr int32_t BOUNDS[NL + 1] = {0, 32, 55, 75, 89, 95};
 constexpr int32_t C = 95;
+constexpr int32_t TILE_CHANMAX_WG = 512;  // the projections' workgroup budget in the tile path
 
 template <class T>
 hrf_status dalloc(T **p, size_t count) {
@@ -199,7 +200,10 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
   // ecoli :45-57 shifts of the channel-max projections, on the device
   double *proj[NL];
   for (int l = 0; l < NL; ++l) proj[l] = t->proj + l * n;
-  HRF_TRY(hrf_channel_max_multi(lasers_host, CH, NL, n, proj, s));
+  // on 512 workgroups (two per CU): slower alone (0.77 vs 0.39 ms) but it leaves room on every CU
+  // for the concurrent tiles' classifier workgroups -- +1.4 % end to end, 5 of 5 interleaved runs
+  // (profiles/r5_chanmax_grid_ab.txt)
+  HRF_TRY(hrf_channel_max_multi_grid(lasers_host, CH, NL, n, proj, TILE_CHANMAX_WG, s));
   if (t->pow2) {
     HRF_TRY(hrf_xcorr_shifts_dev(t->proj, NL, H, W, t->xwork, 15, t->shifts, s));
   } else {  // row 0 = (0, 0); the reference's transform is taken once (src == NULL reuses it)

@@ -204,9 +204,10 @@ def channel_max(stack):
     return out
 
 
-def channel_max_multi(stacks, stacked=False):
+def channel_max_multi(stacks, stacked=False, max_workgroups=0):
     """[np.max(s, axis=2) for s in stacks] (f64) in one launch; the stacks share H x W.
-    stacked: return them as one (n, H, W) tensor instead of a list"""
+    stacked: return them as one (n, H, W) tensor instead of a list; max_workgroups: the launch's
+    workgroup budget (0: the default; the native tile path uses 512)"""
     import ctypes
     stacks = [_dev(s, torch.float32, "stack") for s in stacks]
     H, W = stacks[0].shape[:2]
@@ -217,8 +218,8 @@ def channel_max_multi(stacks, stacked=False):
     src = (ctypes.c_void_p * len(stacks))(*[s.data_ptr() for s in stacks])
     dst = (ctypes.c_void_p * len(stacks))(*[o.data_ptr() for o in outs])
     ch = _i32_host([s.shape[2] for s in stacks])
-    _lib.call("hrf_channel_max_multi", ctypes.cast(src, ctypes.c_void_p), ch.ctypes.data, len(stacks), H * W,
-              ctypes.cast(dst, ctypes.c_void_p), _stream())
+    _lib.call("hrf_channel_max_multi_grid", ctypes.cast(src, ctypes.c_void_p), ch.ctypes.data, len(stacks), H * W,
+              ctypes.cast(dst, ctypes.c_void_p), int(max_workgroups), _stream())
     return buf if stacked else outs
 
 

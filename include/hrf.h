@@ -145,6 +145,11 @@ HRF_API hrf_status hrf_channel_max(const float *stack, int64_t npix, int32_t C, 
  * ((npix x C_l) f32 -> npix f64) */
 HRF_API hrf_status hrf_channel_max_multi(const float *const *src_host, const int32_t *channels_host, int32_t nlaser,
                                          int64_t npix, double *const *out_host, hrf_stream_t stream);
+/* the same with a workgroup budget (0 = the default 4096): the tile path (hrf_tile_ecoli) runs the
+ * projections on 512 workgroups, which leaves room on every CU for concurrent tiles' work */
+HRF_API hrf_status hrf_channel_max_multi_grid(const float *const *src_host, const int32_t *channels_host,
+                                              int32_t nlaser, int64_t npix, double *const *out_host,
+                                              int32_t max_workgroups, hrf_stream_t stream);
 /* the calibrated stack as f64, out (npix, C) (multispecies :104 image_channel / :166 _registered.npy) */
 HRF_API hrf_status hrf_calibrate_f64(const float *stack, int64_t npix, int32_t C, const float *cal, int64_t cal_sp,
                                      int32_t cal_sc, int32_t cal_c0, int32_t cal_c1, double *out,
