@@ -247,8 +247,10 @@ __device__ __forceinline__ void lay_store(float *tile, int tid, const float *v) 
 // table entries -> barrier.
 // (Round 3 also built a prefetching form -- the next strip's loads in flight through this strip's
 // image_cn and pixel-table phases -- equal end to end; removed in round 5.)
-template <int WPE, bool BUF>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
+// Built for four workgroups per CU (128 VGPRs); the lasers are loaded in two rounds (lasers 0-1,
+// then 2-4) so fewer values are live at once.
+template <bool BUF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void assemble_ecoli_kernel(Lasers L, int64_t H, int64_t W, int apply_mask,
                                                              float *__restrict__ dst, double *__restrict__ cn_out,
                                                              int cn_mode, uint4 *__restrict__ ptab,
                                                              uint8_t *__restrict__ pflags) {
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ float invs[5 * AS_P];  // reciprocal segment norms (hrf_pix::ecoli_norms)
   load_shifts(L, sdr, sdc);
   const int tid = threadIdx.x;
-  constexpr int UT = 8 + 6 + 5 + 4 + 2;
+  constexpr int UT = 8 + 6;  // the larger load round (lasers 0-1)
   float v[UT];
   // strips t = blockIdx.x, + gridDim.x, ...: (row, column strip) stepped incrementally in 32 bits
   // (H * W < 2^31), no per-strip 64-bit division
@@ -296,23 +298,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       chi[q] = row_ok ? min(cmax - c0i, np) : 0;
       rbase[q] = ((ri - dr) * Wi + (c0i - dc)) * EcoliLasers<0>::cl(q);
     }
-    if (WPE >= 4) {
-      lay_load_buf<0, 2>(rs, rbase, clo, chi, tid, v);
-      lay_store<0, 2>(tile, tid, v);
-      lay_load_buf<2, 5>(rs, rbase, clo, chi, tid, v);
-      lay_store<2, 5>(tile, tid, v);
-    } else {
-      lay_load_buf<0, 5>(rs, rbase, clo, chi, tid, v);
-      lay_store<0, 5>(tile, tid, v);
-    }
-  } else if (WPE >= 4) {  // two load rounds (lasers 0-1, then 2-4): fewer values live at once
+    lay_load_buf<0, 2>(rs, rbase, clo, chi, tid, v);
+    lay_store<0, 2>(tile, tid, v);
+    lay_load_buf<2, 5>(rs, rbase, clo, chi, tid, v);
+    lay_store<2, 5>(tile, tid, v);
+  } else {
     lay_load<0, 2>(L, sdr, sdc, r, c0, H, W, tid, v);
     lay_store<0, 2>(tile, tid, v);
     lay_load<2, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
     lay_store<2, 5>(tile, tid, v);
-  } else {
-    lay_load<0, 5>(L, sdr, sdc, r, c0, H, W, tid, v);
-    lay_store<0, 5>(tile, tid, v);
   }
   __syncthreads();
   float *out = dst ? dst + (r * W + c0) * (int64_t)C : nullptr;
@@ -396,8 +390,8 @@ template <bool BUF>
 void launch_assemble_b(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
                        uint4 *table, uint8_t *flags, hipStream_t s) {
   const int64_t nstrip = hrf::cdiv(W, AS_P) * H;
-  const unsigned grid = hrf::resident_grid(assemble_ecoli_kernel<4, BUF>, 256, 0, nstrip);
-  assemble_ecoli_kernel<4, BUF><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
+  const unsigned grid = hrf::resident_grid(assemble_ecoli_kernel<BUF>, 256, 0, nstrip);
+  assemble_ecoli_kernel<BUF><<<grid, 256, 0, s>>>(L, H, W, apply_mask, dst, cn_out, cn_mode, table, flags);
 }
 
 void launch_assemble(const Lasers &L, int64_t H, int64_t W, int apply_mask, float *dst, double *cn_out, int cn_mode,
