@@ -171,6 +171,13 @@ def test_channel_max_multi_equals_per_laser(K):
         assert torch.equal(torch.isnan(o), torch.isnan(want))
         assert torch.equal(torch.nan_to_num(o), torch.nan_to_num(want))
     assert torch.isnan(outs[2][5, 7])
+    # the tile path's workgroup budget (hrf_channel_max_multi_grid): the same projections on any grid
+    for budget in (512, 7, 1):
+        got = K.channel_max_multi(lasers, max_workgroups=budget)
+        for o, g in zip(outs, got):
+            assert torch.equal(torch.isnan(o), torch.isnan(g)) and torch.equal(torch.nan_to_num(o), torch.nan_to_num(g))
+    with pytest.raises(ValueError):
+        K.channel_max_multi(lasers, max_workgroups=-1)
 
 
 def test_concurrent_registrations_equal_serial(K):
