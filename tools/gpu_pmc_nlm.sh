@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes over the NL-means kernel (tools/time_kernels.py nlmeans), one counter group per
-# rocprofv3 run; env (HRF_NLM_*) selects the variant.  usage: bash tools/gpu_pmc_nlm.sh <tag>
+# rocprofv3 run (HRF_LIB selects an A/B build).  usage: bash tools/gpu_pmc_nlm.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 out=gpurun_out/pmc_nlm_$1

@@ -1,9 +1,9 @@
 #!/bin/bash
 # lasers label sums, isolated (time_kernels.py path), alternating environment settings on one box
-# usage: bash tools/lsl_ab.sh "<env 1>" "<env 2>" ...   (default: the row-chunk kernel vs the general one)
+# usage: bash tools/lsl_ab.sh "<env 1>" "<env 2>" ...   (e.g. HRF_LIB=ab/libhrf_<tag>.so against HRF_NONE=1)
 set -e
 : > gpurun_out/lsl_ab.txt
-[ $# -eq 0 ] && set -- "HRF_LSL_X=0" "HRF_LSL_ROW=0"
+[ $# -eq 0 ] && { echo "usage: bash tools/lsl_ab.sh \"<env 1>\" \"<env 2>\" ..."; exit 2; }
 for i in 1 2 3; do
   for v in "$@"; do
     echo "== $v" >> gpurun_out/lsl_ab.txt
