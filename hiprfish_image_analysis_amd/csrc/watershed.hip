@@ -447,10 +447,13 @@ struct alignas(16) HeapItem {
 constexpr int32_t HEAP_LDS = 8191;
 constexpr size_t HEAP_LDS_BYTES = (size_t)HEAP_LDS * 16;
 
+// LDS-qualified pointers: through plain pointers the compiler emits FLAT instructions for the
+// heap's LDS levels (the generic address path, with global-memory latency)
+#define HRF_LDS __attribute__((address_space(3)))
 struct HeapView {
-  double *lv;
-  uint32_t *la;
-  int32_t *li;
+  HRF_LDS double *lv;
+  HRF_LDS uint32_t *la;
+  HRF_LDS int32_t *li;
   HeapItem *g;  // indexed by heap position (positions < HEAP_LDS unused)
   __device__ __forceinline__ HeapItem get(int32_t p) const {
     if (p < HEAP_LDS) return HeapItem{lv[p], la[p], li[p]};
@@ -521,6 +524,7 @@ __device__ HeapItem heap_pop(const HeapView &h, int32_t &n) {
 // One 1024-thread workgroup.  Phase 1 (all threads): out = markers where in the mask, and the
 // list of marker pixels in raster order (order-preserving compaction by ballots + a 16-wave
 // scan).  Phase 2 (thread 0): the flood.  heap: (n + 2) items; list: n int32.
+template <bool HASMASK>
 __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__restrict__ f, int negate,
                                                              const int32_t *__restrict__ markers,
                                                              const uint8_t *__restrict__ mask, int32_t H, int32_t W,
@@ -556,8 +560,8 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
   }
   if (tid != 0) return;
   __threadfence_block();  // the other waves' list and label stores, seen by thread 0's loads
-  HeapView h{(double *)heap_smem, (uint32_t *)(heap_smem + HEAP_LDS * 8), (int32_t *)(heap_smem + HEAP_LDS * 12),
-             heap};
+  HeapView h{(HRF_LDS double *)heap_smem, (HRF_LDS uint32_t *)(heap_smem + HEAP_LDS * 8),
+             (HRF_LDS int32_t *)(heap_smem + HEAP_LDS * 12), heap};
   const int32_t nm = base_s;
   int32_t hn = 0;
   for (int32_t k = 0; k < nm; ++k) {
@@ -566,20 +570,33 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
   }
   uint32_t age = 1;
   while (hn > 0) {
-    const HeapItem e = heap_pop(h, hn);
-    const int32_t x = e.idx, r = x / W, c = x - r * W;
+    // the item this iteration pops is the root: its pixel's neighbour state is loaded first, and
+    // the sift-down (heap memory only) runs while those loads are in flight
+    const int32_t x = h.get(0).idx, r = x / W, c = x - r * W;
     const bool ok[4] = {r > 0, c > 0, c + 1 < W, r + 1 < H};
     const int32_t nb[4] = {x - W, x - 1, x + 1, x + W};
-    // the four neighbours' state, read before any of them is written (distinct pixels)
+    // the four neighbours' state, read before any of them is written (distinct pixels): every
+    // load unconditional (a neighbour off the image reads the pixel itself) and combined without
+    // short-circuits, so the twelve loads are one round trip instead of a chain of eight
     bool free_[4];
     double v[4];
+    int32_t q[4], oq[4];
+    uint32_t mq[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) q[d] = ok[d] ? nb[d] : x;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
-      const int32_t q = ok[d] ? nb[d] : x;
-      free_[d] = ok[d] && (!mask || mask[q]) && out[q] == 0;
-      v[d] = negate ? -f[q] : f[q];
+      mq[d] = HASMASK ? mask[q[d]] : 1u;
+      oq[d] = out[q[d]];
+      v[d] = f[q[d]];
     }
     const int32_t lab = out[x];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      free_[d] = ok[d] & (mq[d] != 0u) & (oq[d] == 0);
+      if (negate) v[d] = -v[d];
+    }
+    (void)heap_pop(h, hn);
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       if (!free_[d]) continue;
@@ -600,17 +617,24 @@ hrf_status heap_flood(const double *image, int32_t negate, const int32_t *marker
   char *scratch = nullptr;
   HRF_HIP(hipMallocAsync((void **)&scratch, (size_t)heap_flood_scratch_bytes(n), s));
   static const bool attr = [] {
-    return hipFuncSetAttribute((const void *)ws_heap_flood_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)HEAP_LDS_BYTES) == hipSuccess;
+    return hipFuncSetAttribute((const void *)ws_heap_flood_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)HEAP_LDS_BYTES) == hipSuccess &&
+           hipFuncSetAttribute((const void *)ws_heap_flood_kernel<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)HEAP_LDS_BYTES) == hipSuccess;
   }();
   hrf_status st = HRF_OK;
   if (!attr) {
     ::hrf::set_error("watershed heap replay: cannot reserve %d bytes of LDS", (int)HEAP_LDS_BYTES);
     st = HRF_EHIP;
   } else {
-    ws_heap_flood_kernel<<<1, 1024, HEAP_LDS_BYTES, s>>>(image, negate, markers, mask, (int32_t)H, (int32_t)W, out,
-                                                         (HeapItem *)scratch,
-                                                         (int32_t *)(scratch + (n + 2) * 16));
+    HeapItem *hp = (HeapItem *)scratch;
+    int32_t *lp = (int32_t *)(scratch + (n + 2) * 16);
+    if (mask)
+      ws_heap_flood_kernel<true><<<1, 1024, HEAP_LDS_BYTES, s>>>(image, negate, markers, mask, (int32_t)H, (int32_t)W,
+                                                                 out, hp, lp);
+    else
+      ws_heap_flood_kernel<false><<<1, 1024, HEAP_LDS_BYTES, s>>>(image, negate, markers, mask, (int32_t)H,
+                                                                  (int32_t)W, out, hp, lp);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       ::hrf::set_error("watershed heap replay: launch failed: %s", hipGetErrorString(e));
