@@ -437,7 +437,7 @@ __global__ void ws_reset_labels_kernel(const int32_t *__restrict__ markers, cons
 // reference era, restated in oracle_watershed): markers pushed in raster order with age 0,
 // (value, age) binary heap with strict-less sift up and down, the four neighbours visited up,
 // left, right, down, a pixel labelled when pushed.  The top 13 levels of the heap (8191 items)
-// live in LDS as separate value / age / index arrays, deeper items in global memory (16 B each).
+// live in LDS, deeper items in global memory (16 B each).
 // Serial by nature; rare (no bench tile needs it).
 struct alignas(16) HeapItem {
   double v;
@@ -447,25 +447,32 @@ struct alignas(16) HeapItem {
 constexpr int32_t HEAP_LDS = 8191;
 constexpr size_t HEAP_LDS_BYTES = (size_t)HEAP_LDS * 16;
 
-// LDS-qualified pointers: through plain pointers the compiler emits FLAT instructions for the
-// heap's LDS levels (the generic address path, with global-memory latency)
+// LDS-qualified pointer: through a plain pointer the compiler emits FLAT instructions for the
+// heap's LDS levels (the generic address path, with global-memory latency).  An item is one
+// 16-byte read or write on either side (ds_read_b128 / global_load_dwordx4).
 #define HRF_LDS __attribute__((address_space(3)))
+typedef uint32_t heap_u4 __attribute__((ext_vector_type(4)));
 struct HeapView {
-  HRF_LDS double *lv;
-  HRF_LDS uint32_t *la;
-  HRF_LDS int32_t *li;
-  HeapItem *g;  // indexed by heap position (positions < HEAP_LDS unused)
-  __device__ __forceinline__ HeapItem get(int32_t p) const {
-    if (p < HEAP_LDS) return HeapItem{lv[p], la[p], li[p]};
-    return g[p];
-  }
+  HRF_LDS heap_u4 *l;  // positions < HEAP_LDS
+  HeapItem *g;         // indexed by heap position (positions < HEAP_LDS unused)
+  __device__ __forceinline__ HeapItem lds(int32_t p) const { return __builtin_bit_cast(HeapItem, l[p]); }
+  __device__ __forceinline__ HeapItem get(int32_t p) const { return p < HEAP_LDS ? lds(p) : g[p]; }
   __device__ __forceinline__ void put(int32_t p, const HeapItem &x) const {
-    if (p < HEAP_LDS) {
-      lv[p] = x.v;
-      la[p] = x.age;
-      li[p] = x.idx;
-    } else {
+    if (p < HEAP_LDS)
+      l[p] = __builtin_bit_cast(heap_u4, x);
+    else
       g[p] = x;
+  }
+  // N items from position p on, all on one level (so all in LDS or all in global memory): the
+  // loads issue together, one round trip
+  template <int N>
+  __device__ __forceinline__ void get_run(int32_t p, HeapItem *out) const {
+    if (p < HEAP_LDS) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) out[k] = lds(p + k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; ++k) out[k] = g[p + k];
     }
   }
 };
@@ -489,8 +496,35 @@ __device__ void heap_push(const HeapView &h, int32_t &n, const HeapItem &x) {
   h.put(c, x);
 }
 
-// heappop: the last item moves to the root and sifts down to the smaller child (left wins
-// unless the right one is strictly smaller) while that child is strictly smaller than it
+// field by field, so the item arrays stay in registers
+__device__ __forceinline__ HeapItem heap_select(bool c, const HeapItem &a, const HeapItem &b) {
+  return HeapItem{c ? a.v : b.v, c ? a.age : b.age, c ? a.idx : b.idx};
+}
+
+// one sift-down level: the hole at i (children l, l + 1, given) moves to the smaller child (left
+// wins unless the right one is strictly smaller) while that child is strictly smaller than x
+__device__ __forceinline__ bool sift_level(const HeapView &h, int32_t n, const HeapItem &x, int32_t &i, int32_t l,
+                                           const HeapItem &L, const HeapItem &R) {
+  int32_t s = i;
+  HeapItem b = x;
+  if (heap_smaller(L, x)) {
+    s = l;
+    b = L;
+  }
+  if (l + 1 < n && heap_smaller(R, b)) {
+    s = l + 1;
+    b = R;
+  }
+  if (s == i) return false;
+  h.put(i, b);
+  i = s;
+  return true;
+}
+
+// heappop: the last item moves to the root and sifts down.  Two levels per round trip: the
+// hole's two children and four grandchildren are loaded together (the grandchildren are
+// contiguous, on one level); positions at or past n are never used, and clamped to the first
+// grandchild (which is inside the heap whenever any grandchild is) so no load leaves it.
 __device__ HeapItem heap_pop(const HeapView &h, int32_t &n) {
   const HeapItem top = h.get(0);
   n -= 1;
@@ -500,22 +534,31 @@ __device__ HeapItem heap_pop(const HeapView &h, int32_t &n) {
   for (;;) {
     const int32_t l = 2 * i + 1;
     if (l >= n) break;
-    const int32_t r = l + 1;
-    const HeapItem L = h.get(l);
-    const HeapItem R = h.get(r);  // position n (one past the heap) is allocated: read, unused
-    int32_t s = i;
-    HeapItem b = x;
-    if (heap_smaller(L, x)) {
-      s = l;
-      b = L;
+    const int32_t g0 = 2 * l + 1;
+    HeapItem C[2], G[4];
+    h.get_run<2>(l, C);  // position n (one past the heap) is allocated: read, unused
+    if (g0 < n) {
+      if (g0 + 3 < n) {
+        h.get_run<4>(g0, G);
+      } else {
+        // past the heap: the first grandchild again
+        int32_t p[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) p[k] = g0 + k < n ? g0 + k : g0;
+        if (g0 < HEAP_LDS) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) G[k] = h.lds(p[k]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) G[k] = h.g[p[k]];
+        }
+      }
     }
-    if (r < n && heap_smaller(R, b)) {
-      s = r;
-      b = R;
-    }
-    if (s == i) break;
-    h.put(i, b);
-    i = s;
+    if (!sift_level(h, n, x, i, l, C[0], C[1])) break;
+    const int32_t l2 = 2 * i + 1;
+    if (l2 >= n) break;
+    const bool right = i != l;  // the hole went to the right child: its children are G[2], G[3]
+    if (!sift_level(h, n, x, i, l2, heap_select(right, G[2], G[0]), heap_select(right, G[3], G[1]))) break;
   }
   h.put(i, x);
   return top;
@@ -530,7 +573,7 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
                                                              const uint8_t *__restrict__ mask, int32_t H, int32_t W,
                                                              int32_t *__restrict__ out, HeapItem *__restrict__ heap,
                                                              int32_t *__restrict__ list) {
-  extern __shared__ char heap_smem[];
+  extern __shared__ HeapItem heap_smem[];
   __shared__ int32_t wsum[16];
   __shared__ int32_t base_s;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -560,8 +603,7 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
   }
   if (tid != 0) return;
   __threadfence_block();  // the other waves' list and label stores, seen by thread 0's loads
-  HeapView h{(HRF_LDS double *)heap_smem, (HRF_LDS uint32_t *)(heap_smem + HEAP_LDS * 8),
-             (HRF_LDS int32_t *)(heap_smem + HEAP_LDS * 12), heap};
+  HeapView h{(HRF_LDS heap_u4 *)heap_smem, heap};
   const int32_t nm = base_s;
   int32_t hn = 0;
   for (int32_t k = 0; k < nm; ++k) {
