@@ -438,7 +438,8 @@ __global__ void ws_reset_labels_kernel(const int32_t *__restrict__ markers, cons
 // (value, age) binary heap with strict-less sift up and down, the four neighbours visited up,
 // left, right, down, a pixel labelled when pushed.  The top 13 levels of the heap (8191 items)
 // live in LDS, deeper items in global memory (16 B each).
-// Serial by nature; rare (no bench tile needs it).
+// The flood is serial; one wave runs it, its lanes spreading each heap operation's loads and
+// compares (below).  Rare: no bench tile needs it.
 struct alignas(16) HeapItem {
   double v;
   uint32_t age;
@@ -455,25 +456,14 @@ typedef uint32_t heap_u4 __attribute__((ext_vector_type(4)));
 struct HeapView {
   HRF_LDS heap_u4 *l;  // positions < HEAP_LDS
   HeapItem *g;         // indexed by heap position (positions < HEAP_LDS unused)
-  __device__ __forceinline__ HeapItem lds(int32_t p) const { return __builtin_bit_cast(HeapItem, l[p]); }
-  __device__ __forceinline__ HeapItem get(int32_t p) const { return p < HEAP_LDS ? lds(p) : g[p]; }
+  __device__ __forceinline__ HeapItem get(int32_t p) const {
+    return p < HEAP_LDS ? __builtin_bit_cast(HeapItem, l[p]) : g[p];
+  }
   __device__ __forceinline__ void put(int32_t p, const HeapItem &x) const {
     if (p < HEAP_LDS)
       l[p] = __builtin_bit_cast(heap_u4, x);
     else
       g[p] = x;
-  }
-  // N items from position p on, all on one level (so all in LDS or all in global memory): the
-  // loads issue together, one round trip
-  template <int N>
-  __device__ __forceinline__ void get_run(int32_t p, HeapItem *out) const {
-    if (p < HEAP_LDS) {
-#pragma unroll
-      for (int k = 0; k < N; ++k) out[k] = lds(p + k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < N; ++k) out[k] = g[p + k];
-    }
   }
 };
 
@@ -483,90 +473,86 @@ __device__ __forceinline__ bool heap_smaller(const HeapItem &a, const HeapItem &
   return a.age < b.age;
 }
 
-// heappush: the new item sifts up while strictly smaller than its parent
-__device__ void heap_push(const HeapView &h, int32_t &n, const HeapItem &x) {
-  int32_t c = n++;
-  while (c > 0) {
-    const int32_t p = (c + 1) / 2 - 1;
-    const HeapItem P = h.get(p);
-    if (!heap_smaller(x, P)) break;
-    h.put(c, P);
-    c = p;
-  }
-  h.put(c, x);
+__device__ __forceinline__ int32_t heap_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ double heap_uni(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                                        (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b));
+}
+__device__ __forceinline__ double heap_lane(double v, int src) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  return __builtin_bit_cast(double,
+                            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(b >> 32), src) << 32) |
+                                (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src));
 }
 
-// field by field, so the item arrays stay in registers
-__device__ __forceinline__ HeapItem heap_select(bool c, const HeapItem &a, const HeapItem &b) {
-  return HeapItem{c ? a.v : b.v, c ? a.age : b.age, c ? a.idx : b.idx};
+// heappush, one wave: the new item x sifts up while strictly smaller than its parent.  The
+// ancestors do not change while it climbs (each only moves down one level), so every "x smaller
+// than ancestor j" is decided at once: lane j loads ancestor j of the new slot c, one ballot
+// gives the climb height t (the run of ones from bit 1), lanes 1..t move their ancestors down
+// one level in one store, lane 0 stores x.  One round trip per push instead of one per level.
+__device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const HeapItem &x, int lane) {
+  const int32_t c = n++;
+  const int32_t pj = lane < 32 ? ((c + 1) >> lane) - 1 : -1;  // ancestor lane of c (lane 0: c)
+  const bool va = lane >= 1 && pj >= 0;
+  HeapItem A{0.0, 0u, 0};
+  if (va) A = h.get(pj);
+  const unsigned long long m = __ballot(va && heap_smaller(x, A));
+  const int t = __builtin_ctzll(~(m >> 1));  // bits 1..t set: x climbs t levels
+  if (lane >= 1 && lane <= t) h.put(((c + 1) >> (lane - 1)) - 1, A);
+  if (lane == 0) h.put(((c + 1) >> t) - 1, x);
 }
 
-// one sift-down level: the hole at i (children l, l + 1, given) moves to the smaller child (left
-// wins unless the right one is strictly smaller) while that child is strictly smaller than x
-__device__ __forceinline__ bool sift_level(const HeapView &h, int32_t n, const HeapItem &x, int32_t &i, int32_t l,
-                                           const HeapItem &L, const HeapItem &R) {
-  int32_t s = i;
-  HeapItem b = x;
-  if (heap_smaller(L, x)) {
-    s = l;
-    b = L;
-  }
-  if (l + 1 < n && heap_smaller(R, b)) {
-    s = l + 1;
-    b = R;
-  }
-  if (s == i) return false;
-  h.put(i, b);
-  i = s;
-  return true;
-}
-
-// heappop: the last item moves to the root and sifts down.  Two levels per round trip: the
-// hole's two children and four grandchildren are loaded together (the grandchildren are
-// contiguous, on one level); positions at or past n are never used, and clamped to the first
-// grandchild (which is inside the heap whenever any grandchild is) so no load leaves it.
-__device__ HeapItem heap_pop(const HeapView &h, int32_t &n) {
-  const HeapItem top = h.get(0);
-  n -= 1;
-  if (n == 0) return top;
-  const HeapItem x = h.get(n);
-  int32_t i = 0;
+// heappop's sift-down of x (the heap's former last item) from the hole at the root, n items
+// left, one wave: SD_LEV levels per round trip.  Lane k < 2^SD_LEV - 1 takes the node k places
+// below the hole in breadth-first order (depth d = log2(k + 1), position hole * 2^d + k), loads
+// its two children and decides the three compares the sift can ask there -- left child smaller
+// than x, right child smaller than x, right smaller than left -- into three ballots.  The path
+// is then walked on those bits alone (the rule of heap_general.pxi: the hole moves to the left
+// child if it is smaller than x, unless the right one is smaller still; to the right child if
+// only it is smaller than x; else x stays), and every moved child is written into its parent by
+// the lane that holds it: one store per side.  A child at or past n is never smaller.
+constexpr int SD_LEV = 6;
+__device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, const HeapItem &x, int lane) {
+  const int k = lane;
+  const bool kl = k < (1 << SD_LEV) - 1;
+  const int d = 31 - __builtin_clz((unsigned)k + 1u);
+  int64_t hole = 0;  // wave-uniform
   for (;;) {
-    const int32_t l = 2 * i + 1;
-    if (l >= n) break;
-    const int32_t g0 = 2 * l + 1;
-    HeapItem C[2], G[4];
-    h.get_run<2>(l, C);  // position n (one past the heap) is allocated: read, unused
-    if (g0 < n) {
-      if (g0 + 3 < n) {
-        h.get_run<4>(g0, G);
+    const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
+    const bool vl = kl && l < n, vr = kl && r < n;
+    HeapItem L{0.0, 0u, 0}, R{0.0, 0u, 0};
+    if (vl) L = h.get((int32_t)l);
+    if (vr) R = h.get((int32_t)r);
+    const unsigned long long mlx = __ballot(vl && heap_smaller(L, x));
+    const unsigned long long mrx = __ballot(vr && heap_smaller(R, x));
+    const unsigned long long mrl = __ballot(vr && heap_smaller(R, L));
+    unsigned long long mvl = 0, mvr = 0;
+    int kk = 0, dep = 0;
+    for (; dep < SD_LEV; ++dep) {
+      const bool lx = (mlx >> kk) & 1ull;
+      const bool gor = lx ? ((mrl >> kk) & 1ull) : ((mrx >> kk) & 1ull);
+      if (!lx && !gor) break;
+      if (gor) {
+        mvr |= 1ull << kk;
+        kk = 2 * kk + 2;
       } else {
-        // past the heap: the first grandchild again
-        int32_t p[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) p[k] = g0 + k < n ? g0 + k : g0;
-        if (g0 < HEAP_LDS) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) G[k] = h.lds(p[k]);
-        } else {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) G[k] = h.g[p[k]];
-        }
+        mvl |= 1ull << kk;
+        kk = 2 * kk + 1;
       }
     }
-    if (!sift_level(h, n, x, i, l, C[0], C[1])) break;
-    const int32_t l2 = 2 * i + 1;
-    if (l2 >= n) break;
-    const bool right = i != l;  // the hole went to the right child: its children are G[2], G[3]
-    if (!sift_level(h, n, x, i, l2, heap_select(right, G[2], G[0]), heap_select(right, G[3], G[1]))) break;
+    if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
+    if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
+    // relative node kk at depth dep: position hole * 2^dep + kk
+    hole = (hole << dep) + kk;
+    if (dep < SD_LEV) break;
   }
-  h.put(i, x);
-  return top;
+  if (lane == 0) h.put((int32_t)hole, x);
 }
 
 // One 1024-thread workgroup.  Phase 1 (all threads): out = markers where in the mask, and the
 // list of marker pixels in raster order (order-preserving compaction by ballots + a 16-wave
-// scan).  Phase 2 (thread 0): the flood.  heap: (n + 2) items; list: n int32.
+// scan).  Phase 2 (wave 0): the flood.  heap: (n + 2) items; list: n int32.
 template <bool HASMASK>
 __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__restrict__ f, int negate,
                                                              const int32_t *__restrict__ markers,
@@ -601,50 +587,45 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
     }
     __syncthreads();
   }
-  if (tid != 0) return;
-  __threadfence_block();  // the other waves' list and label stores, seen by thread 0's loads
+  if (wv != 0) return;
+  __threadfence_block();  // the other waves' list and label stores, seen by wave 0's loads
   HeapView h{(HRF_LDS heap_u4 *)heap_smem, heap};
-  const int32_t nm = base_s;
+  const int32_t nm = heap_uni(base_s);
   int32_t hn = 0;
   for (int32_t k = 0; k < nm; ++k) {
-    const int32_t i = list[k];
-    heap_push(h, hn, HeapItem{negate ? -f[i] : f[i], 0u, i});
+    const int32_t i = heap_uni(list[k]);
+    const double fv = heap_uni(f[i]);
+    heap_push_w(h, hn, HeapItem{negate ? -fv : fv, 0u, i}, lane);
   }
   uint32_t age = 1;
   while (hn > 0) {
-    // the item this iteration pops is the root: its pixel's neighbour state is loaded first, and
-    // the sift-down (heap memory only) runs while those loads are in flight
-    const int32_t x = h.get(0).idx, r = x / W, c = x - r * W;
-    const bool ok[4] = {r > 0, c > 0, c + 1 < W, r + 1 < H};
-    const int32_t nb[4] = {x - W, x - 1, x + 1, x + W};
-    // the four neighbours' state, read before any of them is written (distinct pixels): every
-    // load unconditional (a neighbour off the image reads the pixel itself) and combined without
-    // short-circuits, so the twelve loads are one round trip instead of a chain of eight
-    bool free_[4];
-    double v[4];
-    int32_t q[4], oq[4];
-    uint32_t mq[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) q[d] = ok[d] ? nb[d] : x;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      mq[d] = HASMASK ? mask[q[d]] : 1u;
-      oq[d] = out[q[d]];
-      v[d] = f[q[d]];
+    // the popped pixel x (the root) and its four neighbours, up, left, right, down: lane d & 3
+    // loads neighbour d's state, read before any of them is written (distinct pixels); a
+    // neighbour off the image reads the pixel itself and is never free
+    const int32_t x = heap_uni(h.get(0).idx), r = x / W, c = x - r * W;
+    const int dn = lane & 3;
+    const bool okd = dn == 0 ? r > 0 : dn == 1 ? c > 0 : dn == 2 ? c + 1 < W : r + 1 < H;
+    const int32_t nbd = dn == 0 ? x - W : dn == 1 ? x - 1 : dn == 2 ? x + 1 : x + W;
+    const int32_t q = okd ? nbd : x;
+    const uint32_t mq = HASMASK ? mask[q] : 1u;
+    const int32_t oq = out[q];
+    const double vq = f[q];
+    const int32_t lab = heap_uni(out[x]);
+    hn -= 1;
+    if (hn > 0) {
+      const HeapItem last = h.get(hn);
+      heap_sift_down_w(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
+                       lane);
     }
-    const int32_t lab = out[x];
+    const unsigned long long fm = __ballot(lane < 4 && okd && mq != 0u && oq == 0);
+    const double vn = negate ? -vq : vq;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      free_[d] = ok[d] & (mq[d] != 0u) & (oq[d] == 0);
-      if (negate) v[d] = -v[d];
-    }
-    (void)heap_pop(h, hn);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      if (!free_[d]) continue;
+    for (int dd = 0; dd < 4; ++dd) {
+      if (!((fm >> dd) & 1ull)) continue;
+      const int32_t nb = dd == 0 ? x - W : dd == 1 ? x - 1 : dd == 2 ? x + 1 : x + W;
       age += 1;
-      out[nb[d]] = lab;
-      heap_push(h, hn, HeapItem{v[d], age, nb[d]});
+      if (lane == 0) out[nb] = lab;
+      heap_push_w(h, hn, HeapItem{heap_lane(vn, dd), age, nb}, lane);
     }
   }
 }
