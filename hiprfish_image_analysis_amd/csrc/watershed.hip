@@ -465,6 +465,16 @@ struct HeapView {
     else
       g[p] = x;
   }
+  // per lane, position p where valid: the LDS read is issued by every lane (its index clamped
+  // into the LDS levels), the global read only by the lanes whose item lies deeper, each into
+  // its own registers -- with one destination for both the compiler waits on the global reads
+  // in flight before issuing the LDS one
+  __device__ __forceinline__ HeapItem load(int32_t p, bool valid) const {
+    const HeapItem a = __builtin_bit_cast(HeapItem, l[p < HEAP_LDS ? p : 0]);
+    HeapItem b{0.0, 0u, 0};
+    if (valid && p >= HEAP_LDS) b = g[p];
+    return p < HEAP_LDS ? a : b;
+  }
 };
 
 // heap_general.pxi smaller(): value first (IEEE compare, NaN never smaller), then age
@@ -495,8 +505,7 @@ __device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const
   const int32_t c = n++;
   const int32_t pj = lane < 32 ? ((c + 1) >> lane) - 1 : -1;  // ancestor lane of c (lane 0: c)
   const bool va = lane >= 1 && pj >= 0;
-  HeapItem A{0.0, 0u, 0};
-  if (va) A = h.get(pj);
+  const HeapItem A = h.load(pj < 0 ? 0 : pj, va);
   const unsigned long long m = __ballot(va && heap_smaller(x, A));
   const int t = __builtin_ctzll(~(m >> 1));  // bits 1..t set: x climbs t levels
   if (lane >= 1 && lane <= t) h.put(((c + 1) >> (lane - 1)) - 1, A);
@@ -521,25 +530,24 @@ __device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, c
   for (;;) {
     const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
     const bool vl = kl && l < n, vr = kl && r < n;
-    HeapItem L{0.0, 0u, 0}, R{0.0, 0u, 0};
-    if (vl) L = h.get((int32_t)l);
-    if (vr) R = h.get((int32_t)r);
+    const HeapItem L = h.load(vl ? (int32_t)l : 0, vl), R = h.load(vr ? (int32_t)r : 0, vr);
     const unsigned long long mlx = __ballot(vl && heap_smaller(L, x));
     const unsigned long long mrx = __ballot(vr && heap_smaller(R, x));
     const unsigned long long mrl = __ballot(vr && heap_smaller(R, L));
+    // the walk, branch-free (scalar selects): `act` stays 1 while the hole keeps moving
     unsigned long long mvl = 0, mvr = 0;
     int kk = 0, dep = 0;
-    for (; dep < SD_LEV; ++dep) {
-      const bool lx = (mlx >> kk) & 1ull;
-      const bool gor = lx ? ((mrl >> kk) & 1ull) : ((mrx >> kk) & 1ull);
-      if (!lx && !gor) break;
-      if (gor) {
-        mvr |= 1ull << kk;
-        kk = 2 * kk + 2;
-      } else {
-        mvl |= 1ull << kk;
-        kk = 2 * kk + 1;
-      }
+    unsigned act = 1u;
+#pragma unroll
+    for (int lev = 0; lev < SD_LEV; ++lev) {
+      const unsigned lx = (unsigned)(mlx >> kk) & 1u;
+      const unsigned gor = (unsigned)((lx ? mrl : mrx) >> kk) & 1u;
+      const unsigned mv = act & (lx | gor);
+      mvl |= (unsigned long long)(mv & (gor ^ 1u)) << kk;
+      mvr |= (unsigned long long)(mv & gor) << kk;
+      kk = mv ? 2 * kk + 1 + (int)gor : kk;
+      dep += (int)mv;
+      act = mv;
     }
     if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
     if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
@@ -598,11 +606,23 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
     heap_push_w(h, hn, HeapItem{negate ? -fv : fv, 0u, i}, lane);
   }
   uint32_t age = 1;
+  const double invW = 1.0 / (double)W;
+#ifdef HRF_HEAP_PROF
+  unsigned long long tp_top = 0, tp_sift = 0, tp_push = 0, npop = 0;
+#define HP_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define HP_T(v)
+#endif
   while (hn > 0) {
+    HP_T(t0);
     // the popped pixel x (the root) and its four neighbours, up, left, right, down: lane d & 3
     // loads neighbour d's state, read before any of them is written (distinct pixels); a
     // neighbour off the image reads the pixel itself and is never free
-    const int32_t x = heap_uni(h.get(0).idx), r = x / W, c = x - r * W;
+    const int32_t x = heap_uni(h.get(0).idx);
+    int32_t r = (int32_t)((double)x * invW);  // within one of x / W; corrected exactly
+    r -= (int64_t)r * W > x;
+    r += (int64_t)(r + 1) * W <= x;
+    const int32_t c = x - r * W;
     const int dn = lane & 3;
     const bool okd = dn == 0 ? r > 0 : dn == 1 ? c > 0 : dn == 2 ? c + 1 < W : r + 1 < H;
     const int32_t nbd = dn == 0 ? x - W : dn == 1 ? x - 1 : dn == 2 ? x + 1 : x + W;
@@ -611,12 +631,14 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
     const int32_t oq = out[q];
     const double vq = f[q];
     const int32_t lab = heap_uni(out[x]);
+    HP_T(t1);
     hn -= 1;
     if (hn > 0) {
       const HeapItem last = h.get(hn);
       heap_sift_down_w(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
                        lane);
     }
+    HP_T(t2);
     const unsigned long long fm = __ballot(lane < 4 && okd && mq != 0u && oq == 0);
     const double vn = negate ? -vq : vq;
 #pragma unroll
@@ -627,7 +649,19 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
       if (lane == 0) out[nb] = lab;
       heap_push_w(h, hn, HeapItem{heap_lane(vn, dd), age, nb}, lane);
     }
+#ifdef HRF_HEAP_PROF
+    HP_T(t3);
+    tp_top += t1 - t0;
+    tp_sift += t2 - t1;
+    tp_push += t3 - t2;
+    ++npop;
+#endif
   }
+#ifdef HRF_HEAP_PROF
+  if (lane == 0)
+    printf("heap prof: pops %llu cycles/pop: top+loads %.0f sift %.0f wait+push %.0f\n", npop, (double)tp_top / npop,
+           (double)tp_sift / npop, (double)tp_push / npop);
+#endif
 }
 
 int64_t heap_flood_scratch_bytes(int64_t n) { return ((n + 2) * 16 + n * 4 + 255) & ~(int64_t)255; }
