@@ -496,6 +496,13 @@ __device__ __forceinline__ double heap_lane(double v, int src) {
                                 (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, src));
 }
 
+// heap_smaller for every lane as a lane mask: the three primitive compares are the compare
+// instructions' own masks (no per-lane booleans to materialise), combined by scalar operations
+__device__ __forceinline__ unsigned long long heap_smaller_mask(const HeapItem &a, const HeapItem &b) {
+  const unsigned long long ne = __ballot(a.v != b.v), lt = __ballot(a.v < b.v), al = __ballot(a.age < b.age);
+  return (ne & lt) | (~ne & al);
+}
+
 // heappush, one wave: the new item x sifts up while strictly smaller than its parent.  The
 // ancestors do not change while it climbs (each only moves down one level), so every "x smaller
 // than ancestor j" is decided at once: lane j loads ancestor j of the new slot c, one ballot
@@ -506,7 +513,7 @@ __device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const
   const int32_t pj = lane < 32 ? ((c + 1) >> lane) - 1 : -1;  // ancestor lane of c (lane 0: c)
   const bool va = lane >= 1 && pj >= 0;
   const HeapItem A = h.load(pj < 0 ? 0 : pj, va);
-  const unsigned long long m = __ballot(va && heap_smaller(x, A));
+  const unsigned long long m = __ballot(va) & heap_smaller_mask(x, A);
   const int t = __builtin_ctzll(~(m >> 1));  // bits 1..t set: x climbs t levels
   if (lane >= 1 && lane <= t) h.put(((c + 1) >> (lane - 1)) - 1, A);
   if (lane == 0) h.put(((c + 1) >> t) - 1, x);
@@ -531,23 +538,26 @@ __device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, c
     const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
     const bool vl = kl && l < n, vr = kl && r < n;
     const HeapItem L = h.load(vl ? (int32_t)l : 0, vl), R = h.load(vr ? (int32_t)r : 0, vr);
-    const unsigned long long mlx = __ballot(vl && heap_smaller(L, x));
-    const unsigned long long mrx = __ballot(vr && heap_smaller(R, x));
-    const unsigned long long mrl = __ballot(vr && heap_smaller(R, L));
+    const unsigned long long bl = __ballot(vl), br = __ballot(vr);
+    const unsigned long long mlx = bl & heap_smaller_mask(L, x);
+    const unsigned long long mrx = br & heap_smaller_mask(R, x);
+    const unsigned long long mrl = br & heap_smaller_mask(R, L);
+    // per node, where the hole would go from there: left if the left child is smaller than x
+    // and the right one not smaller than it; right if the right one is smaller than the better
+    // of the two
+    const unsigned long long gol = mlx & ~mrl, gor = (mlx & mrl) | (~mlx & mrx);
     // the walk, branch-free (scalar selects): `act` stays 1 while the hole keeps moving
     unsigned long long mvl = 0, mvr = 0;
     int kk = 0, dep = 0;
     unsigned act = 1u;
 #pragma unroll
     for (int lev = 0; lev < SD_LEV; ++lev) {
-      const unsigned lx = (unsigned)(mlx >> kk) & 1u;
-      const unsigned gor = (unsigned)((lx ? mrl : mrx) >> kk) & 1u;
-      const unsigned mv = act & (lx | gor);
-      mvl |= (unsigned long long)(mv & (gor ^ 1u)) << kk;
-      mvr |= (unsigned long long)(mv & gor) << kk;
-      kk = mv ? 2 * kk + 1 + (int)gor : kk;
-      dep += (int)mv;
-      act = mv;
+      const unsigned ml = act & (unsigned)(gol >> kk) & 1u, mr = act & (unsigned)(gor >> kk) & 1u;
+      mvl |= (unsigned long long)ml << kk;
+      mvr |= (unsigned long long)mr << kk;
+      act = ml | mr;
+      kk = act ? 2 * kk + 1 + (int)mr : kk;
+      dep += (int)act;
     }
     if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
     if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
