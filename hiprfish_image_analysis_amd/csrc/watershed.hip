@@ -508,15 +508,29 @@ __device__ __forceinline__ unsigned long long heap_smaller_mask(const HeapItem &
 // than ancestor j" is decided at once: lane j loads ancestor j of the new slot c, one ballot
 // gives the climb height t (the run of ones from bit 1), lanes 1..t move their ancestors down
 // one level in one store, lane 0 stores x.  One round trip per push instead of one per level.
-__device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const HeapItem &x, int lane) {
-  const int32_t c = n++;
+// LDS_ONLY (the new slot lies in LDS, so do all its ancestors): no global access, hence no wait
+// on the label store just issued.
+template <bool LDS_ONLY>
+__device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t c, const HeapItem &x, int lane) {
   const int32_t pj = lane < 32 ? ((c + 1) >> lane) - 1 : -1;  // ancestor lane of c (lane 0: c)
   const bool va = lane >= 1 && pj >= 0;
-  const HeapItem A = h.load(pj < 0 ? 0 : pj, va);
+  const HeapItem A = LDS_ONLY ? __builtin_bit_cast(HeapItem, h.l[pj < 0 ? 0 : pj]) : h.load(pj < 0 ? 0 : pj, va);
   const unsigned long long m = __ballot(va) & heap_smaller_mask(x, A);
   const int t = __builtin_ctzll(~(m >> 1));  // bits 1..t set: x climbs t levels
-  if (lane >= 1 && lane <= t) h.put(((c + 1) >> (lane - 1)) - 1, A);
-  if (lane == 0) h.put(((c + 1) >> t) - 1, x);
+  if (LDS_ONLY) {
+    if (lane >= 1 && lane <= t) h.l[((c + 1) >> (lane - 1)) - 1] = __builtin_bit_cast(heap_u4, A);
+    if (lane == 0) h.l[((c + 1) >> t) - 1] = __builtin_bit_cast(heap_u4, x);
+  } else {
+    if (lane >= 1 && lane <= t) h.put(((c + 1) >> (lane - 1)) - 1, A);
+    if (lane == 0) h.put(((c + 1) >> t) - 1, x);
+  }
+}
+__device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const HeapItem &x, int lane) {
+  const int32_t c = n++;
+  if (c < HEAP_LDS)
+    heap_push_w<true>(h, c, x, lane);
+  else
+    heap_push_w<false>(h, c, x, lane);
 }
 
 // heappop's sift-down of x (the heap's former last item) from the hole at the root, n items
@@ -528,7 +542,11 @@ __device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const
 // child if it is smaller than x, unless the right one is smaller still; to the right child if
 // only it is smaller than x; else x stays), and every moved child is written into its parent by
 // the lane that holds it: one store per side.  A child at or past n is never smaller.
+// LDS_ONLY: the whole heap lies in LDS (n <= HEAP_LDS), so the step holds no global load -- a
+// global load anywhere in the loop makes the compiler wait for every load in flight (the popped
+// pixel's neighbours included) before the first compare.
 constexpr int SD_LEV = 6;
+template <bool LDS_ONLY>
 __device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, const HeapItem &x, int lane) {
   const int k = lane;
   const bool kl = k < (1 << SD_LEV) - 1;
@@ -537,7 +555,14 @@ __device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, c
   for (;;) {
     const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
     const bool vl = kl && l < n, vr = kl && r < n;
-    const HeapItem L = h.load(vl ? (int32_t)l : 0, vl), R = h.load(vr ? (int32_t)r : 0, vr);
+    HeapItem L, R;
+    if (LDS_ONLY) {
+      L = __builtin_bit_cast(HeapItem, h.l[vl ? (int32_t)l : 0]);
+      R = __builtin_bit_cast(HeapItem, h.l[vr ? (int32_t)r : 0]);
+    } else {
+      L = h.load(vl ? (int32_t)l : 0, vl);
+      R = h.load(vr ? (int32_t)r : 0, vr);
+    }
     const unsigned long long bl = __ballot(vl), br = __ballot(vr);
     const unsigned long long mlx = bl & heap_smaller_mask(L, x);
     const unsigned long long mrx = br & heap_smaller_mask(R, x);
@@ -559,8 +584,13 @@ __device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, c
       kk = act ? 2 * kk + 1 + (int)mr : kk;
       dep += (int)act;
     }
-    if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
-    if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
+    if (LDS_ONLY) {
+      if ((mvl >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, L);
+      if ((mvr >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, R);
+    } else {
+      if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
+      if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
+    }
     // relative node kk at depth dep: position hole * 2^dep + kk
     hole = (hole << dep) + kk;
     if (dep < SD_LEV) break;
@@ -640,16 +670,21 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
     const uint32_t mq = HASMASK ? mask[q] : 1u;
     const int32_t oq = out[q];
     const double vq = f[q];
-    const int32_t lab = heap_uni(out[x]);
+    const int32_t labv = out[x];  // read back after the sift-down: the load's wait would hold it up
     HP_T(t1);
     hn -= 1;
-    if (hn > 0) {
+    if (hn > 0 && hn < HEAP_LDS) {  // the heap (positions < hn) and its last item (position hn) in LDS
+      const HeapItem last = __builtin_bit_cast(HeapItem, h.l[hn]);
+      heap_sift_down_w<true>(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
+                             lane);
+    } else if (hn > 0) {
       const HeapItem last = h.get(hn);
-      heap_sift_down_w(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
-                       lane);
+      heap_sift_down_w<false>(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
+                              lane);
     }
     HP_T(t2);
     const unsigned long long fm = __ballot(lane < 4 && okd && mq != 0u && oq == 0);
+    const int32_t lab = heap_uni(labv);
     const double vn = negate ? -vq : vq;
 #pragma unroll
     for (int dd = 0; dd < 4; ++dd) {
