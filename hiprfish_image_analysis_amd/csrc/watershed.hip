@@ -691,9 +691,11 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
       if (!((fm >> dd) & 1ull)) continue;
       const int32_t nb = dd == 0 ? x - W : dd == 1 ? x - 1 : dd == 2 ? x + 1 : x + W;
       age += 1;
-      if (lane == 0) out[nb] = lab;
       heap_push_w(h, hn, HeapItem{heap_lane(vn, dd), age, nb}, lane);
     }
+    // the pushed neighbours' labels, one store by their lanes after the pushes (a store before a
+    // push's global loads would be waited for with them)
+    if ((fm >> lane) & 1ull) out[nbd] = lab;
 #ifdef HRF_HEAP_PROF
     HP_T(t3);
     tp_top += t1 - t0;
