@@ -546,54 +546,74 @@ __device__ __forceinline__ void heap_push_w(const HeapView &h, int32_t &n, const
 // global load anywhere in the loop makes the compiler wait for every load in flight (the popped
 // pixel's neighbours included) before the first compare.
 constexpr int SD_LEV = 6;
-template <bool LDS_ONLY>
-__device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, const HeapItem &x, int lane) {
+// the steps whose nodes all lie on the LDS levels 0..12: a step from a hole on depth
+// s * SD_LEV reaches depth (s + 1) * SD_LEV
+constexpr int SD_LDS_STEPS = 12 / SD_LEV;
+
+// one step from `hole`; false once x has found its place (hole then holds its position)
+template <bool LDS_STEP>
+__device__ __forceinline__ bool heap_sift_step(const HeapView &h, int32_t n, const HeapItem &x, int lane,
+                                               int64_t &hole) {
   const int k = lane;
   const bool kl = k < (1 << SD_LEV) - 1;
   const int d = 31 - __builtin_clz((unsigned)k + 1u);
-  int64_t hole = 0;  // wave-uniform
-  for (;;) {
-    const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
-    const bool vl = kl && l < n, vr = kl && r < n;
-    HeapItem L, R;
-    if (LDS_ONLY) {
-      L = __builtin_bit_cast(HeapItem, h.l[vl ? (int32_t)l : 0]);
-      R = __builtin_bit_cast(HeapItem, h.l[vr ? (int32_t)r : 0]);
-    } else {
-      L = h.load(vl ? (int32_t)l : 0, vl);
-      R = h.load(vr ? (int32_t)r : 0, vr);
-    }
-    const unsigned long long bl = __ballot(vl), br = __ballot(vr);
-    const unsigned long long mlx = bl & heap_smaller_mask(L, x);
-    const unsigned long long mrx = br & heap_smaller_mask(R, x);
-    const unsigned long long mrl = br & heap_smaller_mask(R, L);
-    // per node, where the hole would go from there: left if the left child is smaller than x
-    // and the right one not smaller than it; right if the right one is smaller than the better
-    // of the two
-    const unsigned long long gol = mlx & ~mrl, gor = (mlx & mrl) | (~mlx & mrx);
-    // the walk, branch-free (scalar selects): `act` stays 1 while the hole keeps moving
-    unsigned long long mvl = 0, mvr = 0;
-    int kk = 0, dep = 0;
-    unsigned act = 1u;
+  const int64_t a = (hole << d) + k, l = 2 * a + 1, r = l + 1;
+  const bool vl = kl && l < n, vr = kl && r < n;
+  HeapItem L, R;
+  if (LDS_STEP) {
+    L = __builtin_bit_cast(HeapItem, h.l[vl ? (int32_t)l : 0]);
+    R = __builtin_bit_cast(HeapItem, h.l[vr ? (int32_t)r : 0]);
+  } else {
+    L = h.load(vl ? (int32_t)l : 0, vl);
+    R = h.load(vr ? (int32_t)r : 0, vr);
+  }
+  const unsigned long long bl = __ballot(vl), br = __ballot(vr);
+  const unsigned long long mlx = bl & heap_smaller_mask(L, x);
+  const unsigned long long mrx = br & heap_smaller_mask(R, x);
+  const unsigned long long mrl = br & heap_smaller_mask(R, L);
+  // per node, where the hole would go from there: left if the left child is smaller than x and
+  // the right one not smaller than it; right if the right one is smaller than the better of the two
+  const unsigned long long gol = mlx & ~mrl, gor = (mlx & mrl) | (~mlx & mrx);
+  // the walk, branch-free (scalar selects): `act` stays 1 while the hole keeps moving
+  unsigned long long mvl = 0, mvr = 0;
+  int kk = 0, dep = 0;
+  unsigned act = 1u;
 #pragma unroll
-    for (int lev = 0; lev < SD_LEV; ++lev) {
-      const unsigned ml = act & (unsigned)(gol >> kk) & 1u, mr = act & (unsigned)(gor >> kk) & 1u;
-      mvl |= (unsigned long long)ml << kk;
-      mvr |= (unsigned long long)mr << kk;
-      act = ml | mr;
-      kk = act ? 2 * kk + 1 + (int)mr : kk;
-      dep += (int)act;
+  for (int lev = 0; lev < SD_LEV; ++lev) {
+    const unsigned ml = act & (unsigned)(gol >> kk) & 1u, mr = act & (unsigned)(gor >> kk) & 1u;
+    mvl |= (unsigned long long)ml << kk;
+    mvr |= (unsigned long long)mr << kk;
+    act = ml | mr;
+    kk = act ? 2 * kk + 1 + (int)mr : kk;
+    dep += (int)act;
+  }
+  if (LDS_STEP) {
+    if ((mvl >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, L);
+    if ((mvr >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, R);
+  } else {
+    if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
+    if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
+  }
+  // relative node kk at depth dep: position hole * 2^dep + kk
+  hole = (hole << dep) + kk;
+  return dep == SD_LEV;
+}
+
+// LDS_ONLY: the whole heap lies in LDS.  Otherwise the first SD_LDS_STEPS steps still read LDS
+// only, in code of their own: the global reads of the later steps are waited for in order, and
+// in shared code that wait would take in the popped pixel's neighbour loads before the first
+// compare.
+template <bool LDS_ONLY>
+__device__ __forceinline__ void heap_sift_down_w(const HeapView &h, int32_t n, const HeapItem &x, int lane) {
+  int64_t hole = 0;  // wave-uniform
+  if (LDS_ONLY) {
+    while (heap_sift_step<true>(h, n, x, lane, hole)) {
     }
-    if (LDS_ONLY) {
-      if ((mvl >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, L);
-      if ((mvr >> lane) & 1ull) h.l[(int32_t)a] = __builtin_bit_cast(heap_u4, R);
-    } else {
-      if ((mvl >> lane) & 1ull) h.put((int32_t)a, L);
-      if ((mvr >> lane) & 1ull) h.put((int32_t)a, R);
-    }
-    // relative node kk at depth dep: position hole * 2^dep + kk
-    hole = (hole << dep) + kk;
-    if (dep < SD_LEV) break;
+  } else {
+    bool more = true;
+#pragma unroll
+    for (int s = 0; s < SD_LDS_STEPS && more; ++s) more = heap_sift_step<true>(h, n, x, lane, hole);
+    while (more) more = heap_sift_step<false>(h, n, x, lane, hole);
   }
   if (lane == 0) h.put((int32_t)hole, x);
 }
@@ -659,6 +679,10 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
     // loads neighbour d's state, read before any of them is written (distinct pixels); a
     // neighbour off the image reads the pixel itself and is never free
     const int32_t x = heap_uni(h.get(0).idx);
+    // a last item in global memory is loaded before the neighbours: its wait then takes only it
+    // (loads complete in order)
+    HeapItem lastg{0.0, 0u, 0};
+    if (hn - 1 >= HEAP_LDS) lastg = h.g[hn - 1];
     int32_t r = (int32_t)((double)x * invW);  // within one of x / W; corrected exactly
     r -= (int64_t)r * W > x;
     r += (int64_t)(r + 1) * W <= x;
@@ -678,9 +702,8 @@ __global__ __launch_bounds__(1024) void ws_heap_flood_kernel(const double *__res
       heap_sift_down_w<true>(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
                              lane);
     } else if (hn > 0) {
-      const HeapItem last = h.get(hn);
-      heap_sift_down_w<false>(h, hn, HeapItem{heap_uni(last.v), (uint32_t)heap_uni((int32_t)last.age), heap_uni(last.idx)},
-                              lane);
+      heap_sift_down_w<false>(
+          h, hn, HeapItem{heap_uni(lastg.v), (uint32_t)heap_uni((int32_t)lastg.age), heap_uni(lastg.idx)}, lane);
     }
     HP_T(t2);
     const unsigned long long fm = __ballot(lane < 4 && okd && mq != 0u && oq == 0);
