@@ -19,7 +19,8 @@ LIB = os.path.join(PKG, "libhrf.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
-          "-fvisibility=hidden", "-Wno-unused-result", "-I" + os.path.join(REPO, "include")]
+          "-fvisibility=hidden", "-Wno-unused-result", "-I" + os.path.join(REPO, "include")] + \
+    os.environ.get("HRF_EXTRA_CFLAGS", "").split()   # A/B variants (tools/build_variant.sh)
 HEADERS = glob.glob(os.path.join(CSRC, "*.hpp")) + glob.glob(os.path.join(CSRC, "*.h")) + \
     glob.glob(os.path.join(CSRC, "*.inc")) + \
     [os.path.join(REPO, "include", "hrf.h")]

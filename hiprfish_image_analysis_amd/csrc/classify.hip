@@ -38,6 +38,14 @@ struct Bounds {
 
 constexpr int RCH = 64;  // references per LDS chunk (prefetched into registers)
 
+// workgroups per CU the 16x16x32 sweeps (w16, w16t) are built for.  Round 6: 2 (256 VGPRs).  The
+// runner-up tracking (t2, the refine's certificate) does not fit the 168 VGPRs of three: at three
+// the E. coli table sweep reloaded B operands from scratch every chunk, 2.87 ms per 2048^2 tile
+// against 1.77 ms at two (gpurun_out/r6b; round 5's three-per-CU kernel without t2: 1.69-1.81).
+#ifndef HRF_W16T_OCC
+#define HRF_W16T_OCC 2
+#endif
+
 // refx[r][0..C) = ref / |ref_seg| (0 if the norm is 0), refx[r][C+s] = (norm_s == 0),
 // zero padding to KP columns and to Rpad rows.
 __global__ void ref_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
@@ -62,7 +70,8 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
                                                                   Bounds bd, const float *__restrict__ refx,
                                                                   int32_t R, int32_t Rpad,
                                                                   int32_t *__restrict__ best_idx,
-                                                                  float *__restrict__ best_dist) {
+                                                                  float *__restrict__ best_dist,
+                                                                  float *__restrict__ second) {
   constexpr int KP = 2 * KS;
   constexpr int STRIDE = KP + 2;  // == 2 (mod 4): conflict-free ds_read_b64 over 32 rows
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -121,6 +130,7 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
   }
 
   float best[2] = {-__builtin_inff(), -__builtin_inff()};
+  float sec[2] = {-__builtin_inff(), -__builtin_inff()};  // runner-up score (any row but the best)
   int bidx[2] = {0, 0};
 
   // ---- sweep the reference library in LDS chunks ----
@@ -166,6 +176,10 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
       for (int reg = 0; reg < 16; ++reg) {
         const int r = r0 + rb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
         const bool ok = r < R;
+        if (ok) {
+          sec[0] = fmaxf(sec[0], fminf(best[0], acc0[reg]));
+          sec[1] = fmaxf(sec[1], fminf(best[1], acc1[reg]));
+        }
         if (ok && acc0[reg] > best[0]) {
           best[0] = acc0[reg];
           bidx[0] = r;
@@ -182,6 +196,7 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
   for (int g = 0; g < 2; ++g) {
     const float ob = __shfl_xor(best[g], 32, 64);
     const int oi = __shfl_xor(bidx[g], 32, 64);
+    sec[g] = fmaxf(fmaxf(sec[g], __shfl_xor(sec[g], 32, 64)), fminf(best[g], ob));
     if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
       best[g] = ob;
       bidx[g] = oi;
@@ -190,6 +205,7 @@ __global__ __launch_bounds__(256) void classify_pixels_kernel(const float *__res
     if (h == 0 && p < P) {
       best_idx[p] = bidx[g];
       best_dist[p] = ((float)bd.nseg - best[g]) / (float)bd.nseg;
+      if (second) second[p] = sec[g];
     }
   }
 }
@@ -359,7 +375,8 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
                                                                      int32_t C, Bounds bd,
                                                                      const _Float16 *__restrict__ refh, int32_t R,
                                                                      int32_t Rpad, int32_t *__restrict__ best_idx,
-                                                                     float *__restrict__ best_dist) {
+                                                                     float *__restrict__ best_dist,
+                                                                     float *__restrict__ second) {
   constexpr int KP = 16 * KS16;
   constexpr int ROWB = 4 * KP + 16;
   constexpr int CHB = RCH * ROWB;
@@ -396,6 +413,7 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
   issue(0);
 
   float best0 = -__builtin_inff(), best1 = -__builtin_inff();
+  float sec0 = -__builtin_inff(), sec1 = -__builtin_inff();  // runner-up scores
   int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
   // Software-pipelined argmax: the scores of block b are compared while block b+1's MFMAs
   // run (a slice of the 16 registers after each k-step), so the epilogue's VALU fills the MFMA
@@ -409,6 +427,8 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
     for (int reg = lo; reg < hi; ++reg) {
       const int r = pr + (reg & 3) + 8 * (reg >> 2);
       const float s0 = pv0[reg], s1 = pv1[reg];
+      sec0 = fmaxf(sec0, fminf(best0, s0));
+      sec1 = fmaxf(sec1, fminf(best1, s1));
       if (s0 > best0) {
         best0 = s0;
         bi0 = r;
@@ -451,11 +471,13 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
   }
   epi(0, 16);  // the last block
   float best[2] = {best0, best1};
+  float sec[2] = {sec0, sec1};
   int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const float ob = __shfl_xor(best[g], 32, 64);
     const int oi = __shfl_xor(bidx[g], 32, 64);
+    sec[g] = fmaxf(fmaxf(sec[g], __shfl_xor(sec[g], 32, 64)), fminf(best[g], ob));
     if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
       best[g] = ob;
       bidx[g] = oi;
@@ -464,6 +486,7 @@ __global__ __launch_bounds__(256, 2) void classify_pixels_f16_kernel(const float
     if (h == 0 && p < P) {
       best_idx[p] = bidx[g];
       best_dist[p] = ((float)bd.nseg - best[g]) / (float)bd.nseg;
+      if (second) second[p] = sec[g];
     }
   }
 }
@@ -612,11 +635,22 @@ __device__ __forceinline__ void build_b_lay(const float4 (&v)[LDV], float *stg, 
 // distance reported), and its argmax keeps the reference's tie rule on it -- within a block the
 // code makes the lowest row win equal scores, across blocks (and chunks) only a strictly greater
 // score replaces the running best, so equal scores anywhere in the library go to the lowest r.
+// Runner-up tracking (the refine's certificate, hrf_classify_pixels_refine): the second-largest key
+// of {a >= b} and k is med3(a, b, k) (v_med3_i32); a key's score bits with the 4 position bits set
+// bound every untruncated score that truncates to them (negative keys -- padding rows only -- keep
+// their truncated value, the larger one)
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
+__device__ __forceinline__ float key_score_hi(int k) {
+  return __int_as_float(k >= 0 ? ((k & -16) | 15) : (k & -16));
+}
+// the same bound from a truncated score (keyed sweeps) or the exact one (compare-select sweeps)
+__device__ __forceinline__ float score_hi(float s, bool keyed) { return keyed ? key_score_hi(__float_as_int(s)) : s; }
+
 template <int KS16, int ROWB, int NW, int NSEG, bool ZS, bool KEYED>
 __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w, int h,
                                           const h8 (&bh0)[KS16], const h8 (&bl0)[KS16], const h8 (&bh1)[KS16],
                                           const h8 (&bl1)[KS16], uint32_t zx0, uint32_t zx1, float &best0,
-                                          float &best1, int &bi0, int &bi1) {
+                                          float &best1, int &bi0, int &bi1, float &sec0, float &sec1) {
   constexpr int KP = 16 * KS16;
   constexpr int CHB = RCH * ROWB;
   constexpr int NPC = CHB / 1024;
@@ -638,17 +672,24 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
     bz0[q] = (_Float16)((h == 0 && q < NSEG && ((zx0 >> q) & 1u)) ? 1.0f : 0.0f);
     bz1[q] = (_Float16)((h == 0 && q < NSEG && ((zx1 >> q) & 1u)) ? 1.0f : 0.0f);
   }
-  int bk0 = INT32_MIN, bk1 = INT32_MIN;        // KEYED: the pending block's keys
-  int key0 = INT32_MIN, key1 = INT32_MIN;      // KEYED: best keys so far
+  // KEYED: key = the best so far (a later block's best replaces it on a strictly greater score only);
+  // t1 / t2 = the largest / second-largest keys seen (t1 doubles as the block's best, see sweep_w16)
+  int key0 = INT32_MIN, key1 = INT32_MIN;
+  int t10 = INT32_MIN, t11 = INT32_MIN, t20 = INT32_MIN, t21 = INT32_MIN;
   auto epi = [&](int lo, int hi) {
 #pragma unroll
     for (int reg = lo; reg < hi; ++reg) {
       const int r = pr + (reg & 3) + 8 * (reg >> 2);
       const float s0 = pv0[reg], s1 = pv1[reg];
       if (KEYED) {
-        bk0 = max(bk0, (__float_as_int(s0) & -16) | (15 - reg));
-        bk1 = max(bk1, (__float_as_int(s1) & -16) | (15 - reg));
+        const int q0 = (__float_as_int(s0) & -16) | (15 - reg), q1 = (__float_as_int(s1) & -16) | (15 - reg);
+        t20 = med3i(t10, t20, q0);
+        t21 = med3i(t11, t21, q1);
+        t10 = max(t10, q0);
+        t11 = max(t11, q1);
       } else {
+        sec0 = fmaxf(sec0, fminf(best0, s0));
+        sec1 = fmaxf(sec1, fminf(best1, s1));
         if (s0 > best0) {
           best0 = s0;
           bi0 = r;
@@ -660,15 +701,14 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
       }
     }
     if (KEYED && hi == 16) {  // the pending block is complete: a later block wins on a greater score only
-      if ((bk0 >> 4) > (key0 >> 4)) {
-        key0 = bk0;
+      if ((t10 >> 4) > (key0 >> 4)) {
+        key0 = t10;
         bi0 = pr;
       }
-      if ((bk1 >> 4) > (key1 >> 4)) {
-        key1 = bk1;
+      if ((t11 >> 4) > (key1 >> 4)) {
+        key1 = t11;
         bi1 = pr;
       }
-      bk0 = bk1 = INT32_MIN;
     }
   };
   for (int c = 0; c < nch; ++c) {
@@ -713,6 +753,8 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
     bi1 += (g1 & 3) + 8 * (g1 >> 2);
     best0 = __int_as_float(key0 & -16);
     best1 = __int_as_float(key1 & -16);
+    sec0 = key_score_hi(t20);
+    sec1 = key_score_hi(t21);
   }
 }
 
@@ -720,7 +762,8 @@ template <class L, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(const float *__restrict__ stack, int64_t P,
                                                                      const _Float16 *__restrict__ refh, int32_t R,
                                                                      int32_t Rpad, int32_t *__restrict__ best_idx,
-                                                                     float *__restrict__ best_dist) {
+                                                                     float *__restrict__ best_dist,
+                                                                     float *__restrict__ second) {
   constexpr int KS16 = lay_ks16<L>();
   constexpr int KP = 16 * KS16;
   constexpr int ROWB = 4 * KP + L::PADB;
@@ -744,6 +787,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   // the library's "has a negative value" flag sits in row 0's pad (ref_negflag_kernel)
   const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
   float best0 = -__builtin_inff(), best1 = -__builtin_inff();
+  float sec0 = -__builtin_inff(), sec1 = -__builtin_inff();
   int bi0 = 0, bi1 = 0;  // wave-uniform part of the row index (4h added at the end)
   const char *gref = reinterpret_cast<const char *>(refh);
   char *ldsb = reinterpret_cast<char *>(lds);
@@ -752,7 +796,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   const bool zs = __syncthreads_or((zx0 | zx1) != 0);
   const bool keyed = !libneg && !__syncthreads_or((ng0 | ng1) != 0);
 #define HRF_SWEEP(Z, K) \
-  lay_sweep<KS16, ROWB, NW, L::NSEG, Z, K>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, bi1)
+  lay_sweep<KS16, ROWB, NW, L::NSEG, Z, K>(gref, ldsb, nch, lane, w, h, bh0, bl0, bh1, bl1, zx0, zx1, best0, best1, bi0, \
+                                           bi1, sec0, sec1)
   if (keyed) {
     if (zs) HRF_SWEEP(true, true);
     else HRF_SWEEP(false, true);
@@ -762,11 +807,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
   }
 #undef HRF_SWEEP
   float best[2] = {best0, best1};
+  float sec[2] = {sec0, sec1};
   int bidx[2] = {bi0 + 4 * h, bi1 + 4 * h};
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     const float ob = __shfl_xor(best[g], 32, 64);
     const int oi = __shfl_xor(bidx[g], 32, 64);
+    sec[g] = fmaxf(fmaxf(sec[g], __shfl_xor(sec[g], 32, 64)), fminf(score_hi(best[g], keyed), score_hi(ob, keyed)));
     if (ob > best[g] || (ob == best[g] && oi < bidx[g])) {
       best[g] = ob;
       bidx[g] = oi;
@@ -775,6 +822,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void classify_pixels_lay_kernel(co
     if (h == 0 && p < P) {
       best_idx[p] = bidx[g];
       best_dist[p] = ((float)L::NSEG - best[g]) / (float)L::NSEG;
+      if (second) second[p] = sec[g];
     }
   }
 }
@@ -875,8 +923,8 @@ __device__ __forceinline__ void split_b_w16(const float *stg, int lane, int g, h
 
 template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF, int CR, bool PIPE>
 __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
-                                          const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t (&zx)[4],
-                                          float (&best)[4], int (&bi)[4]) {
+                                          const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t zxp,
+                                          float (&best)[4], int (&bi)[4], float (&sec)[4]) {
   constexpr int KP = 32 * KT;
   constexpr int CHB = CR * ROWB;
   constexpr int NPC = (CHB + 1023) / 1024;  // 1 KiB LDS-DMA pieces per chunk (the last may be partial)
@@ -901,14 +949,23 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[g][i] = -__builtin_inff();
   int pr = 0;  // first row of the pending block
-  h8 bz[4];
+  // ZS: the pixels' indicator B operand (fp16 1.0 = 0x3c00 in slot q < NSEG of quarter 0 where
+  // segment q is all zero), rebuilt per use from zxp (group g's all-zero segments in bits 8g..8g+7)
+  // instead of held in 16 VGPRs
+  auto bz_of = [&](int g) -> h8 {
+    const uint32_t m = Q == 0 ? ((zxp >> (8 * g)) & ((1u << NSEG) - 1u)) : 0u;
+    uint32_t d[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+    for (int i = 0; i < 4; ++i) d[i] = (((m >> (2 * i)) & 1u) * 0x3c00u) | (((m >> (2 * i + 1)) & 1u) * 0x3c000000u);
+    return __builtin_bit_cast(h8, d);
+  };
+  // keyed: key = the running best (replaced by a chunk's best only on a strictly greater score),
+  // t1 / t2 = the largest and second-largest keys seen (t1 also serves as the chunk's best: a key
+  // from an earlier chunk that was not adopted has key's score)
+  int key[4], t1[4], t2[4];
+  uint32_t bic = 0;  // keyed: the chunk of each group's key, 8 bits per group
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bz[g][q] = (_Float16)((Q == 0 && q < NSEG && ((zx[g] >> q) & 1u)) ? 1.0f : 0.0f);
-  int key[4], ck[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) key[g] = ck[g] = INT32_MIN;
+  for (int g = 0; g < 4; ++g) key[g] = t1[g] = t2[g] = INT32_MIN;
   // fold the pending block into the chunk keys, groups [g0, g1); after the chunk's last block,
   // the chunk key against the running best (strictly greater score, the position code left out:
   // earlier chunks win ties, so equal scores keep the lowest row across the whole library)
@@ -922,9 +979,17 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
         const int k1 = (__float_as_int(pv[g][1]) & -16) | (base - 1);
         const int k2 = (__float_as_int(pv[g][2]) & -16) | (base - 2);
         const int k3 = (__float_as_int(pv[g][3]) & -16) | (base - 3);
-        ck[g] = max(ck[g], max(k0, k1));
-        ck[g] = max(ck[g], max(k2, k3));
+        t2[g] = med3i(t1[g], t2[g], k0);
+        t1[g] = max(t1[g], k0);
+        t2[g] = med3i(t1[g], t2[g], k1);
+        t1[g] = max(t1[g], k1);
+        t2[g] = med3i(t1[g], t2[g], k2);
+        t1[g] = max(t1[g], k2);
+        t2[g] = med3i(t1[g], t2[g], k3);
+        t1[g] = max(t1[g], k3);
       } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sec[g] = fmaxf(sec[g], fminf(best[g], pv[g][i]));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (pv[g][i] > best[g]) {
@@ -934,14 +999,13 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
       }
     }
     if (KEYED && g1 == 4 && pb == NB - 1) {
-      const int cb = pr - 16 * pb;
+      const uint32_t cc = (uint32_t)(pr / CR);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        if ((ck[g] >> 4) > (key[g] >> 4)) {
-          key[g] = ck[g];
-          bi[g] = cb;
+        if ((t1[g] >> 4) > (key[g] >> 4)) {  // t1 is then this chunk's
+          key[g] = t1[g];
+          bic = (bic & ~(0xffu << (8 * g))) | (cc << (8 * g));
         }
-        ck[g] = INT32_MIN;
       }
     }
   };
@@ -974,7 +1038,7 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
       }
       if (ZS) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz[g], acc[g], 0, 0, 0);
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz_of(g), acc[g], 0, 0, 0);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) pv[g] = acc[g];
@@ -987,8 +1051,9 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int code = 15 - (key[g] & 15);
-      bi[g] += 16 * (code >> 2) + (code & 3);
+      bi[g] = CR * (int)((bic >> (8 * g)) & 0xffu) + 16 * (code >> 2) + (code & 3);
       best[g] = __int_as_float(key[g] & -16);
+      sec[g] = key_score_hi(t2[g]);
     }
   }
 }
@@ -998,7 +1063,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
                                                                      int64_t P, const _Float16 *__restrict__ refh,
                                                                      int32_t R, int32_t Rpad,
                                                                      int32_t *__restrict__ best_idx,
-                                                                     float *__restrict__ best_dist) {
+                                                                     float *__restrict__ best_dist,
+                                                                     float *__restrict__ second) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   constexpr int KP = 32 * KT;
   constexpr int ROWB = 4 * KP + L::PADB;
@@ -1006,7 +1072,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
   h8 bh[4][KT], bl[4][KT];
-  uint32_t zx[4], ng = 0;
+  uint32_t zxp = 0, ng = 0;  // all-zero segments of the four 16-pixel groups, 8 bits each
   float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
   {
     // both halves' loads in flight at once where the registers allow (two waves per SIMD);
@@ -1024,32 +1090,32 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
         if (e4 < 8 * L::C) reinterpret_cast<float4 *>(stg)[e4] = v[NV == 2 ? half : 0][i];
       }
       __syncthreads();
-      uint32_t zxp, ngp;
-      norm_pixels_w16<L>(stg, lane, zxp, ngp);
+      uint32_t zxh, ngp;
+      norm_pixels_w16<L>(stg, lane, zxh, ngp);
       ng |= ngp;
       __syncthreads();
       split_b_w16<L, KT>(stg, lane, 0, bh[2 * half], bl[2 * half]);
       split_b_w16<L, KT>(stg, lane, 1, bh[2 * half + 1], bl[2 * half + 1]);
-      zx[2 * half] = __shfl(zxp, lane & 15, 64);
-      zx[2 * half + 1] = __shfl(zxp, 16 + (lane & 15), 64);
+      zxp |= ((uint32_t)__shfl(zxh, lane & 15, 64) << (16 * half)) |
+             ((uint32_t)__shfl(zxh, 16 + (lane & 15), 64) << (16 * half + 8));
       __syncthreads();
     }
   }
   const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
-  float best[4];
+  float best[4], sec[4];
   int bi[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    best[g] = -__builtin_inff();
+    best[g] = sec[g] = -__builtin_inff();
     bi[g] = 0;
   }
   const char *gref = reinterpret_cast<const char *>(refh);
   char *ldsb = reinterpret_cast<char *>(lds);
   const int nch = Rpad / CR;
-  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
+  const bool zs = __syncthreads_or(zxp != 0);
   const bool keyed = !libneg && !__syncthreads_or(ng != 0);
 #define HRF_SWEEPW(Z, K) \
-  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
   if (keyed) {
     if (zs) HRF_SWEEPW(true, true);
     else HRF_SWEEPW(false, true);
@@ -1061,12 +1127,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
   const int Q = lane >> 4;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    float b = best[g];
+    float b = best[g], sc = sec[g];
     int idx = bi[g] + 4 * Q;
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float ob = __shfl_xor(b, o, 64);
       const int oi = __shfl_xor(idx, o, 64);
+      sc = fmaxf(fmaxf(sc, __shfl_xor(sc, o, 64)), fminf(score_hi(b, keyed), score_hi(ob, keyed)));
       if (ob > b || (ob == b && oi < idx)) {
         b = ob;
         idx = oi;
@@ -1076,6 +1143,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
     if (Q == 0 && p < P) {
       best_idx[p] = idx;
       best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
+      if (second) second[p] = sc;
     }
   }
 }
@@ -1103,7 +1171,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
                                                                       const uint8_t *__restrict__ flags, int64_t P,
                                                                       const _Float16 *__restrict__ refh, int32_t R,
                                                                       int32_t Rpad, int32_t *__restrict__ best_idx,
-                                                                      float *__restrict__ best_dist) {
+                                                                      float *__restrict__ best_dist,
+                                                                      float *__restrict__ second) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   constexpr int KP = 32 * KT;
   constexpr int ROWB = 4 * KP + L::PADB;
@@ -1111,7 +1180,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
   h8 bh[4][KT], bl[4][KT];
-  uint32_t zx[4], ng = 0;
+  uint32_t zxp = 0, ng = 0;  // all-zero segments of the four 16-pixel groups, 8 bits each
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int64_t g16 = pbase / 16 + g;
@@ -1124,24 +1193,24 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     }
     const int64_t p = pbase + 16 * g + (lane & 15);
     const uint32_t f = p < P ? flags[p] : 0x1fu;
-    zx[g] = f & 0x1fu;
+    zxp |= (f & 0x1fu) << (8 * g);
     ng |= f >> 7;
   }
   const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
-  float best[4];
+  float best[4], sec[4];
   int bi[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    best[g] = -__builtin_inff();
+    best[g] = sec[g] = -__builtin_inff();
     bi[g] = 0;
   }
   const char *gref = reinterpret_cast<const char *>(refh);
   char *ldsb = reinterpret_cast<char *>(lds);
   const int nch = Rpad / CR;
-  const bool zs = __syncthreads_or((zx[0] | zx[1] | zx[2] | zx[3]) != 0);
+  const bool zs = __syncthreads_or(zxp != 0);
   const bool keyed = !libneg && !__syncthreads_or(ng != 0);
 #define HRF_SWEEPW(Z, K) \
-  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zx, best, bi)
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
   if (keyed) {
     if (zs) HRF_SWEEPW(true, true);
     else HRF_SWEEPW(false, true);
@@ -1153,12 +1222,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   const int Q = lane >> 4;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    float b = best[g];
+    float b = best[g], sc = sec[g];
     int idx = bi[g] + 4 * Q;
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float ob = __shfl_xor(b, o, 64);
       const int oi = __shfl_xor(idx, o, 64);
+      sc = fmaxf(fmaxf(sc, __shfl_xor(sc, o, 64)), fminf(score_hi(b, keyed), score_hi(ob, keyed)));
       if (ob > b || (ob == b && oi < idx)) {
         b = ob;
         idx = oi;
@@ -1168,6 +1238,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     if (Q == 0 && p < P) {
       best_idx[p] = idx;
       best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
+      if (second) second[p] = sc;
     }
   }
 }
@@ -1415,14 +1486,14 @@ int choose_ks(int K) {
 
 template <class L, int NW, int NB, int CR, int OCC>
 hrf_status launch_w16_lay(const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad, int32_t *best_idx,
-                          float *best_dist, hipStream_t s) {
+                          float *best_dist, float *second, hipStream_t s) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   const size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
   HRF_REQUIRE(shm * OCC <= 160 * 1024 + 1024, "classify: w16 configuration exceeds the LDS");
   (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   classify_pixels_w16_kernel<L, NW, NB, CR, OCC><<<(unsigned)hrf::cdiv(P, 64 * NW), 64 * NW, shm, s>>>(
-      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist);
+      stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, second);
   return HRF_OK;
 }
 
@@ -1433,6 +1504,521 @@ hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Boun
   for (int s = 0; s <= SMAX; ++s) bd->b[s] = s <= nseg ? bounds_host[s] : C;
   bd->nseg = nseg;
   return HRF_OK;
+}
+
+// ==== exact per-pixel classification: the f64 refine of the screen (round 6) ==================
+// The MFMA sweeps above are a SCREEN: split-fp16 (or f32-MFMA) scores within a bound of the exact
+// segmented-cosine score.  Every sweep also reports, per pixel, an upper bound s2 on the device
+// score of every library row other than its best row b1 (the runner-up, `second`).  The refine:
+//  * rescores b1 in f64 exactly as the restatement does (oracle seg_dist / oracle_segcos variant
+//    0: the three sums in channel order, 1 - d / sqrt(nx * ny), the segment mean) from the pixel's
+//    f32 values -- the stack, or the five shifted acquisitions of a registered tile -- and the f32
+//    library promoted to f64 (the restatement's ref64);
+//  * certifies b1 when D(b1) < 1 - (s2 + eps) / nseg - 1e-12, eps the screen's proven error bound
+//    (screen_eps below): then every other row r has S_exact(r) <= s2 + eps, i.e. its restated
+//    distance exceeds D(b1), so b1 is the restatement's argmin and D(b1) its distance, bit for bit;
+//  * answers an all-zero pixel from the library alone (every segment one-zero or both-zero:
+//    D(r) = (nonzero segments of r) / nseg, its first argmin precomputed at prepare time);
+//  * lists every other pixel (ties, near-ties, NaN / inf values) for refine_list_kernel, which
+//    scores all rows in f32 with its own proven bound (fmaf chains on the raw values), keeps the
+//    rows within twice that bound of the best, and rescores those in f64 -- lowest row on ties.
+// The prepared library (refx) carries the exact section after its MFMA table: a header, the f32
+// library row-major (pitch CP = C rounded to 4, float4 rows), channel-major (pitch RT = R rounded
+// to 64, coalesced for the list kernel), the f64 segment sums of squares ny (the restatement's
+// |y|^2) and f32 reciprocal segment norms iy.
+struct ExactHdr {
+  int32_t R, C, nseg, idx0;  // idx0 / D0: the all-zero pixel's argmin and distance
+  double D0;
+  int32_t tiny;              // some row has 0 < ny < 1e-30: the list kernel's f32 pass is not safe
+};
+struct ExactLayout {
+  int64_t off;  // section offset from the start of refx
+  int32_t CP, RT;
+  int64_t lib32, libT, ny, iy, total;  // offsets inside the section
+};
+inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+ExactLayout exact_layout(int mode, int lay, int kp, int rpad, int R, int C, int nseg) {
+  ExactLayout e;
+  const int64_t rowb = mode == 0 ? 4 * (int64_t)kp : table_rowb(mode, lay, kp);
+  e.off = al256((int64_t)rpad * rowb);
+  e.CP = (C + 3) & ~3;
+  e.RT = (R + 63) & ~63;
+  e.lib32 = 256;
+  e.libT = al256(e.lib32 + (int64_t)R * e.CP * 4);
+  e.ny = al256(e.libT + (int64_t)C * e.RT * 4);
+  e.iy = al256(e.ny + (int64_t)R * nseg * 8);
+  e.total = al256(e.iy + (int64_t)R * nseg * 4);
+  return e;
+}
+struct ExactPtr {
+  const float *lib32, *libT, *iy;
+  const double *ny;
+  int32_t CP, RT;
+};
+
+__global__ __launch_bounds__(256) void exact_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C,
+                                                         Bounds bd, int32_t CP, int32_t RT, float *__restrict__ lib32,
+                                                         float *__restrict__ libT, double *__restrict__ ny,
+                                                         float *__restrict__ iy) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t e = t0; e < (int64_t)R * CP; e += stride) {
+    const int64_t r = e / CP;
+    const int c = (int)(e - r * CP);
+    lib32[e] = c < C ? ref[r * C + c] : 0.0f;
+  }
+  for (int64_t e = t0; e < (int64_t)C * RT; e += stride) {
+    const int64_t c = e / RT, r = e - c * RT;
+    libT[e] = r < R ? ref[r * C + c] : 0.0f;
+  }
+  for (int64_t e = t0; e < (int64_t)R * bd.nseg; e += stride) {
+    const int64_t r = e / bd.nseg;
+    const int sg = (int)(e - r * bd.nseg);
+    double v = 0.0;
+    for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+      const double y = (double)ref[r * C + i];
+      v += y * y;
+    }
+    ny[e] = v;
+    iy[e] = v > 0.0 ? (float)(1.0 / sqrt(v)) : 0.0f;
+  }
+}
+
+// one thread: the all-zero pixel's answer (oracle_classify's loop on x = 0) and the tiny-row flag
+__global__ void exact_hdr_kernel(const double *__restrict__ ny, int32_t R, int32_t C, int32_t nseg,
+                                 ExactHdr *__restrict__ hdr) {
+  double best = __builtin_inf();
+  int32_t bi = 0, tiny = 0;
+  for (int r = 0; r < R; ++r) {
+    double sum = 0.0;
+    for (int sg = 0; sg < nseg; ++sg) {
+      const double v = ny[(int64_t)r * nseg + sg];
+      sum += v == 0.0 ? 0.0 : 1.0;
+      tiny |= (v > 0.0 && v < 1e-30) ? 1 : 0;
+    }
+    const double d = sum / nseg;
+    if (d < best) {
+      best = d;
+      bi = r;
+    }
+  }
+  hdr->R = R;
+  hdr->C = C;
+  hdr->nseg = nseg;
+  hdr->idx0 = bi;
+  hdr->D0 = best;
+  hdr->tiny = tiny;
+}
+
+// Pixel source: the registered value of pixel p (row r = p / W, column c = p % W) at channel k of
+// laser q is src[q][((r - dr_q) W + (c - dc_q)) cl_q + (k - c0_q)], 0 outside the laser's frame and,
+// with apply_mask, outside any laser's frame (register_assemble's stack; stack.hip).  A plain (P, C)
+// stack is one laser with no shift.
+constexpr int XLMAX = 8;
+struct PixSrc {
+  const float *src[XLMAX];
+  int32_t c0[XLMAX + 1];
+  uint64_t mdiv[XLMAX];  // ceil(2^32 / cl): e / cl = (e * mdiv) >> 32 for e < 2^32 / cl
+  int32_t n;
+  const int32_t *dsh;    // device (dr, dc) pairs, or null (no shift)
+  int64_t H, W;
+  int32_t apply_mask;
+};
+
+__device__ __forceinline__ bool src_covered(int64_t r, int64_t c, int64_t H, int64_t W, int dr, int dc) {
+  return r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0) && c >= (dc > 0 ? dc : 0) && c < W + (dc < 0 ? dc : 0);
+}
+
+// element offsets (from src[q]) of pixel p's run in every laser, -1 where it reads as zero
+__device__ __forceinline__ void src_offsets(const PixSrc &S, int64_t p, bool valid, int32_t (&off)[XLMAX]) {
+  const int64_t r = p / S.W, c = p - r * S.W;
+  bool ok = valid;
+  if (S.apply_mask && S.dsh)
+    for (int q = 0; q < S.n; ++q) ok = ok && src_covered(r, c, S.H, S.W, S.dsh[2 * q], S.dsh[2 * q + 1]);
+#pragma unroll
+  for (int q = 0; q < XLMAX; ++q) {
+    off[q] = -1;
+    if (q < S.n && ok) {
+      const int dr = S.dsh ? S.dsh[2 * q] : 0, dc = S.dsh ? S.dsh[2 * q + 1] : 0;
+      if (src_covered(r, c, S.H, S.W, dr, dc))
+        off[q] = (int32_t)(((r - dr) * S.W + (c - dc)) * (int64_t)(S.c0[q + 1] - S.c0[q]));
+    }
+  }
+}
+
+// f64 restated distance of the pixel (f32 values x[0..C), stride 1) to a library row (yv: its f32
+// values, float4-aligned, CP = C rounded to 4; nyr: its segment sums of squares): the
+// restatement's seg_dist per segment in channel order, their sum, / nseg.  nz: the pixel's
+// all-zero segments; in_range: every non-zero segment's sum of squares lies where the screen's f32
+// normalisation is exact to its bound (no f32 overflow, no overflowing f64-redo reciprocal).
+// NC > 0: the channel loop unrolled to NC (yv then indexes registers with constants); 0: a loop.
+constexpr double NX_MIN = 1e-70, NX_MAX = 1e37;
+template <int NC, class YV>
+__device__ __forceinline__ double exact_dist_y(const float *x, YV yv, const double *nyr, int C, const Bounds &bd,
+                                               int *nz, bool *in_range) {
+  double nx = 0.0, dd = 0.0, sum = 0.0;
+  int sg = 0, send = bd.b[1], zc = 0;
+  bool rok = true;
+#pragma unroll
+  for (int c = 0; c < (NC ? NC : C); ++c) {
+    if (NC && c >= C) break;
+    const double xv = (double)x[c], yy = (double)yv(c);
+    dd += xv * yy;
+    nx += xv * xv;
+    if (c + 1 == send) {
+      const double ny = nyr[sg];
+      const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
+      sum += sd;
+      zc += nx == 0.0 ? 1 : 0;
+      rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
+      nx = dd = 0.0;
+      ++sg;
+      send = bd.b[sg + 1];
+    }
+  }
+  *nz = zc;
+  if (in_range) *in_range = rok;
+  return sum / bd.nseg;
+}
+__device__ __forceinline__ double exact_dist(const float *x, const ExactPtr &E, int r, int C, const Bounds &bd,
+                                             int *nz, bool *in_range = nullptr) {
+  const float *yr = E.lib32 + (int64_t)r * E.CP;
+  return exact_dist_y<0>(x, [&](int c) { return yr[c]; }, E.ny + (int64_t)r * bd.nseg, C, bd, nz, in_range);
+}
+
+// One wave = 32 consecutive pixels.  Their values and their screen rows b1 are loaded with every
+// load of the wave in flight at once (lane = channel c and c + 64, unrolled over the 32 pixels:
+// each pixel's registered spectrum is a few contiguous laser runs, each library row one run) and
+// staged in LDS; then lanes 0..31 (lane = pixel) rescore b1 in f64 and certify or list it.
+constexpr int REF_NP = 32;
+__global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, int32_t C, Bounds bd, ExactPtr E,
+                                                         const ExactHdr *__restrict__ hdr, double eps_base,
+                                                         double eps_zero, const float *__restrict__ second,
+                                                         int32_t *__restrict__ best_idx, float *__restrict__ best_dist,
+                                                         int32_t *__restrict__ list, int32_t *__restrict__ cnt) {
+  extern __shared__ float rxs[];  // x: REF_NP x CPX, then y: REF_NP x CPX
+  __shared__ int32_t offs[XLMAX][REF_NP];
+  __shared__ int32_t b1s[REF_NP];
+  const int CPX = C | 1;  // odd pitch: conflict-free lane-per-pixel reads
+  float *ys = rxs + REF_NP * CPX;
+  const int lane = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * REF_NP, p = p0 + lane;
+  const bool valid = lane < REF_NP && p < P;
+  const int Rr = hdr->R;
+  int b1 = valid ? best_idx[p] : 0;
+  const bool brow = b1 >= 0 && b1 < Rr;
+  const float sec2 = valid ? second[p] : 0.0f;
+  if (lane < REF_NP) {
+    int32_t off[XLMAX];
+    src_offsets(S, p, valid, off);
+#pragma unroll
+    for (int q = 0; q < XLMAX; ++q) offs[q][lane] = off[q];
+    b1s[lane] = brow ? b1 : 0;
+  }
+  __syncthreads();
+  // lane = channels c0 = lane and c1 = lane + 64: laser q and local channel fixed per lane
+  const int c0 = lane, c1 = lane + 64;
+  int q0 = 0, q1 = 0;
+  for (int q = 1; q < S.n; ++q) {
+    q0 = c0 >= S.c0[q] ? q : q0;
+    q1 = c1 >= S.c0[q] ? q : q1;
+  }
+  const float *s0 = S.src[q0] + (c0 - S.c0[q0]), *s1 = S.src[q1] + (c1 - S.c0[q1]);
+  const bool v0 = c0 < C, v1 = c1 < C;
+  {
+    float x0[REF_NP], x1[REF_NP], y0[REF_NP], y1[REF_NP];
+#pragma unroll
+    for (int i = 0; i < REF_NP; ++i) {
+      const int o0 = offs[q0][i], o1 = offs[q1][i];
+      const float *yr = E.lib32 + (int64_t)b1s[i] * E.CP;
+      x0[i] = (v0 && o0 >= 0) ? s0[o0] : 0.0f;
+      x1[i] = (v1 && o1 >= 0) ? s1[o1] : 0.0f;
+      y0[i] = v0 ? yr[c0] : 0.0f;
+      y1[i] = v1 ? yr[c1] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < REF_NP; ++i) {
+      if (v0) {
+        rxs[i * CPX + c0] = x0[i];
+        ys[i * CPX + c0] = y0[i];
+      }
+      if (v1) {
+        rxs[i * CPX + c1] = x1[i];
+        ys[i * CPX + c1] = y1[i];
+      }
+    }
+  }
+  __syncthreads();
+  bool listed = false;
+  if (valid) {
+    if (!brow) {  // no real row won the screen (cannot happen with R >= 1): list it
+      listed = true;
+    } else {
+      int nz = 0;
+      bool in_range = true;
+      const float *yl = ys + lane * CPX;
+      const double D = exact_dist_y<0>(rxs + lane * CPX, [&](int c) { return yl[c]; }, E.ny + (int64_t)b1 * bd.nseg,
+                                       C, bd, &nz, &in_range);
+      if (nz == bd.nseg) {  // all-zero pixel: the library's own answer
+        best_idx[p] = hdr->idx0;
+        best_dist[p] = (float)hdr->D0;
+      } else if (!in_range) {  // outside the screen bound's premises
+        listed = true;
+      } else {
+        const double eps = eps_base + eps_zero * nz;
+        const double lim = 1.0 - ((double)sec2 + eps) / bd.nseg - 1e-12;
+        if (D < lim) best_dist[p] = (float)D;  // certified (NaN anywhere fails the compare)
+        else listed = true;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(listed);
+  if (m) {
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(cnt, __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1, 64);
+    if (listed) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+  }
+}
+
+// Listed pixels, in batches of LIST_NP per workgroup (grid-strided over the device count), so
+// each library value read from L2 serves LIST_NP pixels:
+//  1. the batch's values (32 threads per pixel, lane = channel) and finiteness; per pixel and
+//     segment the f64 sum of squares nx (channel order) and the f32 reciprocal norm ix;
+//  2. every row's f32 score for every pixel of the batch (thread = 4 rows): per segment an fmaf
+//     chain of the raw products d, cos = d * ix * iy (both-zero 1, one-zero 0), summed in f32; its
+//     error is at most eps32 (screen_eps) -- so only rows within 2 eps32 of a pixel's best f32
+//     score can be its restated argmin;
+//  3. those rows (every row for a pixel with non-finite values or norms out of the f32 pass's
+//     range) rescored exactly (exact_dist), minimum with the lowest row on ties, as
+//     oracle_classify's first-minimum loop.
+constexpr int LIST_NP = 8;     // pixels per batch
+constexpr int LIST_NT = 256;   // threads per workgroup
+constexpr int LIST_RMAX = 4096;
+__global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t C, Bounds bd, ExactPtr E,
+                                                              const ExactHdr *__restrict__ hdr, int32_t R,
+                                                              double eps32, const int32_t *__restrict__ list,
+                                                              const int32_t *__restrict__ cnt,
+                                                              int32_t *__restrict__ best_idx,
+                                                              float *__restrict__ best_dist) {
+  __shared__ float xb[LIST_NP][128];
+  __shared__ float ixb[LIST_NP][SMAX];
+  __shared__ int fullb[LIST_NP];
+  __shared__ float thrb[LIST_NP];
+  __shared__ double redd[LIST_NT / 64][LIST_NP];
+  __shared__ int redr[LIST_NT / 64][LIST_NP];
+  constexpr int CAND = 1024;  // sparse candidates per batch; a pixel that overflows is scored in full
+  __shared__ int32_t cand[CAND];
+  __shared__ int ncand;
+  extern __shared__ float scb[];  // LIST_NP x RT f32 scores
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int n = *cnt;
+  const int nseg = bd.nseg;
+  for (int64_t b0 = (int64_t)blockIdx.x * LIST_NP; b0 < n; b0 += (int64_t)gridDim.x * LIST_NP) {
+    const int nb = (int)min((int64_t)LIST_NP, n - b0);
+    // 1. values: pixel j = t / 32, channels (t & 31) + 32 m
+    {
+      const int j = t >> 5, k0 = t & 31;
+      bool bad = false;
+      if (j < nb) {
+        const int64_t p = list[b0 + j];
+        int32_t off[XLMAX];
+        src_offsets(S, p, true, off);
+        for (int k = k0; k < C; k += 32) {
+          int q = 0;
+          for (int qq = 1; qq < S.n; ++qq) q = k >= S.c0[qq] ? qq : q;
+          const float v = off[q] >= 0 ? S.src[q][off[q] + k - S.c0[q]] : 0.0f;
+          xb[j][k] = v;
+          bad = bad || !__builtin_isfinite(v);
+        }
+      }
+      if (t < LIST_NP) fullb[t] = hdr->tiny;
+      __syncthreads();
+      if (bad) atomicOr(&fullb[j], 1);
+    }
+    if (t < nb * nseg) {
+      const int j = t / nseg, sg = t - j * nseg;
+      double v = 0.0;
+      for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+        const double xd = (double)xb[j][i];
+        v += xd * xd;
+      }
+      ixb[j][sg] = v > 0.0 ? (float)(1.0 / sqrt(v)) : 0.0f;
+      if (v > 0.0 && (v < 1e-30 || v > 1e30)) atomicOr(&fullb[j], 1);
+    }
+    __syncthreads();
+    // 2. f32 scores, thread = rows r0 + t + 256 u
+    for (int r0 = 0; r0 < E.RT; r0 += 4 * LIST_NT) {
+      float sc[LIST_NP][4];
+#pragma unroll
+      for (int j = 0; j < LIST_NP; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sc[j][u] = 0.0f;
+      for (int sg = 0; sg < nseg; ++sg) {
+        float d[LIST_NP][4];
+#pragma unroll
+        for (int j = 0; j < LIST_NP; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) d[j][u] = 0.0f;
+        for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+          float y[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = r0 + t + LIST_NT * u;
+            y[u] = r < E.RT ? E.libT[(int64_t)i * E.RT + r] : 0.0f;
+          }
+#pragma unroll
+          for (int j = 0; j < LIST_NP; ++j) {
+            const float x = xb[j][i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) d[j][u] = __builtin_fmaf(x, y[u], d[j][u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = r0 + t + LIST_NT * u;
+          const float iyv = r < R ? E.iy[(int64_t)r * nseg + sg] : 0.0f;
+#pragma unroll
+          for (int j = 0; j < LIST_NP; ++j) {
+            const float ix = ixb[j][sg];
+            const float c = ix == 0.0f ? (iyv == 0.0f ? 1.0f : 0.0f) : (iyv == 0.0f ? 0.0f : (d[j][u] * ix) * iyv);
+            sc[j][u] += c;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + t + LIST_NT * u;
+        if (r < E.RT)
+#pragma unroll
+          for (int j = 0; j < LIST_NP; ++j) scb[j * E.RT + r] = r < R ? sc[j][u] : -__builtin_inff();
+      }
+    }
+    __syncthreads();
+    // per pixel: the best f32 score -> the candidate threshold (wave w takes pixels w, w + 4)
+    for (int j = w; j < nb; j += LIST_NT / 64) {
+      float mx = -__builtin_inff();
+      for (int r = lane; r < R; r += 64) mx = fmaxf(mx, scb[j * E.RT + r]);
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      if (lane == 0) {
+        float th = mx - (float)(2.0 * eps32) * 1.0001f;
+        thrb[j] = th - fabsf(th) * 1e-6f;  // the subtraction's own rounding, generously
+      }
+    }
+    __syncthreads();
+    // 3. exact distances: the candidates of the other pixels compacted into one list shared by
+    //    all threads (a handful per pixel), every row of the full-path pixels; per pixel the
+    //    minimum, lowest row on ties, whatever order the rows were visited in
+    if (t == 0) ncand = 0;
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) {
+      if (fullb[j]) continue;
+      const float th = thrb[j];
+      for (int r = t; r < R; r += LIST_NT)
+        if (scb[j * E.RT + r] >= th) {
+          const int k = atomicAdd(&ncand, 1);
+          if (k < CAND) cand[k] = (j << 16) | r;
+          else atomicOr(&fullb[j], 2);
+        }
+    }
+    __syncthreads();
+    double bdv[LIST_NP];
+    int brv[LIST_NP];
+#pragma unroll
+    for (int j = 0; j < LIST_NP; ++j) {
+      bdv[j] = __builtin_inf();
+      brv[j] = 0x7fffffff;
+    }
+    auto take = [&](int j, int r) {
+      int nz = 0;
+      const double D = exact_dist(xb[j], E, r, C, bd, &nz);
+#pragma unroll
+      for (int jj = 0; jj < LIST_NP; ++jj)
+        if (jj == j && (D < bdv[jj] || (D == bdv[jj] && r < brv[jj]))) {
+          bdv[jj] = D;
+          brv[jj] = r;
+        }
+    };
+    const int nc = min(ncand, CAND);
+    for (int k = t; k < nc; k += LIST_NT) {
+      const int j = cand[k] >> 16, r = cand[k] & 0xffff;
+      if (!fullb[j]) take(j, r);
+    }
+    for (int j = 0; j < nb; ++j)
+      if (fullb[j])
+        for (int r = t; r < R; r += LIST_NT) take(j, r);
+#pragma unroll
+    for (int j = 0; j < LIST_NP; ++j) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ob = __shfl_xor(bdv[j], o, 64);
+        const int orr = __shfl_xor(brv[j], o, 64);
+        if (ob < bdv[j] || (ob == bdv[j] && orr < brv[j])) {
+          bdv[j] = ob;
+          brv[j] = orr;
+        }
+      }
+      if (lane == 0) {
+        redd[w][j] = bdv[j];
+        redr[w][j] = brv[j];
+      }
+    }
+    __syncthreads();
+    if (t < nb) {
+      double bv = redd[0][t];
+      int br = redr[0][t];
+      for (int ww = 1; ww < LIST_NT / 64; ++ww) {
+        const double ob = redd[ww][t];
+        const int orr = redr[ww][t];
+        if (ob < bv || (ob == bv && orr < br)) {
+          bv = ob;
+          br = orr;
+        }
+      }
+      const int64_t p = list[b0 + t];
+      best_idx[p] = br == 0x7fffffff ? 0 : br;
+      best_dist[p] = (float)bv;
+    }
+    __syncthreads();
+  }
+}
+
+// The screen's proven error bound, in score units (score = sum over segments of the cosine of the
+// segment-normalised vectors, plus the zero-segment indicators), for a pixel with no all-zero
+// segment (eps_zero per all-zero segment on top).  u = 2^-24.  Terms, per segment s of n_s channels:
+//  (a) the pixel's f32 normalisation: f32 sum of squares (<= n_s u), v_rsq (<= 2 u), the product
+//      (u): the segment cosine moves by <= (n_s / 2 + 4) u;
+//  (b) the library's normalisation (f64, rounded to f32): <= 1.01 u;
+//  (c) split fp16 (v = hi + lo + e, |e| <= 2^-22 |v| + 2^-25; lo * lo' dropped):
+//      <= 3 * 2^-22 + 2^-24 * 1.01 sqrt(n_s)  (sum |x| <= sqrt(n_s) for a unit segment);
+//  (d) the MFMA accumulation: each f16 MFMA output within KMFMA u (|C_in| + sum |a b|) of the exact
+//      (hrf_probe_mfma_f16: tests/test_classify_exact_gpu.py measures <= 7.6 on gfx950 and asserts
+//      <= 12; the bound uses 16), and every partial sum of an output is <= A = sum |products| <=
+//      1.002 nseg (+1 per all-zero segment: the indicator terms), so NM MFMAs per output add
+//      <= KMFMA u NM A.  The f32 MFMA (mode 0) is a k-ordered fmaf chain (cdna_hip_programming.md
+//      "FP32-input MFMA"): <= KP u A.
+// The keyed sweeps' 4 truncated bits are covered by reporting s2 with them set (key_score_hi).
+constexpr double KMFMA = 16.0;
+constexpr double U24 = 1.0 / 16777216.0;
+struct ScreenEps {
+  double base, zero, eps32;
+};
+ScreenEps screen_eps(const Bounds &bd, int nmfma, bool f32chain, int kp) {
+  double a = 0.0, c = 0.0, e32 = 0.0;
+  for (int sg = 0; sg < bd.nseg; ++sg) {
+    const int ns = bd.b[sg + 1] - bd.b[sg];
+    a += ns / 2.0 + 4.0 + 1.01;
+    c += 12.0 + 1.01 * sqrt((double)ns);
+    e32 += ns + 4.01;
+  }
+  e32 += (double)bd.nseg * bd.nseg;
+  const double A = 1.002 * bd.nseg + 0.01;
+  const double per = f32chain ? (double)kp : KMFMA * nmfma;
+  ScreenEps e;
+  e.base = U24 * (a + c + per * A) * 1.01;
+  e.zero = U24 * per * 1.01;
+  e.eps32 = U24 * e32 * 1.01;
+  return e;
 }
 
 }  // namespace
@@ -1479,40 +2065,60 @@ hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, con
   HRF_REQUIRE(ref && refx, "classify_prepare_refs: null buffer");
   HRF_REQUIRE(mode != 2 || layout_id(bd, C) != 0,
               "classify: mode 2 needs the E. coli (0,32,55,75,89,95) or multispecies (0,23,43,57,63) layout");
+  HRF_REQUIRE(C <= 128 && R <= LIST_RMAX, "classify_prepare_refs: C <= 128 and R <= %d required", LIST_RMAX);
+  hipStream_t s = (hipStream_t)stream;
   if (mode == 2) {
-    ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(
+    ref_prep_lay_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, s>>>(
         ref, R, C, bd, kp, rpad, (int32_t)(table_rowb(2, layout_id(bd, C), kp) / 2), (_Float16 *)refx);
-    ref_negflag_kernel<<<1, 256, 0, (hipStream_t)stream>>>(ref, (int64_t)R * C, kp, (_Float16 *)refx);
+    ref_negflag_kernel<<<1, 256, 0, s>>>(ref, (int64_t)R * C, kp, (_Float16 *)refx);
   } else if (mode == 0)
-    ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
-                                                                                      (float *)refx);
+    ref_prep_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, s>>>(ref, R, C, bd, kp, rpad, (float *)refx);
   else
-    ref_prep_f16_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, (hipStream_t)stream>>>(ref, R, C, bd, kp, rpad,
-                                                                                          (_Float16 *)refx);
+    ref_prep_f16_kernel<<<(unsigned)hrf::cdiv(rpad, 128), 128, 0, s>>>(ref, R, C, bd, kp, rpad, (_Float16 *)refx);
+  // the exact section (refine): f32 library row- and channel-major, ny, iy, header
+  const ExactLayout el = exact_layout(mode, layout_id(bd, C), kp, rpad, R, C, nseg);
+  char *sec = (char *)refx + el.off;
+  exact_prep_kernel<<<hrf::stream_grid((int64_t)C * el.RT), 256, 0, s>>>(
+      ref, R, C, bd, el.CP, el.RT, (float *)(sec + el.lib32), (float *)(sec + el.libT), (double *)(sec + el.ny),
+      (float *)(sec + el.iy));
+  exact_hdr_kernel<<<1, 1, 0, s>>>((const double *)(sec + el.ny), R, C, nseg, (ExactHdr *)sec);
   HRF_LAUNCHED();
   return HRF_OK;
 }
 
-hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
-                               const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
-                               float *best_dist, hrf_stream_t stream) {
+int64_t hrf_classify_refx_bytes(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t R, int32_t mode) {
   Bounds bd;
-  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  if (make_bounds(bounds_host, nseg, C, &bd) != HRF_OK) return -1;
   int32_t kp = 0, rpad = 0;
-  if (hrf_status s = hrf_classify_geometry(C, nseg, R, mode, &kp, &rpad)) return s;
+  if (hrf_classify_geometry(C, nseg, R, mode, &kp, &rpad) != HRF_OK) return -1;
+  const ExactLayout el = exact_layout(mode, layout_id(bd, C), kp, rpad, R, C, nseg);
+  return el.off + el.total;
+}
+
+int64_t hrf_classify_refine_work_bytes(int64_t P) { return P < 0 ? -1 : 16 + 4 * (P > 0 ? P : 1); }
+
+}  // extern "C"
+
+namespace {
+
+// the sweep of hrf_classify_pixels (`second`: nullable runner-up bound output)
+hrf_status screen_stack(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R, const Bounds &bd,
+                        int32_t mode, int32_t *best_idx, float *best_dist, float *second, hipStream_t s) {
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status st = hrf_classify_geometry(C, bd.nseg, R, mode, &kp, &rpad)) return st;
   if (P == 0) return HRF_OK;
   HRF_REQUIRE(stack && refx && best_idx && best_dist, "classify_pixels: null buffer");
   const unsigned grid = (unsigned)hrf::cdiv(P, 256);
-  hipStream_t s = (hipStream_t)stream;
   if (mode == 2) {
     const int lay = layout_id(bd, C);
     HRF_REQUIRE(lay != 0, "classify: mode 2 needs the E. coli or multispecies channel layout");
     if (lay == 1) {
       // E. coli layout: the 16x16x32 sweep with the lane-per-pixel prologue
-      // (classify_pixels_w16_kernel) in its measured-best configuration -- 4 waves, 2 buffers of
-      // 64 rows, three workgroups per CU (1.76 vs 1.83 ms for round 2's lay16 form, 2.13-2.20 for
-      // the 32x32x16 form, on a 2048^2 tile at R = 1023; DESIGN.md "Per-pixel classifier")
-      if (hrf_status st = launch_w16_lay<LayEcoli, 4, 2, 64, 3>(stack, P, refx, R, rpad, best_idx, best_dist, s))
+      // (classify_pixels_w16_kernel) -- 4 waves, 2 buffers of 64 rows, HRF_W16T_OCC workgroups per
+      // CU (rounds 3-5: three, 1.76 vs 1.83 ms for round 2's lay16 form, 2.13-2.20 for the 32x32x16
+      // form, on a 2048^2 tile at R = 1023; DESIGN.md "Per-pixel classifier")
+      if (hrf_status st = launch_w16_lay<LayEcoli, 4, 2, 64, HRF_W16T_OCC>(stack, P, refx, R, rpad, best_idx, best_dist,
+                                                                            second, s))
         return st;
       HRF_LAUNCHED();
       return HRF_OK;
@@ -1524,7 +2130,7 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
     (void)hipFuncSetAttribute((const void *)classify_pixels_lay_kernel<LayMulti, 4>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     classify_pixels_lay_kernel<LayMulti, 4><<<(unsigned)hrf::cdiv(P, 256), 256, shm, s>>>(
-        stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist);
+        stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, second);
     HRF_LAUNCHED();
     return HRF_OK;
   }
@@ -1537,7 +2143,7 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
     hipFuncSetAttribute((const void *)classify_pixels_f16_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                         (int)shm);                                                                           \
     classify_pixels_f16_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, (const _Float16 *)refx, R, rpad,     \
-                                                         best_idx, best_dist);                               \
+                                                         best_idx, best_dist, second);                       \
     break;
     switch (ks16) {
       HRF_CP16(1)
@@ -1563,7 +2169,7 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
     hipFuncSetAttribute((const void *)classify_pixels_kernel<K>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                         (int)shm);                                                                         \
     classify_pixels_kernel<K><<<grid, 256, shm, s>>>(stack, P, C, bd, (const float *)refx, R, rpad, best_idx,   \
-                                                     best_dist);                                           \
+                                                     best_dist, second);                                   \
     break;
   switch (ks) {
     HRF_CP(8)
@@ -1582,6 +2188,142 @@ hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const v
 #undef HRF_CP
   HRF_LAUNCHED();
   return HRF_OK;
+}
+
+// MFMAs accumulated into one score by each screen (the bound's NM): screen 0 = mode 0 (f32 chain,
+// KP fmas), 1 = mode 1 (32x32x16, indicator columns), 2 = mode 2 in-kernel (E. coli: the 16x16x32
+// w16 sweep, community: the 32x32x16 lay sweep; + the indicator k-step), 3 = the pixel-table w16t
+ScreenEps eps_of_screen(int screen, const Bounds &bd, int C, int kp) {
+  const int lay = layout_id(bd, C);
+  if (screen == 0) return screen_eps(bd, 0, true, kp);
+  if (screen == 1) return screen_eps(bd, 3 * (kp / 16), false, kp);
+  if (screen == 2 && lay == 2) return screen_eps(bd, 3 * ((C + 1 + 15) / 16) + 1, false, kp);
+  return screen_eps(bd, 3 * ((C + 1 + 31) / 32) + 1, false, kp);  // w16 / w16t
+}
+
+hrf_status refine(const PixSrc &S, int64_t P, int32_t C, const void *refx, int32_t R, const Bounds &bd, int32_t screen,
+                  const float *second, int32_t *best_idx, float *best_dist, void *work, int64_t work_bytes,
+                  hipStream_t s) {
+  HRF_REQUIRE(screen >= 0 && screen <= 3, "classify_refine: screen must be 0..3");
+  const int mode = screen == 3 ? 2 : screen;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status st = hrf_classify_geometry(C, bd.nseg, R, mode, &kp, &rpad)) return st;
+  HRF_REQUIRE(C <= 128 && R <= LIST_RMAX, "classify_refine: C <= 128 and R <= %d required", LIST_RMAX);
+  HRF_REQUIRE(work_bytes >= hrf_classify_refine_work_bytes(P), "classify_refine: work buffer too small");
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(refx && second && best_idx && best_dist && work, "classify_refine: null buffer");
+  const ExactLayout el = exact_layout(mode, layout_id(bd, C), kp, rpad, R, C, bd.nseg);
+  const char *sec = (const char *)refx + el.off;
+  ExactPtr E;
+  E.lib32 = (const float *)(sec + el.lib32);
+  E.libT = (const float *)(sec + el.libT);
+  E.ny = (const double *)(sec + el.ny);
+  E.iy = (const float *)(sec + el.iy);
+  E.CP = el.CP;
+  E.RT = el.RT;
+  const ExactHdr *hdr = (const ExactHdr *)sec;
+  const ScreenEps ep = eps_of_screen(screen, bd, C, kp);
+  int32_t *cnt = (int32_t *)work;
+  int32_t *list = (int32_t *)((char *)work + 16);
+  HRF_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
+  const int CPX = C | 1;
+  refine_best_kernel<<<(unsigned)hrf::cdiv(P, REF_NP), 64, sizeof(float) * 2 * REF_NP * CPX, s>>>(
+      S, P, C, bd, E, hdr, ep.base, ep.zero, second, best_idx, best_dist, list, cnt);
+  HRF_LAUNCHED();
+  const size_t shm = sizeof(float) * LIST_NP * (size_t)el.RT;
+  const unsigned g = hrf::resident_grid(refine_list_kernel, LIST_NT, shm, hrf::cdiv(P, LIST_NP));
+  refine_list_kernel<<<g, LIST_NT, shm, s>>>(S, C, bd, E, hdr, R, ep.eps32, list, cnt, best_idx, best_dist);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}
+
+hrf_status pixsrc_of(const float *const *src_host, const int32_t *channels_host, const int32_t *shifts_dev,
+                     int32_t nlaser, int64_t H, int64_t W, int32_t apply_mask, int32_t C, PixSrc *S) {
+  HRF_REQUIRE(nlaser >= 1 && nlaser <= XLMAX && src_host && channels_host && H >= 0 && W >= 1,
+              "classify_refine: bad pixel source");
+  *S = PixSrc{};
+  S->n = nlaser;
+  S->c0[0] = 0;
+  for (int q = 0; q < nlaser; ++q) {
+    HRF_REQUIRE(src_host[q] && channels_host[q] >= 1, "classify_refine: laser %d missing", q);
+    S->src[q] = src_host[q];
+    S->c0[q + 1] = S->c0[q] + channels_host[q];
+    S->mdiv[q] = ((uint64_t)1 << 32) / (uint64_t)channels_host[q] + (((uint64_t)1 << 32) % (uint64_t)channels_host[q] ? 1 : 0);
+  }
+  for (int q = nlaser; q < XLMAX; ++q) S->c0[q + 1] = S->c0[nlaser];
+  HRF_REQUIRE(S->c0[nlaser] == C, "classify_refine: the lasers hold %d channels, the library %d", S->c0[nlaser], C);
+  HRF_REQUIRE(H * W * (int64_t)C < ((int64_t)1 << 31), "classify_refine: H * W * C must be < 2^31");
+  S->dsh = shifts_dev;
+  S->H = H;
+  S->W = W;
+  S->apply_mask = apply_mask;
+  return HRF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+hrf_status hrf_classify_pixels_screen(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
+                                      const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
+                                      float *best_dist, float *second, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  return screen_stack(stack, P, C, refx, R, bd, mode, best_idx, best_dist, second, (hipStream_t)stream);
+}
+
+hrf_status hrf_classify_pixels_refine(const float *const *src_host, const int32_t *channels_host,
+                                      const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                      int32_t apply_mask, const void *refx, int32_t R, const int32_t *bounds_host,
+                                      int32_t nseg, int32_t screen, const float *second, int32_t *best_idx,
+                                      float *best_dist, void *work, int64_t work_bytes, hrf_stream_t stream) {
+  Bounds bd;
+  const int32_t C = channels_host ? [&] {
+    int32_t c = 0;
+    for (int q = 0; q < nlaser && q < XLMAX; ++q) c += channels_host[q];
+    return c;
+  }() : 0;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  PixSrc S;
+  if (hrf_status s = pixsrc_of(src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, C, &S)) return s;
+  return refine(S, H * W, C, refx, R, bd, screen, second, best_idx, best_dist, work, work_bytes, (hipStream_t)stream);
+}
+
+hrf_status hrf_classify_screen_eps(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t R, int32_t screen,
+                                   double *eps_host) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  HRF_REQUIRE(screen >= 0 && screen <= 3 && eps_host, "classify_screen_eps: bad arguments");
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, screen == 3 ? 2 : screen, &kp, &rpad)) return s;
+  const ScreenEps e = eps_of_screen(screen, bd, C, kp);
+  eps_host[0] = e.base;
+  eps_host[1] = e.zero;
+  eps_host[2] = e.eps32;
+  return HRF_OK;
+}
+
+hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
+                               const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
+                               float *best_dist, hrf_stream_t stream) {
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  if (P == 0) return HRF_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t wb = hrf_classify_refine_work_bytes(P);
+  char *ws = nullptr;
+  HRF_HIP(hipMallocAsync((void **)&ws, (size_t)(al256(4 * P) + wb), s));
+  float *second = (float *)ws;
+  hrf_status st = screen_stack(stack, P, C, refx, R, bd, mode, best_idx, best_dist, second, s);
+  if (!st) {
+    const float *src[1] = {stack};
+    const int32_t ch[1] = {C};
+    PixSrc S;
+    st = pixsrc_of(src, ch, nullptr, 1, 1, P, 0, C, &S);
+    if (!st) st = refine(S, P, C, refx, R, bd, mode, second, best_idx, best_dist, ws + al256(4 * P), wb, s);
+  }
+  HRF_HIP(hipFreeAsync(ws, s));
+  return st;
 }
 
 int64_t hrf_pixtable_bytes(int64_t P, int32_t C, const int32_t *bounds_host, int32_t nseg) {
@@ -1612,7 +2354,7 @@ hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C, const 
 
 hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C, const void *refx,
                                      int32_t R, const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
-                                     float *best_dist, hrf_stream_t stream) {
+                                     float *best_dist, float *second, hrf_stream_t stream) {
   Bounds bd;
   if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
   int32_t kp = 0, rpad = 0;
@@ -1627,11 +2369,11 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
     const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
-    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, 3>,
+    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    classify_pixels_w16t_kernel<L, 4, 2, 64, 3><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
+    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
                                                                         (const _Float16 *)refx, R, rpad, best_idx,
-                                                                        best_dist);
+                                                                        best_dist, second);
     return HRF_OK;
   };
   hrf_status st = lay == 1 ? go(LayEcoli{}) : go(LayMulti{});
@@ -1721,3 +2463,61 @@ hrf_status hrf_classify_cells(const double *x, int64_t N, const double *ref, int
 }
 
 }  // extern "C"
+
+// ---- MFMA accumulation probe ------------------------------------------------------------------
+// The per-pixel screen's error bound (hrf_classify_pixels_refine) assumes how an f16 MFMA adds
+// its products to the f32 accumulator.  This runs ONE v_mfma_f32_16x16x32_f16 (shape 0) or
+// v_mfma_f32_32x32x16_f16 (shape 1) per tile on caller data so tests/test_classify_exact_gpu.py
+// can pin that model on the device: A (M x K) and B (K x N) f16 row-major, C and D (M x N) f32.
+namespace {
+__global__ __launch_bounds__(64) void mfma_probe_kernel(int shape, const _Float16 *__restrict__ a,
+                                                        const _Float16 *__restrict__ b, const float *__restrict__ c,
+                                                        float *__restrict__ d) {
+  const int t = blockIdx.x, lane = threadIdx.x;
+  h8 av, bv;
+  if (shape == 0) {  // 16 x 16 x 32: lane row/col lane & 15, k 8Q..8Q+7, D rows 4Q..4Q+3
+    const _Float16 *A = a + (int64_t)t * 16 * 32, *B = b + (int64_t)t * 32 * 16;
+    const float *Cm = c + (int64_t)t * 256;
+    float *Dm = d + (int64_t)t * 256;
+    const int j = lane & 15, Q = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      av[q] = A[j * 32 + 8 * Q + q];
+      bv[q] = B[(8 * Q + q) * 16 + j];
+    }
+    f32x4 acc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = Cm[(4 * Q + i) * 16 + j];
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Dm[(4 * Q + i) * 16 + j] = acc[i];
+  } else {  // 32 x 32 x 16: lane row/col lane & 31, k 8h..8h+7, D rows (reg & 3) + 8 (reg >> 2) + 4h
+    const _Float16 *A = a + (int64_t)t * 32 * 16, *B = b + (int64_t)t * 16 * 32;
+    const float *Cm = c + (int64_t)t * 1024;
+    float *Dm = d + (int64_t)t * 1024;
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      av[q] = A[j * 16 + 8 * h + q];
+      bv[q] = B[(8 * h + q) * 32 + j];
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = Cm[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + j];
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, bv, acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Dm[((r & 3) + 8 * (r >> 2) + 4 * h) * 32 + j] = acc[r];
+  }
+}
+}  // namespace
+
+extern "C" hrf_status hrf_probe_mfma_f16(int32_t shape, const void *a, const void *b, const float *c, float *d,
+                                         int32_t ntiles, hrf_stream_t stream) {
+  HRF_REQUIRE((shape == 0 || shape == 1) && ntiles >= 0 && (ntiles == 0 || (a && b && c && d)),
+              "probe_mfma_f16: bad arguments");
+  if (ntiles == 0) return HRF_OK;
+  mfma_probe_kernel<<<(unsigned)ntiles, 64, 0, (hipStream_t)stream>>>(shape, (const _Float16 *)a,
+                                                                      (const _Float16 *)b, c, d);
+  HRF_LAUNCHED();
+  return HRF_OK;
+}

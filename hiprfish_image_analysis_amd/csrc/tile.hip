@@ -50,6 +50,9 @@ struct hrf_tile_ctx {
   double *cn = nullptr;         // image_cn
   void *table = nullptr;        // pixel table
   uint8_t *flags = nullptr;
+  float *second = nullptr;      // the screen's runner-up bounds
+  void *rwork = nullptr;        // the refine's list (hrf_classify_refine_work_bytes)
+  int64_t rwork_bytes = 0;
   // per-label buffers, grown on demand (capacity cap labels + 1)
   int64_t cap = 0;
   double *sums = nullptr;
@@ -146,8 +149,10 @@ hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out) {
   if ((r = hrf_seg_ctx_create(H, W, &t->seg))) return fail(r);
   if ((r = dalloc(&t->proj, NL * n)) || (r = dalloc((char **)&t->xwork, (size_t)xb)) ||
       (r = dalloc(&t->shifts, 2 * NL)) || (r = dalloc(&t->cn, n)) || (r = dalloc((char **)&t->table, (size_t)tb)) ||
-      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)))
+      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)) || (r = dalloc(&t->second, n)) ||
+      (r = dalloc((char **)&t->rwork, (size_t)hrf_classify_refine_work_bytes((int64_t)n))))
     return fail(r);
+  t->rwork_bytes = hrf_classify_refine_work_bytes((int64_t)n);
   if (hipEventCreateWithFlags(&t->ev_reg, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&t->ev_pix, hipEventDisableTiming) != hipSuccess) {
     ::hrf::set_error("tile_ctx: event creation failed");
@@ -166,6 +171,8 @@ hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *t) {
   hipFree(t->cn);
   hipFree(t->table);
   hipFree(t->flags);
+  hipFree(t->second);
+  hipFree(t->rwork);
   hipFree(t->nrows);
   hipFree(t->sums);
   hipFree(t->counts);
@@ -175,6 +182,12 @@ hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *t) {
   if (t->ev_reg) hipEventDestroy(t->ev_reg);
   if (t->ev_pix) hipEventDestroy(t->ev_pix);
   delete t;
+  return HRF_OK;
+}
+
+hrf_status hrf_tile_ctx_pixel_listed(hrf_tile_ctx *t, int32_t *n_host) {
+  HRF_REQUIRE(t && n_host, "tile_ctx_pixel_listed: bad arguments");
+  HRF_HIP(hipMemcpy(n_host, t->rwork, sizeof(int32_t), hipMemcpyDeviceToHost));
   return HRF_OK;
 }
 
@@ -222,7 +235,12 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
       HRF_HIP(hipStreamWaitEvent(side, t->ev_reg, 0));
     }
     if (pix_start) HRF_HIP(hipEventRecord((hipEvent_t)pix_start, side));
-    HRF_TRY(hrf_classify_pixels_table(t->table, t->flags, n, C, refx, R, BOUNDS, NL, pixel_idx, pixel_dist, side));
+    // the split-fp16 screen from the assembly's table, then its exact f64 refine reading the
+    // pixels from the five shifted acquisitions (hrf_classify_pixels_refine, screen 3)
+    HRF_TRY(hrf_classify_pixels_table(t->table, t->flags, n, C, refx, R, BOUNDS, NL, pixel_idx, pixel_dist, t->second,
+                                      side));
+    HRF_TRY(hrf_classify_pixels_refine(lasers_host, CH, t->shifts, NL, H, W, 1, refx, R, BOUNDS, NL, 3, t->second,
+                                       pixel_idx, pixel_dist, t->rwork, t->rwork_bytes, side));
     if (pix_end) HRF_HIP(hipEventRecord((hipEvent_t)pix_end, side));
     if (side != s) HRF_HIP(hipEventRecord(t->ev_pix, side));
   }

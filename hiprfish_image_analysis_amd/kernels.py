@@ -656,6 +656,7 @@ def register_assemble_pixtable(lasers, shifts_dev, apply_mask=True, cn_mode=1, b
     H, W = srcs[0].shape[:2]
     dev = srcs[0].device
     pt = pixtable_alloc((H, W), int(ch.sum()), bounds, dev)
+    pt.source = LaserSource(srcs, sd, apply_mask)
     cn = torch.empty((H, W), dtype=torch.float64, device=dev)
     stack = torch.empty((H, W, int(ch.sum())), dtype=torch.float32, device=dev) if want_stack else None
     _lib.call("hrf_register_assemble_pixtable", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data, _ptr(sd), len(srcs),
@@ -770,19 +771,32 @@ def classify_table_row_bytes(C, bounds, mode):
     return rb.value
 
 
+def classify_refx_bytes(C, bounds, R, mode):
+    b = _i32_host(bounds)
+    n = int(_lib.lib().hrf_classify_refx_bytes(C, b.ctypes.data, len(b) - 1, R, mode))
+    if n < 0:
+        raise ValueError("classify_refx_bytes: bad layout")
+    return n
+
+
 def classify_prepare(ref, bounds, mode=None):
     """-> prepared reference table for classify_pixels (mode 0: f32; 1: fp16 hi/lo with
-    zero-segment indicator columns; 2: fp16 hi/lo, reference layouts, indicators in the epilogue)"""
+    zero-segment indicator columns; 2: fp16 hi/lo, reference layouts, indicators in the epilogue),
+    rows of the mode's pitch; past the MFMA table's Rpad rows the exact section the f64 refine
+    reads (hrf_classify_refx_bytes)"""
     mode = _mode(bounds, mode)
     ref = _dev(ref, torch.float32, "ref")
     R, C = ref.shape
     b = _i32_host(bounds)
     kp, rp = classify_geometry(C, len(b) - 1, R, mode)
+    nbytes = classify_refx_bytes(C, bounds, R, mode)
     if mode == 0:
-        refx = torch.empty((rp, kp), dtype=torch.float32, device=ref.device)
+        rows = -(-nbytes // (4 * kp))
+        refx = torch.empty((rows, kp), dtype=torch.float32, device=ref.device)
     else:
         rowh = classify_table_row_bytes(C, bounds, mode) // 2                            # hi | lo | pad
-        refx = torch.empty((rp, rowh), dtype=torch.float16, device=ref.device)
+        rows = -(-nbytes // (2 * rowh))
+        refx = torch.empty((rows, rowh), dtype=torch.float16, device=ref.device)
     _lib.call("hrf_classify_prepare_refs", _ptr(ref), R, C, b.ctypes.data, len(b) - 1, mode, _ptr(refx), _stream())
     return refx
 
@@ -797,11 +811,23 @@ def refx_mode(refx, C, bounds):
     return 1
 
 
+def _check_refx(refx, R, C, bounds, mode, where):
+    if not isinstance(refx, torch.Tensor) or not refx.is_cuda or not refx.is_contiguous():
+        raise ValueError("%s: the prepared library must be a contiguous device tensor" % where)
+    need = classify_refx_bytes(C, bounds, R, mode)
+    if refx.numel() * refx.element_size() < need:
+        raise ValueError("%s: prepared library holds %d bytes, %d rows of mode %d need %d (classify_prepare)"
+                         % (where, refx.numel() * refx.element_size(), R, mode, need))
+
+
 def classify_pixels(stack, refx, R, bounds, mode=None):
+    """per-pixel classification, exact: the restatement's argmin (lowest row on ties) and its
+    f64 distance rounded to f32 (hrf_classify_pixels = MFMA screen + f64 refine)"""
     stack = _dev(stack, torch.float32, "stack")
     C = stack.shape[-1]
     if mode is None:
         mode = refx_mode(refx, C, bounds)
+    _check_refx(refx, R, C, bounds, mode, "classify_pixels")
     P = stack.numel() // C
     b = _i32_host(bounds)
     idx = torch.empty(stack.shape[:-1], dtype=torch.int32, device=stack.device)
@@ -811,12 +837,89 @@ def classify_pixels(stack, refx, R, bounds, mode=None):
     return idx, dist
 
 
+def classify_pixels_screen(stack, refx, R, bounds, mode=None):
+    """the MFMA screen alone -> (device argmax, device distance, runner-up score bound)"""
+    stack = _dev(stack, torch.float32, "stack")
+    C = stack.shape[-1]
+    if mode is None:
+        mode = refx_mode(refx, C, bounds)
+    _check_refx(refx, R, C, bounds, mode, "classify_pixels_screen")
+    P = stack.numel() // C
+    b = _i32_host(bounds)
+    idx = torch.empty(stack.shape[:-1], dtype=torch.int32, device=stack.device)
+    dist = torch.empty(stack.shape[:-1], dtype=torch.float32, device=stack.device)
+    sec = torch.empty(stack.shape[:-1], dtype=torch.float32, device=stack.device)
+    _lib.call("hrf_classify_pixels_screen", _ptr(stack), P, C, _ptr(refx), R, b.ctypes.data, len(b) - 1, mode,
+              _ptr(idx), _ptr(dist), _ptr(sec), _stream())
+    return idx, dist, sec
+
+
+def classify_screen_eps(C, bounds, R, screen):
+    """the refine's bounds for `screen` (hrf_classify_screen_eps) -> (base, per zero segment, f32 pass)"""
+    import ctypes
+    b = _i32_host(bounds)
+    out = (ctypes.c_double * 3)()
+    _lib.call("hrf_classify_screen_eps", C, b.ctypes.data, len(b) - 1, R, int(screen), ctypes.addressof(out))
+    return tuple(out)
+
+
+class StackSource:
+    """the pixels' f32 values for the refine: a plain (..., C) stack"""
+
+    def __init__(self, stack):
+        self.stack = _dev(stack, torch.float32, "stack")
+
+
+class LaserSource:
+    """the pixels' f32 values for the refine: the per-laser acquisitions at their device shifts
+    (register_assemble's registered stack, never materialised)"""
+
+    def __init__(self, lasers, shifts, apply_mask=True):
+        self.lasers, self.shifts, self.apply_mask = list(lasers), shifts, bool(apply_mask)
+
+
+def classify_refine(source, refx, R, bounds, screen, idx, dist, second, want_listed=False):
+    """hrf_classify_pixels_refine in place on a screen's (idx, dist, second).  source: StackSource
+    or LaserSource.  screen: 0/1/2 = classify_pixels_screen mode, 3 = classify_pixels_table.
+    -> the number of pixels the certificate did not settle (want_listed; synchronises) or None"""
+    import ctypes
+    if isinstance(source, StackSource):
+        st = source.stack
+        C = st.shape[-1]
+        P = st.numel() // C
+        ptrs = (ctypes.c_void_p * 1)(st.data_ptr())
+        ch = _i32_host([C])
+        n, H, W, sd, mask = 1, 1, P, None, 0
+    elif isinstance(source, LaserSource):
+        srcs, ch, ptrs, sd = _laser_args(source.lasers, source.shifts)
+        C = int(ch.sum())
+        n = len(srcs)
+        H, W = srcs[0].shape[:2]
+        P, mask = H * W, int(source.apply_mask)
+    else:
+        raise ValueError("classify_refine: a StackSource or LaserSource is required")
+    if idx.numel() != P:
+        raise ValueError("classify_refine: %d screened pixels, the source holds %d" % (idx.numel(), P))
+    _check_refx(refx, R, C, bounds, 2 if screen == 3 else screen, "classify_refine")
+    b = _i32_host(bounds)
+    wb = int(_lib.lib().hrf_classify_refine_work_bytes(P))
+    work = torch.empty(wb, dtype=torch.uint8, device=idx.device)
+    _lib.call("hrf_classify_pixels_refine", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data,
+              _ptr(sd) if sd is not None else None, n, H, W, mask, _ptr(refx), R, b.ctypes.data, len(b) - 1,
+              int(screen), _ptr(second), _ptr(idx), _ptr(dist), _ptr(work), wb, _stream())
+    if want_listed:
+        return int(work[:4].view(torch.int32).item())
+    return None
+
+
 class PixTable:
     """the per-pixel classifier's prepared operands (pixtable.hpp): split-fp16 segment-normalised
-    pixels in the MFMA register layout + a flag byte per pixel"""
+    pixels in the MFMA register layout + a flag byte per pixel; `source` (StackSource or
+    LaserSource) holds the f32 values the table was made from (the refine reads them)"""
 
-    def __init__(self, table, flags, shape, C, bounds):
+    def __init__(self, table, flags, shape, C, bounds, source=None):
         self.table, self.flags, self.shape, self.C, self.bounds = table, flags, tuple(shape), C, tuple(bounds)
+        self.source = source
 
     @property
     def P(self):
@@ -844,6 +947,7 @@ def pixtable_prepare(stack, bounds):
     stack = _dev(stack, torch.float32, "stack")
     C = stack.shape[-1]
     pt = pixtable_alloc(stack.shape[:-1], C, bounds, stack.device)
+    pt.source = StackSource(stack)
     b = _i32_host(bounds)
     _lib.call("hrf_pixtable_prepare", _ptr(stack), pt.P, C, b.ctypes.data, len(b) - 1, _ptr(pt.table), _ptr(pt.flags),
               _stream())
@@ -857,21 +961,29 @@ def check_refx_table(refx, R, C, bounds, where):
         raise ValueError("%s: the prepared library must be a device tensor" % where)
     if 2 not in classify_modes(bounds) or refx_mode(refx, C, bounds) != 2:
         raise ValueError("%s: a mode-2 prepared library (classify_prepare(..., mode=2)) is required" % where)
-    _, rpad = classify_geometry(C, len(bounds) - 1, R, 2)
-    need = rpad * classify_table_row_bytes(C, bounds, 2)
-    if refx.numel() * refx.element_size() < need or not refx.is_contiguous():
-        raise ValueError("%s: prepared library holds %d bytes, %d rows of the mode-2 pitch need %d"
-                         % (where, refx.numel() * refx.element_size(), rpad, need))
+    _check_refx(refx, R, C, bounds, 2, where)
 
 
-def classify_pixels_table(pt, refx, R):
-    """classify_pixels (mode 2) from a PixTable: the same results bit for bit"""
+def classify_pixels_table_screen(pt, refx, R):
+    """the mode-2 screen from a PixTable: classify_pixels_screen(mode=2)'s device scores bit for
+    bit -> (device argmax, device distance, runner-up bound)"""
     check_refx_table(refx, R, pt.C, pt.bounds, "classify_pixels_table")
     b = _i32_host(pt.bounds)
     idx = torch.empty(pt.shape, dtype=torch.int32, device=pt.table.device)
     dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
+    sec = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
     _lib.call("hrf_classify_pixels_table", _ptr(pt.table), _ptr(pt.flags), pt.P, pt.C, _ptr(refx), R, b.ctypes.data,
-              len(b) - 1, _ptr(idx), _ptr(dist), _stream())
+              len(b) - 1, _ptr(idx), _ptr(dist), _ptr(sec), _stream())
+    return idx, dist, sec
+
+
+def classify_pixels_table(pt, refx, R):
+    """exact per-pixel classification from a PixTable: the table screen, then the f64 refine on the
+    table's source values -- classify_pixels' results"""
+    if pt.source is None:
+        raise ValueError("classify_pixels_table: the table has no source values for the exact refine")
+    idx, dist, sec = classify_pixels_table_screen(pt, refx, R)
+    classify_refine(pt.source, refx, R, pt.bounds, 3, idx, dist, sec)
     return idx, dist
 
 
@@ -1085,6 +1197,16 @@ def tile_stats(device, H, W):
         _lib.call("hrf_tile_ctx_seg", ctx, ctypes.addressof(seg))
         _lib.call("hrf_seg_ctx_stats", seg, ctypes.addressof(out))
     return dict(zip(("passes", "contests", "rounds", "marker_ties"), list(out)))
+
+
+def tile_pixel_listed(device, H, W):
+    """pixels of the last native tile whose per-pixel certificate failed (scored in full by the
+    refine's list pass); synchronises"""
+    import ctypes
+    n = ctypes.c_int32(0)
+    with _TILE_CTX.use(device, H, W) as ctx:
+        _lib.call("hrf_tile_ctx_pixel_listed", ctx, ctypes.addressof(n))
+    return n.value
 
 
 _CELL_CAP = {}

@@ -373,6 +373,9 @@ HRF_API hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out)
 HRF_API hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *ctx);
 /* the segmentation context the tile context runs (hrf_seg_ctx_stats of the last tile) */
 HRF_API hrf_status hrf_tile_ctx_seg(hrf_tile_ctx *ctx, hrf_seg_ctx **seg);
+/* pixels of the last tile the per-pixel certificate did not settle (scored in full by the refine's
+ * list pass); synchronises with the device */
+HRF_API hrf_status hrf_tile_ctx_pixel_listed(hrf_tile_ctx *ctx, int32_t *n_host);
 HRF_API hrf_status hrf_tile_ecoli(hrf_tile_ctx *ctx, const float *const *lasers_host, const float *cal,
                                   const void *refx, const double *lib, const double *lib_flags, int32_t R,
                                   int32_t variant, double flag_thr, int32_t per_pixel, int32_t *seg,
@@ -435,20 +438,62 @@ HRF_API hrf_status hrf_classify_table_row_bytes(int32_t C, const int32_t *bounds
                                                 int32_t *row_bytes_host);
 HRF_API hrf_status hrf_classify_prepare_refs(const float *ref, int32_t R, int32_t C, const int32_t *bounds_host,
                                              int32_t nseg, int32_t mode, void *refx, hrf_stream_t stream);
-/* per pixel (north_star mode): best_idx[p] = argmin_r ungated distance, best_dist[p] */
+/* bytes of the prepared library of `mode` for R rows: the MFMA table (rpad rows of
+ * hrf_classify_table_row_bytes) followed by the exact section the refine reads (the f32 library
+ * row- and channel-major, its f64 segment sums of squares, the all-zero pixel's answer) */
+HRF_API int64_t hrf_classify_refx_bytes(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t R, int32_t mode);
+/* per pixel (north_star mode), exact: best_idx[p] = the restatement's argmin_r of the ungated
+ * segmented-cosine distance (oracle_segcos variant 0 in f64 on the f32 values; lowest r on ties),
+ * best_dist[p] = that distance rounded to f32.  = hrf_classify_pixels_screen + hrf_classify_pixels_refine
+ * on the stack (workspace allocated stream-ordered). */
 HRF_API hrf_status hrf_classify_pixels(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
                                        const int32_t *bounds_host, int32_t nseg, int32_t mode, int32_t *best_idx,
                                        float *best_dist, hrf_stream_t stream);
+/* the MFMA screen alone: best_idx = the device argmax of the split-fp16 (mode 1/2) or f32 (mode 0)
+ * scores (lowest row on equal device scores), best_dist = its device distance, second[p]
+ * (nullable) = an upper bound on the device score of every other library row */
+HRF_API hrf_status hrf_classify_pixels_screen(const float *stack, int64_t P, int32_t C, const void *refx, int32_t R,
+                                              const int32_t *bounds_host, int32_t nseg, int32_t mode,
+                                              int32_t *best_idx, float *best_dist, float *second,
+                                              hrf_stream_t stream);
+/* the f64 refine of a screen's output, in place: certify the screen's row by its exact distance
+ * against the screen's proven error bound, else score every row (f32 with its own bound, f64 on the
+ * survivors).  The pixels' f32 values come from nlaser acquisitions (a plain (P, C) stack: nlaser 1,
+ * channels {C}, shifts NULL, H*W = P): pixel p = (p / W, p % W) reads laser q at its device shift
+ * (shifts_dev: nlaser (dr, dc) pairs, or NULL), 0 outside its frame and, with apply_mask, outside
+ * any laser's frame (hrf_register_assemble's stack).  screen: the sweep that produced second
+ * (0/1/2: hrf_classify_pixels_screen mode 0/1/2, 3: hrf_classify_pixels_table); refx prepared for
+ * that mode (3: mode 2).  work: hrf_classify_refine_work_bytes(H*W) device bytes; its first int32
+ * is the number of pixels the certificate did not settle (readable after the stream syncs). */
+HRF_API int64_t hrf_classify_refine_work_bytes(int64_t P);
+/* the refine's error bounds for `screen`, in score units (score = nseg (1 - distance)):
+ * eps_host[0] = the screen's bound for a pixel with no all-zero segment, [1] = the increment per
+ * all-zero segment of the pixel, [2] = the list pass's f32 bound */
+HRF_API hrf_status hrf_classify_screen_eps(int32_t C, const int32_t *bounds_host, int32_t nseg, int32_t R,
+                                           int32_t screen, double *eps_host);
+HRF_API hrf_status hrf_classify_pixels_refine(const float *const *src_host, const int32_t *channels_host,
+                                              const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                              int32_t apply_mask, const void *refx, int32_t R,
+                                              const int32_t *bounds_host, int32_t nseg, int32_t screen,
+                                              const float *second, int32_t *best_idx, float *best_dist, void *work,
+                                              int64_t work_bytes, hrf_stream_t stream);
 /* the per-pixel classifier's operands prepared once (pixtable.hpp): the split-fp16,
  * segment-normalised pixels in the MFMA register layout (table: hrf_pixtable_bytes(P, ...) device
  * bytes) and a flag byte per pixel (flags: P bytes).  Mode-2 layouts (E. coli, multispecies). */
 HRF_API int64_t hrf_pixtable_bytes(int64_t P, int32_t C, const int32_t *bounds_host, int32_t nseg);
 HRF_API hrf_status hrf_pixtable_prepare(const float *stack, int64_t P, int32_t C, const int32_t *bounds_host,
                                         int32_t nseg, void *table, uint8_t *flags, hrf_stream_t stream);
-/* hrf_classify_pixels (mode 2) from a prepared pixel table: the same results bit for bit */
+/* the mode-2 screen (hrf_classify_pixels_screen) from a prepared pixel table: the same device
+ * scores bit for bit; second nullable.  Exact results: hrf_classify_pixels_refine (screen 3). */
 HRF_API hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, int64_t P, int32_t C,
                                              const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
-                                             int32_t *best_idx, float *best_dist, hrf_stream_t stream);
+                                             int32_t *best_idx, float *best_dist, float *second,
+                                             hrf_stream_t stream);
+/* one v_mfma_f32_16x16x32_f16 (shape 0: A 16x32, B 32x16, C/D 16x16 per tile) or
+ * v_mfma_f32_32x32x16_f16 (shape 1: A 32x16, B 16x32, C/D 32x32) per tile, all row-major (A, B
+ * fp16; C, D f32): pins the accumulation model the per-pixel screen's error bound assumes */
+HRF_API hrf_status hrf_probe_mfma_f16(int32_t shape, const void *a, const void *b, const float *c, float *d,
+                                      int32_t ntiles, hrf_stream_t stream);
 /* presence flags of the gated variants on the library path (no classifier bundle): out (N x nseg)
  * f64, 1.0 where max(x[n, bounds[s]:bounds[s+1]]) > thr, else 0.0 (a NaN in the segment: 0.0) */
 HRF_API hrf_status hrf_segment_flags(const double *x, int64_t N, int32_t C, const int32_t *bounds_host, int32_t nseg,

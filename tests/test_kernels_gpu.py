@@ -344,33 +344,32 @@ def test_counts_paint(K, orc):
 
 
 # ---- a19 classification ---------------------------------------------------------------
-# Per-pixel distances hold 1e-5 (abs/rel) of the f64 restatement, so two library rows whose
-# restated distances are more than MARGIN apart can never swap: wherever the oracle's best
-# beats its runner-up by more than MARGIN the device's argmin must be the oracle's, exactly;
-# where it does not, the device's row must be one of the rows within MARGIN of the best.
-MARGIN = 2e-5
+# Per pixel the device answer is exact (round 6): the MFMA screen's row certified by its f64
+# distance against the screen's proven error bound, or every row re-scored (hrf_classify_pixels
+# = screen + hrf_classify_pixels_refine).  So on EVERY pixel the device's argmin is the
+# restatement's (lowest row on ties) and its distance the restatement's f64 distance rounded to
+# f32 (which also meets north_star's 1e-5 relative, asserted as such with atol 1e-9).  Near ties
+# -- restated best and runner-up within NEAR -- are counted and printed: the pixels a screen
+# alone could not have decided.
+NEAR = 2e-5
 
 
-def check_pixel_argmin(orc, gi, gd, x64, ref64, bounds, ncell=0, min_cell_sep=0.99, min_sep=0.0):
-    """gi/gd: the device's per-pixel argmin and distance of the pixels x64, the first `ncell` of
-    them cell pixels.  Distances 1e-5; the argmin the restatement's wherever its best beats the
-    runner-up by > MARGIN, else a row within MARGIN of the best.  The separated fractions are
-    printed for the cell pixels and for all; on cell pixels at least `min_cell_sep` must be
-    separated (the exact check covers them), over all at least `min_sep` (background pixels are
-    the near-ties)."""
+def check_pixel_argmin(orc, gi, gd, x64, ref64, bounds, ncell=0):
+    """gi/gd: the device's per-pixel argmin and distance of the pixels x64 (the first `ncell` of
+    them cell pixels) against the library ref64 -> (near-tie count, max relative distance error)"""
     ra, d1, d2 = orc.classify_top2(x64, ref64, bounds)
-    np.testing.assert_allclose(gd, d1, rtol=1e-5, atol=1e-5)
-    sep = (d2 - d1) > MARGIN
-    assert np.array_equal(gi[sep], ra[sep])
-    for i in np.nonzero(~sep)[0]:
-        assert orc.segcos(x64[i], ref64[gi[i]], bounds, 0) <= d1[i] + MARGIN
-    cell_sep = float(sep[:ncell].mean()) if ncell else float("nan")
-    print("per-pixel argmin: separated by > %g on %.4f of %d cell pixels, %.4f of all %d pixels"
-          % (MARGIN, cell_sep, ncell, float(sep.mean()), sep.size))
-    if ncell:
-        assert cell_sep >= min_cell_sep
-    assert sep.mean() >= min_sep
-    return cell_sep, float(sep.mean())
+    bad = np.nonzero(gi != ra)[0]
+    assert bad.size == 0, "argmin differs on %d of %d pixels, e.g. pixel %d: device row %d, restated row %d " \
+        "(restated best %r, runner-up %r)" % (bad.size, gi.size, bad[0], gi[bad[0]], ra[bad[0]], d1[bad[0]], d2[bad[0]])
+    np.testing.assert_allclose(gd, d1, rtol=1e-5, atol=1e-9)
+    assert np.array_equal(gd, d1.astype(np.float32)), "distances are not the restated f64 ones rounded to f32"
+    fin = np.isfinite(d1) & (d1 > 0)
+    rel = float(np.max(np.abs(gd[fin] - d1[fin]) / d1[fin])) if fin.any() else 0.0
+    near = (d2 - d1) <= NEAR
+    print("per-pixel argmin: equal on all %d pixels (%d cell pixels); %d near ties (runner-up within %g: %d among "
+          "cell pixels); max relative distance error %.2e (the f32 rounding)"
+          % (gi.size, ncell, int(near.sum()), NEAR, int(near[:ncell].sum()), rel))
+    return int(near.sum()), rel
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
@@ -400,8 +399,7 @@ def test_classify_pixels_vs_oracle(K, orc, S, nbit, bounds, mode):
 @pytest.mark.parametrize("nbit,bounds", [(10, (0, 32, 55, 75, 89, 95)), (7, (0, 23, 43, 57, 63))])
 def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
     """mode 2 (indicator terms as an extra k-step) vs mode 1 (indicator columns) on a 512x384
-    tile whose first rows carry zero segments; the cell pixels checked exactly against the
-    restatement"""
+    tile whose first rows carry zero segments: both exact against the restatement, so equal"""
     stack, truth, lay, ref = S.tile(512, 384, nbit=nbit, bounds=bounds, seed=21)
     R, C = ref.shape
     st = stack.clone()
@@ -412,17 +410,15 @@ def test_classify_pixels_modes_agree_on_a_tile(K, orc, S, nbit, bounds):
     for mode in (1, 2):
         refx = K.classify_prepare(dev(ref), bounds, mode=mode)
         out[mode] = [host(t).ravel() for t in K.classify_pixels(st, refx, R, bounds)]
-    np.testing.assert_allclose(out[2][1], out[1][1], rtol=0, atol=2e-6)
     rng = np.random.default_rng(0)
     cells = np.nonzero(truth.ravel() > 0)[0]
     sel = np.concatenate([rng.choice(cells, 4000, replace=False), np.arange(0, 9 * 384), 100 * 384 + np.arange(0, 768),
                           rng.choice(512 * 384, 1000, replace=False)])
     x = host(st).reshape(-1, C)[sel].astype(np.float64)
     for mode in (1, 2):
-        # cell pixels here are the rendered cells' (edges included, where the dome profile is dim),
-        # not a segmentation's interior as in the full-size tests: 0.98
-        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 4000,
-                           min_cell_sep=0.98)
+        check_pixel_argmin(orc, out[mode][0][sel], out[mode][1][sel], x, ref.astype(np.float64), bounds, 4000)
+    # both exact: the same answer everywhere
+    assert np.array_equal(out[1][0], out[2][0]) and np.array_equal(out[1][1], out[2][1])
 
 
 def test_classify_pixels_mode2_negative_values(K, orc, S):
@@ -439,7 +435,7 @@ def test_classify_pixels_mode2_negative_values(K, orc, S):
     for lib in (ref, ref - 0.01):                   # then a library with negative entries
         refx = K.classify_prepare(dev(lib.astype(np.float32)), bounds, mode=2)
         gi, gd = [host(t).ravel()[sel] for t in K.classify_pixels(st, refx, R, bounds)]
-        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 1500, min_cell_sep=0.98)
+        check_pixel_argmin(orc, gi, gd, x, lib.astype(np.float64), bounds, 1500)
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2])
@@ -626,9 +622,11 @@ def test_erosion_seeds_two_threads_two_streams(K, S):
                                                (10, (0, 32, 55, 75, 89, 95), (33, 31)),
                                                (7, (0, 23, 43, 57, 63), (64, 96)),
                                                (10, (0, 32, 55, 75, 89, 95), (512, 512))])
-def test_classify_pixels_table_equals_in_kernel_build(K, S, nbit, bounds, shape):
-    """the prepared pixel table (pixtable.hpp) + classify_pixels_table give the in-kernel build's
-    results bit for bit, incl. all-zero pixels, zero segments, negative values and a ragged tail"""
+def test_classify_pixels_table_equals_in_kernel_build(K, S, orc, nbit, bounds, shape):
+    """the prepared pixel table (pixtable.hpp) + the table screen give the in-kernel screen's device
+    scores bit for bit (E. coli: the same w16 sweep), and after the refine both are the
+    restatement's answer -- incl. all-zero pixels, zero segments, f32-underflowing segment norms,
+    negative values and a ragged tail"""
     H, W = shape
     ref = S.reference_library(nbit, bounds).copy()
     ref[3, bounds[0]:bounds[1]] = 0.0
@@ -637,24 +635,23 @@ def test_classify_pixels_table_equals_in_kernel_build(K, S, nbit, bounds, shape)
     st[:7] = 0.0
     st[7:20, bounds[0]:bounds[1]] = 0.0
     st[20:23, bounds[1]:bounds[2]] = 1e-25        # f32 underflow of the segment norm
-    d = dev(st.reshape(H, W, -1))
     refx = K.classify_prepare(dev(ref), bounds, mode=2)
-    want = K.classify_pixels(d, refx, ref.shape[0], bounds, mode=2)
-    pt = K.pixtable_prepare(d, bounds)
-    got = K.classify_pixels_table(pt, refx, ref.shape[0])
-    if len(bounds) != 6:
-        # the community layout's default in-kernel form is the 32x32x16 kernel (its own norm
-        # arithmetic): equal within the classifier's tolerance
-        torch.testing.assert_close(got[1], want[1], rtol=0, atol=2e-6)
-        assert (got[0] == want[0]).float().mean() > 0.999
-        return
-    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
-    neg = st.copy()
-    neg[100:140, 5] = -0.3                          # the compare-and-select (unkeyed) path
-    d2 = dev(neg.reshape(H, W, -1))
-    want = K.classify_pixels(d2, refx, ref.shape[0], bounds, mode=2)
-    got = K.classify_pixels_table(K.pixtable_prepare(d2, bounds), refx, ref.shape[0])
-    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+    ref64 = ref.astype(np.float64)
+    for case in ("plain", "negative"):
+        if case == "negative":
+            st = st.copy()
+            st[100:140, 5] = -0.3                   # the compare-and-select (unkeyed) path
+        d = dev(st.reshape(H, W, -1))
+        pt = K.pixtable_prepare(d, bounds)
+        if len(bounds) == 6:
+            sw = K.classify_pixels_screen(d, refx, ref.shape[0], bounds, mode=2)
+            sg = K.classify_pixels_table_screen(pt, refx, ref.shape[0])
+            for a, b in zip(sw, sg):
+                assert torch.equal(a, b)
+        want = K.classify_pixels(d, refx, ref.shape[0], bounds, mode=2)
+        got = K.classify_pixels_table(pt, refx, ref.shape[0])
+        assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+        check_pixel_argmin(orc, host(got[0]).ravel(), host(got[1]).ravel(), st.astype(np.float64), ref64, bounds)
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2, "table"])

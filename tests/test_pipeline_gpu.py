@@ -64,7 +64,7 @@ def test_process_tile_classification_and_counts(mods, orc):
     assert (gi == oi).mean() == 1.0
     assert np.array_equal(host(res.counts), orc.barcode_counts(gi, lib.R))
     assert np.array_equal(host(res.identification), orc.paint_ids(o["segmentation"], gi + 1))
-    # per-pixel mode: exact argmin wherever the restatement separates best and runner-up
+    # per-pixel mode: the restatement's argmin and distance on every sampled pixel
     from test_kernels_gpu import check_pixel_argmin
     P_ = 512 * 512
     cells = np.nonzero(host(res.meas.segmentation).ravel() > 0)[0]
@@ -72,8 +72,7 @@ def test_process_tile_classification_and_counts(mods, orc):
     sel = np.concatenate([rng.choice(cells, 3000, replace=False), rng.choice(P_, 1000, replace=False)])
     x = host(stack).reshape(P_, -1)[sel].astype(np.float64)
     pi, pd = host(res.pixel_idx).ravel()[sel], host(res.pixel_dist).ravel()[sel]
-    # a 512^2 tile: 0.98 (the full-size cfg3 / cfg2 tests hold 0.99, tests/test_fullsize_gpu.py)
-    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 3000, min_cell_sep=0.98)
+    check_pixel_argmin(orc, pi, pd, x, ref.astype(np.float64), S.ECOLI_BOUNDS, 3000)
 
 
 def test_concurrent_tiles_equal_isolated(mods):

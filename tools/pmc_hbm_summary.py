@@ -19,9 +19,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-KERNELS = {"channel_max_multi": "channel_max_multi_pf_kernel",
-           "assemble_pixtable": "assemble_ecoli_kernel<4, true>",
-           "label_sums_lasers_cal": "label_sums_lasers_row_kernel<true>"}
+from bench import HBM_KERNELS as KERNELS  # noqa: E402  (the kernel symbols live in one place)
 
 
 def counters(d, counter):
