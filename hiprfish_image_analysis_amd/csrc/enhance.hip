@@ -181,9 +181,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ double tile[E3_LX * E3_LY * E3_LZ];
   const int tid = threadIdx.x;
   const int64_t x0 = (int64_t)blockIdx.z * E3_TX, y0 = (int64_t)blockIdx.y * E3_TY, z0 = (int64_t)blockIdx.x * E3_TZ;
-  // a NaN, an infinity, a negative zero -- or a magnitude above 2^1023, where a window's max - min
-  // could overflow to inf and (c - mn) / r give inf / inf = NaN, on which fmin / fmax and the
-  // reference's `a < b ? a : b` disagree -- sends the tile down the reference's compare-select path
+  // a NaN, an infinity, a negative zero -- or a magnitude of 2^1023 or more, where a window's
+  // max - min could overflow to inf (2^1023 - (-2^1023) = 2^1024 already does) and (c - mn) / r give
+  // inf / inf = NaN, on which fmin / fmax and the reference's `a < b ? a : b` disagree -- sends the
+  // tile down the reference's compare-select path
   int special = 0;
   for (int idx = tid; idx < E3_LX * E3_LY * E3_LZ; idx += 256) {
     const int lx = idx / (E3_LY * E3_LZ);
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int ly = rem / E3_LZ, lz = rem - ly * E3_LZ;
     const int64_t gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
     const double v = (gx < xp && gy < yp && gz < zp) ? pad[(gx * yp + gy) * zp + gz] : 0.0;
-    special |= !(__builtin_fabs(v) <= 0x1p1023) || (v == 0.0 && __builtin_signbit(v));
+    special |= !(__builtin_fabs(v) < 0x1p1023) || (v == 0.0 && __builtin_signbit(v));
     tile[idx] = v;
   }
   const bool fast = !__syncthreads_or(special);

@@ -278,10 +278,12 @@ def watershed(img, markers, mask=None):
     return out
 
 
-def watershed_ordered(img, markers, mask=None):
+def watershed_ordered(img, markers, mask=None, raw=False):
     """ws_order.c: the tie-exact formulation libhrf's watershed implements (NOT a reference
     restatement; checked against watershed() above).  -> (labels, stats) with stats =
-    [contested pixels, walk steps, heap-layout decisions, label rounds]"""
+    [contested pixels, walk steps, heap-layout decisions, label rounds].  Where a decision came
+    down to the heap's layout (stats[2] > 0) the labels are the heap flood's, as in libhrf;
+    raw=True keeps the resolution's own labels there (the order model alone)."""
     im = _c(img, np.float64)
     mk = _c(markers, np.int32)
     out = np.zeros(mk.shape, np.int32)
@@ -290,7 +292,8 @@ def watershed_ordered(img, markers, mask=None):
     if mask is not None:
         m = _c(mask, np.uint8)
         mp = _p(m)
-    lib().oracle_watershed_ordered(_p(im), _p(mk), mp, I64(im.shape[0]), I64(im.shape[1]), _p(out), _p(st))
+    fn = lib().oracle_watershed_ordered_raw if raw else lib().oracle_watershed_ordered
+    fn(_p(im), _p(mk), mp, I64(im.shape[0]), I64(im.shape[1]), _p(out), _p(st))
     return out, st
 
 

@@ -227,8 +227,23 @@ static int walk(wsctx *c, const int64_t *cand, int k, int64_t *stats) {
     return win;
 }
 
+/* the order model alone: the resolution's labels even where a decision came down to the heap
+ * layout (stats[2] > 0), where the composed flow below -- like libhrf -- floods with the heap */
+static void watershed_ordered(const double *img, const int32_t *markers, const uint8_t *mask, int64_t H, int64_t W,
+                              int32_t *out, int64_t *stats, int heap_fallback);
+
 EXPORT void oracle_watershed_ordered(const double *img, const int32_t *markers, const uint8_t *mask, int64_t H,
                                      int64_t W, int32_t *out, int64_t *stats) {
+    watershed_ordered(img, markers, mask, H, W, out, stats, 1);
+}
+
+EXPORT void oracle_watershed_ordered_raw(const double *img, const int32_t *markers, const uint8_t *mask, int64_t H,
+                                         int64_t W, int32_t *out, int64_t *stats) {
+    watershed_ordered(img, markers, mask, H, W, out, stats, 0);
+}
+
+static void watershed_ordered(const double *img, const int32_t *markers, const uint8_t *mask, int64_t H, int64_t W,
+                              int32_t *out, int64_t *stats, int heap_fallback) {
     const int64_t n = H * W;
     wsctx c = {img, mask, markers, H, W, NULL, NULL, NULL, 0};
     c.lam = (double *)malloc(sizeof(double) * n);
@@ -334,5 +349,5 @@ EXPORT void oracle_watershed_ordered(const double *img, const int32_t *markers, 
     free(c.hop);
     free(c.stamp);
     free(ptr);
-    if (stats[2] > 0) oracle_watershed(img, markers, mask, H, W, out);
+    if (heap_fallback && stats[2] > 0) oracle_watershed(img, markers, mask, H, W, out);
 }

@@ -95,6 +95,8 @@ def test_enhance_3d_special_values(K, orc):
     pad[18, 17, 8] = 1.5e308                # finite, span with the next value > DBL_MAX
     pad[18, 18, 8] = -1.5e308
     pad[20, 3, 45] = 1e308                  # finite, span within DBL_MAX but above 2^1023
+    pad[6, 20, 12] = 2.0 ** 1023            # exactly +-2^1023 side by side: span 2^1024 = inf
+    pad[6, 20, 13] = -(2.0 ** 1023)
     same(K.enhance_3d(dev(pad)).cpu().numpy(), orc.enhance_3d(pad))
 
 

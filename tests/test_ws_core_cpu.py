@@ -57,11 +57,23 @@ def test_device_resolution_code_equals_heap(emul, orc, block):
         got, ties = emul(f, markers, mask)
         model, st = orc.watershed_ordered(f, markers, mask)
         # the emulator replays the resolution only; an equal-valued-marker decision (ties[2]) is
-        # where libhrf floods again with the heap (watershed.hip), as the model does (st[2])
+        # where libhrf floods again with the heap (watershed.hip), as the composed model does
+        # (st[2]).  The resolution's own labels (the relabel passes consume them before the replay
+        # overwrites them) are pinned against the model without its fallback in every case.
         assert bool(ties[2]) == bool(st[2]), seed
+        raw, _ = orc.watershed_ordered(f, markers, mask, raw=True)
+        assert np.array_equal(got, raw), seed
         if ties[2] == 0:
             assert np.array_equal(got, model), seed
             assert np.array_equal(got, orc.watershed(f, markers, mask)), seed
         else:
             layout_cases += 1
     assert layout_cases < 100
+
+
+def test_any_marker_seeds_exercise_the_heap_replay(orc):
+    """test_watershed_gpu.py::test_watershed_plateaus_any_markers asserts the device takes the heap
+    replay exactly where the CPU model meets an equal-marker decision; some of its seeds must"""
+    from test_watershed_gpu import ANY_MARKER_SEEDS, any_markers_case
+    hits = [s for s in ANY_MARKER_SEEDS if orc.watershed_ordered(*any_markers_case(s))[1][2] > 0]
+    assert hits, "no seed meets an equal-valued-marker decision"
