@@ -1652,28 +1652,36 @@ __device__ __forceinline__ void src_offsets(const PixSrc &S, int64_t p, bool val
 // normalisation is exact to its bound (no f32 overflow, no overflowing f64-redo reciprocal).
 // NC > 0: the channel loop unrolled to NC (yv then indexes registers with constants); 0: a loop.
 constexpr double NX_MIN = 1e-70, NX_MAX = 1e37;
-template <int NC, class YV>
-__device__ __forceinline__ double exact_dist_y(const float *x, YV yv, const double *nyr, int C, const Bounds &bd,
-                                               int *nz, bool *in_range) {
-  double nx = 0.0, dd = 0.0, sum = 0.0;
-  int sg = 0, send = bd.b[1], zc = 0;
+template <int NC, class YV, class NY>
+__device__ __forceinline__ double exact_dist_y(const float *x, YV yv, NY nyr, int C, const Bounds &bd, int *nz,
+                                               bool *in_range) {
+  double sum = 0.0;
+  int zc = 0;
   bool rok = true;
+  for (int sg = 0; sg < bd.nseg; ++sg) {
+    const double ny = nyr(sg);  // issued before the segment's channels: its latency overlaps them
+    double nx = 0.0, dd = 0.0;
+    // 8 channels' loads issued together, then their sums in channel order (one load latency per 8)
+    const int ce = bd.b[sg + 1];
+    for (int c0 = bd.b[sg]; c0 < ce; c0 += 8) {
+      float xv[8], yy[8];
 #pragma unroll
-  for (int c = 0; c < (NC ? NC : C); ++c) {
-    if (NC && c >= C) break;
-    const double xv = (double)x[c], yy = (double)yv(c);
-    dd += xv * yy;
-    nx += xv * xv;
-    if (c + 1 == send) {
-      const double ny = nyr[sg];
-      const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
-      sum += sd;
-      zc += nx == 0.0 ? 1 : 0;
-      rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
-      nx = dd = 0.0;
-      ++sg;
-      send = bd.b[sg + 1];
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = c0 + u < ce ? x[c0 + u] : 0.0f;
+        yy[u] = c0 + u < ce ? yv(c0 + u) : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + u < ce) {
+          const double xd = (double)xv[u], yd = (double)yy[u];
+          dd += xd * yd;
+          nx += xd * xd;
+        }
     }
+    const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
+    sum += sd;
+    zc += nx == 0.0 ? 1 : 0;
+    rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
   }
   *nz = zc;
   if (in_range) *in_range = rok;
@@ -1682,14 +1690,18 @@ __device__ __forceinline__ double exact_dist_y(const float *x, YV yv, const doub
 __device__ __forceinline__ double exact_dist(const float *x, const ExactPtr &E, int r, int C, const Bounds &bd,
                                              int *nz, bool *in_range = nullptr) {
   const float *yr = E.lib32 + (int64_t)r * E.CP;
-  return exact_dist_y<0>(x, [&](int c) { return yr[c]; }, E.ny + (int64_t)r * bd.nseg, C, bd, nz, in_range);
+  const double *nyr = E.ny + (int64_t)r * bd.nseg;
+  return exact_dist_y<0>(x, [&](int c) { return yr[c]; }, [&](int sg) { return nyr[sg]; }, C, bd, nz, in_range);
 }
 
 // One wave = 32 consecutive pixels.  Their values and their screen rows b1 are loaded with every
 // load of the wave in flight at once (lane = channel c and c + 64, unrolled over the 32 pixels:
 // each pixel's registered spectrum is a few contiguous laser runs, each library row one run) and
 // staged in LDS; then lanes 0..31 (lane = pixel) rescore b1 in f64 and certify or list it.
-constexpr int REF_NP = 32;
+#ifndef HRF_REF_NP
+#define HRF_REF_NP 32
+#endif
+constexpr int REF_NP = HRF_REF_NP;  // pixels per wave (<= 64)
 __global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, int32_t C, Bounds bd, ExactPtr E,
                                                          const ExactHdr *__restrict__ hdr, double eps_base,
                                                          double eps_zero, const float *__restrict__ second,
@@ -1698,6 +1710,7 @@ __global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, in
   extern __shared__ float rxs[];  // x: REF_NP x CPX, then y: REF_NP x CPX
   __shared__ int32_t offs[XLMAX][REF_NP];
   __shared__ int32_t b1s[REF_NP];
+  __shared__ double nyb[REF_NP][SMAX];
   const int CPX = C | 1;  // odd pitch: conflict-free lane-per-pixel reads
   float *ys = rxs + REF_NP * CPX;
   const int lane = threadIdx.x;
@@ -1713,6 +1726,8 @@ __global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, in
 #pragma unroll
     for (int q = 0; q < XLMAX; ++q) offs[q][lane] = off[q];
     b1s[lane] = brow ? b1 : 0;
+#pragma unroll
+    for (int q = 0; q < SMAX; ++q) nyb[lane][q] = q < bd.nseg ? E.ny[(int64_t)(brow ? b1 : 0) * bd.nseg + q] : 0.0;
   }
   __syncthreads();
   // lane = channels c0 = lane and c1 = lane + 64: laser q and local channel fixed per lane
@@ -1756,8 +1771,8 @@ __global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, in
       int nz = 0;
       bool in_range = true;
       const float *yl = ys + lane * CPX;
-      const double D = exact_dist_y<0>(rxs + lane * CPX, [&](int c) { return yl[c]; }, E.ny + (int64_t)b1 * bd.nseg,
-                                       C, bd, &nz, &in_range);
+      const double D = exact_dist_y<0>(
+          rxs + lane * CPX, [&](int c) { return yl[c]; }, [&](int sg) { return nyb[lane][sg]; }, C, bd, &nz, &in_range);
       if (nz == bd.nseg) {  // all-zero pixel: the library's own answer
         best_idx[p] = hdr->idx0;
         best_dist[p] = (float)hdr->D0;
@@ -1809,6 +1824,8 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
   constexpr int CAND = 1024;  // sparse candidates per batch; a pixel that overflows is scored in full
   __shared__ int32_t cand[CAND];
   __shared__ int ncand;
+  // one wave per sparse candidate: its exact products (lane = channel), then one lane per segment
+  __shared__ double prw[LIST_NT / 64][128], sqw[LIST_NT / 64][128], sdw[LIST_NT / 64][SMAX];
   extern __shared__ float scb[];  // LIST_NP x RT f32 scores
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = *cnt;
@@ -1929,9 +1946,7 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
       bdv[j] = __builtin_inf();
       brv[j] = 0x7fffffff;
     }
-    auto take = [&](int j, int r) {
-      int nz = 0;
-      const double D = exact_dist(xb[j], E, r, C, bd, &nz);
+    auto take = [&](int j, int r, double D) {
 #pragma unroll
       for (int jj = 0; jj < LIST_NP; ++jj)
         if (jj == j && (D < bdv[jj] || (D == bdv[jj] && r < brv[jj]))) {
@@ -1939,14 +1954,51 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
           brv[jj] = r;
         }
     };
+    // sparse candidates, one wave each: the products x*y and x*x are exact in f64 (f32 operands),
+    // so lanes form them in parallel; lane s then sums segment s in channel order, lane 0 the
+    // segments in order -- the restatement's arithmetic (exact_dist) bit for bit
     const int nc = min(ncand, CAND);
-    for (int k = t; k < nc; k += LIST_NT) {
+    for (int k = w; k < nc; k += LIST_NT / 64) {
       const int j = cand[k] >> 16, r = cand[k] & 0xffff;
-      if (!fullb[j]) take(j, r);
+      if (fullb[j]) continue;
+      const float *yr = E.lib32 + (int64_t)r * E.CP;
+      double nyv = 0.0;
+      if (lane < nseg) nyv = E.ny[(int64_t)r * nseg + lane];
+      for (int c = lane; c < C; c += 64) {
+        const double xv = (double)xb[j][c], yy = (double)yr[c];
+        prw[w][c] = xv * yy;
+        sqw[w][c] = xv * xv;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (lane < nseg) {
+        double dd = 0.0, nx = 0.0;
+        for (int c = bd.b[lane]; c < bd.b[lane + 1]; ++c) {
+          dd += prw[w][c];
+          nx += sqw[w][c];
+        }
+        sdw[w][lane] = (nx == 0.0 && nyv == 0.0) ? 0.0
+                                                 : ((nx == 0.0 || nyv == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * nyv));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (lane == 0) {
+        double sum = 0.0;
+        for (int sg = 0; sg < nseg; ++sg) sum += sdw[w][sg];
+        take(j, r, sum / nseg);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     for (int j = 0; j < nb; ++j)
       if (fullb[j])
-        for (int r = t; r < R; r += LIST_NT) take(j, r);
+        for (int r = t; r < R; r += LIST_NT) {
+          int nz = 0;
+          take(j, r, exact_dist(xb[j], E, r, C, bd, &nz));
+        }
 #pragma unroll
     for (int j = 0; j < LIST_NP; ++j) {
 #pragma unroll
