@@ -46,6 +46,327 @@ constexpr int RCH = 64;  // references per LDS chunk (prefetched into registers)
 #define HRF_W16T_OCC 2
 #endif
 
+// ==== exact per-pixel classification: the f64 refine of the screen (round 6) ==================
+// The MFMA sweeps above are a SCREEN: split-fp16 (or f32-MFMA) scores within a bound of the exact
+// segmented-cosine score.  Every sweep also reports, per pixel, an upper bound s2 on the device
+// score of every library row other than its best row b1 (the runner-up, `second`).  The refine:
+//  * rescores b1 in f64 exactly as the restatement does (oracle seg_dist / oracle_segcos variant
+//    0: the three sums in channel order, 1 - d / sqrt(nx * ny), the segment mean) from the pixel's
+//    f32 values -- the stack, or the five shifted acquisitions of a registered tile -- and the f32
+//    library promoted to f64 (the restatement's ref64);
+//  * certifies b1 when D(b1) < 1 - (s2 + eps) / nseg - 1e-12, eps the screen's proven error bound
+//    (screen_eps below): then every other row r has S_exact(r) <= s2 + eps, i.e. its restated
+//    distance exceeds D(b1), so b1 is the restatement's argmin and D(b1) its distance, bit for bit;
+//  * answers an all-zero pixel from the library alone (every segment one-zero or both-zero:
+//    D(r) = (nonzero segments of r) / nseg, its first argmin precomputed at prepare time);
+//  * lists every other pixel (ties, near-ties, NaN / inf values) for refine_list_kernel, which
+//    scores all rows in f32 with its own proven bound (fmaf chains on the raw values), keeps the
+//    rows within twice that bound of the best, and rescores those in f64 -- lowest row on ties.
+// The prepared library (refx) carries the exact section after its MFMA table: a header, the f32
+// library row-major (pitch CP = C rounded to 4, float4 rows), channel-major (pitch RT = R rounded
+// to 64, coalesced for the list kernel), the f64 segment sums of squares ny (the restatement's
+// |y|^2) and f32 reciprocal segment norms iy.
+struct ExactHdr {
+  int32_t R, C, nseg, idx0;  // idx0 / D0: the all-zero pixel's argmin and distance
+  double D0;
+  int32_t tiny;              // some row has 0 < ny < 1e-30: the list kernel's f32 pass is not safe
+};
+struct ExactLayout {
+  int64_t off;  // section offset from the start of refx
+  int32_t CP, RT;
+  int64_t lib32, libT, ny, iy, total;  // offsets inside the section
+};
+inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+int64_t table_rowb(int mode, int lay, int kp);
+ExactLayout exact_layout(int mode, int lay, int kp, int rpad, int R, int C, int nseg) {
+  ExactLayout e;
+  const int64_t rowb = mode == 0 ? 4 * (int64_t)kp : table_rowb(mode, lay, kp);
+  e.off = al256((int64_t)rpad * rowb);
+  e.CP = (C + 3) & ~3;
+  e.RT = (R + 63) & ~63;
+  e.lib32 = 256;
+  e.libT = al256(e.lib32 + (int64_t)R * e.CP * 4);
+  e.ny = al256(e.libT + (int64_t)C * e.RT * 4);
+  e.iy = al256(e.ny + (int64_t)R * nseg * 8);
+  e.total = al256(e.iy + (int64_t)R * nseg * 4);
+  return e;
+}
+struct ExactPtr {
+  const float *lib32, *libT, *iy;
+  const double *ny;
+  int32_t CP, RT;
+};
+
+__global__ __launch_bounds__(256) void exact_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C,
+                                                         Bounds bd, int32_t CP, int32_t RT, float *__restrict__ lib32,
+                                                         float *__restrict__ libT, double *__restrict__ ny,
+                                                         float *__restrict__ iy) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t e = t0; e < (int64_t)R * CP; e += stride) {
+    const int64_t r = e / CP;
+    const int c = (int)(e - r * CP);
+    lib32[e] = c < C ? ref[r * C + c] : 0.0f;
+  }
+  for (int64_t e = t0; e < (int64_t)C * RT; e += stride) {
+    const int64_t c = e / RT, r = e - c * RT;
+    libT[e] = r < R ? ref[r * C + c] : 0.0f;
+  }
+  for (int64_t e = t0; e < (int64_t)R * bd.nseg; e += stride) {
+    const int64_t r = e / bd.nseg;
+    const int sg = (int)(e - r * bd.nseg);
+    double v = 0.0;
+    for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
+      const double y = (double)ref[r * C + i];
+      v += y * y;
+    }
+    ny[e] = v;
+    iy[e] = v > 0.0 ? (float)(1.0 / sqrt(v)) : 0.0f;
+  }
+}
+
+// one thread: the all-zero pixel's answer (oracle_classify's loop on x = 0) and the tiny-row flag
+__global__ void exact_hdr_kernel(const double *__restrict__ ny, int32_t R, int32_t C, int32_t nseg,
+                                 ExactHdr *__restrict__ hdr) {
+  double best = __builtin_inf();
+  int32_t bi = 0, tiny = 0;
+  for (int r = 0; r < R; ++r) {
+    double sum = 0.0;
+    for (int sg = 0; sg < nseg; ++sg) {
+      const double v = ny[(int64_t)r * nseg + sg];
+      sum += v == 0.0 ? 0.0 : 1.0;
+      tiny |= (v > 0.0 && v < 1e-30) ? 1 : 0;
+    }
+    const double d = sum / nseg;
+    if (d < best) {
+      best = d;
+      bi = r;
+    }
+  }
+  hdr->R = R;
+  hdr->C = C;
+  hdr->nseg = nseg;
+  hdr->idx0 = bi;
+  hdr->D0 = best;
+  hdr->tiny = tiny;
+}
+
+// Pixel source: the registered value of pixel p (row r = p / W, column c = p % W) at channel k of
+// laser q is src[q][((r - dr_q) W + (c - dc_q)) cl_q + (k - c0_q)], 0 outside the laser's frame and,
+// with apply_mask, outside any laser's frame (register_assemble's stack; stack.hip).  A plain (P, C)
+// stack is one laser with no shift.
+constexpr int XLMAX = 8;
+struct PixSrc {
+  const float *src[XLMAX];
+  int32_t c0[XLMAX + 1];
+  uint64_t mdiv[XLMAX];  // ceil(2^32 / cl): e / cl = (e * mdiv) >> 32 for e < 2^32 / cl
+  int32_t n;
+  const int32_t *dsh;    // device (dr, dc) pairs, or null (no shift)
+  int64_t H, W;
+  int32_t apply_mask;
+};
+
+__device__ __forceinline__ bool src_covered(int64_t r, int64_t c, int64_t H, int64_t W, int dr, int dc) {
+  return r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0) && c >= (dc > 0 ? dc : 0) && c < W + (dc < 0 ? dc : 0);
+}
+
+// element offsets (from src[q]) of pixel p's run in every laser, -1 where it reads as zero
+__device__ __forceinline__ void src_offsets(const PixSrc &S, int64_t p, bool valid, int32_t (&off)[XLMAX]) {
+  const int64_t r = p / S.W, c = p - r * S.W;
+  bool ok = valid;
+  if (S.apply_mask && S.dsh)
+    for (int q = 0; q < S.n; ++q) ok = ok && src_covered(r, c, S.H, S.W, S.dsh[2 * q], S.dsh[2 * q + 1]);
+#pragma unroll
+  for (int q = 0; q < XLMAX; ++q) {
+    off[q] = -1;
+    if (q < S.n && ok) {
+      const int dr = S.dsh ? S.dsh[2 * q] : 0, dc = S.dsh ? S.dsh[2 * q + 1] : 0;
+      if (src_covered(r, c, S.H, S.W, dr, dc))
+        off[q] = (int32_t)(((r - dr) * S.W + (c - dc)) * (int64_t)(S.c0[q + 1] - S.c0[q]));
+    }
+  }
+}
+
+// f64 restated distance of the pixel (f32 values x[0..C), stride 1) to a library row (yv: its f32
+// values, float4-aligned, CP = C rounded to 4; nyr: its segment sums of squares): the
+// restatement's seg_dist per segment in channel order, their sum, / nseg.  nz: the pixel's
+// all-zero segments; in_range: every non-zero segment's sum of squares lies where the screen's f32
+// normalisation is exact to its bound (no f32 overflow, no overflowing f64-redo reciprocal).
+// NC > 0: the channel loop unrolled to NC (yv then indexes registers with constants); 0: a loop.
+constexpr double NX_MIN = 1e-70, NX_MAX = 1e37;
+template <int NC, class YV, class NY>
+__device__ __forceinline__ double exact_dist_y(const float *x, YV yv, NY nyr, int C, const Bounds &bd, int *nz,
+                                               bool *in_range) {
+  double sum = 0.0;
+  int zc = 0;
+  bool rok = true;
+  for (int sg = 0; sg < bd.nseg; ++sg) {
+    const double ny = nyr(sg);  // issued before the segment's channels: its latency overlaps them
+    double nx = 0.0, dd = 0.0;
+    // 8 channels' loads issued together, then their sums in channel order (one load latency per 8)
+    const int ce = bd.b[sg + 1];
+    for (int c0 = bd.b[sg]; c0 < ce; c0 += 8) {
+      float xv[8], yy[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = c0 + u < ce ? x[c0 + u] : 0.0f;
+        yy[u] = c0 + u < ce ? yv(c0 + u) : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (c0 + u < ce) {
+          const double xd = (double)xv[u], yd = (double)yy[u];
+          dd += xd * yd;
+          nx += xd * xd;
+        }
+    }
+    const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
+    sum += sd;
+    zc += nx == 0.0 ? 1 : 0;
+    rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
+  }
+  *nz = zc;
+  if (in_range) *in_range = rok;
+  return sum / bd.nseg;
+}
+__device__ __forceinline__ double exact_dist(const float *x, const ExactPtr &E, int r, int C, const Bounds &bd,
+                                             int *nz, bool *in_range = nullptr) {
+  const float *yr = E.lib32 + (int64_t)r * E.CP;
+  const double *nyr = E.ny + (int64_t)r * bd.nseg;
+  return exact_dist_y<0>(x, [&](int c) { return yr[c]; }, [&](int sg) { return nyr[sg]; }, C, bd, nz, in_range);
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Everything the refine of a screen's output needs (kernel argument of the fused sweep)
+struct RefineArgs {
+  PixSrc S;
+  ExactPtr E;
+  const ExactHdr *hdr;
+  double eps_base, eps_zero;
+  int32_t *list, *cnt;
+  Bounds bd;  // (kernel-argument memory: indexed by a runtime segment without a scratch copy)
+};
+
+// One wave refines the 64 consecutive pixels p0 .. p0 + 63 (lane = pixel: b1 = its screen row,
+// sec2 = the runner-up bound).  The values and rows stream through the wave's LDS slice in chunks
+// of RCK channels (lane = (pixel, channel) pairs, every load of a chunk in flight, stored as
+// (x, y) pairs), and every lane carries its pixel's f64 sums across the chunks in channel order,
+// so the slice stays small (more waves resident) and all 64 lanes do the f64 work.  Then the
+// certificate: best_dist (and best_idx with write_idx) for a certified row, the header's answer
+// for an all-zero pixel, the list otherwise.
+constexpr int RCK = 16;  // channels per chunk
+__host__ __device__ constexpr int64_t refine_slice_bytes() {
+  return (int64_t)64 * (8 * SMAX + 4 * XLMAX + 4) + (int64_t)64 * (RCK + 1) * 8;
+}
+__device__ __forceinline__ void refine_pixels64(const RefineArgs &A, int C, const Bounds &bd, int64_t p0, int64_t P,
+                                                int b1, float sec2, char *slice, int32_t *__restrict__ best_idx,
+                                                float *__restrict__ best_dist, bool write_idx) {
+  double *nyb = reinterpret_cast<double *>(slice);                    // 64 x SMAX
+  int32_t *offs = reinterpret_cast<int32_t *>(nyb + 64 * SMAX);       // XLMAX x 64
+  int32_t *b1s = offs + XLMAX * 64;                                   // 64
+  float2 *xy = reinterpret_cast<float2 *>(b1s + 64);                  // 64 x (RCK + 1) (x, y)
+  const PixSrc &S = A.S;
+  const ExactPtr &E = A.E;
+  const int lane = threadIdx.x & 63;
+  const int64_t p = p0 + lane;
+  const bool valid = p < P;
+  const int Rr = A.hdr->R;
+  const bool brow = b1 >= 0 && b1 < Rr;
+  {
+    int32_t off[XLMAX];
+    src_offsets(S, p, valid, off);
+#pragma unroll
+    for (int q = 0; q < XLMAX; ++q) offs[q * 64 + lane] = off[q];
+    b1s[lane] = brow ? b1 : 0;
+#pragma unroll
+    for (int q = 0; q < SMAX; ++q) nyb[lane * SMAX + q] = q < bd.nseg ? E.ny[(int64_t)(brow ? b1 : 0) * bd.nseg + q] : 0.0;
+  }
+  wave_lds_sync();
+  // staging: element lane + 64 u of a chunk = pixel il + 4 u, channel k0 + kl
+  const int kl = lane & (RCK - 1), il = lane / RCK;
+  double nx = 0.0, dd = 0.0, sum = 0.0;
+  int sg = 0, send = bd.b[1], zc = 0;
+  bool rok = true;
+  for (int k0 = 0; k0 < C; k0 += RCK) {
+    const int c = k0 + kl;
+    const bool vc = c < C;
+    // this lane's laser for channel c (uniform candidates, per-lane selects: no indexed registers)
+    int qc = 0, cq = 0;
+    const float *sp = S.src[0];
+    for (int q = 1; q < S.n; ++q)
+      if (c >= S.c0[q]) {
+        qc = q;
+        sp = S.src[q];
+        cq = S.c0[q];
+      }
+    float xv[RCK], yv[RCK];
+#pragma unroll
+    for (int u = 0; u < RCK; ++u) {
+      const int i = il + (64 / RCK) * u;
+      const int o = offs[qc * 64 + i];
+      xv[u] = (vc && o >= 0) ? sp[o + c - cq] : 0.0f;
+      yv[u] = vc ? E.lib32[(int64_t)b1s[i] * E.CP + c] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < RCK; ++u) xy[(il + (64 / RCK) * u) * (RCK + 1) + kl] = make_float2(xv[u], yv[u]);
+    wave_lds_sync();
+    const float2 *row = xy + lane * (RCK + 1);
+#pragma unroll
+    for (int k = 0; k < RCK; ++k) {
+      if (k0 + k >= C) break;
+      const float2 v = row[k];
+      const double xd = (double)v.x, yd = (double)v.y;
+      dd += xd * yd;
+      nx += xd * xd;
+      if (k0 + k + 1 == send) {  // the segment's restated distance, in segment order
+        const double ny = nyb[lane * SMAX + sg];
+        const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
+        sum += sd;
+        zc += nx == 0.0 ? 1 : 0;
+        rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
+        nx = dd = 0.0;
+        ++sg;
+        send = bd.b[sg + 1];
+      }
+    }
+    wave_lds_sync();  // the chunk is consumed before the next one is staged
+  }
+  const double D = sum / bd.nseg;
+  bool listed = false;
+  if (valid) {
+    if (!brow) {  // no real row won the screen (cannot happen with R >= 1): list it
+      listed = true;
+    } else if (zc == bd.nseg) {  // all-zero pixel: the library's own answer
+      best_idx[p] = A.hdr->idx0;
+      best_dist[p] = (float)A.hdr->D0;
+    } else if (!rok) {  // outside the screen bound's premises
+      listed = true;
+    } else {
+      const double eps = A.eps_base + A.eps_zero * zc;
+      const double lim = 1.0 - ((double)sec2 + eps) / bd.nseg - 1e-12;
+      if (D < lim) {  // certified (NaN anywhere fails the compare)
+        if (write_idx) best_idx[p] = b1;
+        best_dist[p] = (float)D;
+      } else {
+        listed = true;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(listed);
+  if (m) {
+    int base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(A.cnt, __popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1, 64);
+    if (listed) A.list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
+  }
+}
+
+
+
 // refx[r][0..C) = ref / |ref_seg| (0 if the norm is 0), refx[r][C+s] = (norm_s == 0),
 // zero padding to KP columns and to Rpad rows.
 __global__ void ref_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C, Bounds bd, int32_t KP,
@@ -1024,17 +1345,24 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
       const char *row = buf + (rb + rl) * ROWB + 16 * Q;
       h8 az;
       if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + rl) * ROWB + 4 * KP);
+      // the cross products (hi * lo', lo * hi', each ~2^-11 of a score) first, then the hi * hi'
+      // products: the accumulator the small products meet stays ~2^-10 of a score, so only KT
+      // (+ the indicator step) MFMAs per score round at the score's magnitude (screen_eps)
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
         const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 64 * t);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
-#pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
         if (PIPE) epi((4 * t) / KT, (4 * (t + 1)) / KT);  // previous block, slice t
+      }
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
       }
       if (ZS) {
 #pragma unroll
@@ -1165,14 +1493,17 @@ __global__ __launch_bounds__(256) void pixtable_prep_kernel(const float *__restr
   hrf_pix::prep_tile<L>(tile, nullptr, np, p0, table, flags);
 }
 
-// classify_pixels_w16_kernel with the prologue replaced by direct loads of the prepared operands
-template <class L, int NW, int NBUF, int CR, int OCC>
+// classify_pixels_w16_kernel with the prologue replaced by direct loads of the prepared operands.
+// FUSE (round 6): the f64 refine follows the sweep in the same workgroup (refine_pixels on the
+// freed chunk buffers, each wave its four 16-pixel groups), so its loads and f64 work overlap the
+// other resident workgroup's MFMA sweep, and the screen's rows and bounds never leave registers.
+template <class L, int NW, int NBUF, int CR, int OCC, bool FUSE>
 __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(const uint4 *__restrict__ table,
                                                                       const uint8_t *__restrict__ flags, int64_t P,
                                                                       const _Float16 *__restrict__ refh, int32_t R,
                                                                       int32_t Rpad, int32_t *__restrict__ best_idx,
                                                                       float *__restrict__ best_dist,
-                                                                      float *__restrict__ second) {
+                                                                      float *__restrict__ second, RefineArgs A) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   constexpr int KP = 32 * KT;
   constexpr int ROWB = 4 * KP + L::PADB;
@@ -1220,6 +1551,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   }
 #undef HRF_SWEEPW
   const int Q = lane >> 4;
+  int b1g[4];
+  float s2g[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     float b = best[g], sc = sec[g];
@@ -1234,12 +1567,23 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
         idx = oi;
       }
     }
+    b1g[g] = idx;  // every quarter lane holds pixel (lane & 15) + 16 g's merged result
+    s2g[g] = sc;
     const int64_t p = pbase + 16 * g + (lane & 15);
-    if (Q == 0 && p < P) {
+    if (!FUSE && Q == 0 && p < P) {
       best_idx[p] = idx;
       best_dist[p] = ((float)L::NSEG - b) / (float)L::NSEG;
       if (second) second[p] = sc;
     }
+  }
+  if constexpr (FUSE) {
+    __syncthreads();  // every wave is done with the chunk buffers: they become the refine's slices
+    constexpr int64_t SL = (refine_slice_bytes() + 15) / 16 * 16;
+    char *slice = ldsb + w * SL;
+    // lane l holds pixel pbase + l's merged result in quarter Q = l >> 4's slot
+    const int b1 = Q == 0 ? b1g[0] : Q == 1 ? b1g[1] : Q == 2 ? b1g[2] : b1g[3];
+    const float s2 = Q == 0 ? s2g[0] : Q == 1 ? s2g[1] : Q == 2 ? s2g[2] : s2g[3];
+    refine_pixels64(A, L::C, A.bd, pbase, P, b1, s2, slice, best_idx, best_dist, true);
   }
 }
 
@@ -1506,293 +1850,18 @@ hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Boun
   return HRF_OK;
 }
 
-// ==== exact per-pixel classification: the f64 refine of the screen (round 6) ==================
-// The MFMA sweeps above are a SCREEN: split-fp16 (or f32-MFMA) scores within a bound of the exact
-// segmented-cosine score.  Every sweep also reports, per pixel, an upper bound s2 on the device
-// score of every library row other than its best row b1 (the runner-up, `second`).  The refine:
-//  * rescores b1 in f64 exactly as the restatement does (oracle seg_dist / oracle_segcos variant
-//    0: the three sums in channel order, 1 - d / sqrt(nx * ny), the segment mean) from the pixel's
-//    f32 values -- the stack, or the five shifted acquisitions of a registered tile -- and the f32
-//    library promoted to f64 (the restatement's ref64);
-//  * certifies b1 when D(b1) < 1 - (s2 + eps) / nseg - 1e-12, eps the screen's proven error bound
-//    (screen_eps below): then every other row r has S_exact(r) <= s2 + eps, i.e. its restated
-//    distance exceeds D(b1), so b1 is the restatement's argmin and D(b1) its distance, bit for bit;
-//  * answers an all-zero pixel from the library alone (every segment one-zero or both-zero:
-//    D(r) = (nonzero segments of r) / nseg, its first argmin precomputed at prepare time);
-//  * lists every other pixel (ties, near-ties, NaN / inf values) for refine_list_kernel, which
-//    scores all rows in f32 with its own proven bound (fmaf chains on the raw values), keeps the
-//    rows within twice that bound of the best, and rescores those in f64 -- lowest row on ties.
-// The prepared library (refx) carries the exact section after its MFMA table: a header, the f32
-// library row-major (pitch CP = C rounded to 4, float4 rows), channel-major (pitch RT = R rounded
-// to 64, coalesced for the list kernel), the f64 segment sums of squares ny (the restatement's
-// |y|^2) and f32 reciprocal segment norms iy.
-struct ExactHdr {
-  int32_t R, C, nseg, idx0;  // idx0 / D0: the all-zero pixel's argmin and distance
-  double D0;
-  int32_t tiny;              // some row has 0 < ny < 1e-30: the list kernel's f32 pass is not safe
-};
-struct ExactLayout {
-  int64_t off;  // section offset from the start of refx
-  int32_t CP, RT;
-  int64_t lib32, libT, ny, iy, total;  // offsets inside the section
-};
-inline int64_t al256(int64_t x) { return (x + 255) & ~(int64_t)255; }
-ExactLayout exact_layout(int mode, int lay, int kp, int rpad, int R, int C, int nseg) {
-  ExactLayout e;
-  const int64_t rowb = mode == 0 ? 4 * (int64_t)kp : table_rowb(mode, lay, kp);
-  e.off = al256((int64_t)rpad * rowb);
-  e.CP = (C + 3) & ~3;
-  e.RT = (R + 63) & ~63;
-  e.lib32 = 256;
-  e.libT = al256(e.lib32 + (int64_t)R * e.CP * 4);
-  e.ny = al256(e.libT + (int64_t)C * e.RT * 4);
-  e.iy = al256(e.ny + (int64_t)R * nseg * 8);
-  e.total = al256(e.iy + (int64_t)R * nseg * 4);
-  return e;
-}
-struct ExactPtr {
-  const float *lib32, *libT, *iy;
-  const double *ny;
-  int32_t CP, RT;
-};
-
-__global__ __launch_bounds__(256) void exact_prep_kernel(const float *__restrict__ ref, int32_t R, int32_t C,
-                                                         Bounds bd, int32_t CP, int32_t RT, float *__restrict__ lib32,
-                                                         float *__restrict__ libT, double *__restrict__ ny,
-                                                         float *__restrict__ iy) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (int64_t e = t0; e < (int64_t)R * CP; e += stride) {
-    const int64_t r = e / CP;
-    const int c = (int)(e - r * CP);
-    lib32[e] = c < C ? ref[r * C + c] : 0.0f;
-  }
-  for (int64_t e = t0; e < (int64_t)C * RT; e += stride) {
-    const int64_t c = e / RT, r = e - c * RT;
-    libT[e] = r < R ? ref[r * C + c] : 0.0f;
-  }
-  for (int64_t e = t0; e < (int64_t)R * bd.nseg; e += stride) {
-    const int64_t r = e / bd.nseg;
-    const int sg = (int)(e - r * bd.nseg);
-    double v = 0.0;
-    for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
-      const double y = (double)ref[r * C + i];
-      v += y * y;
-    }
-    ny[e] = v;
-    iy[e] = v > 0.0 ? (float)(1.0 / sqrt(v)) : 0.0f;
-  }
-}
-
-// one thread: the all-zero pixel's answer (oracle_classify's loop on x = 0) and the tiny-row flag
-__global__ void exact_hdr_kernel(const double *__restrict__ ny, int32_t R, int32_t C, int32_t nseg,
-                                 ExactHdr *__restrict__ hdr) {
-  double best = __builtin_inf();
-  int32_t bi = 0, tiny = 0;
-  for (int r = 0; r < R; ++r) {
-    double sum = 0.0;
-    for (int sg = 0; sg < nseg; ++sg) {
-      const double v = ny[(int64_t)r * nseg + sg];
-      sum += v == 0.0 ? 0.0 : 1.0;
-      tiny |= (v > 0.0 && v < 1e-30) ? 1 : 0;
-    }
-    const double d = sum / nseg;
-    if (d < best) {
-      best = d;
-      bi = r;
-    }
-  }
-  hdr->R = R;
-  hdr->C = C;
-  hdr->nseg = nseg;
-  hdr->idx0 = bi;
-  hdr->D0 = best;
-  hdr->tiny = tiny;
-}
-
-// Pixel source: the registered value of pixel p (row r = p / W, column c = p % W) at channel k of
-// laser q is src[q][((r - dr_q) W + (c - dc_q)) cl_q + (k - c0_q)], 0 outside the laser's frame and,
-// with apply_mask, outside any laser's frame (register_assemble's stack; stack.hip).  A plain (P, C)
-// stack is one laser with no shift.
-constexpr int XLMAX = 8;
-struct PixSrc {
-  const float *src[XLMAX];
-  int32_t c0[XLMAX + 1];
-  uint64_t mdiv[XLMAX];  // ceil(2^32 / cl): e / cl = (e * mdiv) >> 32 for e < 2^32 / cl
-  int32_t n;
-  const int32_t *dsh;    // device (dr, dc) pairs, or null (no shift)
-  int64_t H, W;
-  int32_t apply_mask;
-};
-
-__device__ __forceinline__ bool src_covered(int64_t r, int64_t c, int64_t H, int64_t W, int dr, int dc) {
-  return r >= (dr > 0 ? dr : 0) && r < H + (dr < 0 ? dr : 0) && c >= (dc > 0 ? dc : 0) && c < W + (dc < 0 ? dc : 0);
-}
-
-// element offsets (from src[q]) of pixel p's run in every laser, -1 where it reads as zero
-__device__ __forceinline__ void src_offsets(const PixSrc &S, int64_t p, bool valid, int32_t (&off)[XLMAX]) {
-  const int64_t r = p / S.W, c = p - r * S.W;
-  bool ok = valid;
-  if (S.apply_mask && S.dsh)
-    for (int q = 0; q < S.n; ++q) ok = ok && src_covered(r, c, S.H, S.W, S.dsh[2 * q], S.dsh[2 * q + 1]);
-#pragma unroll
-  for (int q = 0; q < XLMAX; ++q) {
-    off[q] = -1;
-    if (q < S.n && ok) {
-      const int dr = S.dsh ? S.dsh[2 * q] : 0, dc = S.dsh ? S.dsh[2 * q + 1] : 0;
-      if (src_covered(r, c, S.H, S.W, dr, dc))
-        off[q] = (int32_t)(((r - dr) * S.W + (c - dc)) * (int64_t)(S.c0[q + 1] - S.c0[q]));
-    }
-  }
-}
-
-// f64 restated distance of the pixel (f32 values x[0..C), stride 1) to a library row (yv: its f32
-// values, float4-aligned, CP = C rounded to 4; nyr: its segment sums of squares): the
-// restatement's seg_dist per segment in channel order, their sum, / nseg.  nz: the pixel's
-// all-zero segments; in_range: every non-zero segment's sum of squares lies where the screen's f32
-// normalisation is exact to its bound (no f32 overflow, no overflowing f64-redo reciprocal).
-// NC > 0: the channel loop unrolled to NC (yv then indexes registers with constants); 0: a loop.
-constexpr double NX_MIN = 1e-70, NX_MAX = 1e37;
-template <int NC, class YV, class NY>
-__device__ __forceinline__ double exact_dist_y(const float *x, YV yv, NY nyr, int C, const Bounds &bd, int *nz,
-                                               bool *in_range) {
-  double sum = 0.0;
-  int zc = 0;
-  bool rok = true;
-  for (int sg = 0; sg < bd.nseg; ++sg) {
-    const double ny = nyr(sg);  // issued before the segment's channels: its latency overlaps them
-    double nx = 0.0, dd = 0.0;
-    // 8 channels' loads issued together, then their sums in channel order (one load latency per 8)
-    const int ce = bd.b[sg + 1];
-    for (int c0 = bd.b[sg]; c0 < ce; c0 += 8) {
-      float xv[8], yy[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xv[u] = c0 + u < ce ? x[c0 + u] : 0.0f;
-        yy[u] = c0 + u < ce ? yv(c0 + u) : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (c0 + u < ce) {
-          const double xd = (double)xv[u], yd = (double)yy[u];
-          dd += xd * yd;
-          nx += xd * xd;
-        }
-    }
-    const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
-    sum += sd;
-    zc += nx == 0.0 ? 1 : 0;
-    rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
-  }
-  *nz = zc;
-  if (in_range) *in_range = rok;
-  return sum / bd.nseg;
-}
-__device__ __forceinline__ double exact_dist(const float *x, const ExactPtr &E, int r, int C, const Bounds &bd,
-                                             int *nz, bool *in_range = nullptr) {
-  const float *yr = E.lib32 + (int64_t)r * E.CP;
-  const double *nyr = E.ny + (int64_t)r * bd.nseg;
-  return exact_dist_y<0>(x, [&](int c) { return yr[c]; }, [&](int sg) { return nyr[sg]; }, C, bd, nz, in_range);
-}
-
-// One wave = 32 consecutive pixels.  Their values and their screen rows b1 are loaded with every
-// load of the wave in flight at once (lane = channel c and c + 64, unrolled over the 32 pixels:
-// each pixel's registered spectrum is a few contiguous laser runs, each library row one run) and
-// staged in LDS; then lanes 0..31 (lane = pixel) rescore b1 in f64 and certify or list it.
-#ifndef HRF_REF_NP
-#define HRF_REF_NP 32
-#endif
-constexpr int REF_NP = HRF_REF_NP;  // pixels per wave (<= 64)
-__global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, int32_t C, Bounds bd, ExactPtr E,
-                                                         const ExactHdr *__restrict__ hdr, double eps_base,
-                                                         double eps_zero, const float *__restrict__ second,
-                                                         int32_t *__restrict__ best_idx, float *__restrict__ best_dist,
-                                                         int32_t *__restrict__ list, int32_t *__restrict__ cnt) {
-  extern __shared__ float rxs[];  // x: REF_NP x CPX, then y: REF_NP x CPX
-  __shared__ int32_t offs[XLMAX][REF_NP];
-  __shared__ int32_t b1s[REF_NP];
-  __shared__ double nyb[REF_NP][SMAX];
-  const int CPX = C | 1;  // odd pitch: conflict-free lane-per-pixel reads
-  float *ys = rxs + REF_NP * CPX;
+// The unfused refine: one wave = 64 consecutive pixels of a screen's output (refine_pixels64).
+__global__ __launch_bounds__(64) void refine_best_kernel(RefineArgs A, int64_t P, int32_t C, Bounds bd,
+                                                         const float *__restrict__ second,
+                                                         int32_t *__restrict__ best_idx,
+                                                         float *__restrict__ best_dist) {
+  extern __shared__ __attribute__((aligned(16))) char rslice[];
   const int lane = threadIdx.x;
-  const int64_t p0 = (int64_t)blockIdx.x * REF_NP, p = p0 + lane;
-  const bool valid = lane < REF_NP && p < P;
-  const int Rr = hdr->R;
-  int b1 = valid ? best_idx[p] : 0;
-  const bool brow = b1 >= 0 && b1 < Rr;
+  const int64_t p0 = (int64_t)blockIdx.x * 64, p = p0 + lane;
+  const bool valid = p < P;
+  const int b1 = valid ? best_idx[p] : 0;
   const float sec2 = valid ? second[p] : 0.0f;
-  if (lane < REF_NP) {
-    int32_t off[XLMAX];
-    src_offsets(S, p, valid, off);
-#pragma unroll
-    for (int q = 0; q < XLMAX; ++q) offs[q][lane] = off[q];
-    b1s[lane] = brow ? b1 : 0;
-#pragma unroll
-    for (int q = 0; q < SMAX; ++q) nyb[lane][q] = q < bd.nseg ? E.ny[(int64_t)(brow ? b1 : 0) * bd.nseg + q] : 0.0;
-  }
-  __syncthreads();
-  // lane = channels c0 = lane and c1 = lane + 64: laser q and local channel fixed per lane
-  const int c0 = lane, c1 = lane + 64;
-  int q0 = 0, q1 = 0;
-  for (int q = 1; q < S.n; ++q) {
-    q0 = c0 >= S.c0[q] ? q : q0;
-    q1 = c1 >= S.c0[q] ? q : q1;
-  }
-  const float *s0 = S.src[q0] + (c0 - S.c0[q0]), *s1 = S.src[q1] + (c1 - S.c0[q1]);
-  const bool v0 = c0 < C, v1 = c1 < C;
-  {
-    float x0[REF_NP], x1[REF_NP], y0[REF_NP], y1[REF_NP];
-#pragma unroll
-    for (int i = 0; i < REF_NP; ++i) {
-      const int o0 = offs[q0][i], o1 = offs[q1][i];
-      const float *yr = E.lib32 + (int64_t)b1s[i] * E.CP;
-      x0[i] = (v0 && o0 >= 0) ? s0[o0] : 0.0f;
-      x1[i] = (v1 && o1 >= 0) ? s1[o1] : 0.0f;
-      y0[i] = v0 ? yr[c0] : 0.0f;
-      y1[i] = v1 ? yr[c1] : 0.0f;
-    }
-#pragma unroll
-    for (int i = 0; i < REF_NP; ++i) {
-      if (v0) {
-        rxs[i * CPX + c0] = x0[i];
-        ys[i * CPX + c0] = y0[i];
-      }
-      if (v1) {
-        rxs[i * CPX + c1] = x1[i];
-        ys[i * CPX + c1] = y1[i];
-      }
-    }
-  }
-  __syncthreads();
-  bool listed = false;
-  if (valid) {
-    if (!brow) {  // no real row won the screen (cannot happen with R >= 1): list it
-      listed = true;
-    } else {
-      int nz = 0;
-      bool in_range = true;
-      const float *yl = ys + lane * CPX;
-      const double D = exact_dist_y<0>(
-          rxs + lane * CPX, [&](int c) { return yl[c]; }, [&](int sg) { return nyb[lane][sg]; }, C, bd, &nz, &in_range);
-      if (nz == bd.nseg) {  // all-zero pixel: the library's own answer
-        best_idx[p] = hdr->idx0;
-        best_dist[p] = (float)hdr->D0;
-      } else if (!in_range) {  // outside the screen bound's premises
-        listed = true;
-      } else {
-        const double eps = eps_base + eps_zero * nz;
-        const double lim = 1.0 - ((double)sec2 + eps) / bd.nseg - 1e-12;
-        if (D < lim) best_dist[p] = (float)D;  // certified (NaN anywhere fails the compare)
-        else listed = true;
-      }
-    }
-  }
-  const unsigned long long m = __ballot(listed);
-  if (m) {
-    int base = 0;
-    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(cnt, __popcll(m));
-    base = __shfl(base, __ffsll((long long)m) - 1, 64);
-    if (listed) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)p;
-  }
+  refine_pixels64(A, C, bd, p0, P, b1, sec2, rslice, best_idx, best_dist, false);
 }
 
 // Listed pixels, in batches of LIST_NP per workgroup (grid-strided over the device count), so
@@ -1806,7 +1875,7 @@ __global__ __launch_bounds__(64) void refine_best_kernel(PixSrc S, int64_t P, in
 //  3. those rows (every row for a pixel with non-finite values or norms out of the f32 pass's
 //     range) rescored exactly (exact_dist), minimum with the lowest row on ties, as
 //     oracle_classify's first-minimum loop.
-constexpr int LIST_NP = 8;     // pixels per batch
+constexpr int LIST_NP = 16;    // pixels per batch
 constexpr int LIST_NT = 256;   // threads per workgroup
 constexpr int LIST_RMAX = 4096;
 __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t C, Bounds bd, ExactPtr E,
@@ -2055,7 +2124,7 @@ constexpr double U24 = 1.0 / 16777216.0;
 struct ScreenEps {
   double base, zero, eps32;
 };
-ScreenEps screen_eps(const Bounds &bd, int nmfma, bool f32chain, int kp) {
+ScreenEps screen_eps(const Bounds &bd, double nmfma, bool f32chain, int kp) {
   double a = 0.0, c = 0.0, e32 = 0.0;
   for (int sg = 0; sg < bd.nseg; ++sg) {
     const int ns = bd.b[sg + 1] - bd.b[sg];
@@ -2250,43 +2319,68 @@ ScreenEps eps_of_screen(int screen, const Bounds &bd, int C, int kp) {
   if (screen == 0) return screen_eps(bd, 0, true, kp);
   if (screen == 1) return screen_eps(bd, 3 * (kp / 16), false, kp);
   if (screen == 2 && lay == 2) return screen_eps(bd, 3 * ((C + 1 + 15) / 16) + 1, false, kp);
-  return screen_eps(bd, 3 * ((C + 1 + 31) / 32) + 1, false, kp);  // w16 / w16t
+  // w16 / w16t: the 2 KT cross-product MFMAs meet accumulators below 2^-9 A (their products are
+  // <= 2^-10 A in all), then KT hi * hi' MFMAs and the indicator step at full magnitude
+  const int kt = (C + 1 + 31) / 32;
+  return screen_eps(bd, kt + 1 + 2.0 * kt * 0x1p-9, false, kp);
 }
 
-hrf_status refine(const PixSrc &S, int64_t P, int32_t C, const void *refx, int32_t R, const Bounds &bd, int32_t screen,
-                  const float *second, int32_t *best_idx, float *best_dist, void *work, int64_t work_bytes,
-                  hipStream_t s) {
+// the refine's arguments for `screen`'s output on refx; fuse: the table sweep (screen 3) runs the
+// certificate itself (classify_pixels_w16t_kernel<..., true>), else refine_best_kernel does
+hrf_status refine_args(const PixSrc &S, int64_t P, int32_t C, const void *refx, int32_t R, const Bounds &bd,
+                       int32_t screen, void *work, int64_t work_bytes, RefineArgs *A, hipStream_t s) {
   HRF_REQUIRE(screen >= 0 && screen <= 3, "classify_refine: screen must be 0..3");
   const int mode = screen == 3 ? 2 : screen;
   int32_t kp = 0, rpad = 0;
   if (hrf_status st = hrf_classify_geometry(C, bd.nseg, R, mode, &kp, &rpad)) return st;
   HRF_REQUIRE(C <= 128 && R <= LIST_RMAX, "classify_refine: C <= 128 and R <= %d required", LIST_RMAX);
   HRF_REQUIRE(work_bytes >= hrf_classify_refine_work_bytes(P), "classify_refine: work buffer too small");
-  if (P == 0) return HRF_OK;
-  HRF_REQUIRE(refx && second && best_idx && best_dist && work, "classify_refine: null buffer");
+  HRF_REQUIRE(refx && work, "classify_refine: null buffer");
   const ExactLayout el = exact_layout(mode, layout_id(bd, C), kp, rpad, R, C, bd.nseg);
   const char *sec = (const char *)refx + el.off;
-  ExactPtr E;
-  E.lib32 = (const float *)(sec + el.lib32);
-  E.libT = (const float *)(sec + el.libT);
-  E.ny = (const double *)(sec + el.ny);
-  E.iy = (const float *)(sec + el.iy);
-  E.CP = el.CP;
-  E.RT = el.RT;
-  const ExactHdr *hdr = (const ExactHdr *)sec;
+  A->S = S;
+  A->E.lib32 = (const float *)(sec + el.lib32);
+  A->E.libT = (const float *)(sec + el.libT);
+  A->E.ny = (const double *)(sec + el.ny);
+  A->E.iy = (const float *)(sec + el.iy);
+  A->E.CP = el.CP;
+  A->E.RT = el.RT;
+  A->hdr = (const ExactHdr *)sec;
   const ScreenEps ep = eps_of_screen(screen, bd, C, kp);
-  int32_t *cnt = (int32_t *)work;
-  int32_t *list = (int32_t *)((char *)work + 16);
-  HRF_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), s));
-  const int CPX = C | 1;
-  refine_best_kernel<<<(unsigned)hrf::cdiv(P, REF_NP), 64, sizeof(float) * 2 * REF_NP * CPX, s>>>(
-      S, P, C, bd, E, hdr, ep.base, ep.zero, second, best_idx, best_dist, list, cnt);
-  HRF_LAUNCHED();
-  const size_t shm = sizeof(float) * LIST_NP * (size_t)el.RT;
+  A->eps_base = ep.base;
+  A->eps_zero = ep.zero;
+  A->cnt = (int32_t *)work;
+  A->list = (int32_t *)((char *)work + 16);
+  A->bd = bd;
+  HRF_HIP(hipMemsetAsync(A->cnt, 0, sizeof(int32_t), s));
+  return HRF_OK;
+}
+
+// the list pass over what the certificate left (device-held count)
+hrf_status refine_list(const RefineArgs &A, int64_t P, int32_t C, int32_t R, const Bounds &bd, int32_t screen,
+                       int32_t *best_idx, float *best_dist, hipStream_t s) {
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status st = hrf_classify_geometry(C, bd.nseg, R, screen == 3 ? 2 : screen, &kp, &rpad)) return st;
+  const ScreenEps ep = eps_of_screen(screen, bd, C, kp);
+  const size_t shm = sizeof(float) * LIST_NP * (size_t)A.E.RT;
   const unsigned g = hrf::resident_grid(refine_list_kernel, LIST_NT, shm, hrf::cdiv(P, LIST_NP));
-  refine_list_kernel<<<g, LIST_NT, shm, s>>>(S, C, bd, E, hdr, R, ep.eps32, list, cnt, best_idx, best_dist);
+  refine_list_kernel<<<g, LIST_NT, shm, s>>>(A.S, C, bd, A.E, A.hdr, R, ep.eps32, A.list, A.cnt, best_idx,
+                                             best_dist);
   HRF_LAUNCHED();
   return HRF_OK;
+}
+
+hrf_status refine(const PixSrc &S, int64_t P, int32_t C, const void *refx, int32_t R, const Bounds &bd, int32_t screen,
+                  const float *second, int32_t *best_idx, float *best_dist, void *work, int64_t work_bytes,
+                  hipStream_t s) {
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(second && best_idx && best_dist, "classify_refine: null buffer");
+  RefineArgs A;
+  if (hrf_status st = refine_args(S, P, C, refx, R, bd, screen, work, work_bytes, &A, s)) return st;
+  refine_best_kernel<<<(unsigned)hrf::cdiv(P, 64), 64, (size_t)refine_slice_bytes(), s>>>(
+      A, P, C, bd, second, best_idx, best_dist);
+  HRF_LAUNCHED();
+  return refine_list(A, P, C, R, bd, screen, best_idx, best_dist, s);
 }
 
 hrf_status pixsrc_of(const float *const *src_host, const int32_t *channels_host, const int32_t *shifts_dev,
@@ -2421,17 +2515,55 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
     const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
-    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC>,
+    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC><<<grid, 256, shm, s>>>((const uint4 *)table, flags, P,
-                                                                        (const _Float16 *)refx, R, rpad, best_idx,
-                                                                        best_dist, second);
+    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, false><<<grid, 256, shm, s>>>(
+        (const uint4 *)table, flags, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, second, RefineArgs{});
     return HRF_OK;
   };
   hrf_status st = lay == 1 ? go(LayEcoli{}) : go(LayMulti{});
   if (st) return st;
   HRF_LAUNCHED();
   return HRF_OK;
+}
+
+hrf_status hrf_classify_pixels_table_exact(const void *table, const uint8_t *flags, const float *const *src_host,
+                                           const int32_t *channels_host, const int32_t *shifts_dev, int32_t nlaser,
+                                           int64_t H, int64_t W, int32_t apply_mask, const void *refx, int32_t R,
+                                           const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                           float *best_dist, void *work, int64_t work_bytes, hrf_stream_t stream) {
+  const int64_t P = H * W;
+  int32_t C = 0;
+  for (int q = 0; src_host && channels_host && q < nlaser && q < XLMAX; ++q) C += channels_host[q];
+  Bounds bd;
+  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  int32_t kp = 0, rpad = 0;
+  if (hrf_status s = hrf_classify_geometry(C, nseg, R, 2, &kp, &rpad)) return s;
+  const int lay = layout_id(bd, C);
+  HRF_REQUIRE(lay != 0, "classify_pixels_table_exact: the E. coli or multispecies channel layout only");
+  if (P == 0) return HRF_OK;
+  HRF_REQUIRE(table && flags && refx && best_idx && best_dist, "classify_pixels_table_exact: null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  PixSrc S;
+  if (hrf_status st = pixsrc_of(src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, C, &S)) return st;
+  RefineArgs A;
+  if (hrf_status st = refine_args(S, P, C, refx, R, bd, 3, work, work_bytes, &A, s)) return st;
+  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
+  auto go = [&](auto lay_tag) -> hrf_status {
+    using L = decltype(lay_tag);
+    constexpr int KT = (L::C + 1 + 31) / 32;
+    constexpr int64_t SL = (refine_slice_bytes() + 15) / 16 * 16;
+    const size_t shm = std::max<size_t>((size_t)2 * 64 * (128 * KT + L::PADB), (size_t)(4 * SL));
+    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, true><<<grid, 256, shm, s>>>(
+        (const uint4 *)table, flags, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, nullptr, A);
+    return HRF_OK;
+  };
+  hrf_status st = lay == 1 ? go(LayEcoli{}) : go(LayMulti{});
+  if (st) return st;
+  HRF_LAUNCHED();
+  return refine_list(A, P, C, R, bd, 3, best_idx, best_dist, s);
 }
 
 }  // extern "C"

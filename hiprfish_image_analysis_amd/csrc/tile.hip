@@ -50,7 +50,6 @@ struct hrf_tile_ctx {
   double *cn = nullptr;         // image_cn
   void *table = nullptr;        // pixel table
   uint8_t *flags = nullptr;
-  float *second = nullptr;      // the screen's runner-up bounds
   void *rwork = nullptr;        // the refine's list (hrf_classify_refine_work_bytes)
   int64_t rwork_bytes = 0;
   // per-label buffers, grown on demand (capacity cap labels + 1)
@@ -149,7 +148,7 @@ hrf_status hrf_tile_ctx_create(int64_t H, int64_t W, hrf_tile_ctx **out) {
   if ((r = hrf_seg_ctx_create(H, W, &t->seg))) return fail(r);
   if ((r = dalloc(&t->proj, NL * n)) || (r = dalloc((char **)&t->xwork, (size_t)xb)) ||
       (r = dalloc(&t->shifts, 2 * NL)) || (r = dalloc(&t->cn, n)) || (r = dalloc((char **)&t->table, (size_t)tb)) ||
-      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)) || (r = dalloc(&t->second, n)) ||
+      (r = dalloc(&t->flags, n)) || (r = dalloc(&t->nrows, 4)) ||
       (r = dalloc((char **)&t->rwork, (size_t)hrf_classify_refine_work_bytes((int64_t)n))))
     return fail(r);
   t->rwork_bytes = hrf_classify_refine_work_bytes((int64_t)n);
@@ -171,7 +170,6 @@ hrf_status hrf_tile_ctx_destroy(hrf_tile_ctx *t) {
   hipFree(t->cn);
   hipFree(t->table);
   hipFree(t->flags);
-  hipFree(t->second);
   hipFree(t->rwork);
   hipFree(t->nrows);
   hipFree(t->sums);
@@ -235,12 +233,11 @@ hrf_status hrf_tile_ecoli(hrf_tile_ctx *t, const float *const *lasers_host, cons
       HRF_HIP(hipStreamWaitEvent(side, t->ev_reg, 0));
     }
     if (pix_start) HRF_HIP(hipEventRecord((hipEvent_t)pix_start, side));
-    // the split-fp16 screen from the assembly's table, then its exact f64 refine reading the
-    // pixels from the five shifted acquisitions (hrf_classify_pixels_refine, screen 3)
-    HRF_TRY(hrf_classify_pixels_table(t->table, t->flags, n, C, refx, R, BOUNDS, NL, pixel_idx, pixel_dist, t->second,
-                                      side));
-    HRF_TRY(hrf_classify_pixels_refine(lasers_host, CH, t->shifts, NL, H, W, 1, refx, R, BOUNDS, NL, 3, t->second,
-                                       pixel_idx, pixel_dist, t->rwork, t->rwork_bytes, side));
+    // the split-fp16 screen from the assembly's table with its exact f64 refine fused in, reading
+    // the pixels from the five shifted acquisitions, then the list pass
+    // (hrf_classify_pixels_table_exact)
+    HRF_TRY(hrf_classify_pixels_table_exact(t->table, t->flags, lasers_host, CH, t->shifts, NL, H, W, 1, refx, R,
+                                            BOUNDS, NL, pixel_idx, pixel_dist, t->rwork, t->rwork_bytes, side));
     if (pix_end) HRF_HIP(hipEventRecord((hipEvent_t)pix_end, side));
     if (side != s) HRF_HIP(hipEventRecord(t->ev_pix, side));
   }

@@ -977,13 +977,46 @@ def classify_pixels_table_screen(pt, refx, R):
     return idx, dist, sec
 
 
-def classify_pixels_table(pt, refx, R):
-    """exact per-pixel classification from a PixTable: the table screen, then the f64 refine on the
-    table's source values -- classify_pixels' results"""
+def _source_args(source):
+    """(ptrs, channels, shifts, nlaser, H, W, apply_mask, C) of a StackSource / LaserSource"""
+    import ctypes
+    if isinstance(source, StackSource):
+        st = source.stack
+        C = st.shape[-1]
+        return (ctypes.c_void_p * 1)(st.data_ptr()), _i32_host([C]), None, 1, 1, st.numel() // C, 0, C
+    if isinstance(source, LaserSource):
+        srcs, ch, ptrs, sd = _laser_args(source.lasers, source.shifts)
+        H, W = srcs[0].shape[:2]
+        return ptrs, ch, sd, len(srcs), H, W, int(source.apply_mask), int(ch.sum())
+    raise ValueError("a StackSource or LaserSource is required")
+
+
+def classify_pixels_table(pt, refx, R, fused=True, want_listed=False):
+    """exact per-pixel classification from a PixTable, reading the pixels' values from the table's
+    source: fused (hrf_classify_pixels_table_exact: the sweep certifies its own rows, then the list
+    pass) or screen + hrf_classify_pixels_refine -- the same results bit for bit.
+    -> (idx, dist), and the number of listed pixels with want_listed (synchronises)"""
+    import ctypes
     if pt.source is None:
         raise ValueError("classify_pixels_table: the table has no source values for the exact refine")
-    idx, dist, sec = classify_pixels_table_screen(pt, refx, R)
-    classify_refine(pt.source, refx, R, pt.bounds, 3, idx, dist, sec)
+    if not fused:
+        idx, dist, sec = classify_pixels_table_screen(pt, refx, R)
+        n = classify_refine(pt.source, refx, R, pt.bounds, 3, idx, dist, sec, want_listed=want_listed)
+        return (idx, dist, n) if want_listed else (idx, dist)
+    check_refx_table(refx, R, pt.C, pt.bounds, "classify_pixels_table")
+    ptrs, ch, sd, n, H, W, mask, C = _source_args(pt.source)
+    if H * W != pt.P or C != pt.C:
+        raise ValueError("classify_pixels_table: the source does not match the table")
+    b = _i32_host(pt.bounds)
+    idx = torch.empty(pt.shape, dtype=torch.int32, device=pt.table.device)
+    dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
+    wb = int(_lib.lib().hrf_classify_refine_work_bytes(pt.P))
+    work = torch.empty(wb, dtype=torch.uint8, device=idx.device)
+    _lib.call("hrf_classify_pixels_table_exact", _ptr(pt.table), _ptr(pt.flags), ctypes.cast(ptrs, ctypes.c_void_p),
+              ch.ctypes.data, _ptr(sd) if sd is not None else None, n, H, W, mask, _ptr(refx), R, b.ctypes.data,
+              len(b) - 1, _ptr(idx), _ptr(dist), _ptr(work), wb, _stream())
+    if want_listed:
+        return idx, dist, int(work[:4].view(torch.int32).item())
     return idx, dist
 
 

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 tag=${1:-r6}
 o=gpurun_out/$tag
 mkdir -p $o
-timeout -k 10 400 python -u -m pytest tests/test_classify_exact_gpu.py tests/test_kernels_gpu.py -k "classif" -m gpu -x -q \
+timeout -k 10 500 python -u -m pytest tests/test_classify_exact_gpu.py tests/test_kernels_gpu.py tests/test_regtile_gpu.py tests/test_tile_gpu.py -k "classif or regtile or tile or assembly" -m gpu -x -q \
   --timeout 300 --timeout-method thread > $o/pytest.txt 2>&1
 rc=$?
 tail -3 $o/pytest.txt

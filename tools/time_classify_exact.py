@@ -47,11 +47,15 @@ def main():
     i2.copy_(idx)
     d2.copy_(dist)
     listed = K.classify_refine(pt.source, refx, R, S.ECOLI_BOUNDS, 3, i2, d2, sec, want_listed=True)
+    t_unf = ev(lambda: K.classify_pixels_table(pt, refx, R, fused=False), n)
     t_full = ev(lambda: K.classify_pixels_table(pt, refx, R), n)
+    fi, fd, flisted = K.classify_pixels_table(pt, refx, R, want_listed=True)
+    assert torch.equal(fi, i2) and torch.equal(fd, d2) and flisted == listed, "fused != unfused"
     Pn = 2048 * 2048
     changed = int((i2 != idx).sum().item())
-    print("w16t screen %.3f ms | refine %.3f ms | exact total %.3f ms | listed %d of %d pixels (%.3f %%) | "
-          "screen row changed on %d pixels" % (t_screen, t_ref, t_full, listed, Pn, 100.0 * listed / Pn, changed))
+    print("w16t screen %.3f ms | refine %.3f ms | exact unfused %.3f ms | exact fused %.3f ms | listed %d of %d "
+          "pixels (%.3f %%) | screen row changed on %d pixels" % (t_screen, t_ref, t_unf, t_full, listed, Pn,
+                                                                  100.0 * listed / Pn, changed))
     eps = K.classify_screen_eps(95, S.ECOLI_BOUNDS, R, 3)
     print("bounds (score units): screen %.3e, per zero segment %.3e, list pass %.3e" % eps)
 
