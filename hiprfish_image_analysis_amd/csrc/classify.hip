@@ -1875,9 +1875,10 @@ __global__ __launch_bounds__(64) void refine_best_kernel(RefineArgs A, int64_t P
 //  3. those rows (every row for a pixel with non-finite values or norms out of the f32 pass's
 //     range) rescored exactly (exact_dist), minimum with the lowest row on ties, as
 //     oracle_classify's first-minimum loop.
-constexpr int LIST_NP = 16;    // pixels per batch
+constexpr int LIST_NP = 8;     // pixels per batch (stage 1 maps 32 threads per pixel)
 constexpr int LIST_NT = 256;   // threads per workgroup
 constexpr int LIST_RMAX = 4096;
+static_assert(LIST_NP * 32 == LIST_NT, "stage 1 loads one pixel per 32 threads");
 __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t C, Bounds bd, ExactPtr E,
                                                               const ExactHdr *__restrict__ hdr, int32_t R,
                                                               double eps32, const int32_t *__restrict__ list,
