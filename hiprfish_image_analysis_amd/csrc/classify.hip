@@ -70,6 +70,7 @@ struct ExactHdr {
   int32_t R, C, nseg, idx0;  // idx0 / D0: the all-zero pixel's argmin and distance
   double D0;
   int32_t tiny;              // some row has 0 < ny < 1e-30: the list kernel's f32 pass is not safe
+  float zero[4];             // 0: what an uncovered pixel's channel reads (a load that needs no branch)
 };
 struct ExactLayout {
   int64_t off;  // section offset from the start of refx
@@ -148,6 +149,7 @@ __global__ void exact_hdr_kernel(const double *__restrict__ ny, int32_t R, int32
   hdr->idx0 = bi;
   hdr->D0 = best;
   hdr->tiny = tiny;
+  for (int i = 0; i < 4; ++i) hdr->zero[i] = 0.0f;
 }
 
 // Pixel source: the registered value of pixel p (row r = p / W, column c = p % W) at channel k of
@@ -202,22 +204,24 @@ __device__ __forceinline__ double exact_dist_y(const float *x, YV yv, NY nyr, in
   for (int sg = 0; sg < bd.nseg; ++sg) {
     const double ny = nyr(sg);  // issued before the segment's channels: its latency overlaps them
     double nx = 0.0, dd = 0.0;
-    // 8 channels' loads issued together, then their sums in channel order (one load latency per 8)
-    const int ce = bd.b[sg + 1];
-    for (int c0 = bd.b[sg]; c0 < ce; c0 += 8) {
-      float xv[8], yy[8];
+    // 16 channels' loads issued together (clamped channel, the sum selected: a branch around the
+    // sums would take the loads with it and wait for each), then their sums in channel order
+    const int cb = bd.b[sg], ce = bd.b[sg + 1];
+    for (int c0 = cb; c0 < ce; c0 += 16) {
+      float xv[16], yy[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xv[u] = c0 + u < ce ? x[c0 + u] : 0.0f;
-        yy[u] = c0 + u < ce ? yv(c0 + u) : 0.0f;
+      for (int u = 0; u < 16; ++u) {
+        const int c = min(c0 + u, ce - 1);
+        xv[u] = x[c];
+        yy[u] = yv(c);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (c0 + u < ce) {
-          const double xd = (double)xv[u], yd = (double)yy[u];
-          dd += xd * yd;
-          nx += xd * xd;
-        }
+      for (int u = 0; u < 16; ++u) {
+        const bool ok = c0 + u < ce;
+        const double xd = (double)xv[u], yd = (double)yy[u];
+        dd = ok ? dd + xd * yd : dd;
+        nx = ok ? nx + xd * xd : nx;
+      }
     }
     const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
     sum += sd;
@@ -258,15 +262,26 @@ struct RefineArgs {
 // so the slice stays small (more waves resident) and all 64 lanes do the f64 work.  Then the
 // certificate: best_dist (and best_idx with write_idx) for a certified row, the header's answer
 // for an all-zero pixel, the list otherwise.
-constexpr int RCK = 16;  // channels per chunk
+// G chunks' loads are issued together (branch-free: clamped addresses, the value selected after
+// the load), so a wave waits for memory once per G chunks rather than once per chunk.
+#ifndef HRF_REFINE_WPE
+#define HRF_REFINE_WPE 3  // refine_best_kernel: waves per SIMD the register budget allows
+#endif
+#ifndef HRF_REFINE_RCK
+#define HRF_REFINE_RCK 16
+#endif
+constexpr int RCK = HRF_REFINE_RCK;  // channels per chunk
+#ifndef HRF_REFINE_G
+#define HRF_REFINE_G 2  // chunks whose loads are in flight together
+#endif
 __host__ __device__ constexpr int64_t refine_slice_bytes() {
-  return (int64_t)64 * (8 * SMAX + 4 * XLMAX + 4) + (int64_t)64 * (RCK + 1) * 8;
+  return (int64_t)64 * (4 * XLMAX + 4) + (int64_t)64 * (RCK + 1) * 8;
 }
+template <int G>
 __device__ __forceinline__ void refine_pixels64(const RefineArgs &A, int C, const Bounds &bd, int64_t p0, int64_t P,
                                                 int b1, float sec2, char *slice, int32_t *__restrict__ best_idx,
                                                 float *__restrict__ best_dist, bool write_idx) {
-  double *nyb = reinterpret_cast<double *>(slice);                    // 64 x SMAX
-  int32_t *offs = reinterpret_cast<int32_t *>(nyb + 64 * SMAX);       // XLMAX x 64
+  int32_t *offs = reinterpret_cast<int32_t *>(slice);                 // XLMAX x 64
   int32_t *b1s = offs + XLMAX * 64;                                   // 64
   float2 *xy = reinterpret_cast<float2 *>(b1s + 64);                  // 64 x (RCK + 1) (x, y)
   const PixSrc &S = A.S;
@@ -276,14 +291,17 @@ __device__ __forceinline__ void refine_pixels64(const RefineArgs &A, int C, cons
   const bool valid = p < P;
   const int Rr = A.hdr->R;
   const bool brow = b1 >= 0 && b1 < Rr;
+  const int64_t brw = brow ? b1 : 0;
+  // the row's segment sums of squares, every load in flight (clamped index, constant register index)
+  double nyv[SMAX];
+#pragma unroll
+  for (int q = 0; q < SMAX; ++q) nyv[q] = E.ny[brw * bd.nseg + (q < bd.nseg ? q : 0)];
   {
     int32_t off[XLMAX];
     src_offsets(S, p, valid, off);
 #pragma unroll
     for (int q = 0; q < XLMAX; ++q) offs[q * 64 + lane] = off[q];
-    b1s[lane] = brow ? b1 : 0;
-#pragma unroll
-    for (int q = 0; q < SMAX; ++q) nyb[lane * SMAX + q] = q < bd.nseg ? E.ny[(int64_t)(brow ? b1 : 0) * bd.nseg + q] : 0.0;
+    b1s[lane] = (int32_t)brw;
   }
   wave_lds_sync();
   // staging: element lane + 64 u of a chunk = pixel il + 4 u, channel k0 + kl
@@ -291,49 +309,67 @@ __device__ __forceinline__ void refine_pixels64(const RefineArgs &A, int C, cons
   double nx = 0.0, dd = 0.0, sum = 0.0;
   int sg = 0, send = bd.b[1], zc = 0;
   bool rok = true;
-  for (int k0 = 0; k0 < C; k0 += RCK) {
-    const int c = k0 + kl;
-    const bool vc = c < C;
-    // this lane's laser for channel c (uniform candidates, per-lane selects: no indexed registers)
-    int qc = 0, cq = 0;
-    const float *sp = S.src[0];
-    for (int q = 1; q < S.n; ++q)
-      if (c >= S.c0[q]) {
-        qc = q;
-        sp = S.src[q];
-        cq = S.c0[q];
+  for (int k00 = 0; k00 < C; k00 += G * RCK) {
+    float xv[G][RCK], yv[G][RCK];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int c = k00 + g * RCK + kl;
+      const int ca = c < C ? c : C - 1;  // a readable channel for the padding lanes
+      // this lane's laser for channel ca (uniform candidates, per-lane selects: no indexed registers)
+      int qc = 0, cq = 0;
+      const float *sp = S.src[0];
+      for (int q = 1; q < S.n; ++q)
+        if (ca >= S.c0[q]) {
+          qc = q;
+          sp = S.src[q];
+          cq = S.c0[q];
+        }
+      int o[RCK], rb[RCK];
+#pragma unroll
+      for (int u = 0; u < RCK; ++u) {
+        const int i = il + (64 / RCK) * u;
+        o[u] = offs[qc * 64 + i];
+        rb[u] = b1s[i];
       }
-    float xv[RCK], yv[RCK];
 #pragma unroll
-    for (int u = 0; u < RCK; ++u) {
-      const int i = il + (64 / RCK) * u;
-      const int o = offs[qc * 64 + i];
-      xv[u] = (vc && o >= 0) ? sp[o + c - cq] : 0.0f;
-      yv[u] = vc ? E.lib32[(int64_t)b1s[i] * E.CP + c] : 0.0f;
-    }
-#pragma unroll
-    for (int u = 0; u < RCK; ++u) xy[(il + (64 / RCK) * u) * (RCK + 1) + kl] = make_float2(xv[u], yv[u]);
-    wave_lds_sync();
-    const float2 *row = xy + lane * (RCK + 1);
-#pragma unroll
-    for (int k = 0; k < RCK; ++k) {
-      if (k0 + k >= C) break;
-      const float2 v = row[k];
-      const double xd = (double)v.x, yd = (double)v.y;
-      dd += xd * yd;
-      nx += xd * xd;
-      if (k0 + k + 1 == send) {  // the segment's restated distance, in segment order
-        const double ny = nyb[lane * SMAX + sg];
-        const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
-        sum += sd;
-        zc += nx == 0.0 ? 1 : 0;
-        rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
-        nx = dd = 0.0;
-        ++sg;
-        send = bd.b[sg + 1];
+      for (int u = 0; u < RCK; ++u) {
+        // unconditional loads (a selected address, not a selected value: the compiler would sink a
+        // load whose value is selected into a branch and wait for it there); the padding lanes'
+        // values are never read
+        xv[g][u] = *(o[u] >= 0 ? sp + (o[u] + ca - cq) : A.hdr->zero);
+        yv[g][u] = E.lib32[(int64_t)rb[u] * E.CP + ca];
       }
     }
-    wave_lds_sync();  // the chunk is consumed before the next one is staged
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int k0 = k00 + g * RCK;
+      if (k0 >= C) break;
+#pragma unroll
+      for (int u = 0; u < RCK; ++u) xy[(il + (64 / RCK) * u) * (RCK + 1) + kl] = make_float2(xv[g][u], yv[g][u]);
+      wave_lds_sync();
+      const float2 *row = xy + lane * (RCK + 1);
+#pragma unroll
+      for (int k = 0; k < RCK; ++k) {
+        if (k0 + k >= C) break;
+        const float2 v = row[k];
+        const double xd = (double)v.x, yd = (double)v.y;
+        dd += xd * yd;
+        nx += xd * xd;
+        if (k0 + k + 1 == send) {  // the segment's restated distance, in segment order
+          double ny = nyv[0];
+#pragma unroll
+          for (int q = 1; q < SMAX; ++q) ny = sg == q ? nyv[q] : ny;
+          const double sd = (nx == 0.0 && ny == 0.0) ? 0.0 : ((nx == 0.0 || ny == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * ny));
+          sum += sd;
+          zc += nx == 0.0 ? 1 : 0;
+          rok = rok && (nx == 0.0 || (nx >= NX_MIN && nx <= NX_MAX));
+          nx = dd = 0.0;
+          ++sg;
+          send = bd.b[sg + 1];
+        }
+      }
+      wave_lds_sync();  // the chunk is consumed before the next one is staged
+    }
   }
   const double D = sum / bd.nseg;
   bool listed = false;
@@ -1583,7 +1619,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     // lane l holds pixel pbase + l's merged result in quarter Q = l >> 4's slot
     const int b1 = Q == 0 ? b1g[0] : Q == 1 ? b1g[1] : Q == 2 ? b1g[2] : b1g[3];
     const float s2 = Q == 0 ? s2g[0] : Q == 1 ? s2g[1] : Q == 2 ? s2g[2] : s2g[3];
-    refine_pixels64(A, L::C, A.bd, pbase, P, b1, s2, slice, best_idx, best_dist, true);
+    refine_pixels64<HRF_REFINE_G>(A, L::C, A.bd, pbase, P, b1, s2, slice, best_idx, best_dist, true);
   }
 }
 
@@ -1851,7 +1887,7 @@ hrf_status make_bounds(const int32_t *bounds_host, int32_t nseg, int32_t C, Boun
 }
 
 // The unfused refine: one wave = 64 consecutive pixels of a screen's output (refine_pixels64).
-__global__ __launch_bounds__(64) void refine_best_kernel(RefineArgs A, int64_t P, int32_t C, Bounds bd,
+__global__ __launch_bounds__(64, HRF_REFINE_WPE) void refine_best_kernel(RefineArgs A, int64_t P, int32_t C, Bounds bd,
                                                          const float *__restrict__ second,
                                                          int32_t *__restrict__ best_idx,
                                                          float *__restrict__ best_dist) {
@@ -1861,7 +1897,7 @@ __global__ __launch_bounds__(64) void refine_best_kernel(RefineArgs A, int64_t P
   const bool valid = p < P;
   const int b1 = valid ? best_idx[p] : 0;
   const float sec2 = valid ? second[p] : 0.0f;
-  refine_pixels64(A, C, bd, p0, P, b1, sec2, rslice, best_idx, best_dist, false);
+  refine_pixels64<HRF_REFINE_G>(A, C, bd, p0, P, b1, sec2, rslice, best_idx, best_dist, false);
 }
 
 // Listed pixels, in batches of LIST_NP per workgroup (grid-strided over the device count), so
@@ -1883,6 +1919,7 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
                                                               const ExactHdr *__restrict__ hdr, int32_t R,
                                                               double eps32, const int32_t *__restrict__ list,
                                                               const int32_t *__restrict__ cnt,
+                                                              int32_t *__restrict__ stats,
                                                               int32_t *__restrict__ best_idx,
                                                               float *__restrict__ best_dist) {
   __shared__ float xb[LIST_NP][128];
@@ -1894,8 +1931,6 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
   constexpr int CAND = 1024;  // sparse candidates per batch; a pixel that overflows is scored in full
   __shared__ int32_t cand[CAND];
   __shared__ int ncand;
-  // one wave per sparse candidate: its exact products (lane = channel), then one lane per segment
-  __shared__ double prw[LIST_NT / 64][128], sqw[LIST_NT / 64][128], sdw[LIST_NT / 64][SMAX];
   extern __shared__ float scb[];  // LIST_NP x RT f32 scores
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int n = *cnt;
@@ -1946,18 +1981,31 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
         for (int j = 0; j < LIST_NP; ++j)
 #pragma unroll
           for (int u = 0; u < 4; ++u) d[j][u] = 0.0f;
-        for (int i = bd.b[sg]; i < bd.b[sg + 1]; ++i) {
-          float y[4];
+        // LV channels' loads in flight together (clamped addresses, no branch around a load; rows
+        // past RT are never stored), then their fmaf chains in channel order
+        constexpr int LV = 4;
+        const int ce = bd.b[sg + 1];
+        for (int i0 = bd.b[sg]; i0 < ce; i0 += LV) {
+          float y[LV][4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int r = r0 + t + LIST_NT * u;
-            y[u] = r < E.RT ? E.libT[(int64_t)i * E.RT + r] : 0.0f;
+          for (int v = 0; v < LV; ++v) {
+            const int i = min(i0 + v, ce - 1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int r = min(r0 + t + LIST_NT * u, E.RT - 1);
+              y[v][u] = E.libT[(int64_t)i * E.RT + r];
+            }
           }
 #pragma unroll
-          for (int j = 0; j < LIST_NP; ++j) {
-            const float x = xb[j][i];
+          for (int v = 0; v < LV; ++v) {
+            const bool ok = i0 + v < ce;  // (a select, not a branch: a branch would take the loads with it)
+            const int i = ok ? i0 + v : i0;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) d[j][u] = __builtin_fmaf(x, y[u], d[j][u]);
+            for (int j = 0; j < LIST_NP; ++j) {
+              const float x = xb[j][i];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) d[j][u] = ok ? __builtin_fmaf(x, y[v][u], d[j][u]) : d[j][u];
+            }
           }
         }
 #pragma unroll
@@ -2024,44 +2072,16 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
           brv[jj] = r;
         }
     };
-    // sparse candidates, one wave each: the products x*y and x*x are exact in f64 (f32 operands),
-    // so lanes form them in parallel; lane s then sums segment s in channel order, lane 0 the
-    // segments in order -- the restatement's arithmetic (exact_dist) bit for bit
+    // sparse candidates, one thread each (all of a batch's candidates at once): the restatement's
+    // arithmetic (exact_dist) bit for bit
     const int nc = min(ncand, CAND);
-    for (int k = w; k < nc; k += LIST_NT / 64) {
+    if (t < nb && fullb[t]) atomicAdd(stats + 1, 1);  // statistics: pixels scored in full
+    if (t == 0) atomicAdd(stats, nc);                  // and sparse candidates
+    for (int k = t; k < nc; k += LIST_NT) {
       const int j = cand[k] >> 16, r = cand[k] & 0xffff;
       if (fullb[j]) continue;
-      const float *yr = E.lib32 + (int64_t)r * E.CP;
-      double nyv = 0.0;
-      if (lane < nseg) nyv = E.ny[(int64_t)r * nseg + lane];
-      for (int c = lane; c < C; c += 64) {
-        const double xv = (double)xb[j][c], yy = (double)yr[c];
-        prw[w][c] = xv * yy;
-        sqw[w][c] = xv * xv;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (lane < nseg) {
-        double dd = 0.0, nx = 0.0;
-        for (int c = bd.b[lane]; c < bd.b[lane + 1]; ++c) {
-          dd += prw[w][c];
-          nx += sqw[w][c];
-        }
-        sdw[w][lane] = (nx == 0.0 && nyv == 0.0) ? 0.0
-                                                 : ((nx == 0.0 || nyv == 0.0) ? 1.0 : 1.0 - dd / sqrt(nx * nyv));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      if (lane == 0) {
-        double sum = 0.0;
-        for (int sg = 0; sg < nseg; ++sg) sum += sdw[w][sg];
-        take(j, r, sum / nseg);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      int nz = 0;
+      take(j, r, exact_dist(xb[j], E, r, C, bd, &nz));
     }
     for (int j = 0; j < nb; ++j)
       if (fullb[j])
@@ -2217,7 +2237,11 @@ int64_t hrf_classify_refx_bytes(int32_t C, const int32_t *bounds_host, int32_t n
   return el.off + el.total;
 }
 
-int64_t hrf_classify_refine_work_bytes(int64_t P) { return P < 0 ? -1 : 16 + 4 * (P > 0 ? P : 1); }
+// {listed count (16 B), the list (4 P B)}, then the table sweep's runner-up bounds (4 P B) for
+// hrf_classify_pixels_table_exact
+int64_t hrf_classify_refine_work_bytes(int64_t P) {
+  return P < 0 ? -1 : al256(16 + 4 * (P > 0 ? P : 1)) + 4 * (P > 0 ? P : 1);
+}
 
 }  // extern "C"
 
@@ -2353,7 +2377,7 @@ hrf_status refine_args(const PixSrc &S, int64_t P, int32_t C, const void *refx, 
   A->cnt = (int32_t *)work;
   A->list = (int32_t *)((char *)work + 16);
   A->bd = bd;
-  HRF_HIP(hipMemsetAsync(A->cnt, 0, sizeof(int32_t), s));
+  HRF_HIP(hipMemsetAsync(A->cnt, 0, 4 * sizeof(int32_t), s));  // count + the list pass's statistics
   return HRF_OK;
 }
 
@@ -2365,7 +2389,7 @@ hrf_status refine_list(const RefineArgs &A, int64_t P, int32_t C, int32_t R, con
   const ScreenEps ep = eps_of_screen(screen, bd, C, kp);
   const size_t shm = sizeof(float) * LIST_NP * (size_t)A.E.RT;
   const unsigned g = hrf::resident_grid(refine_list_kernel, LIST_NT, shm, hrf::cdiv(P, LIST_NP));
-  refine_list_kernel<<<g, LIST_NT, shm, s>>>(A.S, C, bd, A.E, A.hdr, R, ep.eps32, A.list, A.cnt, best_idx,
+  refine_list_kernel<<<g, LIST_NT, shm, s>>>(A.S, C, bd, A.E, A.hdr, R, ep.eps32, A.list, A.cnt, A.cnt + 1, best_idx,
                                              best_dist);
   HRF_LAUNCHED();
   return HRF_OK;
@@ -2528,25 +2552,34 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
   return HRF_OK;
 }
 
-hrf_status hrf_classify_pixels_table_exact(const void *table, const uint8_t *flags, const float *const *src_host,
-                                           const int32_t *channels_host, const int32_t *shifts_dev, int32_t nlaser,
-                                           int64_t H, int64_t W, int32_t apply_mask, const void *refx, int32_t R,
-                                           const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
-                                           float *best_dist, void *work, int64_t work_bytes, hrf_stream_t stream) {
+// the table sweep, exact: fused (the sweep certifies its own rows) or the sweep with its runner-up
+// bounds, then refine_best_kernel; both followed by the list pass
+static hrf_status table_exact(const void *table, const uint8_t *flags, const float *const *src_host,
+                              const int32_t *channels_host, const int32_t *shifts_dev, int32_t nlaser, int64_t H,
+                              int64_t W, int32_t apply_mask, const void *refx, int32_t R, const int32_t *bounds_host,
+                              int32_t nseg, int32_t *best_idx, float *best_dist, void *work, int64_t work_bytes,
+                              bool fused, hipStream_t s) {
   const int64_t P = H * W;
   int32_t C = 0;
   for (int q = 0; src_host && channels_host && q < nlaser && q < XLMAX; ++q) C += channels_host[q];
   Bounds bd;
-  if (hrf_status s = make_bounds(bounds_host, nseg, C, &bd)) return s;
+  if (hrf_status st = make_bounds(bounds_host, nseg, C, &bd)) return st;
   int32_t kp = 0, rpad = 0;
-  if (hrf_status s = hrf_classify_geometry(C, nseg, R, 2, &kp, &rpad)) return s;
+  if (hrf_status st = hrf_classify_geometry(C, nseg, R, 2, &kp, &rpad)) return st;
   const int lay = layout_id(bd, C);
   HRF_REQUIRE(lay != 0, "classify_pixels_table_exact: the E. coli or multispecies channel layout only");
   if (P == 0) return HRF_OK;
   HRF_REQUIRE(table && flags && refx && best_idx && best_dist, "classify_pixels_table_exact: null buffer");
-  hipStream_t s = (hipStream_t)stream;
   PixSrc S;
   if (hrf_status st = pixsrc_of(src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, C, &S)) return st;
+  if (!fused) {
+    HRF_REQUIRE(work && work_bytes >= hrf_classify_refine_work_bytes(P), "classify_pixels_table_exact: work buffer too small");
+    float *second = (float *)((char *)work + al256(16 + 4 * P));
+    if (hrf_status st = hrf_classify_pixels_table(table, flags, P, C, refx, R, bounds_host, nseg, best_idx, best_dist,
+                                                  second, s))
+      return st;
+    return refine(S, P, C, refx, R, bd, 3, second, best_idx, best_dist, work, work_bytes, s);
+  }
   RefineArgs A;
   if (hrf_status st = refine_args(S, P, C, refx, R, bd, 3, work, work_bytes, &A, s)) return st;
   const unsigned grid = (unsigned)hrf::cdiv(P, 256);
@@ -2565,6 +2598,26 @@ hrf_status hrf_classify_pixels_table_exact(const void *table, const uint8_t *fla
   if (st) return st;
   HRF_LAUNCHED();
   return refine_list(A, P, C, R, bd, 3, best_idx, best_dist, s);
+}
+
+hrf_status hrf_classify_pixels_table_exact(const void *table, const uint8_t *flags, const float *const *src_host,
+                                           const int32_t *channels_host, const int32_t *shifts_dev, int32_t nlaser,
+                                           int64_t H, int64_t W, int32_t apply_mask, const void *refx, int32_t R,
+                                           const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                           float *best_dist, void *work, int64_t work_bytes, hrf_stream_t stream) {
+  return table_exact(table, flags, src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, refx, R, bounds_host,
+                     nseg, best_idx, best_dist, work, work_bytes, false, (hipStream_t)stream);
+}
+
+hrf_status hrf_classify_pixels_table_exact_fused(const void *table, const uint8_t *flags,
+                                                 const float *const *src_host, const int32_t *channels_host,
+                                                 const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
+                                                 int32_t apply_mask, const void *refx, int32_t R,
+                                                 const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                                 float *best_dist, void *work, int64_t work_bytes,
+                                                 hrf_stream_t stream) {
+  return table_exact(table, flags, src_host, channels_host, shifts_dev, nlaser, H, W, apply_mask, refx, R, bounds_host,
+                     nseg, best_idx, best_dist, work, work_bytes, true, (hipStream_t)stream);
 }
 
 }  // extern "C"

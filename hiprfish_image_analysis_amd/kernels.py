@@ -881,7 +881,8 @@ class LaserSource:
 def classify_refine(source, refx, R, bounds, screen, idx, dist, second, want_listed=False):
     """hrf_classify_pixels_refine in place on a screen's (idx, dist, second).  source: StackSource
     or LaserSource.  screen: 0/1/2 = classify_pixels_screen mode, 3 = classify_pixels_table.
-    -> the number of pixels the certificate did not settle (want_listed; synchronises) or None"""
+    -> the number of pixels the certificate did not settle (want_listed; synchronises), with
+    want_listed="stats" also the list pass's sparse candidates and its pixels scored in full, or None"""
     import ctypes
     if isinstance(source, StackSource):
         st = source.stack
@@ -907,6 +908,8 @@ def classify_refine(source, refx, R, bounds, screen, idx, dist, second, want_lis
     _lib.call("hrf_classify_pixels_refine", ctypes.cast(ptrs, ctypes.c_void_p), ch.ctypes.data,
               _ptr(sd) if sd is not None else None, n, H, W, mask, _ptr(refx), R, b.ctypes.data, len(b) - 1,
               int(screen), _ptr(second), _ptr(idx), _ptr(dist), _ptr(work), wb, _stream())
+    if want_listed == "stats":  # (listed pixels, sparse candidates scored in f64, pixels scored in full)
+        return tuple(int(v) for v in work[:12].view(torch.int32).tolist())
     if want_listed:
         return int(work[:4].view(torch.int32).item())
     return None
@@ -991,15 +994,16 @@ def _source_args(source):
     raise ValueError("a StackSource or LaserSource is required")
 
 
-def classify_pixels_table(pt, refx, R, fused=True, want_listed=False):
+def classify_pixels_table(pt, refx, R, fused=False, composed=False, want_listed=False):
     """exact per-pixel classification from a PixTable, reading the pixels' values from the table's
-    source: fused (hrf_classify_pixels_table_exact: the sweep certifies its own rows, then the list
-    pass) or screen + hrf_classify_pixels_refine -- the same results bit for bit.
+    source: hrf_classify_pixels_table_exact (sweep, certificate pass, list pass), its _fused form
+    (the sweep certifies its own rows) or, composed, classify_pixels_table_screen + classify_refine
+    -- the same results bit for bit.
     -> (idx, dist), and the number of listed pixels with want_listed (synchronises)"""
     import ctypes
     if pt.source is None:
         raise ValueError("classify_pixels_table: the table has no source values for the exact refine")
-    if not fused:
+    if composed:
         idx, dist, sec = classify_pixels_table_screen(pt, refx, R)
         n = classify_refine(pt.source, refx, R, pt.bounds, 3, idx, dist, sec, want_listed=want_listed)
         return (idx, dist, n) if want_listed else (idx, dist)
@@ -1012,7 +1016,7 @@ def classify_pixels_table(pt, refx, R, fused=True, want_listed=False):
     dist = torch.empty(pt.shape, dtype=torch.float32, device=pt.table.device)
     wb = int(_lib.lib().hrf_classify_refine_work_bytes(pt.P))
     work = torch.empty(wb, dtype=torch.uint8, device=idx.device)
-    _lib.call("hrf_classify_pixels_table_exact", _ptr(pt.table), _ptr(pt.flags), ctypes.cast(ptrs, ctypes.c_void_p),
+    _lib.call("hrf_classify_pixels_table_exact_fused" if fused else "hrf_classify_pixels_table_exact", _ptr(pt.table), _ptr(pt.flags), ctypes.cast(ptrs, ctypes.c_void_p),
               ch.ctypes.data, _ptr(sd) if sd is not None else None, n, H, W, mask, _ptr(refx), R, b.ctypes.data,
               len(b) - 1, _ptr(idx), _ptr(dist), _ptr(work), wb, _stream())
     if want_listed:

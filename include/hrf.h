@@ -489,9 +489,11 @@ HRF_API hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *f
                                              const void *refx, int32_t R, const int32_t *bounds_host, int32_t nseg,
                                              int32_t *best_idx, float *best_dist, float *second,
                                              hrf_stream_t stream);
-/* hrf_classify_pixels_table + hrf_classify_pixels_refine (screen 3) in two launches: the table sweep
- * certifies its own rows (the f64 refine fused into the sweep's workgroups), then the list pass.
- * Pixel source and work as hrf_classify_pixels_refine; exact results, the same bit for bit. */
+/* hrf_classify_pixels_table + hrf_classify_pixels_refine (screen 3): the table sweep with its
+ * runner-up bounds (held in `work`), the certificate pass, the list pass.  Pixel source and work as
+ * hrf_classify_pixels_refine; exact results.  _fused: the sweep certifies its own rows (the f64
+ * refine in the sweep's workgroups), then the list pass -- the same results bit for bit (slower
+ * beside concurrent tiles: DESIGN.md). */
 HRF_API hrf_status hrf_classify_pixels_table_exact(const void *table, const uint8_t *flags,
                                                    const float *const *src_host, const int32_t *channels_host,
                                                    const int32_t *shifts_dev, int32_t nlaser, int64_t H, int64_t W,
@@ -499,6 +501,13 @@ HRF_API hrf_status hrf_classify_pixels_table_exact(const void *table, const uint
                                                    const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
                                                    float *best_dist, void *work, int64_t work_bytes,
                                                    hrf_stream_t stream);
+HRF_API hrf_status hrf_classify_pixels_table_exact_fused(const void *table, const uint8_t *flags,
+                                                         const float *const *src_host, const int32_t *channels_host,
+                                                         const int32_t *shifts_dev, int32_t nlaser, int64_t H,
+                                                         int64_t W, int32_t apply_mask, const void *refx, int32_t R,
+                                                         const int32_t *bounds_host, int32_t nseg, int32_t *best_idx,
+                                                         float *best_dist, void *work, int64_t work_bytes,
+                                                         hrf_stream_t stream);
 /* one v_mfma_f32_16x16x32_f16 (shape 0: A 16x32, B 32x16, C/D 16x16 per tile) or
  * v_mfma_f32_32x32x16_f16 (shape 1: A 32x16, B 16x32, C/D 32x32) per tile, all row-major (A, B
  * fp16; C, D f32): pins the accumulation model the per-pixel screen's error bound assumes */

@@ -234,8 +234,9 @@ def test_special_pixels_exact(K, S, orc, mode):
 
 def test_refine_from_lasers_equals_stack(K, S, orc):
     """a registered tile's table refined from the five shifted acquisitions (LaserSource, the
-    bench path), fused into the sweep and as a separate kernel, = the registered stack refined as a
-    plain stack = the restatement, with the coverage mask and a ragged width"""
+    bench path) -- sweep + certificate pass, the certificate fused into the sweep, and the Python
+    composition of screen + refine -- = the registered stack refined as a plain stack = the
+    restatement, with the coverage mask and a ragged width"""
     from hiprfish_image_analysis_amd import pipeline as P
     from test_kernels_gpu import check_pixel_argmin
     for H, W in ((128, 192), (96, 80)):
@@ -245,10 +246,11 @@ def test_refine_from_lasers_equals_stack(K, S, orc):
         reg, _ = K.register_assemble(lasers, shifts, True, cn_mode=1)
         cn, pt, _ = K.register_assemble_pixtable(lasers, shifts, True)
         refx = K.classify_prepare(torch.from_numpy(ref).cuda(), ECOLI, mode=2)
-        a = K.classify_pixels_table(pt, refx, ref.shape[0])                 # the refine fused into the sweep
-        u = K.classify_pixels_table(pt, refx, ref.shape[0], fused=False)    # screen, then the refine kernel
+        a = K.classify_pixels_table(pt, refx, ref.shape[0])                 # sweep, then the certificate kernel
+        f = K.classify_pixels_table(pt, refx, ref.shape[0], fused=True)     # the certificate in the sweep
+        u = K.classify_pixels_table(pt, refx, ref.shape[0], composed=True)  # screen + classify_refine
         b = K.classify_pixels(reg, refx, ref.shape[0], ECOLI, mode=2)
-        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
-        assert torch.equal(u[0], b[0]) and torch.equal(u[1], b[1])
+        for v in (a, f, u):
+            assert torch.equal(v[0], b[0]) and torch.equal(v[1], b[1])
         x = host(reg).reshape(H * W, -1).astype(np.float64)
         check_pixel_argmin(orc, host(a[0]).ravel(), host(a[1]).ravel(), x, ref.astype(np.float64), ECOLI)

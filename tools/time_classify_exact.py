@@ -47,15 +47,21 @@ def main():
     i2.copy_(idx)
     d2.copy_(dist)
     listed = K.classify_refine(pt.source, refx, R, S.ECOLI_BOUNDS, 3, i2, d2, sec, want_listed=True)
-    t_unf = ev(lambda: K.classify_pixels_table(pt, refx, R, fused=False), n)
-    t_full = ev(lambda: K.classify_pixels_table(pt, refx, R), n)
-    fi, fd, flisted = K.classify_pixels_table(pt, refx, R, want_listed=True)
-    assert torch.equal(fi, i2) and torch.equal(fd, d2) and flisted == listed, "fused != unfused"
+    t_unf = ev(lambda: K.classify_pixels_table(pt, refx, R), n)
+    t_full = ev(lambda: K.classify_pixels_table(pt, refx, R, fused=True), n)
+    for fu in (False, True):
+        fi, fd, flisted = K.classify_pixels_table(pt, refx, R, fused=fu, want_listed=True)
+        assert torch.equal(fi, i2) and torch.equal(fd, d2) and flisted == listed, "exact paths differ"
     Pn = 2048 * 2048
     changed = int((i2 != idx).sum().item())
     print("w16t screen %.3f ms | refine %.3f ms | exact unfused %.3f ms | exact fused %.3f ms | listed %d of %d "
           "pixels (%.3f %%) | screen row changed on %d pixels" % (t_screen, t_ref, t_unf, t_full, listed, Pn,
                                                                   100.0 * listed / Pn, changed))
+    i2.copy_(idx)
+    d2.copy_(dist)
+    st = K.classify_refine(pt.source, refx, R, S.ECOLI_BOUNDS, 3, i2, d2, sec, want_listed="stats")
+    print("list pass: %d pixels, %d sparse f64 candidates (%.1f per pixel), %d pixels scored in full"
+          % (st[0], st[1], st[1] / max(st[0], 1), st[2]))
     eps = K.classify_screen_eps(95, S.ECOLI_BOUNDS, R, 3)
     print("bounds (score units): screen %.3e, per zero segment %.3e, list pass %.3e" % eps)
 
