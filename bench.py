@@ -332,18 +332,23 @@ def _hbm_kernels(lasers, cal, lib):
     return out
 
 
-def _watershed_ties(dev, sizes=(512, 1024)):
+def _watershed_ties(dev, sizes=(512, 1024, 2048)):
     """The watershed's tie path on adversarial n x n images: a plateau-heavy integer image (4
     levels in 4x4 blocks, multi-pixel markers with distinct values per label, 10 % of pixels outside
     the mask) forces contests that the resolver decides exactly; at 1024^2 the 1e-3 label offsets
     overlap the integer levels, so some decisions come down to equal-valued markers of different
     labels and the tile is flooded again by skimage's binary heap on the device (the heap replay,
     watershed.hip); the same markers on a continuous image have none.  Mean time of
-    hrf_watershed_ex (HIP events) and the tie statistics of each.  (The bench tiles -- continuous,
-    k/4095, k/255 -- have at most a contest or two; see the quantised lines.)"""
+    hrf_watershed_ex (HIP events; the 2048^2 replay timed once, without the untimed call) and the
+    tie statistics of each.  (The bench tiles -- continuous, k/4095, k/255 -- have at most a contest
+    or two; see the quantised lines.)  `tile_chain`: a 2048^2 synthetic.tie_tile through the native
+    tile (hrf_tile_ecoli: registration, segmentation with the heap replay, cells, per-pixel) against
+    the same tile with an even corridor (no equal-marker decision)."""
     import torch
 
     from hiprfish_image_analysis_amd import kernels as K
+    from hiprfish_image_analysis_amd import pipeline as P
+    from hiprfish_image_analysis_amd import synthetic as S
     out = {}
     for n in sizes:
         rng = np.random.default_rng(7)
@@ -359,11 +364,32 @@ def _watershed_ties(dev, sizes=(512, 1024)):
         for name, img in (("plateaus", f), ("continuous", f + rng.random((n, n)))):
             x = torch.from_numpy(img).to(dev)
             ties = []
-            K.watershed(x, mk, mm, ties=ties)
-            ms = _event_ms(lambda: K.watershed(x, mk, mm), 3 if n <= 512 else 1)
+            if n >= 2048:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                a.record()
+                K.watershed(x, mk, mm, ties=ties)
+                b.record()
+                torch.cuda.synchronize()
+                ms = a.elapsed_time(b)
+            else:
+                K.watershed(x, mk, mm, ties=ties)
+                ms = _event_ms(lambda: K.watershed(x, mk, mm), 3 if n <= 512 else 1)
             rec[name] = {"ms": round(ms, 3), "contested_px": int(ties[0]), "resolution_rounds": int(ties[1]),
                          "equal_marker_decisions": int(ties[2]), "heap_replay": bool(ties[2] > 0)}
         out["n%d" % n] = rec
+    lib = P.Library(torch.from_numpy(S.reference_library(10, S.ECOLI_BOUNDS).astype(np.float64)).to(dev),
+                    S.ECOLI_BOUNDS, 10)
+    rec = {"size": [2048, 2048]}
+    for name, gap in (("odd_corridors", 1), ("even_corridors", 2)):
+        lasers = S.laser_split(S.tie_tile(2048, 2048, gap=gap, device=dev))
+        P.process_tile_native(lasers, lib)
+        torch.cuda.synchronize()
+        st = K.tile_stats(dev, 2048, 2048)
+        ms = _event_ms(lambda: P.process_tile_native(lasers, lib), 1)
+        rec[name] = {"ms": round(ms, 3), "contested_px": st["contests"], "equal_marker_decisions": st["marker_ties"],
+                     "heap_replay": bool(st["marker_ties"] > 0)}
+    out["tile_chain"] = rec
     return out
 
 

@@ -129,6 +129,31 @@ def tile(H: int = 2048, W: int = 2048, nbit: int = 10, bounds=ECOLI_BOUNDS, seed
     return stack, truth, lay, ref
 
 
+def tie_tile(H: int = 256, W: int = 256, gap: int = 1, cell: int = 14, bright: float = 1.0, mid: float = 0.3,
+             device="cuda"):
+    """A registered (H, W, 95) stack whose E. coli watershed (ecoli measurement.py:113) makes
+    decisions between equal-valued markers of different labels: pairs of equal, uniform cells
+    (cell x cell, brightness `bright`, one spectrum) `gap` pixels apart inside a uniform halo of
+    brightness `mid` (the rough mask, not the interior), so the seeds are whole cells of one value
+    and the corridor pixels between a pair are reached in the same FIFO layer from both -- which
+    cell's label they take is the heap layout's (skimage pops equal-valued age-0 markers in
+    whatever order its binary heap holds them).  An odd gap makes such decisions."""
+    import torch
+    img = np.zeros((H, W), np.float64)
+    y0 = 20
+    while y0 + cell + 3 < H - 10:
+        x0 = 20
+        while x0 + 2 * cell + gap + 3 < W - 10:
+            img[y0 - 3:y0 + cell + 3, x0 - 3:x0 + 2 * cell + gap + 3] = mid
+            img[y0:y0 + cell, x0:x0 + cell] = bright
+            img[y0:y0 + cell, x0 + cell + gap:x0 + 2 * cell + gap] = bright
+            x0 += 2 * cell + gap + 20
+        y0 += cell + 26
+    spec = np.linspace(0.5, 1.5, 95)
+    st = (img[:, :, None] * spec[None, None, :]).astype(np.float32)
+    return torch.from_numpy(st).to(device).contiguous()
+
+
 # the misregistration applied to each laser's channels by laser_split (E. coli lasers
 # 405/488/514/561/633, ecoli measurement.py:45-70 estimates and undoes it)
 LASER_SHIFTS = ((0, 0), (2, -1), (0, 3), (-1, 0), (1, 1))

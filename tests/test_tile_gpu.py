@@ -268,3 +268,34 @@ def test_pixel_table_needs_mode2_table(mods):
     got = P.process_tile_native(lasers, lib1, variant=1)
     torch.cuda.synchronize()
     _check(got, want)
+
+
+def test_tile_native_equal_marker_ties(mods, orc):
+    """ecoli measurement.py:113 inside the native tile chain (hrf_tile_ecoli) on a tile whose
+    watershed decisions come down to equal-valued markers of different labels (synthetic.tie_tile):
+    the chain floods the tile again with the heap replay and its label map, cells and barcodes
+    equal oracle/pipeline.py's (skimage's heap restated) on the registered lasers -- where the
+    order model alone (raw) would label corridor pixels differently"""
+    import pipeline as OP
+    K, P, S = mods
+    H = W = 256
+    stack = S.tie_tile(H, W, gap=1)
+    lasers = S.laser_split(stack)
+    lib = _lib(P, S)
+    nat = P.process_tile_native(lasers, lib, variant=1)
+    torch.cuda.synchronize()
+    st = K.tile_stats(stack.device, H, W)
+    assert st["marker_ties"] > 0 and st["contests"] > 0, st
+    lh = [l.cpu().numpy() for l in lasers]
+    reg = OP.register_stacks(lh, OP.estimate_shifts(lh), True)
+    ref = lib.spectra.cpu().numpy()
+    keep = {}
+    OP.segment_ecoli(reg, keep=keep)
+    raw, rs = orc.watershed_ordered(-keep["image_cn"], keep["seeds"], keep["rough_mask"], raw=True)
+    assert rs[2] > 0 and (raw != keep["watershed"]).any()   # the layout decides some pixels
+    o = OP.process_tile(reg, ref, S.ECOLI_BOUNDS, variant=1)
+    assert np.array_equal(nat.meas.segmentation.cpu().numpy(), o["segmentation"])
+    assert nat.ncells == len(o["cell_idx"]) and nat.ncells >= 16
+    assert np.array_equal(nat.cell_idx.cpu().numpy()[:nat.ncells], o["cell_idx"])
+    comp = P.process_tile(P.register_tile(lasers), lib, per_pixel=True, variant=1)
+    _check(nat, comp)
