@@ -1911,6 +1911,9 @@ __global__ __launch_bounds__(64, HRF_REFINE_WPE) void refine_best_kernel(RefineA
 //  3. those rows (every row for a pixel with non-finite values or norms out of the f32 pass's
 //     range) rescored exactly (exact_dist), minimum with the lowest row on ties, as
 //     oracle_classify's first-minimum loop.
+#ifndef HRF_LIST_LV
+#define HRF_LIST_LV 4  // list pass: channels whose library loads are in flight together
+#endif
 constexpr int LIST_NP = 8;     // pixels per batch (stage 1 maps 32 threads per pixel)
 constexpr int LIST_NT = 256;   // threads per workgroup
 constexpr int LIST_RMAX = 4096;
@@ -1983,7 +1986,7 @@ __global__ __launch_bounds__(LIST_NT) void refine_list_kernel(PixSrc S, int32_t 
           for (int u = 0; u < 4; ++u) d[j][u] = 0.0f;
         // LV channels' loads in flight together (clamped addresses, no branch around a load; rows
         // past RT are never stored), then their fmaf chains in channel order
-        constexpr int LV = 4;
+        constexpr int LV = HRF_LIST_LV;
         const int ce = bd.b[sg + 1];
         for (int i0 = bd.b[sg]; i0 < ce; i0 += LV) {
           float y[LV][4];
