@@ -784,10 +784,15 @@ def main():
             "refine": {"ms": round(ms_exact - ms_iso, 4), "exact_ms": round(ms_exact, 4),
                        "listed_pixels": listed, "listed_frac": round(listed / (H * W), 6),
                        "eps_score": K.classify_screen_eps(C, bounds, lib.R, 3 if REGTILE else mode)[0],
+                       "pixel_value_bytes": 4 * C * H * W,
+                       "achieved_gbs": round(4 * C * H * W / ((ms_exact - ms_iso) * 1e-3) / 1e9, 1),
                        "note": "the f64 refine after the screen (hrf_classify_pixels_refine): b1 rescored from the "
-                               "pixel's f32 values, certified against the screen's proven bound eps_score; "
-                               "listed pixels scored in full (f32 pass + f64 on the survivors).  exact_ms = "
-                               "screen + refine, isolated, HIP events, mean of 5"},
+                               "pixel's f32 values (re-read: pixel_value_bytes per tile, achieved_gbs over the "
+                               "refine's time incl. the list pass), certified against the screen's proven bound "
+                               "eps_score; listed pixels scored in full (f32 pass + f64 on the survivors).  "
+                               "exact_ms = screen + refine, isolated, HIP events, mean of 5.  In the timed "
+                               "region the exact answer costs ~0.6 ms per tile (DESIGN.md: 977 Mpix/s with the "
+                               "screen's answers in an A/B build vs 846-853 exact)"},
             "aggregate": {"achieved": round(agg, 2), "frac": round(agg / peak, 4),
                           "note": "classifier flops of the %d tiles per step / the step time (ms_per_step): the "
                                   "classifier's share of the whole-job rate, per GPU" % T},
