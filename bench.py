@@ -48,8 +48,8 @@ F16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak 
 F64_VALU_PEAK_TOPS = 39.3      # AMD MI355X spec FP64 vector 78.6 TFLOP/s = 39.3 T f64 VALU lane-ops/s
 # the timed path classifies from the registered tile's pixel table (pipeline.register_tile)
 KERNEL_NAME = {0: "classify_pixels_kernel<50>", 1: "classify_pixels_f16_kernel<7>",
-               2: "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 2>",
-               "t": "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 2>"}
+               2: "classify_pixels_w16_kernel<LayEcoli, 4, 2, 64, 3, 3>",
+               "t": "classify_pixels_w16t_kernel<LayEcoli, 4, 2, 64, 3, false, 3>"}
 REGTILE = os.environ.get("HRF_REGTILE", "1") != "0"   # A/B switch: 0 = register_stack + in-kernel operand build
 # one native call per tile (hrf_tile_ecoli: registration, both classifications, segmentation,
 # spectra, counts, identification map); HRF_TILE_NATIVE=0: the composed path (register_tile +

@@ -45,6 +45,18 @@ constexpr int RCH = 64;  // references per LDS chunk (prefetched into registers)
 #ifndef HRF_W16T_OCC
 #define HRF_W16T_OCC 2
 #endif
+// the table screen (hrf_classify_pixels_table): 16-pixel groups per wave and workgroups per CU
+// The screens (hrf_classify_pixels_screen mode 2, hrf_classify_pixels_table): three 16-pixel groups
+// per wave (72 B-operand VGPRs instead of 96) fit three workgroups per CU with the runner-up keys
+// (165 VGPRs, no spills): 1.76-1.78 ms alone against 1.75 at four groups and two per CU, but
+// 866 vs 842 Mpix/s in the bench (three interleaved pairs, profiles/r6_screen_ng3_ab.txt).  The
+// fused certificate keeps four groups (64 pixels per wave) at two per CU.
+#ifndef HRF_W16T_NG
+#define HRF_W16T_NG 3
+#endif
+#ifndef HRF_W16T_SCREEN_OCC
+#define HRF_W16T_SCREEN_OCC 3
+#endif
 
 // ==== exact per-pixel classification: the f64 refine of the screen (round 6) ==================
 // The MFMA sweeps above are a SCREEN: split-fp16 (or f32-MFMA) scores within a bound of the exact
@@ -612,8 +624,8 @@ __global__ void ref_prep_f16_kernel(const float *__restrict__ ref, int32_t R, in
 // once per tile instead of once per element.
 constexpr int LDV = 16;
 __device__ __forceinline__ void load_group(const float *__restrict__ stack, int64_t P, int32_t C, int64_t p0, int lane,
-                                           float4 (&v)[LDV]) {
-  const int64_t np = std::max<int64_t>(0, std::min<int64_t>(32, P - p0));
+                                           float4 (&v)[LDV], int npmax = 32) {
+  const int64_t np = std::max<int64_t>(0, std::min<int64_t>(npmax, P - p0));
   const int64_t nel = np * C;  // valid floats of this group
   const float *src = stack + p0 * C;
   const int nv = 8 * C;
@@ -1278,10 +1290,11 @@ __device__ __forceinline__ void split_b_w16(const float *stg, int lane, int g, h
   }
 }
 
-template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF, int CR, bool PIPE>
+template <int KT, int ROWB, int NW, int NSEG, bool ZS, bool KEYED, int NBUF, int CR, bool PIPE, int NG = 4>
 __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *ldsb, int nch, int lane, int w,
-                                          const h8 (&bh)[4][KT], const h8 (&bl)[4][KT], const uint32_t zxp,
-                                          float (&best)[4], int (&bi)[4], float (&sec)[4]) {
+                                          const h8 (&bh)[NG][KT], const h8 (&bl)[NG][KT], const uint32_t zxp,
+                                          float (&best)[NG], int (&bi)[NG], float (&sec)[NG]) {
+  static_assert(NG >= 1 && NG <= 4, "16-pixel groups per wave: 8 bits of zxp / bic each");
   constexpr int KP = 32 * KT;
   constexpr int CHB = CR * ROWB;
   constexpr int NPC = (CHB + 1023) / 1024;  // 1 KiB LDS-DMA pieces per chunk (the last may be partial)
@@ -1300,9 +1313,9 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
   constexpr int MINE_LO = NPC / NW;
   issue(0);
   if (NBUF >= 3 && nch > 1) issue(1);
-  f32x4 pv[4];
+  f32x4 pv[NG];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+  for (int g = 0; g < NG; ++g)
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[g][i] = -__builtin_inff();
   int pr = 0;  // first row of the pending block
@@ -1319,10 +1332,10 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
   // keyed: key = the running best (replaced by a chunk's best only on a strictly greater score),
   // t1 / t2 = the largest and second-largest keys seen (t1 also serves as the chunk's best: a key
   // from an earlier chunk that was not adopted has key's score)
-  int key[4], t1[4], t2[4];
+  int key[NG], t1[NG], t2[NG];
   uint32_t bic = 0;  // keyed: the chunk of each group's key, 8 bits per group
 #pragma unroll
-  for (int g = 0; g < 4; ++g) key[g] = t1[g] = t2[g] = INT32_MIN;
+  for (int g = 0; g < NG; ++g) key[g] = t1[g] = t2[g] = INT32_MIN;
   // fold the pending block into the chunk keys, groups [g0, g1); after the chunk's last block,
   // the chunk key against the running best (strictly greater score, the position code left out:
   // earlier chunks win ties, so equal scores keep the lowest row across the whole library)
@@ -1355,10 +1368,10 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
           }
       }
     }
-    if (KEYED && g1 == 4 && pb == NB - 1) {
+    if (KEYED && g1 == NG && pb == NB - 1) {
       const uint32_t cc = (uint32_t)(pr / CR);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < NG; ++g) {
         if ((t1[g] >> 4) > (key[g] >> 4)) {  // t1 is then this chunk's
           key[g] = t1[g];
           bic = (bic & ~(0xffu << (8 * g))) | (cc << (8 * g));
@@ -1375,9 +1388,9 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
     const char *buf = ldsb + (c % NBUF) * CHB;
 #pragma unroll
     for (int rb = 0; rb < CR; rb += 16) {
-      f32x4 acc[4];
+      f32x4 acc[NG];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int g = 0; g < NG; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
       const char *row = buf + (rb + rl) * ROWB + 16 * Q;
       h8 az;
       if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + rl) * ROWB + 4 * KP);
@@ -1389,31 +1402,31 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
         const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
         const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 64 * t);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
+        for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl[g][t], acc[g], 0, 0, 0);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
-        if (PIPE) epi((4 * t) / KT, (4 * (t + 1)) / KT);  // previous block, slice t
+        for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh[g][t], acc[g], 0, 0, 0);
+        if (PIPE) epi((NG * t) / KT, (NG * (t + 1)) / KT);  // previous block, slice t
       }
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
         const h8 ah = *reinterpret_cast<const h8 *>(row + 64 * t);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
+        for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh[g][t], acc[g], 0, 0, 0);
       }
       if (ZS) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz_of(g), acc[g], 0, 0, 0);
+        for (int g = 0; g < NG; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(az, bz_of(g), acc[g], 0, 0, 0);
       }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) pv[g] = acc[g];
+      for (int g = 0; g < NG; ++g) pv[g] = acc[g];
       pr = c * CR + rb;
-      if (!PIPE) epi(0, 4);  // this block at once (the other waves on the SIMD cover the MFMA latency)
+      if (!PIPE) epi(0, NG);  // this block at once (the other waves on the SIMD cover the MFMA latency)
     }
   }
-  if (PIPE) epi(0, 4);  // the last block (the end of the last chunk: finalises its key)
+  if (PIPE) epi(0, NG);  // the last block (the end of the last chunk: finalises its key)
   if (KEYED) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
       const int code = 15 - (key[g] & 15);
       bi[g] = CR * (int)((bic >> (8 * g)) & 0xffu) + 16 * (code >> 2) + (code & 3);
       best[g] = __int_as_float(key[g] & -16);
@@ -1422,7 +1435,7 @@ __device__ __forceinline__ void sweep_w16(const char *__restrict__ gref, char *l
   }
 }
 
-template <class L, int NW, int NBUF, int CR, int OCC>
+template <class L, int NW, int NBUF, int CR, int OCC, int NG = 4>
 __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const float *__restrict__ stack,
                                                                      int64_t P, const _Float16 *__restrict__ refh,
                                                                      int32_t R, int32_t Rpad,
@@ -1434,20 +1447,22 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
   constexpr int ROWB = 4 * KP + L::PADB;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
-  h8 bh[4][KT], bl[4][KT];
-  uint32_t zxp = 0, ng = 0;  // all-zero segments of the four 16-pixel groups, 8 bits each
+  static_assert(NG == 3 || NG == 4, "a wave holds 3 or 4 16-pixel groups");
+  const int64_t pbase = (int64_t)blockIdx.x * (16 * NG * NW) + w * (16 * NG);
+  h8 bh[NG][KT], bl[NG][KT];
+  uint32_t zxp = 0, ng = 0;  // all-zero segments of the NG 16-pixel groups, 8 bits each
   float *stg = lds + w * (32 * L::C);  // staging aliases the chunk buffers (before the first DMA)
   {
     // both halves' loads in flight at once where the registers allow (two waves per SIMD);
     // at three, the second half is loaded after the first is staged
     constexpr int NV = OCC < 3 ? 2 : 1;
     float4 v[NV][LDV];
+    // (NG = 3: the second half is one 16-pixel group; the rest of its staging reads as zero)
     load_group(stack, P, L::C, pbase, lane, v[0]);
-    if (NV == 2) load_group(stack, P, L::C, pbase + 32, lane, v[NV - 1]);
+    if (NV == 2) load_group(stack, P, L::C, pbase + 32, lane, v[NV - 1], 16 * (NG - 2));
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
-      if (NV == 1 && half == 1) load_group(stack, P, L::C, pbase + 32, lane, v[0]);
+      if (NV == 1 && half == 1) load_group(stack, P, L::C, pbase + 32, lane, v[0], 16 * (NG - 2));
 #pragma unroll
       for (int i = 0; i < LDV; ++i) {
         const int e4 = lane + 64 * i;
@@ -1459,17 +1474,17 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
       ng |= ngp;
       __syncthreads();
       split_b_w16<L, KT>(stg, lane, 0, bh[2 * half], bl[2 * half]);
-      split_b_w16<L, KT>(stg, lane, 1, bh[2 * half + 1], bl[2 * half + 1]);
-      zxp |= ((uint32_t)__shfl(zxh, lane & 15, 64) << (16 * half)) |
-             ((uint32_t)__shfl(zxh, 16 + (lane & 15), 64) << (16 * half + 8));
+      if (2 * half + 1 < NG) split_b_w16<L, KT>(stg, lane, 1, bh[(2 * half + 1) % NG], bl[(2 * half + 1) % NG]);
+      zxp |= (uint32_t)__shfl(zxh, lane & 15, 64) << (16 * half);
+      if (2 * half + 1 < NG) zxp |= (uint32_t)__shfl(zxh, 16 + (lane & 15), 64) << (16 * half + 8);
       __syncthreads();
     }
   }
   const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
-  float best[4], sec[4];
-  int bi[4];
+  float best[NG], sec[NG];
+  int bi[NG];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < NG; ++g) {
     best[g] = sec[g] = -__builtin_inff();
     bi[g] = 0;
   }
@@ -1479,7 +1494,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
   const bool zs = __syncthreads_or(zxp != 0);
   const bool keyed = !libneg && !__syncthreads_or(ng != 0);
 #define HRF_SWEEPW(Z, K) \
-  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3), NG>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
   if (keyed) {
     if (zs) HRF_SWEEPW(true, true);
     else HRF_SWEEPW(false, true);
@@ -1490,7 +1505,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16_kernel(const
 #undef HRF_SWEEPW
   const int Q = lane >> 4;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < NG; ++g) {
     float b = best[g], sc = sec[g];
     int idx = bi[g] + 4 * Q;
 #pragma unroll
@@ -1533,7 +1548,7 @@ __global__ __launch_bounds__(256) void pixtable_prep_kernel(const float *__restr
 // FUSE (round 6): the f64 refine follows the sweep in the same workgroup (refine_pixels on the
 // freed chunk buffers, each wave its four 16-pixel groups), so its loads and f64 work overlap the
 // other resident workgroup's MFMA sweep, and the screen's rows and bounds never leave registers.
-template <class L, int NW, int NBUF, int CR, int OCC, bool FUSE>
+template <class L, int NW, int NBUF, int CR, int OCC, bool FUSE, int NG = 4>
 __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(const uint4 *__restrict__ table,
                                                                       const uint8_t *__restrict__ flags, int64_t P,
                                                                       const _Float16 *__restrict__ refh, int32_t R,
@@ -1545,16 +1560,19 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   constexpr int ROWB = 4 * KP + L::PADB;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t pbase = (int64_t)blockIdx.x * (64 * NW) + w * 64;
-  h8 bh[4][KT], bl[4][KT];
-  uint32_t zxp = 0, ng = 0;  // all-zero segments of the four 16-pixel groups, 8 bits each
+  static_assert(!FUSE || NG == 4, "the fused refine takes 64 pixels per wave");
+  const int64_t pbase = (int64_t)blockIdx.x * (16 * NG * NW) + w * (16 * NG);
+  h8 bh[NG][KT], bl[NG][KT];
+  uint32_t zxp = 0, ng = 0;  // all-zero segments of the NG 16-pixel groups, 8 bits each
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < NG; ++g) {
     const int64_t g16 = pbase / 16 + g;
     const uint4 *e = table + g16 * (int64_t)(KT * 128) + lane;
+    // (NG < 4: the table holds whole 256-pixel blocks, a 16 NG NW-pixel workgroup can pass them)
+    const bool gv = NG == 4 || 16 * g16 < P;
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
-      const uint4 hv = e[t * 128], lv = e[t * 128 + 64];
+      const uint4 hv = gv ? e[t * 128] : uint4{0, 0, 0, 0}, lv = gv ? e[t * 128 + 64] : uint4{0, 0, 0, 0};
       bh[g][t] = *reinterpret_cast<const h8 *>(&hv);
       bl[g][t] = *reinterpret_cast<const h8 *>(&lv);
     }
@@ -1564,10 +1582,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     ng |= f >> 7;
   }
   const uint32_t libneg = *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(refh) + 4 * KP + 12);
-  float best[4], sec[4];
-  int bi[4];
+  float best[NG], sec[NG];
+  int bi[NG];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < NG; ++g) {
     best[g] = sec[g] = -__builtin_inff();
     bi[g] = 0;
   }
@@ -1577,7 +1595,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   const bool zs = __syncthreads_or(zxp != 0);
   const bool keyed = !libneg && !__syncthreads_or(ng != 0);
 #define HRF_SWEEPW(Z, K) \
-  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3)>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
+  sweep_w16<KT, ROWB, NW, L::NSEG, Z, K, NBUF, CR, (OCC < 3), NG>(gref, ldsb, nch, lane, w, bh, bl, zxp, best, bi, sec)
   if (keyed) {
     if (zs) HRF_SWEEPW(true, true);
     else HRF_SWEEPW(false, true);
@@ -1587,10 +1605,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
   }
 #undef HRF_SWEEPW
   const int Q = lane >> 4;
-  int b1g[4];
-  float s2g[4];
+  int b1g[NG];
+  float s2g[NG];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
+  for (int g = 0; g < NG; ++g) {
     float b = best[g], sc = sec[g];
     int idx = bi[g] + 4 * Q;
 #pragma unroll
@@ -1617,8 +1635,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void classify_pixels_w16t_kernel(cons
     constexpr int64_t SL = (refine_slice_bytes() + 15) / 16 * 16;
     char *slice = ldsb + w * SL;
     // lane l holds pixel pbase + l's merged result in quarter Q = l >> 4's slot
-    const int b1 = Q == 0 ? b1g[0] : Q == 1 ? b1g[1] : Q == 2 ? b1g[2] : b1g[3];
-    const float s2 = Q == 0 ? s2g[0] : Q == 1 ? s2g[1] : Q == 2 ? s2g[2] : s2g[3];
+    const int b1 = Q == 0 ? b1g[0] : Q == 1 ? b1g[1 % NG] : Q == 2 ? b1g[2 % NG] : b1g[3 % NG];
+    const float s2 = Q == 0 ? s2g[0] : Q == 1 ? s2g[1 % NG] : Q == 2 ? s2g[2 % NG] : s2g[3 % NG];
     refine_pixels64<HRF_REFINE_G>(A, L::C, A.bd, pbase, P, b1, s2, slice, best_idx, best_dist, true);
   }
 }
@@ -1864,15 +1882,15 @@ int choose_ks(int K) {
   return -1;
 }
 
-template <class L, int NW, int NB, int CR, int OCC>
+template <class L, int NW, int NB, int CR, int OCC, int NG>
 hrf_status launch_w16_lay(const float *stack, int64_t P, const void *refx, int32_t R, int32_t rpad, int32_t *best_idx,
                           float *best_dist, float *second, hipStream_t s) {
   constexpr int KT = (L::C + 1 + 31) / 32;
   const size_t shm = std::max<size_t>((size_t)NB * CR * (128 * KT + L::PADB), sizeof(float) * NW * 32 * L::C);
   HRF_REQUIRE(shm * OCC <= 160 * 1024 + 1024, "classify: w16 configuration exceeds the LDS");
-  (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC>,
+  (void)hipFuncSetAttribute((const void *)classify_pixels_w16_kernel<L, NW, NB, CR, OCC, NG>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-  classify_pixels_w16_kernel<L, NW, NB, CR, OCC><<<(unsigned)hrf::cdiv(P, 64 * NW), 64 * NW, shm, s>>>(
+  classify_pixels_w16_kernel<L, NW, NB, CR, OCC, NG><<<(unsigned)hrf::cdiv(P, 16 * NG * NW), 64 * NW, shm, s>>>(
       stack, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, second);
   return HRF_OK;
 }
@@ -2266,7 +2284,7 @@ hrf_status screen_stack(const float *stack, int64_t P, int32_t C, const void *re
       // (classify_pixels_w16_kernel) -- 4 waves, 2 buffers of 64 rows, HRF_W16T_OCC workgroups per
       // CU (rounds 3-5: three, 1.76 vs 1.83 ms for round 2's lay16 form, 2.13-2.20 for the 32x32x16
       // form, on a 2048^2 tile at R = 1023; DESIGN.md "Per-pixel classifier")
-      if (hrf_status st = launch_w16_lay<LayEcoli, 4, 2, 64, HRF_W16T_OCC>(stack, P, refx, R, rpad, best_idx, best_dist,
+      if (hrf_status st = launch_w16_lay<LayEcoli, 4, 2, 64, HRF_W16T_SCREEN_OCC, HRF_W16T_NG>(stack, P, refx, R, rpad, best_idx, best_dist,
                                                                             second, s))
         return st;
       HRF_LAUNCHED();
@@ -2538,14 +2556,15 @@ hrf_status hrf_classify_pixels_table(const void *table, const uint8_t *flags, in
   if (P == 0) return HRF_OK;
   HRF_REQUIRE(table && flags && refx && best_idx && best_dist, "classify_pixels_table: null buffer");
   hipStream_t s = (hipStream_t)stream;
-  const unsigned grid = (unsigned)hrf::cdiv(P, 256);
+  const unsigned grid = (unsigned)hrf::cdiv(P, 64 * HRF_W16T_NG);
   auto go = [&](auto lay_tag) -> hrf_status {
     using L = decltype(lay_tag);
     constexpr int KT = (L::C + 1 + 31) / 32;
     const size_t shm = (size_t)2 * 64 * (128 * KT + L::PADB);
-    (void)hipFuncSetAttribute((const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_OCC, false><<<grid, 256, shm, s>>>(
+    (void)hipFuncSetAttribute(
+        (const void *)classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_SCREEN_OCC, false, HRF_W16T_NG>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    classify_pixels_w16t_kernel<L, 4, 2, 64, HRF_W16T_SCREEN_OCC, false, HRF_W16T_NG><<<grid, 256, shm, s>>>(
         (const uint4 *)table, flags, P, (const _Float16 *)refx, R, rpad, best_idx, best_dist, second, RefineArgs{});
     return HRF_OK;
   };
