@@ -30,10 +30,12 @@ def main():
         m = K.refx_mode(refx, 95, S.ECOLI_BOUNDS)
         kp, _ = K.classify_geometry(95, 5, R, m)
         def once():
+            # the MFMA screen (the roofline's kernel); the exact path adds the f64 refine
+            # (tools/time_classify_exact.py)
             if table:
-                K.classify_pixels_table(pt, refx, R)
+                K.classify_pixels_table_screen(pt, refx, R)
             else:
-                K.classify_pixels(stack, refx, R, S.ECOLI_BOUNDS)
+                K.classify_pixels_screen(stack, refx, R, S.ECOLI_BOUNDS, mode=m)
         for _ in range(2):
             once()
         torch.cuda.synchronize()
