@@ -1094,17 +1094,23 @@ __device__ __forceinline__ void lay_sweep(const char *__restrict__ gref, char *l
       const char *row = buf + (rb + j) * ROWB + 16 * h;
       h8 az;
       if (ZS) az = *reinterpret_cast<const h8 *>(buf + (rb + j) * ROWB + 4 * KP);
+      // the cross products (hi * lo', lo * hi') first, then hi * hi': the small products meet an
+      // accumulator of ~2^-10 of a score (screen_eps counts KS16 + 1 full-magnitude MFMAs)
 #pragma unroll
       for (int s = 0; s < KS16; ++s) {
         const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
         const h8 al = *reinterpret_cast<const h8 *>(row + 2 * KP + 32 * s);
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0[s], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1[s], acc1, 0, 0, 0);
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl1[s], acc1, 0, 0, 0);
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh0[s], acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh1[s], acc1, 0, 0, 0);
         epi((16 * s) / KS16, (16 * (s + 1)) / KS16);  // previous block, slice s
+      }
+#pragma unroll
+      for (int s = 0; s < KS16; ++s) {
+        const h8 ah = *reinterpret_cast<const h8 *>(row + 32 * s);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh0[s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh1[s], acc1, 0, 0, 0);
       }
       if (ZS) {
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(az, bz0, acc0, 0, 0, 0);
@@ -2364,7 +2370,10 @@ ScreenEps eps_of_screen(int screen, const Bounds &bd, int C, int kp) {
   const int lay = layout_id(bd, C);
   if (screen == 0) return screen_eps(bd, 0, true, kp);
   if (screen == 1) return screen_eps(bd, 3 * (kp / 16), false, kp);
-  if (screen == 2 && lay == 2) return screen_eps(bd, 3 * ((C + 1 + 15) / 16) + 1, false, kp);
+  if (screen == 2 && lay == 2) {  // classify_pixels_lay_kernel: cross products first, as w16
+    const int ks = (C + 1 + 15) / 16;
+    return screen_eps(bd, ks + 1 + 2.0 * ks * 0x1p-9, false, kp);
+  }
   // w16 / w16t: the 2 KT cross-product MFMAs meet accumulators below 2^-9 A (their products are
   // <= 2^-10 A in all), then KT hi * hi' MFMAs and the indicator step at full magnitude
   const int kt = (C + 1 + 31) / 32;
