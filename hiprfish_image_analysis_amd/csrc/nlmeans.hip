@@ -199,12 +199,18 @@ __global__ __launch_bounds__(NT, NT == 256 ? 2 : 4) void nl_means_pairs_kernel(c
 // each of the 256 CUs -- 48-row tiles left the sixth round 3/8 full (3.42 vs 3.80 ms, two
 // alternating rounds, profiles/r5_nlm_ab.txt)
 constexpr int NL_TILE_H = 52;
+#ifndef HRF_NLM_RSEG
+#define HRF_NLM_RSEG 8  // row-phase segment (columns per item)
+#endif
+#ifndef HRF_NLM_CSEG
+#define HRF_NLM_CSEG 4  // column-phase segment (rows per item)
+#endif
 
 template <bool VAR>
 void launch_pairs(hipStream_t st, const double *img, int64_t H, int64_t W, double inv, double lim, double var,
                   double *out) {
   dim3 g((unsigned)hrf::cdiv(W, NP_TW), (unsigned)hrf::cdiv(H, NL_TILE_H));
-  nl_means_pairs_kernel<VAR, 8, 4, 1024, NL_TILE_H><<<g, 1024, 0, st>>>(img, H, W, inv, lim, var, out);
+  nl_means_pairs_kernel<VAR, HRF_NLM_RSEG, HRF_NLM_CSEG, 1024, NL_TILE_H><<<g, 1024, 0, st>>>(img, H, W, inv, lim, var, out);
 }
 
 }  // namespace

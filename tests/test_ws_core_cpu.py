@@ -77,3 +77,22 @@ def test_any_marker_seeds_exercise_the_heap_replay(orc):
     from test_watershed_gpu import ANY_MARKER_SEEDS, any_markers_case
     hits = [s for s in ANY_MARKER_SEEDS if orc.watershed_ordered(*any_markers_case(s))[1][2] > 0]
     assert hits, "no seed meets an equal-valued-marker decision"
+
+
+def test_tie_tile_decisions_come_down_to_the_heap_layout(orc):
+    """synthetic.tie_tile's premise (the tile-chain GPU test relies on it): through the restated E. coli
+    segmentation its watershed makes equal-marker decisions, and the order model alone (raw) labels
+    corridor pixels differently from skimage's heap, so only the replay gives the heap's map; an even
+    corridor makes none"""
+    torch = pytest.importorskip("torch")
+    import pipeline as OP
+    from hiprfish_image_analysis_amd import synthetic as S
+    for gap, want in ((1, True), (2, False)):
+        lasers = [l.numpy() for l in S.laser_split(S.tie_tile(160, 160, gap=gap, device="cpu"))]
+        reg = OP.register_stacks(lasers, OP.estimate_shifts(lasers), True)
+        keep = {}
+        OP.segment_ecoli(reg, keep=keep)
+        raw, st = orc.watershed_ordered(-keep["image_cn"], keep["seeds"], keep["rough_mask"], raw=True)
+        assert (st[2] > 0) == want, st
+        assert ((raw != keep["watershed"]).any()) == want
+    del torch
