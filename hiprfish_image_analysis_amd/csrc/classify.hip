@@ -2417,7 +2417,8 @@ hrf_status refine_list(const RefineArgs &A, int64_t P, int32_t C, int32_t R, con
   int32_t kp = 0, rpad = 0;
   if (hrf_status st = hrf_classify_geometry(C, bd.nseg, R, screen == 3 ? 2 : screen, &kp, &rpad)) return st;
   const ScreenEps ep = eps_of_screen(screen, bd, C, kp);
-  const size_t shm = sizeof(float) * LIST_NP * (size_t)A.E.RT;
+  const size_t shm = sizeof(float) * LIST_NP * (size_t)A.E.RT;  // 128 KB at R = LIST_RMAX
+  (void)hipFuncSetAttribute((const void *)refine_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
   const unsigned g = hrf::resident_grid(refine_list_kernel, LIST_NT, shm, hrf::cdiv(P, LIST_NP));
   refine_list_kernel<<<g, LIST_NT, shm, s>>>(A.S, C, bd, A.E, A.hdr, R, ep.eps32, A.list, A.cnt, A.cnt + 1, best_idx,
                                              best_dist);

@@ -254,3 +254,31 @@ def test_refine_from_lasers_equals_stack(K, S, orc):
             assert torch.equal(v[0], b[0]) and torch.equal(v[1], b[1])
         x = host(reg).reshape(H * W, -1).astype(np.float64)
         check_pixel_argmin(orc, host(a[0]).ravel(), host(a[1]).ravel(), x, ref.astype(np.float64), ECOLI)
+
+
+@pytest.mark.parametrize("mode", [2, "table"])
+def test_largest_library_exact(K, S, orc, mode):
+    """R = 4095 (12-bit barcodes, LIST_RMAX = 4096: the list pass's 128 KB of LDS scores) with
+    near-duplicate rows, so the list pass runs at the largest library the refine accepts; one
+    row more is refused"""
+    from test_kernels_gpu import check_pixel_argmin
+    bounds = ECOLI
+    ref = S.reference_library(12, bounds).astype(np.float32).copy()
+    R, C = ref.shape
+    assert R == 4095
+    rng = np.random.default_rng(5)
+    ref[R // 2:R // 2 + 64] = ref[:64] * np.float32(1 + 3e-7)   # near ties the screen cannot separate
+    x = ref[rng.integers(0, R, 4096)] * rng.uniform(0.5, 1, (4096, 1)) + rng.normal(0, 0.01, (4096, C))
+    x = np.clip(x, 0, None).astype(np.float32)
+    st = dev(x.reshape(64, 64, C))
+    if mode == "table":
+        refx = K.classify_prepare(dev(ref), bounds, mode=2)
+        gi, gd, n = K.classify_pixels_table(K.pixtable_prepare(st, bounds), refx, R, want_listed=True)
+        assert n > 0
+    else:
+        refx = K.classify_prepare(dev(ref), bounds, mode=2)
+        gi, gd = K.classify_pixels(st, refx, R, bounds)
+    check_pixel_argmin(orc, host(gi).ravel(), host(gd).ravel(), x.astype(np.float64), ref.astype(np.float64), bounds)
+    big = np.concatenate([ref, ref[:2]])
+    with pytest.raises(Exception):
+        K.classify_prepare(dev(big), bounds, mode=2)
