@@ -282,3 +282,22 @@ def test_largest_library_exact(K, S, orc, mode):
     big = np.concatenate([ref, ref[:2]])
     with pytest.raises(Exception):
         K.classify_prepare(dev(big), bounds, mode=2)
+
+
+@pytest.mark.parametrize("npx", [1, 5, 63, 65, 191, 193, 257])
+def test_small_and_ragged_pixel_counts(K, S, orc, npx):
+    """pixel counts that end inside a 16-pixel group, a 64-pixel certificate wave, a 192-pixel screen
+    workgroup and a 256-pixel table block: both screens and the exact answers on every pixel"""
+    from test_kernels_gpu import check_pixel_argmin
+    bounds = ECOLI
+    ref = S.reference_library(10, bounds).astype(np.float32)
+    R, C = ref.shape
+    rng = np.random.default_rng(npx)
+    x = ref[rng.integers(0, R, npx)] * rng.uniform(0.5, 1, (npx, 1)) + rng.normal(0, 0.02, (npx, C))
+    x = np.clip(x, 0, None).astype(np.float32)
+    st = dev(x.reshape(1, npx, C))
+    refx = K.classify_prepare(dev(ref), bounds, mode=2)
+    a = K.classify_pixels(st, refx, R, bounds)
+    b = K.classify_pixels_table(K.pixtable_prepare(st, bounds), refx, R)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    check_pixel_argmin(orc, host(a[0]).ravel(), host(a[1]).ravel(), x.astype(np.float64), ref.astype(np.float64), bounds)
