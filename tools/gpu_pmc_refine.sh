@@ -10,6 +10,8 @@ run() {  # name, counters...
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $out/$name -o pmc -- \
     python3 tools/time_classify_exact.py 3 > $out/$name.log 2>&1
 }
+run fetch FETCH_SIZE &&
+run write WRITE_SIZE &&
 run sq1 SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE &&
 run sq2 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_INSTS_SMEM &&
 run tcc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum &&
